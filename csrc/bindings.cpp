@@ -1,0 +1,336 @@
+// Python bindings of the gfx950 kernels (torch extension module `pytorch_distributed_template_amd._C`).
+//
+// The binding layer is deliberately thin: it validates tensors (device, dtype, contiguity, sizes
+// that the kernels' grids assume) and forwards raw pointers plus the current PyTorch HIP stream to
+// the launchers in csrc/kernels/*.hip.  Every kernel is enqueued on the caller's current stream, so
+// the ops compose with PyTorch's stream semantics, hipGraph capture and RCCL's stream ordering.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <cstdio>
+#include <optional>
+#include <stdexcept>
+#include <string>
+
+#include "dtypes.h"
+#include "kernels/bn.h"
+#include "kernels/conv_fwd.h"
+#include "kernels/conv_wgrad.h"
+#include "kernels/loss.h"
+#include "kernels/optim.h"
+#include "kernels/pool.h"
+
+void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s failed: %s (%s:%d)", expr, hipGetErrorString(e), file, line);
+  throw std::runtime_error(buf);
+}
+
+namespace {
+
+using at::Tensor;
+using OptT = std::optional<Tensor>;
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, ": expected a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, ": expected a contiguous tensor");
+}
+
+int dt16(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  if (t.scalar_type() == at::kBFloat16) return pdt::kBF16;
+  if (t.scalar_type() == at::kHalf) return pdt::kF16;
+  TORCH_CHECK(false, name, ": expected bfloat16 or float16, got ", t.scalar_type());
+}
+
+uint16_t* p16(const Tensor& t, const char* name) {
+  dt16(t, name);
+  return reinterpret_cast<uint16_t*>(t.data_ptr());
+}
+const uint16_t* p16o(const OptT& t, const char* name) { return t.has_value() ? p16(*t, name) : nullptr; }
+uint16_t* p16m(const OptT& t, const char* name) { return t.has_value() ? p16(*t, name) : nullptr; }
+
+float* pf(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, ": expected float32");
+  return t.data_ptr<float>();
+}
+float* pfo(const OptT& t, const char* name) { return t.has_value() ? pf(*t, name) : nullptr; }
+
+double* pd(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kDouble, name, ": expected float64");
+  return t.data_ptr<double>();
+}
+
+// ------------------------------------------------------------------------------------------ conv
+void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N, int64_t H,
+              int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t ist_h,
+              int64_t ist_w, int64_t ioff_h, int64_t ioff_w, int64_t tstep_h, int64_t tstep_w, int64_t OH, int64_t OW,
+              int64_t ost_h, int64_t ost_w, int64_t ooff_h, int64_t ooff_w, int64_t bm, int64_t bn, int64_t bk) {
+  const int dt = dt16(x, "x");
+  TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv_fwd: mixed dtypes");
+  TORCH_CHECK(x.numel() == N * H * W * C, "conv_fwd: x has ", x.numel(), " elements, geometry needs ", N * H * W * C);
+  TORCH_CHECK(w.numel() == Kout * T * U * C, "conv_fwd: w size mismatch");
+  TORCH_CHECK(y.numel() == N * OH * OW * Kout, "conv_fwd: y size mismatch");
+  TORCH_CHECK(C % bk == 0 && Kout % bn == 0, "conv_fwd: C % bk / Kout % bn must be 0 (C=", C, " Kout=", Kout, ")");
+  TORCH_CHECK(ost_h >= 1 && ost_w >= 1 && (Pm - 1) * ost_h + ooff_h < OH && (Qm - 1) * ost_w + ooff_w < OW,
+              "conv_fwd: output sub-grid exceeds the output tensor");
+  pdt::ConvFwdArgs a{};
+  a.x = p16(x, "x");
+  a.w = p16(w, "w");
+  a.y = p16(y, "y");
+  if (res.has_value()) {
+    TORCH_CHECK(res->numel() == y.numel(), "conv_fwd: residual size mismatch");
+    a.res = p16(*res, "res");
+  }
+  const int64_t M = N * Pm * Qm;
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::conv_fwd_m_tiles(M, (int)bm) * Kout * 2, "conv_fwd: stats buffer too small");
+    a.stats = pf(*stats, "stats");
+  }
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
+  a.ist_h = ist_h; a.ist_w = ist_w; a.ioff_h = ioff_h; a.ioff_w = ioff_w; a.tstep_h = tstep_h; a.tstep_w = tstep_w;
+  a.OH = OH; a.OW = OW; a.ost_h = ost_h; a.ost_w = ost_w; a.ooff_h = ooff_h; a.ooff_w = ooff_w;
+  a.M = M;
+  pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+}
+
+int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (int)bm); }
+
+std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks) {
+  pdt::ConvWgradArgs a{};
+  a.Kout = Kout; a.T = T; a.U = U; a.C = C; a.P = P;
+  pdt::conv_wgrad_plan(a, (int)target_blocks);
+  return {a.splits, a.pix_per_split};
+}
+
+void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
+                int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride_h, int64_t stride_w, int64_t pad_h,
+                int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t ldw, int64_t splits, int64_t pix_per_split) {
+  const int dt = dt16(x, "x");
+  TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad: mixed dtypes");
+  TORCH_CHECK(C % 64 == 0 && Kout % 64 == 0, "conv_wgrad: C and Kout must be multiples of 64");
+  TORCH_CHECK(x.numel() == N * H * W * C && dy.numel() == N * Pm * Qm * Kout, "conv_wgrad: size mismatch");
+  TORCH_CHECK(ldw >= T * U * C && ws.numel() >= splits * Kout * ldw, "conv_wgrad: workspace too small");
+  TORCH_CHECK(N * Pm * Qm < (1 << 24), "conv_wgrad: pixel count exceeds the fp32-reciprocal divide range");
+  pdt::ConvWgradArgs a{};
+  a.x = p16(x, "x");
+  a.dy = p16(dy, "dy");
+  a.ws = pf(ws, "ws");
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
+  a.stride_h = stride_h; a.stride_w = stride_w; a.pad_h = pad_h; a.pad_w = pad_w; a.dil_h = dil_h; a.dil_w = dil_w;
+  a.P = N * Pm * Qm; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
+  TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad: bad split plan");
+  pdt::conv_wgrad_launch(a, dt, cur_stream());
+}
+
+void wgrad_reduce(const Tensor& ws, int64_t splits, int64_t rows, int64_t cols, int64_t ldw, int64_t split_stride,
+                  Tensor& out, int64_t ldo, double scale, bool accumulate) {
+  TORCH_CHECK(ws.numel() >= (splits - 1) * split_stride + (rows - 1) * ldw + cols, "wgrad_reduce: ws too small");
+  TORCH_CHECK(out.numel() >= (rows - 1) * ldo + cols, "wgrad_reduce: out too small");
+  pdt::wgrad_reduce_launch(pf(ws, "ws"), splits, rows, cols, ldw, split_stride, pf(out, "out"), ldo, (float)scale,
+                           accumulate, cur_stream());
+}
+
+// -------------------------------------------------------------------------------------------- bn
+void bn_partial_reduce(const Tensor& part, int64_t tiles, int64_t C, int64_t K, Tensor& scratch, Tensor& sums) {
+  TORCH_CHECK(part.numel() >= tiles * C * K, "bn_partial_reduce: partials too small");
+  TORCH_CHECK(scratch.numel() >= 64 * C * K && sums.numel() >= C * K, "bn_partial_reduce: scratch/sums too small");
+  pdt::bn_partial_reduce_launch(pf(part, "part"), tiles, C, K, pd(scratch, "scratch"), pd(sums, "sums"), cur_stream());
+}
+
+void bn_finalize(const Tensor& sums, double count, const Tensor& gamma, const Tensor& beta, double eps, double momentum,
+                 Tensor& rm, Tensor& rv, Tensor& coef, bool update_running) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(coef.numel() >= 4 * C && sums.numel() >= 2 * C, "bn_finalize: size mismatch");
+  pdt::bn_finalize_launch(pd(sums, "sums"), count, pf(gamma, "gamma"), pf(beta, "beta"), (float)eps, (float)momentum,
+                          pf(rm, "running_mean"), pf(rv, "running_var"), pf(coef, "coef"), C, update_running,
+                          cur_stream());
+}
+
+void bn_eval_coef(const Tensor& gamma, const Tensor& beta, const Tensor& rm, const Tensor& rv, double eps, Tensor& coef) {
+  const int64_t C = gamma.numel();
+  pdt::bn_eval_coef_launch(pf(gamma, "gamma"), pf(beta, "beta"), pf(rm, "rm"), pf(rv, "rv"), (float)eps, pf(coef, "coef"),
+                           C, cur_stream());
+}
+
+void bn_apply(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& rcoef, Tensor& out, int64_t C,
+              int64_t resmode, bool relu) {
+  const int dt = dt16(y, "y");
+  TORCH_CHECK(C % 8 == 0 && y.numel() % C == 0 && out.numel() == y.numel(), "bn_apply: bad sizes");
+  if (resmode != 0) TORCH_CHECK(res.has_value() && res->numel() == y.numel(), "bn_apply: residual missing/mismatch");
+  if (resmode == 2) TORCH_CHECK(rcoef.has_value(), "bn_apply: residual coefficients missing");
+  pdt::bn_apply_launch(dt, p16(y, "y"), pf(coef, "coef"), p16o(res, "res"), pfo(rcoef, "rcoef"), p16(out, "out"),
+                       y.numel(), C, (int)resmode, relu, cur_stream());
+}
+
+int64_t bn_bwd_reduce_blocks(int64_t rows, int64_t C) { return pdt::bn_bwd_reduce_blocks(rows, (int)C); }
+
+void bn_bwd_reduce(const Tensor& g, const OptT& out, const Tensor& y1, const Tensor& coef1, const OptT& y2,
+                   const OptT& coef2, Tensor& part, int64_t blocks, int64_t rows, int64_t C) {
+  const int dt = dt16(g, "g");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && g.numel() == rows * C && y1.numel() == rows * C, "bn_bwd_reduce: bad sizes");
+  const int K = y2.has_value() ? 4 : 2;
+  TORCH_CHECK(part.numel() >= blocks * C * K, "bn_bwd_reduce: partials too small");
+  pdt::bn_bwd_reduce_launch(dt, p16(g, "g"), p16o(out, "out"), p16(y1, "y1"), pf(coef1, "coef1"), p16o(y2, "y2"),
+                            pfo(coef2, "coef2"), pf(part, "part"), (int)blocks, rows, (int)C, cur_stream());
+}
+
+void bn_bwd_finalize(const Tensor& sums, double count, const Tensor& coef, const Tensor& gamma, const OptT& dgamma,
+                     const OptT& dbeta, double gscale, Tensor& bcoef) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(bcoef.numel() >= 3 * C, "bn_bwd_finalize: bcoef too small");
+  pdt::bn_bwd_finalize_launch(pd(sums, "sums"), count, pf(coef, "coef"), pf(gamma, "gamma"), pfo(dgamma, "dgamma"),
+                              pfo(dbeta, "dbeta"), (float)gscale, pf(bcoef, "bcoef"), C, cur_stream());
+}
+
+void bn_bwd_apply(const Tensor& g, const OptT& out, const Tensor& y1, const Tensor& b1, Tensor& dy1, const OptT& y2,
+                  const OptT& b2, const OptT& dy2, const OptT& dz, int64_t C) {
+  const int dt = dt16(g, "g");
+  TORCH_CHECK(C % 8 == 0 && g.numel() % C == 0 && dy1.numel() == g.numel(), "bn_bwd_apply: bad sizes");
+  pdt::bn_bwd_apply_launch(dt, p16(g, "g"), p16o(out, "out"), p16(y1, "y1"), pf(b1, "b1"), p16(dy1, "dy1"),
+                           p16o(y2, "y2"), pfo(b2, "b2"), p16m(dy2, "dy2"), p16m(dz, "dz"), g.numel(), C, cur_stream());
+}
+
+// ------------------------------------------------------------------------------------------ pool
+void bn_relu_maxpool(const Tensor& y, const Tensor& coef, Tensor& out, Tensor& idx, int64_t N, int64_t H, int64_t W,
+                     int64_t C) {
+  const int dt = dt16(y, "y");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(y.numel() == N * H * W * C && out.numel() == N * OH * OW * C && idx.numel() == out.numel() && C % 8 == 0,
+              "bn_relu_maxpool: bad sizes");
+  check_dev(idx, "idx");
+  pdt::bn_relu_maxpool_launch(dt, p16(y, "y"), pf(coef, "coef"), p16(out, "out"), idx.data_ptr<uint8_t>(), N, H, W, C,
+                              cur_stream());
+}
+
+void maxpool_bwd_relu(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& dz, int64_t N,
+                      int64_t H, int64_t W, int64_t C) {
+  const int dt = dt16(dp, "dp");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dp.numel() == N * OH * OW * C && y.numel() == N * H * W * C && dz.numel() == y.numel(),
+              "maxpool_bwd_relu: bad sizes");
+  check_dev(idx, "idx");
+  pdt::maxpool_bwd_relu_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"), p16(dz, "dz"),
+                               N, H, W, C, cur_stream());
+}
+
+void avgpool_fwd(const Tensor& x, Tensor& feat, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
+  const int dt = dt16(x, "x");
+  TORCH_CHECK(x.numel() == N * HW * C && feat.numel() >= N * ldf && C % 8 == 0, "avgpool_fwd: bad sizes");
+  pdt::avgpool_fwd_launch(dt, p16(x, "x"), p16(feat, "feat"), N, HW, C, ldf, cur_stream());
+}
+
+void avgpool_bwd(const Tensor& dfeat, Tensor& g, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
+  const int dt = dt16(dfeat, "dfeat");
+  TORCH_CHECK(g.numel() == N * HW * C && dfeat.numel() >= N * ldf && C % 8 == 0, "avgpool_bwd: bad sizes");
+  pdt::avgpool_bwd_launch(dt, p16(dfeat, "dfeat"), p16(g, "g"), N, HW, C, ldf, cur_stream());
+}
+
+// ------------------------------------------------------------------------------------------ loss
+void xent(const Tensor& logits, int64_t ldl, const OptT& bias, const Tensor& target, int64_t B, int64_t ncls,
+          const OptT& out_logits, const OptT& dlogits, const OptT& loss_scale, double grad_div, Tensor& row_loss,
+          Tensor& row_correct) {
+  const int dt = dt16(logits, "logits");
+  check_dev(target, "target");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == B, "xent: target must be int64 [B]");
+  TORCH_CHECK(logits.numel() >= B * ldl && ncls <= ldl, "xent: logits too small");
+  if (out_logits.has_value()) TORCH_CHECK(out_logits->numel() == B * ncls, "xent: out_logits size");
+  if (dlogits.has_value()) TORCH_CHECK(dlogits->numel() >= B * ldl, "xent: dlogits size");
+  pdt::xent_launch(dt, p16(logits, "logits"), ldl, pfo(bias, "bias"), target.data_ptr<int64_t>(), B, ncls,
+                   pfo(out_logits, "out_logits"), p16m(dlogits, "dlogits"), pfo(loss_scale, "loss_scale"),
+                   (float)grad_div, pf(row_loss, "row_loss"), pf(row_correct, "row_correct"), cur_stream());
+}
+
+void metrics(const Tensor& row_loss, const Tensor& row_correct, int64_t B, Tensor& out) {
+  pdt::metrics_launch(pf(row_loss, "row_loss"), pf(row_correct, "row_correct"), B, pf(out, "out"), cur_stream());
+}
+
+void colsum(const Tensor& d, int64_t B, int64_t ld, int64_t ncols, Tensor& out, double scale) {
+  const int dt = dt16(d, "d");
+  TORCH_CHECK(d.numel() >= B * ld && out.numel() >= ncols, "colsum: bad sizes");
+  pdt::colsum_launch(dt, p16(d, "d"), B, ld, ncols, pf(out, "out"), (float)scale, cur_stream());
+}
+
+// ----------------------------------------------------------------------------------------- optim
+void nonfinite_check(const Tensor& g, Tensor& found) {
+  pdt::nonfinite_check_launch(pf(g, "g"), g.numel(), pf(found, "found"), cur_stream());
+}
+
+void sgd(Tensor& p, const Tensor& g, Tensor& buf, const OptT& shadow, const OptT& wd_mask, double lr, double momentum,
+         double wd, double gscale, const OptT& loss_scale, const OptT& found_inf, bool first) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && buf.numel() == n, "sgd: size mismatch");
+  int dt = pdt::kBF16;
+  if (shadow.has_value()) {
+    dt = dt16(*shadow, "shadow");
+    TORCH_CHECK(shadow->numel() == n, "sgd: shadow size mismatch");
+  }
+  if (wd_mask.has_value()) TORCH_CHECK(wd_mask->numel() == n, "sgd: wd_mask size mismatch");
+  pdt::sgd_launch(dt, pf(p, "p"), pf(g, "g"), pf(buf, "buf"), p16m(shadow, "shadow"), pfo(wd_mask, "wd_mask"), n,
+                  (float)lr, (float)momentum, (float)wd, (float)gscale, pfo(loss_scale, "loss_scale"),
+                  pfo(found_inf, "found_inf"), first, cur_stream());
+}
+
+void cast16(const Tensor& p, Tensor& out) {
+  TORCH_CHECK(p.numel() == out.numel(), "cast16: size mismatch");
+  pdt::cast16_launch(dt16(out, "out"), pf(p, "p"), p16(out, "out"), p.numel(), cur_stream());
+}
+
+void amp_update(Tensor& scale, Tensor& tracker, Tensor& found_inf, double growth, double backoff, int64_t interval) {
+  check_dev(tracker, "tracker");
+  TORCH_CHECK(tracker.scalar_type() == at::kInt, "amp_update: tracker must be int32");
+  pdt::amp_update_launch(pf(scale, "scale"), tracker.data_ptr<int>(), pf(found_inf, "found_inf"), (float)growth,
+                         (float)backoff, (int)interval, cur_stream());
+}
+
+void gather16(const Tensor& src, const Tensor& idx, Tensor& dst) {
+  check_dev(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == dst.numel(), "gather16: idx must be int32 like dst");
+  pdt::gather16_launch(p16(src, "src"), idx.data_ptr<int>(), p16(dst, "dst"), dst.numel(), cur_stream());
+}
+
+void im2col(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
+            int64_t stride, int64_t pad, int64_t ldk) {
+  const int dt = dt16(out, "out");
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * OH * OW * ldk && ldk % 8 == 0 && ldk >= R * S * C,
+              "im2col: bad sizes");
+  pdt::im2col_launch(dt, pf(x, "x"), p16(out, "out"), N, C, H, W, R, S, stride, pad, ldk, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels of pytorch_distributed_template_amd";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_m_tiles", &conv_m_tiles);
+  m.def("conv_wgrad_plan", &conv_wgrad_plan);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("wgrad_reduce", &wgrad_reduce);
+  m.def("bn_partial_reduce", &bn_partial_reduce);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_eval_coef", &bn_eval_coef);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce_blocks", &bn_bwd_reduce_blocks);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bn_relu_maxpool", &bn_relu_maxpool);
+  m.def("maxpool_bwd_relu", &maxpool_bwd_relu);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("xent", &xent);
+  m.def("metrics", &metrics);
+  m.def("colsum", &colsum);
+  m.def("nonfinite_check", &nonfinite_check);
+  m.def("sgd", &sgd);
+  m.def("cast16", &cast16);
+  m.def("amp_update", &amp_update);
+  m.def("gather16", &gather16);
+  m.def("im2col", &im2col);
+}

@@ -1,0 +1,74 @@
+// Shared definitions for the gfx950 (CDNA4 / MI355X) kernels of pytorch_distributed_template_amd.
+//
+// Activations are NHWC, 16-bit (bf16 or fp16) storage; accumulation and all statistics are fp32.
+// Every kernel is written for wave64; block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dtypes.h"
+
+#define PDT_DEVICE __device__ __forceinline__
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+namespace pdt {
+
+// 16-bit element traits: storage is uint16_t, math is fp32.
+template <int DT> struct E16;
+template <> struct E16<kBF16> {
+  typedef bf16x8_t vec8;
+  static PDT_DEVICE float to_f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+  static PDT_DEVICE uint16_t from_f(float f) {
+    __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN stays NaN
+    return __builtin_bit_cast(uint16_t, b);
+  }
+  static PDT_DEVICE f32x4_t mfma16x16x32(vec8 a, vec8 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct E16<kF16> {
+  typedef f16x8_t vec8;
+  static PDT_DEVICE float to_f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+  static PDT_DEVICE uint16_t from_f(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+  static PDT_DEVICE f32x4_t mfma16x16x32(vec8 a, vec8 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+// Zero bytes used as the global source for out-of-bounds LDS-DMA lanes (zero padding).
+static __device__ uint4 g_zero16[8];
+
+PDT_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+PDT_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block index: blocks b and b+8 share an XCD under the
+// observed round-robin dispatch, so give each XCD a contiguous range of logical tiles
+// (speed only, never correctness: any placement is valid).
+PDT_DEVICE int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, local = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+}  // namespace pdt
+
+#define PDT_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) pdt_hip_fail(#expr, _e, __FILE__, __LINE__);             \
+  } while (0)
+
+void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line);

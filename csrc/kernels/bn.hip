@@ -1,0 +1,374 @@
+// BatchNorm (+ReLU, +residual) kernels over NHWC 16-bit activations, fp32 math.
+//
+// Training forward:  conv epilogue emits per-M-tile (sum, sumsq) partials
+//                    -> bn_partial_reduce (fp64 per-channel sums; SyncBN all-reduces these)
+//                    -> bn_finalize (mean, invstd, folded scale/shift, running-stat update)
+//                    -> bn_apply (y*scale+shift [+ residual | + BN(residual)] -> ReLU)
+// Training backward: bn_bwd_reduce (dz = g * relu'(out); sum dz, sum dz*xhat for up to two BN
+//                    branches that share dz, e.g. the main and downsample branch of a residual block)
+//                    -> bn_partial_reduce -> bn_bwd_finalize (dgamma/dbeta into the grad buffer,
+//                    per-channel coefficients) -> bn_bwd_apply (dy = a*dz + b*y + c per branch).
+#include "../common.h"
+#include "bn.h"
+
+namespace pdt {
+
+// -------------------------------------------------------------------------------------------------
+// partials [tiles][C][K] float  ->  out [G][C][K] double (grid.y = G groups of tiles)
+__global__ __launch_bounds__(256) void bn_partial_reduce_kernel(const float* __restrict__ part, int tiles, int C,
+                                                                int K, double* __restrict__ out) {
+  // block: 64 channels x 4 tile-lanes
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int tl = threadIdx.x >> 6;
+  const int G = gridDim.y, g = blockIdx.y;
+  double acc[4] = {0, 0, 0, 0};
+  if (c < C) {
+    for (int t = g * 4 + tl; t < tiles; t += G * 4) {
+      const float* p = part + ((int64_t)t * C + c) * K;
+      for (int k = 0; k < K; ++k) acc[k] += (double)p[k];
+    }
+  }
+  __shared__ double red[4][64][4];
+  for (int k = 0; k < 4; ++k) red[tl][threadIdx.x & 63][k] = acc[k];
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    for (int k = 0; k < K; ++k) {
+      const double s = red[0][threadIdx.x][k] + red[1][threadIdx.x][k] + red[2][threadIdx.x][k] + red[3][threadIdx.x][k];
+      out[((int64_t)g * C + c) * K + k] = s;
+    }
+  }
+}
+
+// [G][C][K] double -> sums[k*C + c] double  (channel-major per quantity, SyncBN message layout)
+__global__ void bn_group_sum_kernel(const double* __restrict__ in, int G, int C, int K, double* __restrict__ sums) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= C * K) return;
+  const int c = idx / K, k = idx - (idx / K) * K;
+  double s = 0;
+  for (int g = 0; g < G; ++g) s += in[((int64_t)g * C + c) * K + k];
+  sums[k * C + c] = s;
+}
+
+void bn_partial_reduce_launch(const float* part, int tiles, int C, int K, double* scratch, double* sums,
+                              hipStream_t s) {
+  int G = (tiles + 255) / 256;
+  if (G > 64) G = 64;
+  if (G < 1) G = 1;
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, s, part, tiles, C, K, scratch);
+  hipLaunchKernelGGL(bn_group_sum_kernel, dim3((C * K + 255) / 256), dim3(256), 0, s, scratch, G, C, K, sums);
+}
+
+// -------------------------------------------------------------------------------------------------
+// sums[0:C] = sum x, sums[C:2C] = sum x^2, count = number of elements per channel (global)
+// coef[0:C] = scale = gamma*invstd, coef[C:2C] = shift = beta - mean*scale,
+// coef[2C:3C] = mean, coef[3C:4C] = invstd
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, double count, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float momentum,
+                                   float* __restrict__ running_mean, float* __restrict__ running_var,
+                                   float* __restrict__ coef, int C, int update_running) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = sums[c] / count;
+  double var = sums[C + c] / count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  coef[c] = sc;
+  coef[C + c] = beta[c] - (float)mean * sc;
+  coef[2 * C + c] = (float)mean;
+  coef[3 * C + c] = invstd;
+  if (update_running) {
+    const double unbiased = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+// eval-mode coefficients from running statistics
+__global__ void bn_eval_coef_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    const float* __restrict__ running_mean, const float* __restrict__ running_var,
+                                    float eps, float* __restrict__ coef, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(running_var[c] + eps);
+  const float sc = gamma[c] * invstd;
+  coef[c] = sc;
+  coef[C + c] = beta[c] - running_mean[c] * sc;
+  coef[2 * C + c] = running_mean[c];
+  coef[3 * C + c] = invstd;
+}
+
+void bn_finalize_launch(const double* sums, double count, const float* gamma, const float* beta, float eps,
+                        float momentum, float* rm, float* rv, float* coef, int C, bool update_running,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, count, gamma, beta, eps,
+                     momentum, rm, rv, coef, C, (int)update_running);
+}
+
+void bn_eval_coef_launch(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                         float* coef, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, gamma, beta, rm, rv, eps, coef, C);
+}
+
+// -------------------------------------------------------------------------------------------------
+// out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift
+template <int DT, int RESMODE, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ coef,
+                                                       const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ rcoef, uint16_t* __restrict__ out,
+                                                       int64_t n8, int C) {
+  using E = E16<DT>;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((v * 8) % C);
+    const uint4 yy = ((const uint4*)y)[v];
+    uint4 rr;
+    if constexpr (RESMODE != 0) rr = ((const uint4*)res)[v];
+    const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
+    uint32_t rw[4];
+    if constexpr (RESMODE != 0) { rw[0] = rr.x; rw[1] = rr.y; rw[2] = rr.z; rw[3] = rr.w; }
+    uint32_t ow[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float o2[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = c0 + 2 * e + h;
+        float val = E::to_f((uint16_t)(yw[e] >> (16 * h))) * coef[c] + coef[C + c];
+        if constexpr (RESMODE == 1) val += E::to_f((uint16_t)(rw[e] >> (16 * h)));
+        if constexpr (RESMODE == 2) val += E::to_f((uint16_t)(rw[e] >> (16 * h))) * rcoef[c] + rcoef[C + c];
+        if constexpr (RELU) val = fmaxf(val, 0.f);
+        o2[h] = val;
+      }
+      ow[e] = (uint32_t)E::from_f(o2[0]) | ((uint32_t)E::from_f(o2[1]) << 16);
+    }
+    ((uint4*)out)[v] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+}
+
+static int ew_blocks(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (int)(b < 1 ? 1 : b);
+}
+
+template <int DT>
+static void bn_apply_dt(const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef, uint16_t* out,
+                        int64_t n, int C, int resmode, bool relu, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  dim3 g(ew_blocks(n8)), b(256);
+#define PDT_AP(RM, RL)                                                                          \
+  if (resmode == RM && relu == RL) {                                                            \
+    hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL>), g, b, 0, s, y, coef, res, rcoef, out, n8, C); \
+    return;                                                                                     \
+  }
+  PDT_AP(0, true) PDT_AP(1, true) PDT_AP(2, true) PDT_AP(0, false) PDT_AP(1, false) PDT_AP(2, false)
+#undef PDT_AP
+}
+
+void bn_apply_launch(int dtype, const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef,
+                     uint16_t* out, int64_t n, int C, int resmode, bool relu, hipStream_t s) {
+  if (dtype == kBF16)
+    bn_apply_dt<kBF16>(y, coef, res, rcoef, out, n, C, resmode, relu, s);
+  else
+    bn_apply_dt<kF16>(y, coef, res, rcoef, out, n, C, resmode, relu, s);
+}
+
+// -------------------------------------------------------------------------------------------------
+// Backward reduce.  dz = g * (out > 0) (mask optional).  For branch b in {1,2}:
+//   part[blk][c][2b-2] += dz ; part[blk][c][2b-1] += dz * (y_b - mean_b) * invstd_b
+// Each thread owns 8 consecutive channels of a row; rows are strided over the grid.
+template <int DT, bool MASK, int NBR>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
+                                                            const uint16_t* __restrict__ out,
+                                                            const uint16_t* __restrict__ y1,
+                                                            const float* __restrict__ coef1,
+                                                            const uint16_t* __restrict__ y2,
+                                                            const float* __restrict__ coef2,
+                                                            float* __restrict__ part, int64_t rows, int C) {
+  using E = E16<DT>;
+  const int vpr = C / 8;              // 16-byte vectors per row
+  const int rpi = 256 / vpr;          // rows per block iteration (C <= 2048)
+  const int cv = threadIdx.x % vpr;   // vector (channel group) index
+  const int rl = threadIdx.x / vpr;   // row lane
+  const int c0 = cv * 8;
+  float s[NBR * 2][8];
+#pragma unroll
+  for (int k = 0; k < NBR * 2; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[k][e] = 0.f;
+  float m1[8], i1[8], m2[8], i2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    m1[e] = coef1[2 * C + c0 + e];
+    i1[e] = coef1[3 * C + c0 + e];
+    if constexpr (NBR == 2) { m2[e] = coef2[2 * C + c0 + e]; i2[e] = coef2[3 * C + c0 + e]; }
+  }
+  if (rl < rpi) {
+    for (int64_t r = (int64_t)blockIdx.x * rpi + rl; r < rows; r += (int64_t)gridDim.x * rpi) {
+      const int64_t off = r * C + c0;
+      const uint4 gv = *(const uint4*)(g + off);
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+      uint32_t ow[4] = {0, 0, 0, 0};
+      if constexpr (MASK) { const uint4 ov = *(const uint4*)(out + off); ow[0] = ov.x; ow[1] = ov.y; ow[2] = ov.z; ow[3] = ov.w; }
+      const uint4 y1v = *(const uint4*)(y1 + off);
+      const uint32_t y1w[4] = {y1v.x, y1v.y, y1v.z, y1v.w};
+      uint32_t y2w[4] = {0, 0, 0, 0};
+      if constexpr (NBR == 2) { const uint4 y2v = *(const uint4*)(y2 + off); y2w[0] = y2v.x; y2w[1] = y2v.y; y2w[2] = y2v.z; y2w[3] = y2v.w; }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int sh = 16 * (e & 1);
+        float dz = E::to_f((uint16_t)(gw[e >> 1] >> sh));
+        if constexpr (MASK) dz = E::to_f((uint16_t)(ow[e >> 1] >> sh)) > 0.f ? dz : 0.f;
+        const float x1 = (E::to_f((uint16_t)(y1w[e >> 1] >> sh)) - m1[e]) * i1[e];
+        s[0][e] += dz;
+        s[1][e] += dz * x1;
+        if constexpr (NBR == 2) {
+          const float x2 = (E::to_f((uint16_t)(y2w[e >> 1] >> sh)) - m2[e]) * i2[e];
+          s[2][e] += dz;
+          s[3][e] += dz * x2;
+        }
+      }
+    }
+  }
+  // block reduction over row lanes: LDS [rpi][C][NBR*2]
+  extern __shared__ float red[];
+  const int K = NBR * 2;
+  if (rl < rpi) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < NBR * 2; ++k) red[((int64_t)rl * C + c0 + e) * K + k] = s[k][e];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < C * K; idx += 256) {
+    float t = 0.f;
+    for (int r = 0; r < rpi; ++r) t += red[(int64_t)r * C * K + idx];
+    part[(int64_t)blockIdx.x * C * K + idx] = t;
+  }
+}
+
+int bn_bwd_reduce_blocks(int64_t rows, int C) {
+  const int rpi = 256 / (C / 8);
+  int64_t b = (rows + rpi * 16 - 1) / (rpi * 16);  // >= 16 rows per thread
+  if (b > 1024) b = 1024;
+  return (int)(b < 1 ? 1 : b);
+}
+
+void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* coef1,
+                          const uint16_t* y2, const float* coef2, float* part, int blocks, int64_t rows, int C,
+                          hipStream_t s) {
+  const int rpi = 256 / (C / 8);
+  const int nbr = y2 ? 2 : 1;
+  const size_t smem = (size_t)rpi * C * nbr * 2 * sizeof(float);
+  const bool mask = out != nullptr;
+#define PDT_BR(DT_, M_, NB_)                                                                              \
+  if (mask == M_ && nbr == NB_) {                                                                         \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<DT_, M_, NB_>), dim3(blocks), dim3(256), smem, s, g, out, y1, \
+                       coef1, y2, coef2, part, rows, C);                                                  \
+    return;                                                                                               \
+  }
+  if (dtype == kBF16) {
+    PDT_BR(kBF16, true, 1) PDT_BR(kBF16, true, 2) PDT_BR(kBF16, false, 1) PDT_BR(kBF16, false, 2)
+  } else {
+    PDT_BR(kF16, true, 1) PDT_BR(kF16, true, 2) PDT_BR(kF16, false, 1) PDT_BR(kF16, false, 2)
+  }
+#undef PDT_BR
+}
+
+// -------------------------------------------------------------------------------------------------
+// sums[0:C] = sum dz, sums[C:2C] = sum dz*xhat (global over the batch, all ranks for SyncBN).
+// Writes dgamma/dbeta (scaled by gscale) into the grad buffer and the elementwise coefficients
+//   dy = A*dz + B*y + Cc,   A = gamma*invstd, B = -A*invstd*mean_dzx... (expanded below)
+// dy = gamma*invstd*(dz - mean_dz - xhat*mean_dzx) with xhat = (y-mean)*invstd
+//    = A*dz + (-A*invstd*mean_dzx)*y + (-A*mean_dz + A*invstd*mean_dzx*mean)
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, double count, const float* __restrict__ coef,
+                                       const float* __restrict__ gamma, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float gscale, float* __restrict__ bcoef, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sdz = sums[c], sdzx = sums[C + c];
+  if (dgamma) dgamma[c] = (float)sdzx * gscale;
+  if (dbeta) dbeta[c] = (float)sdz * gscale;
+  const float mean = coef[2 * C + c], invstd = coef[3 * C + c];
+  const float A = gamma[c] * invstd;
+  const float mdz = (float)(sdz / count), mdzx = (float)(sdzx / count);
+  bcoef[c] = A;
+  bcoef[C + c] = -A * invstd * mdzx;
+  bcoef[2 * C + c] = -A * mdz + A * invstd * mdzx * mean;
+}
+
+void bn_bwd_finalize_launch(const double* sums, double count, const float* coef, const float* gamma, float* dgamma,
+                            float* dbeta, float gscale, float* bcoef, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, count, coef, gamma, dgamma,
+                     dbeta, gscale, bcoef, C);
+}
+
+// dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad)
+template <int DT, bool MASK, int NBR, bool WDZ>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ g,
+                                                           const uint16_t* __restrict__ out,
+                                                           const uint16_t* __restrict__ y1,
+                                                           const float* __restrict__ b1, uint16_t* __restrict__ dy1,
+                                                           const uint16_t* __restrict__ y2,
+                                                           const float* __restrict__ b2, uint16_t* __restrict__ dy2,
+                                                           uint16_t* __restrict__ dz_out, int64_t n8, int C) {
+  using E = E16<DT>;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((v * 8) % C);
+    const uint4 gv = ((const uint4*)g)[v];
+    const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+    uint32_t ow[4] = {0, 0, 0, 0};
+    if constexpr (MASK) { const uint4 ov = ((const uint4*)out)[v]; ow[0] = ov.x; ow[1] = ov.y; ow[2] = ov.z; ow[3] = ov.w; }
+    const uint4 y1v = ((const uint4*)y1)[v];
+    const uint32_t y1w[4] = {y1v.x, y1v.y, y1v.z, y1v.w};
+    uint32_t y2w[4] = {0, 0, 0, 0};
+    if constexpr (NBR == 2) { const uint4 y2v = ((const uint4*)y2)[v]; y2w[0] = y2v.x; y2w[1] = y2v.y; y2w[2] = y2v.z; y2w[3] = y2v.w; }
+    uint32_t o1[4], o2[4], oz[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t r1[2], r2[2], rz[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = c0 + 2 * e + h;
+        float dz = E::to_f((uint16_t)(gw[e] >> (16 * h)));
+        if constexpr (MASK) dz = E::to_f((uint16_t)(ow[e] >> (16 * h))) > 0.f ? dz : 0.f;
+        rz[h] = E::from_f(dz);
+        r1[h] = E::from_f(b1[c] * dz + b1[C + c] * E::to_f((uint16_t)(y1w[e] >> (16 * h))) + b1[2 * C + c]);
+        if constexpr (NBR == 2)
+          r2[h] = E::from_f(b2[c] * dz + b2[C + c] * E::to_f((uint16_t)(y2w[e] >> (16 * h))) + b2[2 * C + c]);
+      }
+      o1[e] = (uint32_t)r1[0] | ((uint32_t)r1[1] << 16);
+      if constexpr (NBR == 2) o2[e] = (uint32_t)r2[0] | ((uint32_t)r2[1] << 16);
+      oz[e] = (uint32_t)rz[0] | ((uint32_t)rz[1] << 16);
+    }
+    ((uint4*)dy1)[v] = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+    if constexpr (NBR == 2) ((uint4*)dy2)[v] = make_uint4(o2[0], o2[1], o2[2], o2[3]);
+    if constexpr (WDZ) ((uint4*)dz_out)[v] = make_uint4(oz[0], oz[1], oz[2], oz[3]);
+  }
+}
+
+void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* b1,
+                         uint16_t* dy1, const uint16_t* y2, const float* b2, uint16_t* dy2, uint16_t* dz_out, int64_t n,
+                         int C, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  dim3 gr(ew_blocks(n8)), bl(256);
+  const bool mask = out != nullptr, wdz = dz_out != nullptr;
+  const int nbr = y2 ? 2 : 1;
+#define PDT_BA(DT_, M_, NB_, WZ_)                                                                     \
+  if (mask == M_ && nbr == NB_ && wdz == WZ_) {                                                       \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<DT_, M_, NB_, WZ_>), gr, bl, 0, s, g, out, y1, b1, dy1, y2, b2, \
+                       dy2, dz_out, n8, C);                                                           \
+    return;                                                                                           \
+  }
+  if (dtype == kBF16) {
+    PDT_BA(kBF16, true, 1, false) PDT_BA(kBF16, true, 1, true) PDT_BA(kBF16, true, 2, false)
+    PDT_BA(kBF16, false, 1, false) PDT_BA(kBF16, false, 2, false) PDT_BA(kBF16, false, 1, true)
+  } else {
+    PDT_BA(kF16, true, 1, false) PDT_BA(kF16, true, 1, true) PDT_BA(kF16, true, 2, false)
+    PDT_BA(kF16, false, 1, false) PDT_BA(kF16, false, 2, false) PDT_BA(kF16, false, 1, true)
+  }
+#undef PDT_BA
+  pdt_hip_fail("bn_bwd_apply: unsupported variant", hipErrorInvalidValue, __FILE__, __LINE__);
+}
+
+}  // namespace pdt

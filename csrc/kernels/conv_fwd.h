@@ -1,0 +1,25 @@
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pdt {
+
+// Generalised implicit-GEMM convolution (see conv_fwd.hip for the geometry contract).
+struct ConvFwdArgs {
+  const uint16_t* x;    // [N][H][W][C] input activations
+  const uint16_t* w;    // [Kout][T*U][C] weights (taps already ordered/flipped for the role)
+  uint16_t* y;          // [N][OH][OW][Kout] output
+  const uint16_t* res;  // optional: residual in y's layout, added before rounding (nullptr = none)
+  float* stats;         // optional: [m_tiles][Kout] float2 (sum, sumsq) BN partials (nullptr = none)
+  int N, H, W, C, Kout, T, U;
+  int Pm, Qm;                                          // GEMM-M sub-grid (M = N*Pm*Qm)
+  int ist_h, ist_w, ioff_h, ioff_w, tstep_h, tstep_w;  // in = i*ist + ioff + t*tstep
+  int OH, OW, ost_h, ost_w, ooff_h, ooff_w;            // out = i*ost + ooff
+  int64_t M;
+  int m_tiles, n_tiles;                                // filled by the launcher
+};
+
+void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s);
+int conv_fwd_m_tiles(int64_t M, int bm);
+
+}  // namespace pdt

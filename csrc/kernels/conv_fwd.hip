@@ -1,0 +1,296 @@
+// Implicit-GEMM convolution on MFMA (gfx950), NHWC activations, [Cout][taps][Cin] weights.
+//
+// One kernel serves three roles:
+//   * forward conv:        out(n,i,j,k) = sum_{t,u,c} X(n, i*s-p+t, j*s-p+u, c) * W(k,t,u,c)
+//   * backward-data conv:  one launch per sub-pixel phase of the stride; the phase's taps form a
+//                          small stride-1 conv over dY with flipped weights, written to the
+//                          phase's output sub-grid (no MFMA work is wasted on structural zeros)
+//   * linear layers:       a 1x1 "conv" over [B,1,1,K]
+// The generalised geometry is
+//   in_h  = i*ist_h + ioff_h + t*tstep_h      (t in [0,T)),  same for w / u
+//   out_h = i*ost_h + ooff_h
+// GEMM view: D[n=cout][m=pixel] = sum_k Wt[n][k] * X[m][k]; MFMA A = weights, B = activations, so a
+// lane's accumulator holds 4 consecutive output channels of one pixel (8-byte NHWC stores).
+//
+// Tiles are staged global->LDS with LDS-DMA (global_load_lds_dwordx4, 16 B/lane) into two LDS
+// buffers; out-of-bounds rows (padding, M tail) DMA from a zero page.  The LDS image is linear per
+// wave-instruction and XOR-swizzled through the SOURCE address (chunk ^= (row>>1)&(chunks-1)), which
+// makes the ds_read_b128 fragment reads bank-conflict free.  Optional epilogues: residual add (used
+// to fuse the identity-gradient add of a residual block into dgrad) and per-channel BatchNorm
+// partial statistics (sum, sum of squares of the rounded outputs) for each M tile.
+#include "../common.h"
+#include "conv_fwd.h"
+
+namespace pdt {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+template <int CHUNKS>
+PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
+
+template <int DT, int BM, int BN, int BK, int WAVES_N, bool STATS, bool RES>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int WAVES_M = 4 / WAVES_N;
+  constexpr int WN = BN / WAVES_N;
+  constexpr int WM = BM / WAVES_M;
+  constexpr int FN = WN / 16, FM = WM / 16;
+  constexpr int ROWB = BK * 2;
+  constexpr int CHUNKS = ROWB / 16;
+  constexpr int RPI = 1024 / ROWB;               // rows per wave LDS-DMA instruction
+  constexpr int A_INSTR = BN / RPI / 4;          // weight-tile instructions per wave
+  constexpr int B_INSTR = BM / RPI / 4;          // activation-tile instructions per wave
+  constexpr int A_BYTES = BN * ROWB;
+  constexpr int STAGE = (BN + BM) * ROWB;
+  static_assert(A_INSTR * RPI * 4 == BN && B_INSTR * RPI * 4 == BM, "tile/instr mismatch");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WAVES_N, wm = wave / WAVES_N;
+
+  const int nwg = a.m_tiles * a.n_tiles;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile_m = bid / a.n_tiles, tile_n = bid % a.n_tiles;
+  const int64_t m0 = (int64_t)tile_m * BM;
+  const int n0 = tile_n * BN;
+
+  const int PQ = a.Pm * a.Qm;
+  const int TU = a.T * a.U;
+  const int csteps = a.C / BK;
+  const int ksteps = TU * csteps;
+
+  // ---- per-lane source rows for the activation tile ----
+  const int lrow = lane / CHUNKS;      // row within one DMA instruction
+  const int pchunk = lane % CHUNKS;    // physical (LDS) chunk this lane writes
+  const uint16_t* brow_base[B_INSTR];
+  int brow_h[B_INSTR], brow_w[B_INSTR], bchunk[B_INSTR];
+#pragma unroll
+  for (int j = 0; j < B_INSTR; ++j) {
+    const int row = (wave * B_INSTR + j) * RPI + lrow;
+    const int64_t m = m0 + row;
+    bchunk[j] = pchunk ^ swz<CHUNKS>(row);
+    if (m < a.M) {
+      const int nimg = (int)(m / PQ);
+      const int rem = (int)(m - (int64_t)nimg * PQ);
+      const int i = rem / a.Qm, jj = rem - (rem / a.Qm) * a.Qm;
+      brow_h[j] = i * a.ist_h + a.ioff_h;
+      brow_w[j] = jj * a.ist_w + a.ioff_w;
+      brow_base[j] = a.x + (int64_t)nimg * a.H * a.W * a.C;
+    } else {
+      brow_h[j] = -(1 << 29);
+      brow_w[j] = 0;
+      brow_base[j] = a.x;
+    }
+  }
+  const uint16_t* arow_base[A_INSTR];
+  int achunk[A_INSTR];
+#pragma unroll
+  for (int j = 0; j < A_INSTR; ++j) {
+    const int row = (wave * A_INSTR + j) * RPI + lrow;
+    achunk[j] = pchunk ^ swz<CHUNKS>(row);
+    arow_base[j] = a.w + (int64_t)(n0 + row) * TU * a.C;
+  }
+
+  auto stage_load = [&](int ks, int buf) {
+    const int tap = ks / csteps;
+    const int c0 = (ks - tap * csteps) * BK;
+    const int t = tap / a.U, u = tap - (tap / a.U) * a.U;
+    char* sbase = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j) {
+      const uint16_t* src = arow_base[j] + tap * a.C + c0 + achunk[j] * 8;
+      lds_void* dst = (lds_void*)(sbase + (wave * A_INSTR + j) * 1024);
+      __builtin_amdgcn_global_load_lds((glb_void*)src, dst, 16, 0, 0);
+    }
+    const int dh = t * a.tstep_h, dw = u * a.tstep_w;
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j) {
+      const int h = brow_h[j] + dh, w = brow_w[j] + dw;
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const uint16_t* src = ok ? brow_base[j] + ((int64_t)h * a.W + w) * a.C + c0 + bchunk[j] * 8
+                               : (const uint16_t*)g_zero16;
+      lds_void* dst = (lds_void*)(sbase + A_BYTES + (wave * B_INSTR + j) * 1024);
+      __builtin_amdgcn_global_load_lds((glb_void*)src, dst, 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes within a stage), per kk-independent part
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_off[FN], b_off[FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) a_off[i] = (wn * WN + i * 16 + fr) * ROWB;
+#pragma unroll
+  for (int j = 0; j < FM; ++j) b_off[j] = A_BYTES + (wm * WM + j * 16 + fr) * ROWB;
+
+  if (ksteps > 0) {
+    stage_load(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < ksteps) stage_load(ks + 1, cur ^ 1);
+      const char* sb = smem + cur * STAGE;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        vec8 af[FN], bfr[FM];
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int row = wn * WN + i * 16 + fr;
+          const int ch = (kk * 4 + fq) ^ swz<CHUNKS>(row);
+          af[i] = *(const vec8*)(sb + a_off[i] + ch * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int row = wm * WM + j * 16 + fr;
+          const int ch = (kk * 4 + fq) ^ swz<CHUNKS>(row);
+          bfr[j] = *(const vec8*)(sb + b_off[j] + ch * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: lane holds channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
+  float csum[FN][4], csq[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
+
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int64_t m = m0 + wm * WM + j * 16 + fr;
+    if (m < a.M) {
+      const int nimg = (int)(m / PQ);
+      const int rem = (int)(m - (int64_t)nimg * PQ);
+      const int i_ = rem / a.Qm, j_ = rem - (rem / a.Qm) * a.Qm;
+      const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
+      const int64_t obase = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + 4 * fq;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (RES) {
+          const uint2 rr = *(const uint2*)(a.res + obase + n);
+          v[0] += E::to_f((uint16_t)(rr.x & 0xffff));
+          v[1] += E::to_f((uint16_t)(rr.x >> 16));
+          v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
+          v[3] += E::to_f((uint16_t)(rr.y >> 16));
+        }
+        uint16_t o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = E::from_f(v[r]);
+        uint2 packed;
+        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        *(uint2*)(a.y + obase + n) = packed;
+        if constexpr (STATS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float q = E::to_f(o[r]);
+            csum[i][r] += q;
+            csq[i][r] += q * q;
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (STATS) {
+    // reduce over the 16 lanes (pixels) that share fq, then over the WAVES_M waves
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          csum[i][r] += __shfl_xor(csum[i][r], o, 64);
+          csq[i][r] += __shfl_xor(csq[i][r], o, 64);
+        }
+      }
+    float* red = (float*)smem;  // [WAVES_M][BN][2]
+    __syncthreads();
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * WN + i * 16 + 4 * fq + r;
+          red[(wm * BN + nl) * 2 + 0] = csum[i][r];
+          red[(wm * BN + nl) * 2 + 1] = csq[i][r];
+        }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w) {
+        s += red[(w * BN + tid) * 2 + 0];
+        q += red[(w * BN + tid) * 2 + 1];
+      }
+      float2* dst = (float2*)a.stats + (int64_t)tile_m * a.Kout + n0 + tid;
+      *dst = make_float2(s, q);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+template <int DT, int BM, int BN, int BK, int WAVES_N>
+static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
+  dim3 grid(a.m_tiles * a.n_tiles), block(256);
+  const bool st = a.stats != nullptr, rs = a.res != nullptr;
+  if (st && rs)
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, true>), grid, block, 0, s, a);
+  else if (st)
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, false>), grid, block, 0, s, a);
+  else if (rs)
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, true>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, false>), grid, block, 0, s, a);
+}
+
+template <int DT>
+static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
+  a.m_tiles = (int)((a.M + bm - 1) / bm);
+  a.n_tiles = a.Kout / bn;
+  if (a.m_tiles * a.n_tiles == 0) return;
+#define PDT_CFG(BM_, BN_, BK_, WN_)                                      \
+  if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
+    launch_cfg<DT, BM_, BN_, BK_, WN_>(a, s);                            \
+    return;                                                              \
+  }
+  PDT_CFG(128, 128, 64, 2)
+  PDT_CFG(256, 64, 64, 1)
+  PDT_CFG(128, 64, 64, 1)
+  PDT_CFG(128, 128, 32, 2)
+  PDT_CFG(256, 64, 32, 1)
+  PDT_CFG(64, 128, 64, 4)
+#undef PDT_CFG
+  pdt_hip_fail("conv_fwd: unsupported tile config", hipErrorInvalidValue, __FILE__, __LINE__);
+}
+
+void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s) {
+  if (dtype == kBF16)
+    launch_dt<kBF16>(a, bm, bn, bk, s);
+  else
+    launch_dt<kF16>(a, bm, bn, bk, s);
+}
+
+int conv_fwd_m_tiles(int64_t M, int bm) { return (int)((M + bm - 1) / bm); }
+
+}  // namespace pdt

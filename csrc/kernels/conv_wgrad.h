@@ -1,0 +1,24 @@
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pdt {
+
+struct ConvWgradArgs {
+  const uint16_t* x;   // [N][H][W][C] forward input
+  const uint16_t* dy;  // [P][Kout] gradient of the forward output (P = N*Pm*Qm pixels, NHWC)
+  float* ws;           // [splits][Kout][ldw] fp32 partials
+  int N, H, W, C, Kout, T, U;
+  int Pm, Qm;
+  int stride_h, stride_w, pad_h, pad_w, dil_h, dil_w;
+  int P;               // N*Pm*Qm
+  int ldw;             // >= T*U*C
+  int splits, pix_per_split;  // filled by conv_wgrad_plan
+};
+
+void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks);
+void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s);
+void wgrad_reduce_launch(const float* ws, int splits, int rows, int cols, int ldw, int64_t split_stride,
+                         float* out, int ldo, float scale, bool accumulate, hipStream_t s);
+
+}  // namespace pdt

@@ -1,0 +1,226 @@
+// Convolution weight gradient on MFMA (gfx950), split-K over pixels.
+//
+//   dW[k][tap][c] = sum_{pixels p} dY[p][k] * X[in(p, tap)][c]
+//
+// GEMM view: rows = input channels c of one tap (MFMA A = gathered X), cols = output channels k
+// (MFMA B = dY), reduction over pixels.  Both operands are pixel-major in NHWC memory, so tiles are
+// DMA'd into LDS as [pixel][channel] rows (global_load_lds_dwordx4, 16 B/lane) and the MFMA fragments
+// are read with the gfx950 transposing LDS read ds_read_b64_tr_b16.  The LDS image is XOR-swizzled
+// through the DMA source address so those transposed reads are bank-conflict free.
+//
+// Block tile: 64 (c) x 64 (k) x 128 pixels per K-step, 4 waves each owning a 32-pixel slice of every
+// K-step and a full 64x64 accumulator; the waves are summed through LDS at the end and each block
+// writes one fp32 partial tile.  Partials over the split-K axis are summed by wgrad_reduce, which
+// writes (and scales) straight into the fp32 gradient buffer (the DDP bucket view).
+#include "../common.h"
+#include "conv_wgrad.h"
+
+namespace pdt {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+
+// chunk swizzle for a [pixel][64 ch] (128-B row) image read by ds_read_b64_tr_b16
+PDT_DEVICE int tr_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
+
+// floor(n / d) for 0 <= n < 2^24 using an fp32 reciprocal + one correction step
+PDT_DEVICE int fdiv(int n, int d, float inv_d) {
+  int q = (int)((float)n * inv_d);
+  int r = n - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 128;       // pixels per K-step
+  constexpr int ROWB = 128;      // 64 channels * 2 B
+  constexpr int XB = BKP * ROWB; // bytes of the X tile
+  constexpr int STAGE = 2 * XB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // block -> (k tile, (tap, c) tile, split)
+  const int c_tiles = a.C / 64;
+  const int n_tiles = a.T * a.U * c_tiles;
+  const int k_tiles = a.Kout / 64;
+  const int nwg = k_tiles * n_tiles * a.splits;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int split = bid % a.splits;
+  const int tile = bid / a.splits;
+  const int kt = tile % k_tiles;
+  const int nt = tile / k_tiles;
+  const int tap = nt / c_tiles;
+  const int c0 = (nt - tap * c_tiles) * 64;
+  const int k0 = kt * 64;
+  const int t = tap / a.U, u = tap - (tap / a.U) * a.U;
+
+  const int pix_begin = split * a.pix_per_split;
+  const int pix_end = min(a.P, pix_begin + a.pix_per_split);
+  const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
+
+  const int PQ = a.Pm * a.Qm;
+  const float inv_pq = 1.0f / (float)PQ, inv_q = 1.0f / (float)a.Qm;
+
+  // DMA lane geometry: 8 rows x 8 chunks per 1 KiB instruction
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  auto stage_load = [&](int step, int buf) {
+    const int pbase = pix_begin + step * BKP;
+    char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (wave * 4 + j) * 8 + lrow;  // 0..127
+      const int lch = pch ^ tr_swz(row);
+      const int p = pbase + row;
+      // X row (gathered through the tap)
+      const uint16_t* xs = (const uint16_t*)g_zero16;
+      const uint16_t* ys = (const uint16_t*)g_zero16;
+      if (p < pix_end) {
+        const int nimg = fdiv(p, PQ, inv_pq);
+        const int rem = p - nimg * PQ;
+        const int i = fdiv(rem, a.Qm, inv_q);
+        const int jj = rem - i * a.Qm;
+        const int h = i * a.stride_h - a.pad_h + t * a.dil_h;
+        const int w = jj * a.stride_w - a.pad_w + u * a.dil_w;
+        if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+          xs = a.x + (((int64_t)nimg * a.H + h) * a.W + w) * a.C + c0 + lch * 8;
+        ys = a.dy + (int64_t)p * a.Kout + k0 + lch * 8;
+      }
+      __builtin_amdgcn_global_load_lds((glb_void*)xs, (lds_void*)(sb + (wave * 4 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)ys, (lds_void*)(sb + XB + (wave * 4 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry: group g = lane>>4 holds k = 8g..8g+7 of the 32-pixel slice
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+
+  if (nsteps > 0) {
+    stage_load(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < nsteps) stage_load(s + 1, cur ^ 1);
+      const char* sb = smem + cur * STAGE;
+      vec8 af[4], bfr[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        s16x4_t lo, hi;
+        {
+          const int row0 = wave * 32 + 8 * g + q;
+          const int col = f * 16 + 4 * p4;  // element within the 64-wide row
+          const int ch = col >> 3, off = (col & 7) * 2;
+          const int r0 = row0, r1 = row0 + 4;
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + r0 * ROWB + ((ch ^ tr_swz(r0)) << 4) + off));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + r1 * ROWB + ((ch ^ tr_swz(r1)) << 4) + off));
+        }
+        af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        {
+          const int row0 = wave * 32 + 8 * g + q;
+          const int col = f * 16 + 4 * p4;
+          const int ch = col >> 3, off = (col & 7) * 2;
+          const int r0 = row0, r1 = row0 + 4;
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + XB + r0 * ROWB + ((ch ^ tr_swz(r0)) << 4) + off));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + XB + r1 * ROWB + ((ch ^ tr_swz(r1)) << 4) + off));
+        }
+        bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // ---- sum the 4 waves' 64x64 tiles through LDS, write one fp32 partial tile ----
+  // acc[i][j]: rows c = 16i + 4*(lane>>4) + r, col k = 16j + (lane&15)
+  float* red = (float*)smem;  // [4 waves][64 k][64 c]
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 16 * j + (lane & 15);
+      const int c = 16 * i + 4 * (lane >> 4);
+      *(f32x4_t*)(red + (wave * 64 + k) * 64 + c) = acc[i][j];
+    }
+  __syncthreads();
+  float* dst = a.ws + ((int64_t)split * a.Kout + k0) * a.ldw + tap * a.C + c0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int idx = (e * 256 + tid) * 4;  // 0..4095
+    const int k = idx >> 6, c = idx & 63;
+    f32x4_t v = *(f32x4_t*)(red + k * 64 + c);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += *(f32x4_t*)(red + (w * 64 + k) * 64 + c);
+    *(f32x4_t*)(dst + (int64_t)k * a.ldw + c) = v;
+  }
+}
+
+// out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int rows,
+                                                            int cols, int ldw, int64_t split_stride,
+                                                            float* __restrict__ out, int ldo, float scale,
+                                                            int accumulate) {
+  const int64_t n = (int64_t)rows * cols;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * 256) {
+    const int r = (int)(idx / cols), c = (int)(idx - (int64_t)(idx / cols) * cols);
+    const float* p = ws + (int64_t)r * ldw + c;
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += p[k * split_stride];
+    float* o = out + (int64_t)r * ldo + c;
+    *o = accumulate ? (*o + scale * s) : scale * s;
+  }
+}
+
+void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
+  const int tiles = (a.Kout / 64) * a.T * a.U * (a.C / 64);
+  int splits = (target_blocks + tiles - 1) / tiles;
+  const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
+  splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
+  int pps = (a.P + splits - 1) / splits;
+  pps = (pps + 127) / 128 * 128;
+  splits = (a.P + pps - 1) / pps;
+  a.splits = splits;
+  a.pix_per_split = pps;
+}
+
+void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s) {
+  const int nwg = (a.Kout / 64) * a.T * a.U * (a.C / 64) * a.splits;
+  if (nwg == 0) return;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(conv_wgrad_kernel<kBF16>, dim3(nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv_wgrad_kernel<kF16>, dim3(nwg), dim3(256), 0, s, a);
+}
+
+void wgrad_reduce_launch(const float* ws, int splits, int rows, int cols, int ldw, int64_t split_stride,
+                         float* out, int ldo, float scale, bool accumulate, hipStream_t s) {
+  const int64_t n = (int64_t)rows * cols;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, splits, rows, cols, ldw,
+                     split_stride, out, ldo, scale, (int)accumulate);
+}
+
+}  // namespace pdt

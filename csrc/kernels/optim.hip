@@ -1,0 +1,176 @@
+// Optimizer / AMP / weight-layout kernels.
+//
+//   * nonfinite_check: GradScaler's found_inf over the flat fp32 gradient buffer (device flag, no
+//     host sync).
+//   * sgd_fused: torch.optim.SGD semantics (d_p = g + wd*p; buf = d_p on the first step, else
+//     momentum*buf + d_p; p -= lr*buf) over the flat fp32 parameter/gradient/momentum buffers, with
+//     the gradient pre-scale (1/world for DDP averaging, 1/loss_scale for AMP unscale) folded in,
+//     the whole step skipped when found_inf is set, and the 16-bit compute copy of every parameter
+//     written in the same pass (no per-forward autocast weight casts).
+//   * amp_update_scale: GradScaler's growth/backoff update on device.
+//   * gather16: builds every derived weight layout (dgrad tap-transposes, padded stem / fc
+//     matrices) from the 16-bit shadow in one launch, driven by a precomputed index map.
+#include "../common.h"
+#include "optim.h"
+
+namespace pdt {
+
+static int ew_blocks(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (int)(b < 1 ? 1 : b);
+}
+
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ found) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = g[i];
+    bad |= !isfinite(v);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) *found = 1.f;
+}
+
+void nonfinite_check_launch(const float* g, int64_t n, float* found, hipStream_t s) {
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, g, n, found);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ buf, uint16_t* __restrict__ shadow,
+                                                  const float* __restrict__ wd_mask, int64_t n, float lr,
+                                                  float momentum, float wd, float gscale,
+                                                  const float* __restrict__ loss_scale_ptr,
+                                                  const float* __restrict__ found_inf, int first) {
+  using E = E16<DT>;
+  if (found_inf && *found_inf != 0.f) return;
+  const float gs = gscale * (loss_scale_ptr ? 1.f / *loss_scale_ptr : 1.f);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float pv = p[i];
+    float d = g[i] * gs + wd * pv * (wd_mask ? wd_mask[i] : 1.f);
+    float b;
+    if (momentum != 0.f) {
+      b = first ? d : momentum * buf[i] + d;
+      buf[i] = b;
+    } else {
+      b = d;
+    }
+    pv -= lr * b;
+    p[i] = pv;
+    if (shadow) shadow[i] = E::from_f(pv);
+  }
+}
+
+void sgd_launch(int dtype, float* p, const float* g, float* buf, uint16_t* shadow, const float* wd_mask, int64_t n,
+                float lr, float momentum, float wd, float gscale, const float* loss_scale, const float* found_inf,
+                bool first, hipStream_t s) {
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(sgd_kernel<kBF16>, dim3(ew_blocks(n)), dim3(256), 0, s, p, g, buf, shadow, wd_mask, n, lr, momentum,
+                       wd, gscale, loss_scale, found_inf, (int)first);
+  else
+    hipLaunchKernelGGL(sgd_kernel<kF16>, dim3(ew_blocks(n)), dim3(256), 0, s, p, g, buf, shadow, wd_mask, n, lr, momentum,
+                       wd, gscale, loss_scale, found_inf, (int)first);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void cast16_kernel(const float* __restrict__ p, uint16_t* __restrict__ out, int64_t n) {
+  using E = E16<DT>;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = E::from_f(p[i]);
+}
+
+void cast16_launch(int dtype, const float* p, uint16_t* out, int64_t n, hipStream_t s) {
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(cast16_kernel<kBF16>, dim3(ew_blocks(n)), dim3(256), 0, s, p, out, n);
+  else
+    hipLaunchKernelGGL(cast16_kernel<kF16>, dim3(ew_blocks(n)), dim3(256), 0, s, p, out, n);
+}
+
+// GradScaler._amp_update_scale_: scale *= backoff on inf (tracker = 0), else tracker += 1 and
+// scale *= growth when tracker reaches the interval (tracker = 0).  Resets found_inf for the next step.
+__global__ void amp_update_kernel(float* scale, int* tracker, float* found_inf, float growth, float backoff,
+                                  int interval) {
+  if (threadIdx.x != 0) return;
+  if (*found_inf != 0.f) {
+    *scale = *scale * backoff;
+    *tracker = 0;
+  } else {
+    const int t = *tracker + 1;
+    if (t == interval) {
+      const float ns = *scale * growth;
+      if (isfinite(ns)) *scale = ns;
+      *tracker = 0;
+    } else {
+      *tracker = t;
+    }
+  }
+}
+
+void amp_update_launch(float* scale, int* tracker, float* found_inf, float growth, float backoff, int interval,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(64), 0, s, scale, tracker, found_inf, growth, backoff, interval);
+}
+
+__global__ __launch_bounds__(256) void gather16_kernel(const uint16_t* __restrict__ src, const int* __restrict__ idx,
+                                                       uint16_t* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int j = idx[i];
+    dst[i] = j >= 0 ? src[j] : (uint16_t)0;
+  }
+}
+
+void gather16_launch(const uint16_t* src, const int* idx, uint16_t* dst, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(gather16_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, src, idx, dst, n);
+}
+
+// Stem input: fp32 NCHW image batch -> 16-bit im2col rows [N*OH*OW][ldk], column k = (r*S + s)*C + c
+// for k < R*S*C, zero padding beyond (and outside the image).  One thread per 8 columns of a row.
+template <int DT>
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x, uint16_t* __restrict__ out, int N, int C,
+                                                     int H, int W, int R, int S, int stride, int pad, int OH, int OW,
+                                                     int ldk) {
+  using E = E16<DT>;
+  const int kv = ldk / 8;
+  const int KK = R * S * C;
+  const int64_t total = (int64_t)N * OH * OW * kv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int k0 = (int)(v % kv) * 8;
+    int64_t pix = v / kv;
+    const int ow = (int)(pix % OW);
+    pix /= OW;
+    const int oh = (int)(pix % OH);
+    const int n = (int)(pix / OH);
+    uint16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = k0 + e;
+      float val = 0.f;
+      if (k < KK) {
+        const int c = k % C;
+        const int rs = k / C;
+        const int r = rs / S, s = rs - (rs / S) * S;
+        const int h = oh * stride - pad + r, w = ow * stride - pad + s;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) val = x[(((int64_t)n * C + c) * H + h) * W + w];
+      }
+      o[e] = E::from_f(val);
+    }
+    uint4 q;
+    q.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    q.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+    q.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
+    q.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+    *(uint4*)(out + v * 8) = q;
+  }
+}
+
+void im2col_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H, int W, int R, int S, int stride, int pad,
+                   int ldk, hipStream_t s) {
+  const int OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  const int64_t total = (int64_t)N * OH * OW * (ldk / 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(im2col_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W, R, S, stride, pad,
+                       OH, OW, ldk);
+  else
+    hipLaunchKernelGGL(im2col_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W, R, S, stride, pad,
+                       OH, OW, ldk);
+}
+
+}  // namespace pdt

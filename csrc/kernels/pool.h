@@ -1,0 +1,11 @@
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+namespace pdt {
+void bn_relu_maxpool_launch(int dtype, const uint16_t* y, const float* coef, uint16_t* out, uint8_t* idx, int N, int H,
+                            int W, int C, hipStream_t s);
+void maxpool_bwd_relu_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y, const float* coef,
+                             uint16_t* dz, int N, int H, int W, int C, hipStream_t s);
+void avgpool_fwd_launch(int dtype, const uint16_t* x, uint16_t* feat, int N, int HW, int C, int ldf, hipStream_t s);
+void avgpool_bwd_launch(int dtype, const uint16_t* dfeat, uint16_t* g, int N, int HW, int C, int ldf, hipStream_t s);
+}  // namespace pdt

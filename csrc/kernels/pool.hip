@@ -1,0 +1,216 @@
+// Pooling kernels, NHWC 16-bit.
+//   * bn_relu_maxpool3x3s2: the ResNet stem's BN-apply + ReLU fused with MaxPool(3, 2, 1); the
+//     112x112 post-ReLU tensor is never written.  The window argmax (0..8) is kept as uint8.
+//   * maxpool_bwd_relu: gather form of the max-pool backward (each input pixel collects from the
+//     <= 4 windows that selected it) fused with the ReLU mask recomputed from the BN input.
+//   * avgpool (global, HxW -> 1) forward and backward.
+#include "../common.h"
+#include "pool.h"
+
+namespace pdt {
+
+static int ew_blocks(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 16384) b = 16384;
+  return (int)(b < 1 ? 1 : b);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __restrict__ y, const float* __restrict__ coef,
+                                                              uint16_t* __restrict__ out, uint8_t* __restrict__ idx,
+                                                              int N, int H, int W, int C, int OH, int OW) {
+  using E = E16<DT>;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cv) * 8;
+    int64_t pix = v / cv;
+    const int ow = (int)(pix % OW);
+    pix /= OW;
+    const int oh = (int)(pix % OH);
+    const int n = (int)(pix / OH);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -1.f; bi[e] = 0; }
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = coef[c0 + e]; sh[e] = coef[C + c0 + e]; }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = oh * 2 - 1 + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = ow * 2 - 1 + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const uint4 q = *(const uint4*)(y + (((int64_t)n * H + h) * W + w) * C + c0);
+        const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float val = fmaxf(E::to_f((uint16_t)(qw[e >> 1] >> (16 * (e & 1)))) * sc[e] + sh[e], 0.f);
+          if (val > best[e]) { best[e] = val; bi[e] = (uint8_t)(kh * 3 + kw); }
+        }
+      }
+    }
+    uint32_t ow_[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ow_[e] = (uint32_t)E::from_f(best[2 * e]) | ((uint32_t)E::from_f(best[2 * e + 1]) << 16);
+    const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+    *(uint4*)(out + o) = make_uint4(ow_[0], ow_[1], ow_[2], ow_[3]);
+    uint2 ib;
+    ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(uint2*)(idx + o) = ib;
+  }
+}
+
+// eval / generic variant without index output is the same kernel with idx == nullptr handled by caller
+void bn_relu_maxpool_launch(int dtype, const uint16_t* y, const float* coef, uint16_t* out, uint8_t* idx, int N, int H,
+                            int W, int C, hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, y, coef, out, idx, N, H, W,
+                       C, OH, OW);
+  else
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, y, coef, out, idx, N, H, W,
+                       C, OH, OW);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void maxpool_bwd_relu_kernel(const uint16_t* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                                               const uint16_t* __restrict__ y, const float* __restrict__ coef,
+                                                               uint16_t* __restrict__ dz, int N, int H, int W, int C,
+                                                               int OH, int OW) {
+  using E = E16<DT>;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * H * W * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cv) * 8;
+    int64_t pix = v / cv;
+    const int w = (int)(pix % W);
+    pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // candidate windows: oh with 2*oh-1 <= h <= 2*oh+1
+    const int oh_lo = (h) / 2, oh_hi = (h + 1) / 2;  // h even: {h/2}; h odd: {(h-1)/2, (h+1)/2}
+    const int ow_lo = (w) / 2, ow_hi = (w + 1) / 2;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      if (oh >= OH) continue;
+      const int kh = h - (oh * 2 - 1);
+      if (kh < 0 || kh > 2) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        if (ow >= OW) continue;
+        const int kw = w - (ow * 2 - 1);
+        if (kw < 0 || kw > 2) continue;
+        const uint8_t pos = (uint8_t)(kh * 3 + kw);
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+        const uint2 ib = *(const uint2*)(idx + o);
+        const uint4 g = *(const uint4*)(dp + o);
+        const uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t b = (uint8_t)(((e < 4) ? ib.x : ib.y) >> (8 * (e & 3)));
+          if (b == pos) acc[e] += E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1))));
+        }
+      }
+    }
+    const int64_t i = (((int64_t)n * H + h) * W + w) * C + c0;
+    const uint4 yy = *(const uint4*)(y + i);
+    const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
+    uint32_t o_[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t r[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int c = c0 + 2 * e + hh;
+        const float pre = E::to_f((uint16_t)(yw[e] >> (16 * hh))) * coef[c] + coef[C + c];
+        r[hh] = E::from_f(pre > 0.f ? acc[2 * e + hh] : 0.f);
+      }
+      o_[e] = (uint32_t)r[0] | ((uint32_t)r[1] << 16);
+    }
+    *(uint4*)(dz + i) = make_uint4(o_[0], o_[1], o_[2], o_[3]);
+  }
+}
+
+void maxpool_bwd_relu_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y, const float* coef,
+                             uint16_t* dz, int N, int H, int W, int C, hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(maxpool_bwd_relu_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef, dz, N, H,
+                       W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_relu_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef, dz, N, H,
+                       W, C, OH, OW);
+}
+
+// feat[n][c] = mean_{hw} x[n][hw][c]    (one thread per (n, 8 channels))
+template <int DT>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ feat, int N,
+                                                          int HW, int C, int ldf) {
+  using E = E16<DT>;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cv) * 8;
+    const int n = (int)(v / cv);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint16_t* p = x + (int64_t)n * HW * C + c0;
+    for (int i = 0; i < HW; ++i) {
+      const uint4 q = *(const uint4*)(p + (int64_t)i * C);
+      const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += E::to_f((uint16_t)(qw[e >> 1] >> (16 * (e & 1))));
+    }
+    const float inv = 1.f / (float)HW;
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (uint32_t)E::from_f(acc[2 * e] * inv) | ((uint32_t)E::from_f(acc[2 * e + 1] * inv) << 16);
+    *(uint4*)(feat + (int64_t)n * ldf + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// g[n][hw][c] = dfeat[n][c] / HW
+template <int DT>
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const uint16_t* __restrict__ dfeat, uint16_t* __restrict__ g, int N,
+                                                          int HW, int C, int ldf) {
+  using E = E16<DT>;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * HW * cv;
+  const float inv = 1.f / (float)HW;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cv) * 8;
+    const int n = (int)(v / ((int64_t)cv * HW));
+    const uint4 q = *(const uint4*)(dfeat + (int64_t)n * ldf + c0);
+    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = E::to_f((uint16_t)(qw[e] & 0xffff)) * inv, b = E::to_f((uint16_t)(qw[e] >> 16)) * inv;
+      o[e] = (uint32_t)E::from_f(a) | ((uint32_t)E::from_f(b) << 16);
+    }
+    *(uint4*)(g + v * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+void avgpool_fwd_launch(int dtype, const uint16_t* x, uint16_t* feat, int N, int HW, int C, int ldf, hipStream_t s) {
+  const int64_t total = (int64_t)N * (C / 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, feat, N, HW, C, ldf);
+  else
+    hipLaunchKernelGGL(avgpool_fwd_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, feat, N, HW, C, ldf);
+}
+
+void avgpool_bwd_launch(int dtype, const uint16_t* dfeat, uint16_t* g, int N, int HW, int C, int ldf, hipStream_t s) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dfeat, g, N, HW, C, ldf);
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dfeat, g, N, HW, C, ldf);
+}
+
+}  // namespace pdt

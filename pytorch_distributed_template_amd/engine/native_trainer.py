@@ -1,0 +1,81 @@
+"""One data-parallel training step on the native (HIP kernel) path.
+
+Mirrors the reference step (`distributed.py:237-263`, `distributed_syncBN_amp.py:250-278`):
+
+    [DDP buffer broadcast] -> forward -> CE loss -> top-1 accuracy -> [metric all-reduce]
+    -> (scaled) backward with bucketed gradient all-reduce -> (unscale, overflow check) SGD step
+    -> (scaler update)
+
+with every piece on device and no host synchronisation inside the step: the loss/accuracy pair is
+returned as a device tensor (reduced across ranks with ONE 2-float all-reduce instead of a barrier and
+two scalar all-reduces) and read by the caller only when it logs.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..amp.scaler import DeviceGradScaler
+from ..models.executor import ResNetExecutor
+from ..optim.flat import FlatBuffers, FlatParams
+from ..optim.sgd import FusedSGD
+from ..parallel.ddp import GradBucketer, broadcast_parameters, sync_buffers
+
+
+class NativeTrainer:
+    def __init__(self, model, device, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1, momentum: float = 0.9,
+                 weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
+                 bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
+                 process_group=None, reduce_metrics: bool = True):
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.model = model
+        self.pg = process_group
+        self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
+        self.world = dist.get_world_size(process_group) if self.distributed else 1
+        self.flat = FlatParams(model, self.device, dtype)
+        self.buffers = FlatBuffers(model, self.device)
+        broadcast_parameters(self.flat, self.buffers, process_group)
+        self.bucketer = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb,
+                                     enabled=self.distributed)
+        self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
+                                       syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed)
+                                       else None)
+        self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
+        self.optimizer.post_step_hooks.append(self.executor.update_derived)
+        # fp16 needs dynamic loss scaling; bf16 has fp32's exponent range and does not
+        self.scaler = DeviceGradScaler(self.device, enabled=use_amp and dtype == torch.float16)
+        self.broadcast_buffers = broadcast_buffers and self.distributed
+        self.reduce_metrics = reduce_metrics and self.distributed
+        self._steps = 0
+
+    def _reduce(self, met: torch.Tensor) -> torch.Tensor:
+        if self.reduce_metrics:
+            dist.all_reduce(met, group=self.pg)
+            met.div_(self.world)
+        return met
+
+    def train_step(self, images: torch.Tensor, target: torch.Tensor):
+        if self.broadcast_buffers and self._steps > 0:
+            sync_buffers(self.buffers, self.pg)
+        logits, met = self.executor.train_step(images, target, loss_scale=self.scaler.scale_tensor,
+                                               grad_div=float(images.shape[0]))
+        if self.buffers.n_int:
+            self.buffers.idata.add_(1)  # BatchNorm num_batches_tracked
+        met = self._reduce(met)
+        self.bucketer.finish()
+        self.scaler.unscale_check(self.flat.grad)
+        self.optimizer.step(grad_scale=self.bucketer.grad_scale(), loss_scale=self.scaler.scale_tensor,
+                            found_inf=self.scaler.found_inf)
+        self.scaler.update()
+        self._steps += 1
+        return logits, met
+
+    @torch.no_grad()
+    def eval_step(self, images: torch.Tensor, target: torch.Tensor):
+        if self.broadcast_buffers and self._steps > 0:
+            sync_buffers(self.buffers, self.pg)
+        logits, met = self.executor.eval_step(images, target)
+        return logits, self._reduce(met)

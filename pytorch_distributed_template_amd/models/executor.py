@@ -1,0 +1,449 @@
+"""Native ResNet executor: explicit NHWC forward/backward over the gfx950 kernels.
+
+Instead of tracing a graph or dispatching op-by-op through autograd, the executor walks the ResNet
+topology (torchvision-compatible :class:`~.resnet.ResNet`, Basic and Bottleneck blocks) and launches
+our HIP kernels directly, with the cross-op fusions a CNN training step needs on MI355X:
+
+* conv forward = implicit-GEMM MFMA kernel whose epilogue emits the BatchNorm batch statistics
+  (no extra pass over the conv output to compute mean/var);
+* BN-apply + residual (+ BN of the downsample branch) + ReLU = one elementwise pass;
+* stem BN + ReLU + 3x3/2 max-pool = one pass (the 112x112 post-ReLU tensor never exists);
+* backward: one reduction pass per block output computes the BN-backward sums of BOTH residual
+  branches; the identity-gradient add of a residual block happens in the dgrad epilogue;
+* weight gradients are written straight into the flat fp32 gradient buffer (DDP bucket views) and
+  the bucketer is notified per parameter so RCCL all-reduces overlap the rest of backward;
+* cross-entropy forward+backward+accuracy is one kernel with the AMP loss scale folded in.
+
+Numerics: 16-bit (bf16 or fp16) activations and weights, fp32 accumulation/statistics, fp32 master
+weights and gradients.  Reference call sites mirrored here:
+`distributed.py:246-263` (forward, loss, backward, step) and `distributed_syncBN_amp.py:259-278`.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops import native
+from ..ops.conv import conv_tile as _conv_tile, dgrad_phases, dgrad_weight_index
+from .resnet import BasicBlock, Bottleneck, ResNet
+
+class _Conv:
+    """Static description of one convolution and its derived (dgrad) weight layouts."""
+
+    def __init__(self, conv: nn.Conv2d, flat, derived_maps: List[torch.Tensor], derived_off: List[int]):
+        assert conv.groups == 1 and conv.dilation == (1, 1), "native executor: groups/dilation unsupported"
+        self.mod = conv
+        self.cin, self.cout = conv.in_channels, conv.out_channels
+        self.R, self.S = conv.kernel_size
+        self.st = conv.stride[0]
+        self.pad = conv.padding[0]
+        assert conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+        self.slot = flat.slot(conv.weight)
+        self.pid = self.slot.index
+        self.phases = []  # (ph, pw, T, U, ioff_h, ioff_w, derived offset, derived numel)
+        base = self.slot.offset
+        for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(self.R, self.S, self.st, self.pad):
+            m = (base + dgrad_weight_index(self.cout, self.cin, self.R, self.S, rs, ss)).to(torch.int32)
+            self.phases.append((ph, pw, len(rs), len(ss), ioff_h, ioff_w, derived_off[0], m.numel()))
+            derived_maps.append(m)
+            derived_off[0] += m.numel()
+
+    def out_hw(self, H: int, W: int) -> Tuple[int, int]:
+        return (H + 2 * self.pad - self.R) // self.st + 1, (W + 2 * self.pad - self.S) // self.st + 1
+
+
+class _BN:
+    def __init__(self, bn: nn.BatchNorm2d, flat, device):
+        self.mod = bn
+        self.C = bn.num_features
+        self.eps = bn.eps
+        self.momentum = bn.momentum if bn.momentum is not None else 0.1
+        self.gslot = flat.slot(bn.weight)
+        self.bslot = flat.slot(bn.bias)
+        self.coef = torch.zeros(4 * self.C, dtype=torch.float32, device=device)
+        self.bcoef = torch.zeros(3 * self.C, dtype=torch.float32, device=device)
+        self.sums = torch.zeros(2 * self.C, dtype=torch.float64, device=device)
+        self.bsums = torch.zeros(4 * self.C, dtype=torch.float64, device=device)
+
+
+class ResNetExecutor:
+    """Runs a :class:`ResNet` on one GPU with the native kernels.
+
+    ``train_step`` = forward + loss/accuracy + backward (gradients into ``flat.grad``);
+    ``eval_step`` = forward with running statistics.  The optimizer step is separate
+    (:class:`~pytorch_distributed_template_amd.optim.sgd.FusedSGD`).
+    """
+
+    def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
+                 grad_ready: Optional[Callable[[int], None]] = None,
+                 syncbn_group=None, wgrad_blocks: int = 2048):
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError("native executor computes in bf16 or fp16")
+        if not isinstance(model, ResNet) or model.groups != 1:
+            raise NotImplementedError("native executor supports torchvision-style ResNets with groups=1")
+        self.C = native.C
+        self.model = model
+        self.flat = flat
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.grad_ready = grad_ready or (lambda pid: None)
+        self.syncbn_group = syncbn_group
+        self.wgrad_blocks = wgrad_blocks
+        derived_maps: List[torch.Tensor] = []
+        off = [0]
+
+        def conv(c):
+            return _Conv(c, flat, derived_maps, off)
+
+        self.stem = conv(model.conv1)
+        self.stem_bn = _BN(model.bn1, flat, self.device)
+        self.blocks: List[dict] = []
+        for layer in (model.layer1, model.layer2, model.layer3, model.layer4):
+            for blk in layer:
+                d = {"kind": "basic" if isinstance(blk, BasicBlock) else "bottleneck"}
+                convs = [blk.conv1, blk.conv2] + ([blk.conv3] if d["kind"] == "bottleneck" else [])
+                bns = [blk.bn1, blk.bn2] + ([blk.bn3] if d["kind"] == "bottleneck" else [])
+                d["convs"] = [conv(c) for c in convs]
+                d["bns"] = [_BN(b, flat, self.device) for b in bns]
+                if blk.downsample is not None:
+                    d["ds_conv"] = conv(blk.downsample[0])
+                    d["ds_bn"] = _BN(blk.downsample[1], flat, self.device)
+                else:
+                    d["ds_conv"] = None
+                    d["ds_bn"] = None
+                self.blocks.append(d)
+        # stem weight as a padded [64][KP] matrix over the im2col columns (k = (r*7+s)*3+c)
+        st = self.stem
+        self.stem_k = st.R * st.S * st.cin
+        self.stem_kp = (self.stem_k + 63) // 64 * 64
+        k = torch.arange(st.cout).view(-1, 1)
+        j = torch.arange(self.stem_kp).view(1, -1)
+        m = torch.where(j < self.stem_k, st.slot.offset + k * self.stem_k + j, torch.full_like(j, -1))
+        self.stem_w_off = off[0]
+        derived_maps.append(m.reshape(-1).to(torch.int32))
+        off[0] += m.numel()
+        # fc: padded [NP][F] (forward) and its transpose [F][NP] (backward-data)
+        fc = model.fc
+        self.ncls, self.feat = fc.out_features, fc.in_features
+        self.ncls_pad = (self.ncls + 127) // 128 * 128
+        self.fc_slot = flat.slot(fc.weight)
+        self.fcb_slot = flat.slot(fc.bias)
+        o = torch.arange(self.ncls_pad).view(-1, 1)
+        f = torch.arange(self.feat).view(1, -1)
+        m = torch.where(o < self.ncls, self.fc_slot.offset + o * self.feat + f, torch.full_like(o * f, -1))
+        self.fc_w_off = off[0]
+        derived_maps.append(m.reshape(-1).to(torch.int32))
+        off[0] += m.numel()
+        self.fc_wt_off = off[0]
+        mt = m.t().contiguous()
+        derived_maps.append(mt.reshape(-1))
+        off[0] += mt.numel()
+        self.derived_idx = torch.cat([m.to(torch.int32) for m in derived_maps]).to(self.device)
+        self.derived = torch.zeros(off[0], dtype=dtype, device=self.device)
+        self._bufs: Dict[Tuple, torch.Tensor] = {}
+        self._plans: Dict[Tuple, Tuple[int, int]] = {}
+        self.update_derived()
+
+    # ---------------------------------------------------------------------------------- helpers
+    def update_derived(self) -> None:
+        """Rebuild every derived 16-bit weight layout from the shadow (after each optimizer step)."""
+        self.C.gather16(self.flat.shadow, self.derived_idx, self.derived)
+
+    def _buf(self, key, numel: int, dtype=None) -> torch.Tensor:
+        dtype = dtype or self.dtype
+        k = (key, dtype)
+        t = self._bufs.get(k)
+        if t is None or t.numel() < numel:
+            t = torch.empty(numel, dtype=dtype, device=self.device)
+            self._bufs[k] = t
+        return t[:numel]
+
+    def _w(self, c: _Conv) -> torch.Tensor:
+        s = c.slot
+        return self.flat.shadow[s.offset:s.offset + s.numel]
+
+    def _p(self, slot):
+        return self.flat.data[slot.offset:slot.offset + slot.numel]
+
+    def _g(self, slot):
+        return self.flat.grad[slot.offset:slot.offset + slot.numel]
+
+    # ---------------------------------------------------------------------------------- conv ops
+    def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None):
+        cin = cin or c.cin
+        R = R or c.R
+        S = S or c.S
+        st = st or c.st
+        pad = c.pad if pad is None else pad
+        P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+        bm, bn = _conv_tile(c.cout)
+        bk = 64 if cin % 64 == 0 else 32
+        M = N * P * Q
+        sp = None
+        if stats:
+            tiles = self.C.conv_m_tiles(M, bm)
+            sp = self._buf("stats", tiles * c.cout * 2, torch.float32)
+        self.C.conv_fwd(x, self._w(c) if w is None else w, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
+                        -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk)
+        return P, Q, sp, (self.C.conv_m_tiles(M, bm) if stats else 0)
+
+    def bn_train_finalize(self, bn: _BN, sp, tiles: int, count: int):
+        C = bn.C
+        self.C.bn_partial_reduce(sp, tiles, C, 2, self._buf("bnred", 64 * C * 4, torch.float64), bn.sums)
+        if self.syncbn_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(bn.sums, group=self.syncbn_group)
+            count = count * dist.get_world_size(self.syncbn_group)
+        self.C.bn_finalize(bn.sums, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
+                           bn.mod.running_mean, bn.mod.running_var, bn.coef, True)
+
+    def bn_eval(self, bn: _BN):
+        self.C.bn_eval_coef(self._p(bn.gslot), self._p(bn.bslot), bn.mod.running_mean, bn.mod.running_var,
+                            bn.eps, bn.coef)
+
+    def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None):
+        """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``."""
+        # --- wgrad
+        if wgrad_geom is None:
+            xg, Hx, Wx, Cx, R, S, st, pad = x, H, W, c.cin, c.R, c.S, c.st, c.pad
+        else:
+            xg, Hx, Wx, Cx, R, S, st, pad = wgrad_geom
+        self._wgrad(c.cout, xg, dy, N, Hx, Wx, Cx, R, S, P, Q, st, pad, self._g(c.slot), R * S * Cx)
+        self.grad_ready(c.pid)
+        # --- dgrad
+        if dx is None:
+            return
+        bm, bn = _conv_tile(c.cin)
+        bk = 64 if c.cout % 64 == 0 else 32
+        for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases:
+            Pm = (H - ph + c.st - 1) // c.st
+            Qm = (W - pw + c.st - 1) // c.st
+            if Pm <= 0 or Qm <= 0:
+                continue
+            wt = self.derived[doff:doff + dn]
+            self.C.conv_fwd(dy, wt, dx, res, None, N, P, Q, c.cout, c.cin, T, U, Pm, Qm, 1, 1, ioff_h, ioff_w, -1, -1,
+                            H, W, c.st, c.st, ph, pw, bm, bn, bk)
+
+    def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None):
+        key = (cout, R, S, C, N * P * Q)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = tuple(self.C.conv_wgrad_plan(cout, R, S, C, N * P * Q, self.wgrad_blocks))
+            self._plans[key] = plan
+        splits, pps = plan
+        ldw = R * S * C
+        ws = self._buf("ws", splits * cout * ldw, torch.float32)
+        self.C.conv_wgrad(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, st, pad, pad, 1, 1, ldw, splits, pps)
+        self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, False)
+
+    def bn_bwd(self, bn1: _BN, y1, g, out, count: int, bn2: Optional[_BN] = None, y2=None):
+        """Reduce pass + finalize (dgamma/dbeta into grad buffer).  Returns nothing; coefficients in bcoef."""
+        C = bn1.C
+        rows = g.numel() // C
+        blocks = self.C.bn_bwd_reduce_blocks(rows, C)
+        K = 4 if bn2 is not None else 2
+        part = self._buf("bnpart", blocks * C * K, torch.float32)
+        self.C.bn_bwd_reduce(g, out, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, part, blocks, rows, C)
+        sums = bn1.bsums[:C * K]
+        self.C.bn_partial_reduce(part, blocks, C, K, self._buf("bnred", 64 * C * 4, torch.float64), sums)
+        if self.syncbn_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(sums, group=self.syncbn_group)
+            count = count * dist.get_world_size(self.syncbn_group)
+        # sums layout: k*C + c for k in [sum dz1, sum dz1*x1, (sum dz2, sum dz2*x2)]
+        self.C.bn_bwd_finalize(sums[:2 * C], float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot),
+                               self._g(bn1.bslot), 1.0, bn1.bcoef)
+        self.grad_ready(bn1.gslot.index)
+        self.grad_ready(bn1.bslot.index)
+        if bn2 is not None:
+            self.C.bn_bwd_finalize(sums[2 * C:4 * C], float(count), bn2.coef, self._p(bn2.gslot), self._g(bn2.gslot),
+                                   self._g(bn2.bslot), 1.0, bn2.bcoef)
+            self.grad_ready(bn2.gslot.index)
+            self.grad_ready(bn2.bslot.index)
+
+    # ---------------------------------------------------------------------------------- forward
+    def _forward(self, images: torch.Tensor, train: bool):
+        Cn = self.C
+        N = images.shape[0]
+        assert images.dim() == 4 and images.shape[1] == 3, "expected NCHW images"
+        x32 = images if images.dtype == torch.float32 else images.float()
+        x32 = x32.contiguous()
+        H, W = images.shape[2], images.shape[3]
+        st = self.stem
+        P0, Q0 = st.out_hw(H, W)
+        saved = {"N": N, "H": H, "W": W}
+        # stem: im2col (fp32 NCHW -> 16-bit [N*P0*Q0][KP]) + GEMM with BN statistics
+        cols = self._buf("im2col", N * P0 * Q0 * self.stem_kp)
+        Cn.im2col(x32, cols, N, 3, H, W, st.R, st.S, st.st, st.pad, self.stem_kp)
+        y0 = self._buf("y0", N * P0 * Q0 * st.cout)
+        wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * self.stem_kp]
+        _, _, sp, tiles = self.conv_fwd(st, cols, N, P0, Q0, y0, train, w=wst, cin=self.stem_kp, R=1, S=1, st=1,
+                                        pad=0)
+        if train:
+            self.bn_train_finalize(self.stem_bn, sp, tiles, N * P0 * Q0)
+        else:
+            self.bn_eval(self.stem_bn)
+        H1, W1 = (P0 - 1) // 2 + 1, (Q0 - 1) // 2 + 1
+        x = self._buf("act_in", N * H1 * W1 * st.cout)
+        idx = self._buf("mp_idx", N * H1 * W1 * st.cout, torch.uint8)
+        Cn.bn_relu_maxpool(y0, self.stem_bn.coef, x, idx, N, P0, Q0, st.cout)
+        saved.update(cols=cols, y0=y0, P0=P0, Q0=Q0, idx=idx, x0=x, H1=H1, W1=W1)
+        Hc, Wc, Cc = H1, W1, st.cout
+        blk_saved = []
+        for bi, b in enumerate(self.blocks):
+            rec = {"x": x, "H": Hc, "W": Wc, "C": Cc, "ys": [], "as": [], "hw": []}
+            cur, h, w = x, Hc, Wc
+            nconv = len(b["convs"])
+            for ci, (c, bn) in enumerate(zip(b["convs"], b["bns"])):
+                P, Q = c.out_hw(h, w)
+                y = self._buf(("y", bi, ci), N * P * Q * c.cout)
+                _, _, sp, tiles = self.conv_fwd(c, cur, N, h, w, y, train)
+                if train:
+                    self.bn_train_finalize(bn, sp, tiles, N * P * Q)
+                else:
+                    self.bn_eval(bn)
+                rec["ys"].append(y)
+                rec["hw"].append((h, w, P, Q))
+                if ci < nconv - 1:
+                    a = self._buf(("a", bi, ci), N * P * Q * c.cout)
+                    Cn.bn_apply(y, bn.coef, None, None, a, c.cout, 0, True)
+                    rec["as"].append(a)
+                    cur, h, w = a, P, Q
+                else:
+                    h, w = P, Q
+            cl, bnl = b["convs"][-1], b["bns"][-1]
+            out = self._buf(("out", bi), N * h * w * cl.cout)
+            if b["ds_conv"] is not None:
+                dc, dbn = b["ds_conv"], b["ds_bn"]
+                yd = self._buf(("yd", bi), N * h * w * dc.cout)
+                _, _, sp, tiles = self.conv_fwd(dc, x, N, Hc, Wc, yd, train)
+                if train:
+                    self.bn_train_finalize(dbn, sp, tiles, N * h * w)
+                else:
+                    self.bn_eval(dbn)
+                Cn.bn_apply(rec["ys"][-1], bnl.coef, yd, dbn.coef, out, cl.cout, 2, True)
+                rec["yd"] = yd
+            else:
+                Cn.bn_apply(rec["ys"][-1], bnl.coef, x, None, out, cl.cout, 1, True)
+            rec["out"] = out
+            blk_saved.append(rec)
+            x, Hc, Wc, Cc = out, h, w, cl.cout
+        # head: global average pool -> fc (1x1 GEMM over the padded class dimension)
+        HW = Hc * Wc
+        feat = self._buf("feat", N * self.feat)
+        Cn.avgpool_fwd(x, feat, N, HW, Cc, self.feat)
+        logits = self._buf("logits16", N * self.ncls_pad)
+        wfc = self.derived[self.fc_w_off:self.fc_w_off + self.ncls_pad * self.feat]
+        bm, bn = _conv_tile(self.ncls_pad)
+        Cn.conv_fwd(feat, wfc, logits, None, None, N, 1, 1, self.feat, self.ncls_pad, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1,
+                    1, 1, 1, 1, 0, 0, bm, bn, 64)
+        saved.update(blocks=blk_saved, feat=feat, logits=logits, Hc=Hc, Wc=Wc, Cc=Cc)
+        return saved
+
+    def _loss(self, saved, target, dlogits, loss_scale, grad_div):
+        N = saved["N"]
+        out = torch.empty(N, self.ncls, dtype=torch.float32, device=self.device)
+        rl = self._buf("row_loss", N, torch.float32)
+        rc = self._buf("row_correct", N, torch.float32)
+        self.C.xent(saved["logits"], self.ncls_pad, self._p(self.fcb_slot), target, N, self.ncls, out, dlogits,
+                    loss_scale, float(grad_div), rl, rc)
+        met = torch.empty(2, dtype=torch.float32, device=self.device)
+        self.C.metrics(rl, rc, N, met)
+        return out, met
+
+    @torch.no_grad()
+    def eval_step(self, images, target):
+        saved = self._forward(images, train=False)
+        return self._loss(saved, target, None, None, 1.0)
+
+    @torch.no_grad()
+    def train_step(self, images, target, loss_scale: Optional[torch.Tensor] = None, grad_div: Optional[float] = None):
+        """Forward + loss + backward.  Gradients (scaled by loss_scale / grad_div) land in flat.grad."""
+        saved = self._forward(images, train=True)
+        N = saved["N"]
+        dlog = self._buf("dlogits", N * self.ncls_pad)
+        logits, met = self._loss(saved, target, dlog, loss_scale, grad_div or N)
+        self._backward(saved, dlog)
+        return logits, met
+
+    # ---------------------------------------------------------------------------------- backward
+    def _backward(self, saved, dlog):
+        Cn = self.C
+        N = saved["N"]
+        # fc: bias grad (column sums), weight grad (1x1 wgrad over the batch), data grad
+        Cn.colsum(dlog, N, self.ncls_pad, self.ncls, self._g(self.fcb_slot), 1.0)
+        self.grad_ready(self.fcb_slot.index)
+        self._wgrad(self.ncls_pad, saved["feat"], dlog, N, 1, 1, self.feat, 1, 1, 1, 1, 1, 0,
+                    self._g(self.fc_slot), self.feat, rows=self.ncls, cols=self.feat)
+        self.grad_ready(self.fc_slot.index)
+        dfeat = self._buf("dfeat", N * self.feat)
+        wt = self.derived[self.fc_wt_off:self.fc_wt_off + self.ncls_pad * self.feat]
+        bm, bn = _conv_tile(self.feat)
+        Cn.conv_fwd(dlog, wt, dfeat, None, None, N, 1, 1, self.ncls_pad, self.feat, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1,
+                    1, 1, 1, 1, 0, 0, bm, bn, 64)
+        Hc, Wc, Cc = saved["Hc"], saved["Wc"], saved["Cc"]
+        g = self._buf("g_a", N * Hc * Wc * Cc)
+        Cn.avgpool_bwd(dfeat, g, N, Hc * Wc, Cc, self.feat)
+        gsel = 0
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b, rec = self.blocks[bi], saved["blocks"][bi]
+            convs, bns = b["convs"], b["bns"]
+            nconv = len(convs)
+            h_last, w_last = rec["hw"][-1][2], rec["hw"][-1][3]
+            cnt = N * h_last * w_last
+            x, Hin, Win, Cin = rec["x"], rec["H"], rec["W"], rec["C"]
+            # block-output reduction: BN of the last conv (+ downsample BN) share dz = g * relu'(out)
+            ds = b["ds_conv"] is not None
+            self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["out"], cnt, b["ds_bn"] if ds else None,
+                        rec["yd"] if ds else None)
+            dy_last = self._buf("dy_a", rec["ys"][-1].numel())
+            if ds:
+                dyd = self._buf("dy_b", rec["yd"].numel())
+                Cn.bn_bwd_apply(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy_last, rec["yd"], b["ds_bn"].bcoef,
+                                dyd, None, convs[-1].cout)
+            else:
+                dz = self._buf("dz_id", g.numel())
+                Cn.bn_bwd_apply(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy_last, None, None, None, dz,
+                                convs[-1].cout)
+            # gradient w.r.t. the block input accumulates in g_next
+            gnext = self._buf("g_b" if gsel == 0 else "g_a", N * Hin * Win * Cin)
+            if ds:
+                dc = b["ds_conv"]
+                P, Q = dc.out_hw(Hin, Win)
+                self.conv_bwd(dc, x, N, Hin, Win, dyd, P, Q, gnext)  # writes every element of gnext
+                res = gnext
+            else:
+                res = dz
+            # chain through the block's convs in reverse
+            dy, dname = dy_last, "dy_a"
+            for ci in range(nconv - 1, -1, -1):
+                c = convs[ci]
+                h, w, P, Q = rec["hw"][ci]
+                xin = rec["as"][ci - 1] if ci > 0 else x
+                if ci > 0:
+                    da = self._buf("da", N * h * w * c.cin)
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, da)
+                    bnp = bns[ci - 1]
+                    a_prev = rec["as"][ci - 1]
+                    self.bn_bwd(bnp, rec["ys"][ci - 1], da, a_prev, N * h * w)
+                    dname = "dy_c" if dname == "dy_a" else "dy_a"
+                    dyp = self._buf(dname, rec["ys"][ci - 1].numel())
+                    Cn.bn_bwd_apply(da, a_prev, rec["ys"][ci - 1], bnp.bcoef, dyp, None, None, None, None, c.cin)
+                    dy = dyp
+                else:
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res)
+            g = gnext
+            gsel ^= 1
+        # stem: max-pool backward + ReLU mask -> BN backward -> weight gradient over im2col columns
+        st, sbn = self.stem, self.stem_bn
+        P0, Q0 = saved["P0"], saved["Q0"]
+        dz0 = self._buf("dz0", N * P0 * Q0 * st.cout)
+        Cn.maxpool_bwd_relu(g, saved["idx"], saved["y0"], sbn.coef, dz0, N, P0, Q0, st.cout)
+        self.bn_bwd(sbn, saved["y0"], dz0, None, N * P0 * Q0)
+        dy0 = self._buf("dy0", dz0.numel())
+        Cn.bn_bwd_apply(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
+        self._wgrad(st.cout, saved["cols"], dy0, N, P0, Q0, self.stem_kp, 1, 1, P0, Q0, 1, 0,
+                    self._g(st.slot), self.stem_k, rows=st.cout, cols=self.stem_k)
+        self.grad_ready(st.pid)

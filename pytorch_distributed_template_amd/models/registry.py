@@ -1,0 +1,54 @@
+"""Model registry by name (reference: `dataparallel.py:36-37` builds ``--arch`` choices from every
+lowercase callable in ``torchvision.models``; `:112-117` instantiates ``models.__dict__[arch]()``).
+
+torchvision is not available offline here, so the registry is ours: the ResNet family with
+torchvision-identical parameter names, shapes and initialisation.  ``pretrained=True`` loads weights
+from a LOCAL torchvision-format checkpoint (``--pretrained-path`` or ``$PDT_PRETRAINED_DIR/<arch>.pth``)
+with the safe ``weights_only`` loader -- the GPU box has no network.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from . import resnet
+
+_REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
+    "resnet18": resnet.resnet18,
+    "resnet34": resnet.resnet34,
+    "resnet50": resnet.resnet50,
+    "resnet101": resnet.resnet101,
+    "resnet152": resnet.resnet152,
+    "resnext50_32x4d": resnet.resnext50_32x4d,
+    "resnext101_32x8d": resnet.resnext101_32x8d,
+    "wide_resnet50_2": resnet.wide_resnet50_2,
+    "wide_resnet101_2": resnet.wide_resnet101_2,
+}
+
+
+def register(name: str, fn: Callable[..., torch.nn.Module]) -> None:
+    if not name.islower():
+        raise ValueError("model names are lowercase (torchvision convention)")
+    _REGISTRY[name] = fn
+
+
+def model_names() -> List[str]:
+    return sorted(_REGISTRY)
+
+
+def create(arch: str, pretrained: bool = False, pretrained_path: Optional[str] = None, **kwargs) -> torch.nn.Module:
+    if arch not in _REGISTRY:
+        raise KeyError(f"unknown arch {arch!r}; choices: {model_names()}")
+    model = _REGISTRY[arch](**kwargs)
+    if pretrained:
+        path = pretrained_path or os.path.join(os.environ.get("PDT_PRETRAINED_DIR", "pretrained"), f"{arch}.pth")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"--pretrained needs local weights (no network): {path} not found")
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and "state_dict" in sd:
+            sd = sd["state_dict"]
+        sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
+        model.load_state_dict(sd)
+    return model

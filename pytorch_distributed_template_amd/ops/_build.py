@@ -1,0 +1,122 @@
+"""In-tree build of the native extension ``pytorch_distributed_template_amd/_C.so``.
+
+HIP kernels (``csrc/kernels/*.hip``) are compiled by ``hipcc --offload-arch=gfx950`` directly (no
+hipify, no CUDA sources, single target), the thin binding layer (``csrc/bindings.cpp``) by the host
+C++ compiler against the installed PyTorch headers, and everything is linked into one shared object
+that lives inside the package so it travels with the repository snapshot to the GPU box.
+
+Objects are rebuilt only when their source, any header under ``csrc/`` or the compile flags change.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO, "csrc")
+BUILD = os.path.join(REPO, "build", "native")
+OUT = os.path.join(PKG_DIR, "_C.so")
+ARCH = os.environ.get("PDT_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension
+
+    inc = cpp_extension.include_paths("cuda")
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _headers_digest() -> str:
+    h = hashlib.sha1()
+    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _needs(obj: str, src: str, sig: str) -> bool:
+    stamp = obj + ".sig"
+    if not (os.path.exists(obj) and os.path.exists(stamp)):
+        return True
+    with open(stamp) as f:
+        if f.read() != sig:
+            return True
+    return os.path.getmtime(src) > os.path.getmtime(obj)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("native build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def _compile(src, obj, cmd, sig, verbose):
+    if not _needs(obj, src, sig):
+        return False
+    _run(cmd, verbose)
+    with open(obj + ".sig", "w") as f:
+        f.write(sig)
+    return True
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:
+    """Compile every HIP kernel for gfx950 and link ``_C.so``; returns its path."""
+    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    cxx = os.environ.get("CXX", shutil.which("g++") or "g++")
+    inc, tlib, abi = _torch_paths()
+    os.makedirs(BUILD, exist_ok=True)
+    hdr = _headers_digest()
+    jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
+
+    hip_flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
+                 "-munsafe-fp-atomics", f"-I{CSRC}"]
+    py_inc = sysconfig.get_paths()["include"]
+    cxx_flags = ["-O2", "-std=c++17", "-fPIC", f"-I{CSRC}", f"-I{py_inc}", "-D__HIP_PLATFORM_AMD__=1",
+                 "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
+                 "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations"] + [f"-I{p}" for p in inc]
+
+    jobs_list = []
+    for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        cmd = [hipcc] + hip_flags + ["-c", src, "-o", obj]
+        jobs_list.append((src, obj, cmd, hashlib.sha1((" ".join(cmd) + hdr).encode()).hexdigest()))
+    bsrc = os.path.join(CSRC, "bindings.cpp")
+    bobj = os.path.join(BUILD, "bindings.o")
+    bcmd = [cxx] + cxx_flags + ["-c", bsrc, "-o", bobj]
+    jobs_list.append((bsrc, bobj, bcmd, hashlib.sha1((" ".join(bcmd) + hdr).encode()).hexdigest()))
+    if force:
+        for _, obj, _, _ in jobs_list:
+            if os.path.exists(obj):
+                os.remove(obj)
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        changed = list(ex.map(lambda j: _compile(*j, verbose), jobs_list))
+
+    objs = [j[1] for j in jobs_list]
+    if any(changed) or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
+        tmp = OUT + ".tmp"
+        link = [cxx, "-shared", "-o", tmp] + objs + [
+            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            f"-L{os.path.join(ROCM, 'lib')}", "-lamdhip64", f"-Wl,-rpath,{tlib}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
+        _run(link, verbose)
+        os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv, force="--force" in sys.argv))

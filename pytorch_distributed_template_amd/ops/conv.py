@@ -1,0 +1,115 @@
+"""Functional NHWC convolution ops over the native implicit-GEMM kernels.
+
+Tensors are NHWC 16-bit activations (``[N, H, W, C]`` contiguous) and KRSC weights
+(``[Cout, kh, kw, Cin]`` contiguous, i.e. a ``channels_last`` PyTorch conv weight's storage).
+
+* :func:`conv_fwd`    forward conv (optionally with BatchNorm partial statistics)
+* :func:`conv_dgrad`  gradient w.r.t. the input, one launch per sub-pixel phase of the stride
+* :func:`conv_wgrad`  gradient w.r.t. the weight (fp32), split-K over pixels
+
+These wrappers allocate their outputs; the ResNet executor calls the same kernels on preallocated
+buffers.  They are the unit-test surface of the kernels (tests/test_kernels_gpu.py).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import native
+
+
+def conv_tile(cout: int) -> Tuple[int, int]:
+    """(BM, BN) tile of the implicit-GEMM kernel for a given GEMM-N (output channels)."""
+    if cout % 128 == 0:
+        return 128, 128
+    return 256, 64
+
+
+def dgrad_phases(R: int, S: int, stride: int, pad: int) -> List[Tuple[int, int, List[int], List[int], int, int]]:
+    """Sub-pixel decomposition of a strided conv's backward-data pass.
+
+    For output phase (ph, pw) of dX (rows h = stride*i + ph), only taps r = r0 + stride*t contribute,
+    with dY row ``i + ioff_h - t``.  Returns ``(ph, pw, rs, ss, ioff_h, ioff_w)`` per phase; ``rs``/``ss``
+    are the contributing tap indices (possibly empty: e.g. odd phases of a 1x1 stride-2 conv).
+    """
+    out = []
+    for ph in range(stride):
+        for pw in range(stride):
+            r0, s0 = (ph + pad) % stride, (pw + pad) % stride
+            rs = list(range(r0, R, stride))
+            ss = list(range(s0, S, stride))
+            out.append((ph, pw, rs, ss, (ph + pad - r0) // stride, (pw + pad - s0) // stride))
+    return out
+
+
+def dgrad_weight_index(cout: int, cin: int, R: int, S: int, rs: List[int], ss: List[int]) -> torch.Tensor:
+    """Index map (into a KRSC weight) of the phase weight ``Wt[c][t][u][k] = W[k][rs[t]][ss[u]][c]``."""
+    if not rs or not ss:
+        return torch.empty(0, dtype=torch.long)
+    c = torch.arange(cin).view(-1, 1, 1, 1)
+    t = torch.tensor(rs).view(1, -1, 1, 1)
+    u = torch.tensor(ss).view(1, 1, -1, 1)
+    k = torch.arange(cout).view(1, 1, 1, -1)
+    return (((k * R + t) * S + u) * cin + c).reshape(-1)
+
+
+def out_hw(H: int, W: int, R: int, S: int, stride: int, pad: int) -> Tuple[int, int]:
+    return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
+             residual: Optional[torch.Tensor] = None):
+    """y = conv(x, w) in NHWC/KRSC.  Returns ``y`` or ``(y, (sum, sumsq) per channel)`` with stats."""
+    N, H, W, C = x.shape
+    K, R, S, C2 = w.shape
+    assert C == C2
+    P, Q = out_hw(H, W, R, S, stride, pad)
+    y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
+    bm, bn = conv_tile(K)
+    bk = 64 if C % 64 == 0 else 32
+    sp = None
+    if stats:
+        tiles = native.C.conv_m_tiles(N * P * Q, bm)
+        sp = torch.empty(tiles * K * 2, dtype=torch.float32, device=x.device)
+    native.C.conv_fwd(x, w, y, residual, sp, N, H, W, C, K, R, S, P, Q, stride, stride, -pad, -pad, 1, 1,
+                      P, Q, 1, 1, 0, 0, bm, bn, bk)
+    if not stats:
+        return y
+    part = sp.view(tiles, K, 2).double().sum(0)
+    return y, (part[:, 0], part[:, 1])
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 1, pad: int = 0,
+               residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dX (NHWC, [N, H, W, Cin]) of ``y = conv(x, w)`` given dY ([N, P, Q, Cout])."""
+    N, P, Q, K = dy.shape
+    K2, R, S, C = w.shape
+    assert K == K2
+    dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    bm, bn = conv_tile(C)
+    bk = 64 if K % 64 == 0 else 32
+    wflat = w.reshape(-1)
+    for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(R, S, stride, pad):
+        Pm, Qm = (H - ph + stride - 1) // stride, (W - pw + stride - 1) // stride
+        if Pm <= 0 or Qm <= 0:
+            continue
+        idx = dgrad_weight_index(K, C, R, S, rs, ss).to(w.device)
+        wt = wflat[idx].contiguous() if idx.numel() else torch.empty(0, dtype=w.dtype, device=w.device)
+        native.C.conv_fwd(dy, wt, dx, residual, None, N, P, Q, K, C, len(rs), len(ss), Pm, Qm, 1, 1, ioff_h, ioff_w,
+                          -1, -1, H, W, stride, stride, ph, pw, bm, bn, bk)
+    return dx
+
+
+def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int = 1, pad: int = 0,
+               target_blocks: int = 2048) -> torch.Tensor:
+    """dW (fp32, KRSC [Cout, R, S, Cin]) of ``y = conv(x, w)``."""
+    N, H, W, C = x.shape
+    _, P, Q, K = dy.shape
+    splits, pps = native.C.conv_wgrad_plan(K, R, S, C, N * P * Q, target_blocks)
+    ldw = R * S * C
+    ws = torch.empty(splits * K * ldw, dtype=torch.float32, device=x.device)
+    native.C.conv_wgrad(x, dy, ws, N, H, W, C, K, R, S, P, Q, stride, stride, pad, pad, 1, 1, ldw, splits, pps)
+    out = torch.empty(K * ldw, dtype=torch.float32, device=x.device)
+    native.C.wgrad_reduce(ws, splits, K, ldw, ldw, K * ldw, out, ldw, 1.0, False)
+    return out.view(K, R, S, C)

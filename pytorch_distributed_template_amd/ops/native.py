@@ -1,0 +1,53 @@
+"""Loader for the in-tree native extension (``pytorch_distributed_template_amd/_C.so``).
+
+``native.C`` is the extension module.  It is imported on first use; if the shared object is missing
+it is built in-tree (set PDT_AUTOBUILD=1 to also rebuild a stale one) with ``ops._build`` (hipcc for gfx950).  There is no silent fallback:
+a GPU code path that needs a kernel raises if the extension cannot be loaded.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+
+
+def _so_path() -> str:
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+
+
+def load(build: bool = True):
+    global _mod
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        import torch  # noqa: F401  (loads libtorch / the HIP runtime the extension links against)
+
+        if build and (not os.path.exists(_so_path()) or os.environ.get("PDT_AUTOBUILD", "0") == "1"):
+            from . import _build
+            _build.build()
+        if not os.path.exists(_so_path()):
+            raise ImportError(f"native extension not found at {_so_path()}; run `python -m "
+                              "pytorch_distributed_template_amd.ops._build`")
+        _mod = importlib.import_module("pytorch_distributed_template_amd._C")
+        return _mod
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:  # pragma: no cover - diagnostic helper
+        return False
+
+
+class _Proxy:
+    def __getattr__(self, name):
+        return getattr(load(), name)
+
+
+C = _Proxy()

@@ -1,0 +1,123 @@
+"""Data-parallel gradient bucketer (our replacement for the C++ DDP Reducer).
+
+Reference behaviour being reproduced (SURVEY §2.3 "DDP", X2-X4): one process per GPU; at
+construction parameters and buffers are broadcast from rank 0 (`T/nn/parallel/distributed.py:862-864`);
+before every grad-enabled forward the BatchNorm buffers are re-broadcast from rank 0 (X3); during
+backward, gradients are averaged across ranks in buckets (reverse registration order, first bucket
+small) with the all-reduces overlapping the rest of backward (X4).
+
+MI355X-native design:
+* gradients live in ONE flat fp32 buffer (:class:`~..optim.flat.FlatParams`), so a bucket is a
+  contiguous slice -- no copy-in/copy-out, no per-bucket division (the 1/world factor is folded into
+  the fused SGD kernel);
+* a bucket's all-reduce is launched (``async_op=True`` on the RCCL communicator, which orders itself
+  after the compute stream's work already enqueued) the moment its last gradient is produced --
+  either by the native executor's explicit backward (``grad_ready(pid)``) or by autograd
+  post-accumulate hooks on the generic path;
+* bucket sizes default to 1 MiB for the first (last-produced-first) bucket and 25 MiB after, which
+  keeps each ring all-reduce large enough to use all seven xGMI links of an MI355X node while the
+  final (stem-side) bucket stays small so the exposed tail after backward is short;
+* ``finish()`` makes the compute stream wait for every bucket (no host synchronisation).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..optim.flat import FlatBuffers, FlatParams
+
+
+class GradBucketer:
+    def __init__(self, flat: FlatParams, process_group=None, bucket_cap_mb: float = 25.0,
+                 first_bucket_mb: float = 1.0, enabled: Optional[bool] = None):
+        self.flat = flat
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.enabled = (self.world > 1) if enabled is None else enabled
+        cap = int(bucket_cap_mb * 1024 * 1024)
+        first = int(first_bucket_mb * 1024 * 1024)
+        # buckets over parameters in reverse registration order (the order gradients are produced)
+        self.buckets: List[dict] = []
+        self.bucket_of = {}
+        cur: List[int] = []
+        cur_bytes = 0
+        limit = first
+        for s in reversed(flat.slots):
+            cur.append(s.index)
+            cur_bytes += s.numel * 4
+            if cur_bytes >= limit:
+                self._close(cur)
+                cur, cur_bytes, limit = [], 0, cap
+        if cur:
+            self._close(cur)
+        self._pending = [len(b["params"]) for b in self.buckets]
+        self._works = []
+
+    def _close(self, idxs: List[int]) -> None:
+        slots = [self.flat.slots[i] for i in idxs]
+        lo = min(s.offset for s in slots)
+        hi = max(s.offset + s.numel for s in slots)
+        b = {"params": list(idxs), "lo": lo, "hi": hi, "id": len(self.buckets)}
+        for i in idxs:
+            self.bucket_of[i] = b["id"]
+        self.buckets.append(b)
+
+    def bucket_sizes_mb(self) -> List[float]:
+        return [(b["hi"] - b["lo"]) * 4 / 2 ** 20 for b in self.buckets]
+
+    # -- per-step protocol ---------------------------------------------------------------------
+    def grad_ready(self, pid: int) -> None:
+        if not self.enabled:
+            return
+        bid = self.bucket_of[pid]
+        self._pending[bid] -= 1
+        if self._pending[bid] == 0:
+            b = self.buckets[bid]
+            view = self.flat.grad[b["lo"]:b["hi"]]
+            self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+
+    def finish(self) -> None:
+        """Wait (stream-wise) for every bucket; launch any bucket whose params produced no grad."""
+        if not self.enabled:
+            return
+        for bid, n in enumerate(self._pending):
+            if n > 0:  # unused parameters: reduce whatever is in the buffer (zeros) to stay in lock-step
+                b = self.buckets[bid]
+                self._works.append(dist.all_reduce(self.flat.grad[b["lo"]:b["hi"]], group=self.pg,
+                                                   async_op=True))
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+        self._pending = [len(b["params"]) for b in self.buckets]
+
+    def grad_scale(self) -> float:
+        """Factor the optimizer applies to the summed gradients (mean over ranks)."""
+        return 1.0 / self.world if self.enabled else 1.0
+
+    # -- autograd path -------------------------------------------------------------------------
+    def register_autograd_hooks(self) -> None:
+        """Generic (autograd) path: notify readiness from post-accumulate-grad hooks."""
+        for s, p in zip(self.flat.slots, self.flat.params):
+            p.register_post_accumulate_grad_hook(lambda _p, i=s.index: self.grad_ready(i))
+
+
+def broadcast_parameters(flat: FlatParams, buffers: Optional[FlatBuffers], process_group=None, src: int = 0) -> None:
+    """DDP constructor semantics: every rank starts from rank 0's parameters and buffers (X2)."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) == 1:
+        return
+    dist.broadcast(flat.data, src=src, group=process_group)
+    if buffers is not None:
+        sync_buffers(buffers, process_group, src)
+    flat.refresh_shadow()
+
+
+def sync_buffers(buffers: FlatBuffers, process_group=None, src: int = 0) -> None:
+    """DDP ``broadcast_buffers=True``: BN running statistics from rank 0 before a forward (X3)."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) == 1:
+        return
+    if buffers.n_float:
+        dist.broadcast(buffers.fdata, src=src, group=process_group)
+    if buffers.n_int:
+        dist.broadcast(buffers.idata, src=src, group=process_group)

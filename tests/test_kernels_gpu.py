@@ -1,0 +1,166 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references (run on an MI355X)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _rand16(*shape, dtype=torch.bfloat16, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(dtype)
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (2, 15, 13, 64, 128, 3, 2, 1),
+    (3, 14, 14, 128, 256, 1, 2, 0),
+    (2, 7, 7, 256, 64, 1, 1, 0),
+    (1, 9, 9, 128, 128, 3, 1, 1),
+    (2, 8, 8, 512, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_fwd_and_stats(case, dtype):
+    from pytorch_distributed_template_amd.ops import conv
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(0)
+    x = _rand16(N, H, W, C, dtype=dtype)
+    w = _rand16(K, R, R, C, dtype=dtype, scale=(1.0 / (C * R * R)) ** 0.5)
+    y, (s, ss) = conv.conv_fwd(x, w, st, pad, stats=True)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=st, padding=pad)
+    ref = ref.permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+    yf = y.float().reshape(-1, K)
+    assert torch.allclose(s.float(), yf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(ss.float(), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad(case):
+    from pytorch_distributed_template_amd.ops import conv
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(1)
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    dy = _rand16(N, P, Q, K)
+    w = _rand16(K, R, R, C, scale=(1.0 / (K * R * R)) ** 0.5)
+    res = _rand16(N, H, W, C)
+    dx = conv.conv_dgrad(dy, w, H, W, st, pad, residual=res)
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                     stride=st, padding=pad).permute(0, 2, 3, 1) + res.float()
+    assert _rel(dx, ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad(case):
+    from pytorch_distributed_template_amd.ops import conv
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(2)
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    x = _rand16(N, H, W, C)
+    dy = _rand16(N, P, Q, K)
+    dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=64)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
+                                      stride=st, padding=pad).permute(0, 2, 3, 1)
+    assert _rel(dw, ref) < 2e-3
+
+
+def test_conv_wgrad_many_splits():
+    from pytorch_distributed_template_amd.ops import conv
+    torch.manual_seed(3)
+    x = _rand16(16, 28, 28, 64)
+    dy = _rand16(16, 28, 28, 64)
+    dw = conv.conv_wgrad(x, dy, 3, 3, 1, 1, target_blocks=4096)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3), dy.float().permute(0, 3, 1, 2),
+                                      stride=1, padding=1).permute(0, 2, 3, 1)
+    assert _rel(dw, ref) < 2e-3
+
+
+def test_sgd_matches_torch():
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(4)
+    n = 10007
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    buf = torch.zeros(n, device=DEV)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ref_p = p.clone().requires_grad_(True)
+    opt = torch.optim.SGD([ref_p], lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for step in range(3):
+        ref_p.grad = g * 0.5
+        opt.step()
+        native.C.sgd(p, g, buf, sh, None, 0.1, 0.9, 1e-4, 0.5, None, None, step == 0)
+    assert torch.allclose(p, ref_p.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(sh, p.to(torch.bfloat16))
+
+
+def test_sgd_skips_on_inf():
+    from pytorch_distributed_template_amd.ops import native
+    p = torch.ones(100, device=DEV)
+    g = torch.ones(100, device=DEV)
+    g[7] = float("inf")
+    found = torch.zeros(1, device=DEV)
+    native.C.nonfinite_check(g, found)
+    assert found.item() == 1.0
+    buf = torch.zeros(100, device=DEV)
+    native.C.sgd(p, g, buf, None, None, 0.1, 0.9, 0.0, 1.0, None, found, True)
+    assert torch.equal(p, torch.ones(100, device=DEV))
+
+
+def test_xent_matches_torch():
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(5)
+    B, ncls, ld = 37, 1000, 1024
+    logits = torch.zeros(B, ld, device=DEV, dtype=torch.bfloat16)
+    logits[:, :ncls] = (torch.randn(B, ncls, device=DEV) * 3).to(torch.bfloat16)
+    bias = torch.randn(ncls, device=DEV) * 0.1
+    tgt = torch.randint(0, ncls, (B,), device=DEV)
+    out = torch.empty(B, ncls, device=DEV)
+    d = torch.empty(B, ld, device=DEV, dtype=torch.bfloat16)
+    rl = torch.empty(B, device=DEV)
+    rc = torch.empty(B, device=DEV)
+    scale = torch.full((1,), 8.0, device=DEV)
+    native.C.xent(logits, ld, bias, tgt, B, ncls, out, d, scale, float(B), rl, rc)
+    met = torch.empty(2, device=DEV)
+    native.C.metrics(rl, rc, B, met)
+    ref_in = (logits[:, :ncls].float() + bias).requires_grad_(True)
+    loss = F.cross_entropy(ref_in, tgt)
+    loss.backward()
+    assert torch.allclose(out, ref_in.detach(), atol=1e-5)
+    assert abs(met[0].item() - loss.item()) < 1e-4
+    acc = (ref_in.detach().argmax(1) == tgt).float().mean().item()
+    assert abs(met[1].item() - acc) < 1e-6
+    assert _rel(d[:, :ncls], ref_in.grad * 8.0) < 1e-2
+    assert d[:, ncls:].abs().max().item() == 0
+
+
+def test_bn_relu_maxpool_and_backward():
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(6)
+    N, H, W, C = 2, 12, 11, 64
+    y = _rand16(N, H, W, C)
+    coef = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1,
+                      torch.zeros(2 * C, device=DEV)])
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=DEV)
+    idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=DEV)
+    native.C.bn_relu_maxpool(y, coef, out, idx, N, H, W, C)
+    a = torch.relu(y.float() * coef[:C] + coef[C:2 * C]).permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(a, 3, 2, 1)
+    assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2
+    dp = _rand16(N, OH, OW, C)
+    ref.backward(dp.float().permute(0, 3, 1, 2))
+    dz = torch.empty_like(y)
+    native.C.maxpool_bwd_relu(dp, idx, y, coef, dz, N, H, W, C)
+    refdz = a.grad * (a.detach() > 0)
+    assert _rel(dz.permute(0, 3, 1, 2), refdz) < 1e-2

@@ -1,0 +1,39 @@
+#!/bin/bash
+# Usage: bash tools/gpu_round.sh <stage...>   (run on the GPU box via gpurun)
+# Each GPU step has its own time limit; after a crash/timeout nothing more runs.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+for stage in "$@"; do
+  case "$stage" in
+    test)
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+      tail -30 gpurun_out/pytest_gpu.log
+      ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    testk)
+      timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q > gpurun_out/pytest_k.log 2>&1; rc=$?
+      tail -30 gpurun_out/pytest_k.log
+      ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    teste)
+      timeout -k 10 600 python -m pytest tests/test_executor_gpu.py -x -q > gpurun_out/pytest_e.log 2>&1; rc=$?
+      tail -30 gpurun_out/pytest_e.log
+      ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1; rc=$?
+      tail -5 gpurun_out/bench.log
+      [ $rc -eq 0 ] || { echo "bench failed rc=$rc"; exit $rc; } ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      tail -5 gpurun_out/prof.log
+      [ $rc -eq 0 ] || { echo "prof failed rc=$rc"; exit $rc; } ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+      tail -5 gpurun_out/smoke.log
+      [ $rc -eq 0 ] || { echo "smoke failed rc=$rc"; exit $rc; } ;;
+  esac
+done
+echo "ALL DONE"
