@@ -70,10 +70,18 @@ double* pd(const Tensor& t, const char* name) {
 void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N, int64_t H,
               int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t ist_h,
               int64_t ist_w, int64_t ioff_h, int64_t ioff_w, int64_t tstep_h, int64_t tstep_w, int64_t OH, int64_t OW,
-              int64_t ost_h, int64_t ost_w, int64_t ooff_h, int64_t ooff_w, int64_t bm, int64_t bn, int64_t bk) {
+              int64_t ost_h, int64_t ost_w, int64_t ooff_h, int64_t ooff_w, int64_t bm, int64_t bn, int64_t bk,
+              int64_t cs) {
   const int dt = dt16(x, "x");
+  if (cs <= 0) cs = C;
   TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv_fwd: mixed dtypes");
-  TORCH_CHECK(x.numel() == N * H * W * C, "conv_fwd: x has ", x.numel(), " elements, geometry needs ", N * H * W * C);
+  TORCH_CHECK(x.numel() == N * H * W * cs, "conv_fwd: x has ", x.numel(), " elements, geometry needs ", N * H * W * cs);
+  if (cs != C) {  // window mode: every tap's C-element chunk must stay inside the padded image
+    TORCH_CHECK(cs == 4 && C % 32 == 0 && tstep_w == 0 && U == 1 && ioff_h >= 0 && ioff_w >= 0 &&
+                    (Pm - 1) * ist_h + ioff_h + (T - 1) * tstep_h < H &&
+                    ((Qm - 1) * ist_w + ioff_w) * cs + C <= W * cs,
+                "conv_fwd: window-mode geometry leaves the padded image");
+  }
   TORCH_CHECK(w.numel() == Kout * T * U * C, "conv_fwd: w size mismatch");
   TORCH_CHECK(y.numel() == N * OH * OW * Kout, "conv_fwd: y size mismatch");
   TORCH_CHECK(C % bk == 0 && Kout % bn == 0, "conv_fwd: C % bk / Kout % bn must be 0 (C=", C, " Kout=", Kout, ")");
@@ -89,10 +97,10 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   }
   const int64_t M = N * Pm * Qm;
   if (stats.has_value()) {
-    TORCH_CHECK(stats->numel() >= pdt::conv_fwd_m_tiles(M, (int)bm) * Kout * 2, "conv_fwd: stats buffer too small");
-    a.stats = pf(*stats, "stats");
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * Kout * 2, "conv_fwd: stats buffer too small");
+    a.stats = pd(*stats, "stats");
   }
-  a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm; a.cs = cs;
   a.ist_h = ist_h; a.ist_w = ist_w; a.ioff_h = ioff_h; a.ioff_w = ioff_w; a.tstep_h = tstep_h; a.tstep_w = tstep_w;
   a.OH = OH; a.OW = OW; a.ost_h = ost_h; a.ost_w = ost_w; a.ooff_h = ooff_h; a.ooff_w = ooff_w;
   a.M = M;
@@ -110,11 +118,20 @@ std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t
 
 void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
                 int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride_h, int64_t stride_w, int64_t pad_h,
-                int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t ldw, int64_t splits, int64_t pix_per_split) {
+                int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t ldw, int64_t splits, int64_t pix_per_split,
+                int64_t cs, bool win) {
   const int dt = dt16(x, "x");
+  if (cs <= 0) cs = C;
   TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad: mixed dtypes");
   TORCH_CHECK(C % 64 == 0 && Kout % 64 == 0, "conv_wgrad: C and Kout must be multiples of 64");
-  TORCH_CHECK(x.numel() == N * H * W * C && dy.numel() == N * Pm * Qm * Kout, "conv_wgrad: size mismatch");
+  TORCH_CHECK(x.numel() == N * H * W * cs && dy.numel() == N * Pm * Qm * Kout, "conv_wgrad: size mismatch");
+  if (win) {  // stem window mode: rows h..h+1 and 8 pixels from w must lie inside the padded image
+    TORCH_CHECK(cs == 4 && C == 64 && U == 1 && pad_h == 0 && pad_w == 0 &&
+                    (Pm - 1) * stride_h + (T - 1) * dil_h + 1 < H && ((Qm - 1) * stride_w + 8) <= W,
+                "conv_wgrad: window-mode geometry leaves the padded image");
+  } else {
+    TORCH_CHECK(cs == C, "conv_wgrad: pixel stride must equal C outside window mode");
+  }
   TORCH_CHECK(ldw >= T * U * C && ws.numel() >= splits * Kout * ldw, "conv_wgrad: workspace too small");
   TORCH_CHECK(N * Pm * Qm < (1 << 24), "conv_wgrad: pixel count exceeds the fp32-reciprocal divide range");
   pdt::ConvWgradArgs a{};
@@ -124,6 +141,7 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
   a.stride_h = stride_h; a.stride_w = stride_w; a.pad_h = pad_h; a.pad_w = pad_w; a.dil_h = dil_h; a.dil_w = dil_w;
   a.P = N * Pm * Qm; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
+  a.cs = cs; a.win = win ? 1 : 0;
   TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad: bad split plan");
   pdt::conv_wgrad_launch(a, dt, cur_stream());
 }
@@ -137,11 +155,12 @@ void wgrad_reduce(const Tensor& ws, int64_t splits, int64_t rows, int64_t cols, 
 }
 
 // -------------------------------------------------------------------------------------------- bn
-void bn_partial_reduce(const Tensor& part, int64_t tiles, int64_t C, int64_t K, Tensor& scratch, Tensor& sums) {
-  TORCH_CHECK(part.numel() >= tiles * C * K, "bn_partial_reduce: partials too small");
-  TORCH_CHECK(scratch.numel() >= 64 * C * K && sums.numel() >= C * K, "bn_partial_reduce: scratch/sums too small");
-  pdt::bn_partial_reduce_launch(pf(part, "part"), tiles, C, K, pd(scratch, "scratch"), pd(sums, "sums"), cur_stream());
+void bn_slot_sum(const Tensor& slots, int64_t C, int64_t K, Tensor& sums) {
+  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K && sums.numel() >= C * K, "bn_slot_sum: bad sizes");
+  pdt::bn_slot_sum_launch(pd(slots, "slots"), C, K, pd(sums, "sums"), cur_stream());
 }
+
+int64_t stat_slots() { return pdt::kStatSlots; }
 
 void bn_finalize(const Tensor& sums, double count, const Tensor& gamma, const Tensor& beta, double eps, double momentum,
                  Tensor& rm, Tensor& rv, Tensor& coef, bool update_running) {
@@ -171,13 +190,13 @@ void bn_apply(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& 
 int64_t bn_bwd_reduce_blocks(int64_t rows, int64_t C) { return pdt::bn_bwd_reduce_blocks(rows, (int)C); }
 
 void bn_bwd_reduce(const Tensor& g, const OptT& out, const Tensor& y1, const Tensor& coef1, const OptT& y2,
-                   const OptT& coef2, Tensor& part, int64_t blocks, int64_t rows, int64_t C) {
+                   const OptT& coef2, Tensor& slots, int64_t blocks, int64_t rows, int64_t C) {
   const int dt = dt16(g, "g");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && g.numel() == rows * C && y1.numel() == rows * C, "bn_bwd_reduce: bad sizes");
   const int K = y2.has_value() ? 4 : 2;
-  TORCH_CHECK(part.numel() >= blocks * C * K, "bn_bwd_reduce: partials too small");
+  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K, "bn_bwd_reduce: slots too small");
   pdt::bn_bwd_reduce_launch(dt, p16(g, "g"), p16o(out, "out"), p16(y1, "y1"), pf(coef1, "coef1"), p16o(y2, "y2"),
-                            pfo(coef2, "coef2"), pf(part, "part"), (int)blocks, rows, (int)C, cur_stream());
+                            pfo(coef2, "coef2"), pd(slots, "slots"), (int)blocks, rows, (int)C, cur_stream());
 }
 
 void bn_bwd_finalize(const Tensor& sums, double count, const Tensor& coef, const Tensor& gamma, const OptT& dgamma,
@@ -303,6 +322,19 @@ void im2col(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64
   pdt::im2col_launch(dt, pf(x, "x"), p16(out, "out"), N, C, H, W, R, S, stride, pad, ldk, cur_stream());
 }
 
+void stem_pack(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t pad, int64_t Hp,
+               int64_t Wp) {
+  TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * Hp * Wp * 4 && C <= 4 && Hp >= H + 2 * pad &&
+                  Wp >= W + 2 * pad, "stem_pack: bad sizes");
+  pdt::stem_pack_launch(dt16(out, "out"), pf(x, "x"), p16(out, "out"), N, C, H, W, pad, Hp, Wp, cur_stream());
+}
+
+void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
+  check_dev(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == dst.numel(), "gather32: idx must be int32 like dst");
+  pdt::gather32_launch(pf(src, "src"), idx.data_ptr<int>(), pf(dst, "dst"), dst.numel(), cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -312,7 +344,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_reduce", &wgrad_reduce);
-  m.def("bn_partial_reduce", &bn_partial_reduce);
+  m.def("bn_slot_sum", &bn_slot_sum);
+  m.def("stat_slots", &stat_slots);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_apply", &bn_apply);
@@ -333,4 +366,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("amp_update", &amp_update);
   m.def("gather16", &gather16);
   m.def("im2col", &im2col);
+  m.def("stem_pack", &stem_pack);
+  m.def("gather32", &gather32);
 }

@@ -3,8 +3,7 @@
 #include <stdint.h>
 
 namespace pdt {
-void bn_partial_reduce_launch(const float* part, int tiles, int C, int K, double* scratch, double* sums,
-                              hipStream_t s);
+void bn_slot_sum_launch(const double* slots, int C, int K, double* sums, hipStream_t s);
 void bn_finalize_launch(const double* sums, double count, const float* gamma, const float* beta, float eps,
                         float momentum, float* rm, float* rv, float* coef, int C, bool update_running,
                         hipStream_t s);
@@ -14,7 +13,7 @@ void bn_apply_launch(int dtype, const uint16_t* y, const float* coef, const uint
                      uint16_t* out, int64_t n, int C, int resmode, bool relu, hipStream_t s);
 int bn_bwd_reduce_blocks(int64_t rows, int C);
 void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* coef1,
-                          const uint16_t* y2, const float* coef2, float* part, int blocks, int64_t rows, int C,
+                          const uint16_t* y2, const float* coef2, double* slots, int blocks, int64_t rows, int C,
                           hipStream_t s);
 void bn_bwd_finalize_launch(const double* sums, double count, const float* coef, const float* gamma, float* dgamma,
                             float* dbeta, float gscale, float* bcoef, int C, hipStream_t s);

@@ -1,61 +1,36 @@
 // BatchNorm (+ReLU, +residual) kernels over NHWC 16-bit activations, fp32 math.
 //
-// Training forward:  conv epilogue emits per-M-tile (sum, sumsq) partials
-//                    -> bn_partial_reduce (fp64 per-channel sums; SyncBN all-reduces these)
+// Training forward:  conv epilogue accumulates per-channel (sum, sumsq) into fp64 slot copies
+//                    -> bn_slot_sum (fp64 per-channel sums; SyncBN all-reduces these)
 //                    -> bn_finalize (mean, invstd, folded scale/shift, running-stat update)
 //                    -> bn_apply (y*scale+shift [+ residual | + BN(residual)] -> ReLU)
 // Training backward: bn_bwd_reduce (dz = g * relu'(out); sum dz, sum dz*xhat for up to two BN
 //                    branches that share dz, e.g. the main and downsample branch of a residual block)
-//                    -> bn_partial_reduce -> bn_bwd_finalize (dgamma/dbeta into the grad buffer,
+//                    -> bn_slot_sum -> bn_bwd_finalize (dgamma/dbeta into the grad buffer,
 //                    per-channel coefficients) -> bn_bwd_apply (dy = a*dz + b*y + c per branch).
 #include "../common.h"
 #include "bn.h"
+#include "conv_fwd.h"
 
 namespace pdt {
 
 // -------------------------------------------------------------------------------------------------
-// partials [tiles][C][K] float  ->  out [G][C][K] double (grid.y = G groups of tiles)
-__global__ __launch_bounds__(256) void bn_partial_reduce_kernel(const float* __restrict__ part, int tiles, int C,
-                                                                int K, double* __restrict__ out) {
-  // block: 64 channels x 4 tile-lanes
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int tl = threadIdx.x >> 6;
-  const int G = gridDim.y, g = blockIdx.y;
-  double acc[4] = {0, 0, 0, 0};
-  if (c < C) {
-    for (int t = g * 4 + tl; t < tiles; t += G * 4) {
-      const float* p = part + ((int64_t)t * C + c) * K;
-      for (int k = 0; k < K; ++k) acc[k] += (double)p[k];
-    }
-  }
-  __shared__ double red[4][64][4];
-  for (int k = 0; k < 4; ++k) red[tl][threadIdx.x & 63][k] = acc[k];
-  __syncthreads();
-  if (tl == 0 && c < C) {
-    for (int k = 0; k < K; ++k) {
-      const double s = red[0][threadIdx.x][k] + red[1][threadIdx.x][k] + red[2][threadIdx.x][k] + red[3][threadIdx.x][k];
-      out[((int64_t)g * C + c) * K + k] = s;
-    }
-  }
-}
-
-// [G][C][K] double -> sums[k*C + c] double  (channel-major per quantity, SyncBN message layout)
-__global__ void bn_group_sum_kernel(const double* __restrict__ in, int G, int C, int K, double* __restrict__ sums) {
+// slots [kStatSlots][C][K] double (accumulated by the conv epilogue / bn_bwd_reduce with fp64 atomics)
+//   -> sums[k*C + c] double  (channel-major per quantity: the SyncBN all-reduce message)
+__global__ void bn_slot_sum_kernel(const double* __restrict__ slots, int C, int K, double* __restrict__ sums) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= C * K) return;
   const int c = idx / K, k = idx - (idx / K) * K;
-  double s = 0;
-  for (int g = 0; g < G; ++g) s += in[((int64_t)g * C + c) * K + k];
-  sums[k * C + c] = s;
+  double s0 = 0, s1 = 0;
+  for (int g = 0; g < kStatSlots; g += 2) {
+    s0 += slots[((int64_t)g * C + c) * K + k];
+    s1 += slots[((int64_t)(g + 1) * C + c) * K + k];
+  }
+  sums[k * C + c] = s0 + s1;
 }
 
-void bn_partial_reduce_launch(const float* part, int tiles, int C, int K, double* scratch, double* sums,
-                              hipStream_t s) {
-  int G = (tiles + 255) / 256;
-  if (G > 64) G = 64;
-  if (G < 1) G = 1;
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, s, part, tiles, C, K, scratch);
-  hipLaunchKernelGGL(bn_group_sum_kernel, dim3((C * K + 255) / 256), dim3(256), 0, s, scratch, G, C, K, sums);
+void bn_slot_sum_launch(const double* slots, int C, int K, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(bn_slot_sum_kernel, dim3((C * K + 255) / 256), dim3(256), 0, s, slots, C, K, sums);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -184,7 +159,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ coef1,
                                                             const uint16_t* __restrict__ y2,
                                                             const float* __restrict__ coef2,
-                                                            float* __restrict__ part, int64_t rows, int C) {
+                                                            double* __restrict__ slots, int64_t rows, int C) {
   using E = E16<DT>;
   const int vpr = C / 8;              // 16-byte vectors per row
   const int rpi = 256 / vpr;          // rows per block iteration (C <= 2048)
@@ -240,10 +215,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       for (int k = 0; k < NBR * 2; ++k) red[((int64_t)rl * C + c0 + e) * K + k] = s[k][e];
   }
   __syncthreads();
+  double* dst = slots + (int64_t)(blockIdx.x % kStatSlots) * C * K;
   for (int idx = threadIdx.x; idx < C * K; idx += 256) {
     float t = 0.f;
     for (int r = 0; r < rpi; ++r) t += red[(int64_t)r * C * K + idx];
-    part[(int64_t)blockIdx.x * C * K + idx] = t;
+    atomicAdd(dst + idx, (double)t);
   }
 }
 
@@ -255,16 +231,17 @@ int bn_bwd_reduce_blocks(int64_t rows, int C) {
 }
 
 void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* coef1,
-                          const uint16_t* y2, const float* coef2, float* part, int blocks, int64_t rows, int C,
+                          const uint16_t* y2, const float* coef2, double* slots, int blocks, int64_t rows, int C,
                           hipStream_t s) {
   const int rpi = 256 / (C / 8);
   const int nbr = y2 ? 2 : 1;
+  PDT_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(double) * kStatSlots * C * nbr * 2, s));
   const size_t smem = (size_t)rpi * C * nbr * 2 * sizeof(float);
   const bool mask = out != nullptr;
 #define PDT_BR(DT_, M_, NB_)                                                                              \
   if (mask == M_ && nbr == NB_) {                                                                         \
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<DT_, M_, NB_>), dim3(blocks), dim3(256), smem, s, g, out, y1, \
-                       coef1, y2, coef2, part, rows, C);                                                  \
+                       coef1, y2, coef2, slots, rows, C);                                                  \
     return;                                                                                               \
   }
   if (dtype == kBF16) {

@@ -4,14 +4,17 @@
 
 namespace pdt {
 
+constexpr int kStatSlots = 64;  // slot copies of per-channel statistics accumulators
+
 // Generalised implicit-GEMM convolution (see conv_fwd.hip for the geometry contract).
 struct ConvFwdArgs {
   const uint16_t* x;    // [N][H][W][C] input activations
   const uint16_t* w;    // [Kout][T*U][C] weights (taps already ordered/flipped for the role)
   uint16_t* y;          // [N][OH][OW][Kout] output
   const uint16_t* res;  // optional: residual in y's layout, added before rounding (nullptr = none)
-  float* stats;         // optional: [m_tiles][Kout] float2 (sum, sumsq) BN partials (nullptr = none)
+  double* stats;        // optional: [kStatSlots][Kout][2] fp64 (sum, sumsq) BN statistics (nullptr = none)
   int N, H, W, C, Kout, T, U;
+  int cs;                                              // elements per input pixel (normally == C)
   int Pm, Qm;                                          // GEMM-M sub-grid (M = N*Pm*Qm)
   int ist_h, ist_w, ioff_h, ioff_w, tstep_h, tstep_w;  // in = i*ist + ioff + t*tstep
   int OH, OW, ost_h, ost_w, ooff_h, ooff_w;            // out = i*ost + ooff

@@ -6,6 +6,9 @@
 //                          small stride-1 conv over dY with flipped weights, written to the
 //                          phase's output sub-grid (no MFMA work is wasted on structural zeros)
 //   * linear layers:       a 1x1 "conv" over [B,1,1,K]
+// ``cs`` is the element stride between input pixels (== C, except for the ResNet stem's "window" mode,
+// where X is the zero-padded NHWC4 image and one 32-wide reduction chunk spans 8 pixels x 4 channels
+// of a kernel row, so the 7x7/2 stem runs with no im2col buffer).
 // The generalised geometry is
 //   in_h  = i*ist_h + ioff_h + t*tstep_h      (t in [0,T)),  same for w / u
 //   out_h = i*ost_h + ooff_h
@@ -17,7 +20,8 @@
 // wave-instruction and XOR-swizzled through the SOURCE address (chunk ^= (row>>1)&(chunks-1)), which
 // makes the ds_read_b128 fragment reads bank-conflict free.  Optional epilogues: residual add (used
 // to fuse the identity-gradient add of a residual block into dgrad) and per-channel BatchNorm
-// partial statistics (sum, sum of squares of the rounded outputs) for each M tile.
+// statistics (sum, sum of squares of the rounded outputs), reduced per block and accumulated with
+// fp64 atomics into kStatSlots slot copies (so no separate statistics pass over the output).
 #include "../common.h"
 #include "conv_fwd.h"
 
@@ -79,7 +83,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
       const int i = rem / a.Qm, jj = rem - (rem / a.Qm) * a.Qm;
       brow_h[j] = i * a.ist_h + a.ioff_h;
       brow_w[j] = jj * a.ist_w + a.ioff_w;
-      brow_base[j] = a.x + (int64_t)nimg * a.H * a.W * a.C;
+      brow_base[j] = a.x + (int64_t)nimg * a.H * a.W * a.cs;
     } else {
       brow_h[j] = -(1 << 29);
       brow_w[j] = 0;
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
     for (int j = 0; j < B_INSTR; ++j) {
       const int h = brow_h[j] + dh, w = brow_w[j] + dw;
       const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const uint16_t* src = ok ? brow_base[j] + ((int64_t)h * a.W + w) * a.C + c0 + bchunk[j] * 8
+      const uint16_t* src = ok ? brow_base[j] + ((int64_t)h * a.W + w) * a.cs + c0 + bchunk[j] * 8
                                : (const uint16_t*)g_zero16;
       lds_void* dst = (lds_void*)(sbase + A_BYTES + (wave * B_INSTR + j) * 1024);
       __builtin_amdgcn_global_load_lds((glb_void*)src, dst, 16, 0, 0);
@@ -243,8 +247,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
         s += red[(w * BN + tid) * 2 + 0];
         q += red[(w * BN + tid) * 2 + 1];
       }
-      float2* dst = (float2*)a.stats + (int64_t)tile_m * a.Kout + n0 + tid;
-      *dst = make_float2(s, q);
+      // fp64 atomics into one of kStatSlots copies (by M tile) keep per-address contention low
+      double* dst = a.stats + ((int64_t)(tile_m % kStatSlots) * a.Kout + n0 + tid) * 2;
+      atomicAdd(dst, (double)s);
+      atomicAdd(dst + 1, (double)q);
     }
   }
 }
@@ -285,6 +291,7 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
 }
 
 void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s) {
+  if (a.stats) PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * 2 * kStatSlots * a.Kout, s));
   if (dtype == kBF16)
     launch_dt<kBF16>(a, bm, bn, bk, s);
   else

@@ -13,6 +13,8 @@ struct ConvWgradArgs {
   int stride_h, stride_w, pad_h, pad_w, dil_h, dil_w;
   int P;               // N*Pm*Qm
   int ldw;             // >= T*U*C
+  int cs;              // elements per pixel of x (== C except in window mode)
+  int win;             // stem window mode (see conv_wgrad.hip)
   int splits, pix_per_split;  // filled by conv_wgrad_plan
 };
 

@@ -24,15 +24,13 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 // chunk swizzle for a [pixel][64 ch] (128-B row) image read by ds_read_b64_tr_b16
 PDT_DEVICE int tr_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
-// floor(n / d) for 0 <= n < 2^24 using an fp32 reciprocal + one correction step
-PDT_DEVICE int fdiv(int n, int d, float inv_d) {
-  int q = (int)((float)n * inv_d);
-  int r = n - q * d;
-  q += (r >= d) - (r < 0);
-  return q;
-}
+// floor(n / d) = (n * ceil(2^40 / d)) >> 40, exact for n < 2^24 and d < 2^16 (n*d < 2^40)
+PDT_DEVICE int mdiv(int n, uint64_t magic) { return (int)(((uint64_t)(uint32_t)n * magic) >> 40); }
 
-template <int DT>
+// WIN: the ResNet stem's "window" mode.  X is the zero-padded NHWC4 image and a 64-wide tile column
+// block covers two kernel rows of 8 pixels x 4 channels: chunk ch (8 elements) reads image row
+// (h + (ch >> 2)) at element offset (ch & 3) * 8 -- im2col is never materialised.
+template <int DT, bool WIN>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -52,8 +50,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int k_tiles = a.Kout / 64;
   const int nwg = k_tiles * n_tiles * a.splits;
   const int bid = xcd_remap(blockIdx.x, nwg);
-  const int split = bid % a.splits;
-  const int tile = bid / a.splits;
+  // consecutive blocks (one XCD after the remap) = different tiles of the SAME pixel range, so the
+  // dY / X rows a split streams are fetched from HBM once and re-read from that XCD's L2
+  const int tile = bid % (k_tiles * n_tiles);
+  const int split = bid / (k_tiles * n_tiles);
   const int kt = tile % k_tiles;
   const int nt = tile / k_tiles;
   const int tap = nt / c_tiles;
@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
 
   const int PQ = a.Pm * a.Qm;
-  const float inv_pq = 1.0f / (float)PQ, inv_q = 1.0f / (float)a.Qm;
+  const uint64_t mag_pq = ((1ull << 40) + PQ - 1) / PQ, mag_q = ((1ull << 40) + a.Qm - 1) / a.Qm;
+  const int64_t img_stride = (int64_t)a.H * a.W * a.cs;
 
   // DMA lane geometry: 8 rows x 8 chunks per 1 KiB instruction
   const int lrow = lane >> 3, pch = lane & 7;
@@ -83,14 +84,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       const uint16_t* xs = (const uint16_t*)g_zero16;
       const uint16_t* ys = (const uint16_t*)g_zero16;
       if (p < pix_end) {
-        const int nimg = fdiv(p, PQ, inv_pq);
+        const int nimg = mdiv(p, mag_pq);
         const int rem = p - nimg * PQ;
-        const int i = fdiv(rem, a.Qm, inv_q);
+        const int i = mdiv(rem, mag_q);
         const int jj = rem - i * a.Qm;
         const int h = i * a.stride_h - a.pad_h + t * a.dil_h;
         const int w = jj * a.stride_w - a.pad_w + u * a.dil_w;
-        if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-          xs = a.x + (((int64_t)nimg * a.H + h) * a.W + w) * a.C + c0 + lch * 8;
+        if constexpr (WIN) {
+          xs = a.x + nimg * img_stride + ((int64_t)(h + (lch >> 2)) * a.W + w) * a.cs + (lch & 3) * 8;
+        } else {
+          if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+            xs = a.x + nimg * img_stride + ((int64_t)h * a.W + w) * a.cs + c0 + lch * 8;
+        }
         ys = a.dy + (int64_t)p * a.Kout + k0 + lch * 8;
       }
       __builtin_amdgcn_global_load_lds((glb_void*)xs, (lds_void*)(sb + (wave * 4 + j) * 1024), 16, 0, 0);
@@ -177,18 +182,58 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)
+// Block = 64 float4 column groups x 4 split lanes; each split lane keeps 4 loads in flight.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int rows,
                                                             int cols, int ldw, int64_t split_stride,
                                                             float* __restrict__ out, int ldo, float scale,
                                                             int accumulate) {
+  const int cv = cols / 4;  // cols % 4 == 0 on this path
+  const int64_t nvec = (int64_t)rows * cv;
+  const int64_t v = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sl = threadIdx.x >> 6;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  int r = 0, c = 0;
+  if (v < nvec) {
+    r = (int)(v / cv);
+    c = (int)(v - (int64_t)r * cv) * 4;
+    const float* p = ws + (int64_t)r * ldw + c;
+    int s = sl;
+    for (; s + 12 < splits; s += 16) {
+      const f32x4_t a0 = *(const f32x4_t*)(p + (int64_t)s * split_stride);
+      const f32x4_t a1 = *(const f32x4_t*)(p + (int64_t)(s + 4) * split_stride);
+      const f32x4_t a2 = *(const f32x4_t*)(p + (int64_t)(s + 8) * split_stride);
+      const f32x4_t a3 = *(const f32x4_t*)(p + (int64_t)(s + 12) * split_stride);
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; s < splits; s += 4) acc += *(const f32x4_t*)(p + (int64_t)s * split_stride);
+  }
+  __shared__ f32x4_t red[4][64];
+  red[sl][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (sl == 0 && v < nvec) {
+    const int t = threadIdx.x;
+    const f32x4_t sum = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    float* o = out + (int64_t)r * ldo + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = accumulate ? (o[e] + scale * sum[e]) : scale * sum[e];
+  }
+}
+
+// scalar fallback for column counts that are not a multiple of 4 (e.g. the 147-wide stem)
+__global__ __launch_bounds__(256) void wgrad_reduce_scalar_kernel(const float* __restrict__ ws, int splits, int rows,
+                                                                   int cols, int ldw, int64_t split_stride,
+                                                                   float* __restrict__ out, int ldo, float scale,
+                                                                   int accumulate) {
   const int64_t n = (int64_t)rows * cols;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * 256) {
     const int r = (int)(idx / cols), c = (int)(idx - (int64_t)(idx / cols) * cols);
     const float* p = ws + (int64_t)r * ldw + c;
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += p[k * split_stride];
+    float s0 = 0.f, s1 = 0.f;
+    int k = 0;
+    for (; k + 1 < splits; k += 2) { s0 += p[k * split_stride]; s1 += p[(k + 1) * split_stride]; }
+    if (k < splits) s0 += p[k * split_stride];
     float* o = out + (int64_t)r * ldo + c;
-    *o = accumulate ? (*o + scale * s) : scale * s;
+    *o = accumulate ? (*o + scale * (s0 + s1)) : scale * (s0 + s1);
   }
 }
 
@@ -207,20 +252,34 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
 void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s) {
   const int nwg = (a.Kout / 64) * a.T * a.U * (a.C / 64) * a.splits;
   if (nwg == 0) return;
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(conv_wgrad_kernel<kBF16>, dim3(nwg), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(conv_wgrad_kernel<kF16>, dim3(nwg), dim3(256), 0, s, a);
+  if (a.win) {
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, true>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_kernel<kF16, true>), dim3(nwg), dim3(256), 0, s, a);
+  } else {
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, false>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_kernel<kF16, false>), dim3(nwg), dim3(256), 0, s, a);
+  }
 }
 
 void wgrad_reduce_launch(const float* ws, int splits, int rows, int cols, int ldw, int64_t split_stride,
                          float* out, int ldo, float scale, bool accumulate, hipStream_t s) {
-  const int64_t n = (int64_t)rows * cols;
-  int blocks = (int)((n + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  if (blocks == 0) return;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, splits, rows, cols, ldw,
-                     split_stride, out, ldo, scale, (int)accumulate);
+  if ((int64_t)rows * cols == 0) return;
+  const bool vec = (cols % 4 == 0) && (ldw % 4 == 0) && (ldo % 4 == 0) && (split_stride % 4 == 0) &&
+                   ((uintptr_t)ws % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (vec) {
+    const int64_t nvec = (int64_t)rows * (cols / 4);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nvec + 63) / 64)), dim3(256), 0, s, ws, splits, rows,
+                       cols, ldw, split_stride, out, ldo, scale, (int)accumulate);
+  } else {
+    int64_t blocks = ((int64_t)rows * cols + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(wgrad_reduce_scalar_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, splits, rows, cols,
+                       ldw, split_stride, out, ldo, scale, (int)accumulate);
+  }
 }
 
 }  // namespace pdt

@@ -12,4 +12,7 @@ void amp_update_launch(float* scale, int* tracker, float* found_inf, float growt
 void gather16_launch(const uint16_t* src, const int* idx, uint16_t* dst, int64_t n, hipStream_t s);
 void im2col_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H, int W, int R, int S, int stride, int pad,
                    int ldk, hipStream_t s);
+void stem_pack_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp, int Wp,
+                      hipStream_t s);
+void gather32_launch(const float* src, const int* idx, float* dst, int64_t n, hipStream_t s);
 }  // namespace pdt

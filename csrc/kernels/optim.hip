@@ -173,4 +173,50 @@ void im2col_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H
                        OH, OW, ldk);
 }
 
+// Stem input: fp32 NCHW image batch -> zero-padded 16-bit NHWC4 image [N][H+2p][W+2p+ex][4]
+// (channel 3 and the border are zero).  The stem conv then reads 8-pixel x 4-channel windows of it
+// directly (window mode of conv_fwd / conv_wgrad): no im2col matrix.
+template <int DT>
+__global__ __launch_bounds__(256) void stem_pack_kernel(const float* __restrict__ x, uint16_t* __restrict__ out, int N,
+                                                        int C, int H, int W, int pad, int Hp, int Wp) {
+  using E = E16<DT>;
+  const int64_t total = (int64_t)N * Hp * Wp;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int wp = (int)(v % Wp);
+    const int64_t t = v / Wp;
+    const int hp = (int)(t % Hp);
+    const int n = (int)(t / Hp);
+    const int h = hp - pad, w = wp - pad;
+    uint16_t o[4] = {0, 0, 0, 0};
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+      for (int c = 0; c < C && c < 4; ++c) o[c] = E::from_f(x[(((int64_t)n * C + c) * H + h) * W + w]);
+    }
+    uint2 q;
+    q.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    q.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+    *(uint2*)(out + v * 4) = q;
+  }
+}
+
+void stem_pack_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp, int Wp,
+                      hipStream_t s) {
+  const int64_t total = (int64_t)N * Hp * Wp;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(stem_pack_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W, pad, Hp, Wp);
+  else
+    hipLaunchKernelGGL(stem_pack_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W, pad, Hp, Wp);
+}
+
+__global__ __launch_bounds__(256) void gather32_kernel(const float* __restrict__ src, const int* __restrict__ idx,
+                                                       float* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int j = idx[i];
+    dst[i] = j >= 0 ? src[j] : 0.f;
+  }
+}
+
+void gather32_launch(const float* src, const int* idx, float* dst, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(gather32_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, src, idx, dst, n);
+}
+
 }  // namespace pdt

@@ -1,0 +1,140 @@
+"""Data pipeline assembly (reference C16-C18: ImageFolder + transforms, DistributedSampler,
+``DataLoader(batch, num_workers=-j, pin_memory=True)``; `distributed.py:157-179`).
+
+GPU-side additions:
+* :class:`DevicePrefetcher` copies the next batch host->device on a side HIP stream while the current
+  step runs (the reference's ``.cuda(non_blocking=True)`` happens on the compute stream);
+* :class:`DeviceSyntheticLoader` produces synthetic ImageNet-shaped batches directly in HBM (no PCIe
+  traffic, no CPU decode), with the same per-rank sample counts as the distributed sampler.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+from torch.utils.data import DataLoader
+
+from .datasets import ImageFolder, SyntheticImageNet
+from .sampler import DistributedSampler
+from .transforms import train_transform, val_transform
+
+
+class DeviceSyntheticLoader:
+    """Synthetic batches generated on the device.
+
+    ``len()`` and the last-batch size follow ``DistributedSampler(n) + DataLoader(batch)``; the
+    contents come from a small pool of distinct device-resident batches (deterministic in the seed).
+    """
+
+    def __init__(self, n_samples: int, batch_size: int, world: int, rank: int, device, image_size: int = 224,
+                 num_classes: int = 1000, seed: int = 0, pool: int = 4):
+        self.num_samples = math.ceil(n_samples / world)
+        self.batch_size = batch_size
+        self.device = torch.device(device)
+        self.image_size = image_size
+        self.num_classes = num_classes
+        self.seed = seed + 7919 * rank
+        self.pool_n = pool
+        self.epoch = 0
+        self._pool = None
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = epoch
+
+    def __len__(self) -> int:
+        return math.ceil(self.num_samples / self.batch_size)
+
+    def _make_pool(self):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(self.seed)
+        bs = min(self.batch_size, self.num_samples)
+        self._pool = [(torch.randn(bs, 3, self.image_size, self.image_size, device=self.device, generator=g),
+                       torch.randint(0, self.num_classes, (bs,), device=self.device, generator=g))
+                      for _ in range(self.pool_n)]
+
+    def __iter__(self):
+        if self._pool is None:
+            self._make_pool()
+        n = len(self)
+        for i in range(n):
+            x, t = self._pool[(i + self.epoch) % self.pool_n]
+            bs = min(self.batch_size, self.num_samples - i * self.batch_size)
+            yield (x[:bs], t[:bs]) if bs < x.shape[0] else (x, t)
+
+
+class DevicePrefetcher:
+    """Wrap a host DataLoader: batch i+1 is copied to the device on a side stream during step i."""
+
+    def __init__(self, loader, device):
+        self.loader = loader
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(device=self.device)
+
+    def __len__(self) -> int:
+        return len(self.loader)
+
+    @property
+    def sampler(self):
+        return getattr(self.loader, "sampler", None)
+
+    def _copy(self, batch):
+        x, t = batch
+        with torch.cuda.stream(self.stream):
+            return x.to(self.device, non_blocking=True), t.to(self.device, non_blocking=True)
+
+    def __iter__(self):
+        it = iter(self.loader)
+        try:
+            nxt = self._copy(next(it))
+        except StopIteration:
+            return
+        cur_stream = torch.cuda.current_stream(self.device)
+        while nxt is not None:
+            cur_stream.wait_stream(self.stream)
+            x, t = nxt
+            x.record_stream(cur_stream)
+            t.record_stream(cur_stream)
+            try:
+                nxt = self._copy(next(it))
+            except StopIteration:
+                nxt = None
+            yield x, t
+
+
+def build_loaders(args, world: int, rank: int, device, distributed: bool, batch_size: int):
+    """Returns ``(train_loader, val_loader, train_sampler, val_sampler)``.
+
+    ``batch_size`` is the per-process batch (the reference divides the node-total ``-b`` by the
+    process count for DDP, `distributed.py:143`; DataParallel uses the node-total batch)."""
+    device = torch.device(device)
+    on_gpu = device.type == "cuda"
+    if args.synthetic and on_gpu:
+        tr = DeviceSyntheticLoader(args.synthetic_train_size, batch_size, world, rank, device, args.image_size,
+                                   args.num_classes, seed=args.seed or 0)
+        va = DeviceSyntheticLoader(args.synthetic_val_size, batch_size, world, rank, device, args.image_size,
+                                   args.num_classes, seed=(args.seed or 0) + 1, pool=2)
+        return tr, va, tr, va
+    if args.synthetic:
+        train_ds = SyntheticImageNet(args.synthetic_train_size, args.image_size, args.num_classes, seed=0)
+        val_ds = SyntheticImageNet(args.synthetic_val_size, args.image_size, args.num_classes, seed=1)
+    else:
+        train_ds = ImageFolder(os.path.join(args.data, "train"), train_transform(args.image_size))
+        val_ds = ImageFolder(os.path.join(args.data, "val"), val_transform(args.image_size))
+    if distributed:
+        train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
+        val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank)
+        train_loader = DataLoader(train_ds, batch_size=batch_size, num_workers=args.workers, pin_memory=on_gpu,
+                                  sampler=train_sampler, persistent_workers=args.workers > 0)
+        val_loader = DataLoader(val_ds, batch_size=batch_size, num_workers=args.workers, pin_memory=on_gpu,
+                                sampler=val_sampler, persistent_workers=args.workers > 0)
+    else:
+        train_sampler = val_sampler = None
+        train_loader = DataLoader(train_ds, batch_size=batch_size, shuffle=True, num_workers=args.workers,
+                                  pin_memory=on_gpu, persistent_workers=args.workers > 0)
+        val_loader = DataLoader(val_ds, batch_size=batch_size, shuffle=False, num_workers=args.workers,
+                                pin_memory=on_gpu, persistent_workers=args.workers > 0)
+    if on_gpu:
+        train_loader, val_loader = DevicePrefetcher(train_loader, device), DevicePrefetcher(val_loader, device)
+    return train_loader, val_loader, train_sampler, val_sampler

@@ -1,0 +1,154 @@
+"""Image transforms with torchvision semantics (torchvision is not installed here).
+
+Reference pipelines (`dataparallel.py:133-151`):
+  train: RandomResizedCrop(224) -> RandomHorizontalFlip() -> ToTensor() -> Normalize(mean, std)
+  val:   Resize(256) -> CenterCrop(224) -> ToTensor() -> Normalize(mean, std)
+
+Implemented on PIL images + numpy; random draws use ``torch``'s global RNG exactly like
+torchvision (``torch.empty(1).uniform_``, ``torch.randint``, ``torch.rand``), so a seeded run draws
+the same crop boxes.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import torch
+from PIL import Image
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+class Compose:
+    def __init__(self, transforms: Sequence):
+        self.transforms = list(transforms)
+
+    def __call__(self, x):
+        for t in self.transforms:
+            x = t(x)
+        return x
+
+
+def _size(img: Image.Image) -> Tuple[int, int]:
+    return img.size  # (w, h)
+
+
+class Resize:
+    """Resize the shorter side to ``size`` (int) keeping the aspect ratio, bilinear."""
+
+    def __init__(self, size, interpolation=Image.BILINEAR):
+        self.size = size
+        self.interpolation = interpolation
+
+    def __call__(self, img: Image.Image) -> Image.Image:
+        if isinstance(self.size, (tuple, list)):
+            h, w = self.size
+            return img.resize((w, h), self.interpolation)
+        w, h = _size(img)
+        short, long_ = (w, h) if w <= h else (h, w)
+        if short == self.size:
+            return img
+        new_short, new_long = self.size, int(self.size * long_ / short)
+        nw, nh = (new_short, new_long) if w <= h else (new_long, new_short)
+        return img.resize((nw, nh), self.interpolation)
+
+
+class CenterCrop:
+    def __init__(self, size):
+        self.size = (size, size) if isinstance(size, int) else tuple(size)
+
+    def __call__(self, img: Image.Image) -> Image.Image:
+        w, h = _size(img)
+        th, tw = self.size
+        if tw > w or th > h:  # pad like torchvision, then crop
+            pad_img = Image.new(img.mode, (max(w, tw), max(h, th)))
+            pad_img.paste(img, ((max(w, tw) - w) // 2, (max(h, th) - h) // 2))
+            img = pad_img
+            w, h = _size(img)
+        top = int(round((h - th) / 2.0))
+        left = int(round((w - tw) / 2.0))
+        return img.crop((left, top, left + tw, top + th))
+
+
+class RandomResizedCrop:
+    def __init__(self, size, scale=(0.08, 1.0), ratio=(3.0 / 4.0, 4.0 / 3.0), interpolation=Image.BILINEAR):
+        self.size = (size, size) if isinstance(size, int) else tuple(size)
+        self.scale = scale
+        self.ratio = ratio
+        self.interpolation = interpolation
+
+    @staticmethod
+    def get_params(img: Image.Image, scale, ratio):
+        width, height = _size(img)
+        area = height * width
+        log_ratio = torch.log(torch.tensor(ratio))
+        for _ in range(10):
+            target_area = area * torch.empty(1).uniform_(scale[0], scale[1]).item()
+            aspect_ratio = torch.exp(torch.empty(1).uniform_(log_ratio[0], log_ratio[1])).item()
+            w = int(round(math.sqrt(target_area * aspect_ratio)))
+            h = int(round(math.sqrt(target_area / aspect_ratio)))
+            if 0 < w <= width and 0 < h <= height:
+                i = torch.randint(0, height - h + 1, size=(1,)).item()
+                j = torch.randint(0, width - w + 1, size=(1,)).item()
+                return i, j, h, w
+        in_ratio = float(width) / float(height)
+        if in_ratio < min(ratio):
+            w = width
+            h = int(round(w / min(ratio)))
+        elif in_ratio > max(ratio):
+            h = height
+            w = int(round(h * max(ratio)))
+        else:
+            w, h = width, height
+        return (height - h) // 2, (width - w) // 2, h, w
+
+    def __call__(self, img: Image.Image) -> Image.Image:
+        i, j, h, w = self.get_params(img, self.scale, self.ratio)
+        th, tw = self.size
+        return img.crop((j, i, j + w, i + h)).resize((tw, th), self.interpolation)
+
+
+class RandomHorizontalFlip:
+    def __init__(self, p: float = 0.5):
+        self.p = p
+
+    def __call__(self, img: Image.Image) -> Image.Image:
+        if torch.rand(1).item() < self.p:
+            return img.transpose(Image.FLIP_LEFT_RIGHT)
+        return img
+
+
+class ToTensor:
+    """HWC uint8 PIL image -> CHW float32 tensor in [0, 1]."""
+
+    def __call__(self, img: Image.Image) -> torch.Tensor:
+        arr = np.asarray(img.convert("RGB"), dtype=np.uint8)
+        return torch.from_numpy(arr.copy()).permute(2, 0, 1).float().div_(255.0)
+
+
+class ToUint8Tensor:
+    """HWC uint8 PIL image -> CHW uint8 tensor (normalisation then happens on the GPU)."""
+
+    def __call__(self, img: Image.Image) -> torch.Tensor:
+        arr = np.asarray(img.convert("RGB"), dtype=np.uint8)
+        return torch.from_numpy(arr.copy()).permute(2, 0, 1).contiguous()
+
+
+class Normalize:
+    def __init__(self, mean: List[float], std: List[float]):
+        self.mean = torch.tensor(mean).view(-1, 1, 1)
+        self.std = torch.tensor(std).view(-1, 1, 1)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return (t - self.mean) / self.std
+
+
+def train_transform(image_size: int = 224) -> Compose:
+    return Compose([RandomResizedCrop(image_size), RandomHorizontalFlip(), ToTensor(),
+                    Normalize(IMAGENET_MEAN, IMAGENET_STD)])
+
+
+def val_transform(image_size: int = 224, resize: int = 256) -> Compose:
+    return Compose([Resize(resize), CenterCrop(image_size), ToTensor(), Normalize(IMAGENET_MEAN, IMAGENET_STD)])

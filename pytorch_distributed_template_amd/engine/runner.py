@@ -1,0 +1,306 @@
+"""Experiment driver: CLI -> distributed setup -> model/trainer -> epoch loop.
+
+Reference: ``main``/``main_worker``/``train``/``validate`` of `dataparallel.py:76-281`,
+`distributed.py:85-334` and `distributed_syncBN_amp.py:88-349`.  One implementation serves the three
+entry scripts (``mode`` = ``dp`` | ``ddp`` | ``ddp_amp``); log lines, TensorBoard tags, output files
+and checkpoint schema are the reference's.
+
+Per-iteration cross-rank metrics: the reference does ``barrier`` + two scalar all-reduces + ``.item()``
+every iteration (`distributed.py:253-257`).  Here the trainer returns ``[loss, acc]`` already averaged
+over ranks by ONE all-reduce, accumulated on device, and read on the host only at print iterations
+(``--strict-sync`` restores the per-iteration barrier and host read for timing parity).
+The printed running averages are identical either way.
+"""
+from __future__ import annotations
+
+import os
+import random
+import time
+import warnings
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import cli
+from ..data.loader import build_loaders
+from ..models import registry
+from ..optim.lr import build_scheduler
+from ..utils.io import load_checkpoint, make_checkpoint_state, output_process, save_checkpoint, write_settings
+from ..utils.logging import close_logger, ddp_print, get_logger
+from ..utils.meters import AverageMeter, get_learning_rate
+from ..utils.tensorboard import SummaryWriter
+
+NATIVE_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2")
+
+
+def seed_everything(seed: int) -> None:
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+def resolve_precision(args, device: torch.device) -> torch.dtype:
+    p = args.precision
+    if p == "auto":
+        if device.type != "cuda":
+            p = "fp32"
+        elif getattr(args, "use_amp", False):
+            p = "fp16"
+        else:
+            p = "bf16"
+    return {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[p]
+
+
+def resolve_engine(args, device: torch.device, dtype: torch.dtype) -> str:
+    e = args.engine
+    native_ok = device.type == "cuda" and args.arch in NATIVE_ARCHS and dtype in (torch.bfloat16, torch.float16)
+    if e == "auto":
+        return "native" if native_ok else "torch"
+    if e == "native" and not native_ok:
+        raise ValueError(f"--engine native needs a GPU, a supported arch ({', '.join(NATIVE_ARCHS)}) and "
+                         f"bf16/fp16 precision (got device={device.type}, arch={args.arch}, dtype={dtype})")
+    return e
+
+
+class _DeviceMeter:
+    """Batch-size weighted running mean of the device-side [loss, acc] pair without host syncs."""
+
+    def __init__(self, device):
+        self.sum = torch.zeros(2, dtype=torch.float64, device=device)
+        self.count = 0
+
+    def update(self, met: torch.Tensor, n: int) -> None:
+        self.sum += met.double() * n
+        self.count += n
+
+    def avg(self):
+        if self.count == 0:
+            return 0.0, 0.0
+        a = (self.sum / self.count).tolist()
+        return a[0], a[1]
+
+
+def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, device):
+    batch_times = AverageMeter("Time", ":6.3f")
+    data_times = AverageMeter("Data", ":6.3f")
+    meter = _DeviceMeter(device)
+    n_iter = len(loader)
+    if args.iters_per_epoch:
+        n_iter = min(n_iter, args.iters_per_epoch)
+    lr = get_learning_rate(trainer.optimizer)
+    end = time.time()
+    for i, (images, target) in enumerate(loader):
+        if i >= n_iter:
+            break
+        data_times.update(time.time() - end)
+        images = images.to(device, non_blocking=True)
+        target = target.to(device, non_blocking=True)
+        _, met = trainer.train_step(images, target)
+        meter.update(met, images.size(0))
+        if args.strict_sync:
+            if dist.is_initialized():
+                dist.barrier()
+            met.tolist()
+        batch_times.update(time.time() - end)
+        end = time.time()
+        if i % args.print_freq == 0:
+            loss_avg, acc_avg = meter.avg()
+            ddp_print("Train epoch: [{:d}/{:d}][{:d}/{:d}]\tlr={:.6f}\tce_loss={:.4f}\ttop1_acc={:.4f}\tdata_time={:6.3f}s"
+                      "\tbatch_time={:6.3f}s".format(epoch, args.epochs, i, n_iter, lr, loss_avg, acc_avg,
+                                                     data_times.avg, batch_times.avg), logger, rank)
+    loss_avg, acc_avg = meter.avg()
+    ddp_print("||==> Train epoch: [{:d}/{:d}]\tlr={:.6f}\tce_loss={:.4f}\ttop1_acc={:.4f}\tbatch_time={:6.3f}s"
+              .format(epoch, args.epochs, lr, loss_avg, acc_avg, batch_times.avg), logger, rank)
+    if rank == 0 and writer is not None:
+        writer.add_scalar("lr", lr, epoch)
+        writer.add_scalar("Train_ce_loss", loss_avg, epoch)
+        writer.add_scalar("Train_top1_accuracy", acc_avg, epoch)
+    return loss_avg, acc_avg
+
+
+def validate(loader, trainer, epoch: int, args, logger, writer, rank: int, device) -> float:
+    batch_times = AverageMeter("Time", ":6.3f")
+    meter = _DeviceMeter(device)
+    n_iter = len(loader)
+    if args.val_iters:
+        n_iter = min(n_iter, args.val_iters)
+    end = time.time()
+    with torch.no_grad():
+        for i, (images, target) in enumerate(loader):
+            if i >= n_iter:
+                break
+            images = images.to(device, non_blocking=True)
+            target = target.to(device, non_blocking=True)
+            _, met = trainer.eval_step(images, target)
+            meter.update(met, images.size(0))
+            if args.strict_sync:
+                if dist.is_initialized():
+                    dist.barrier()
+                met.tolist()
+            batch_times.update(time.time() - end)
+            end = time.time()
+            if i % args.print_freq == 0:
+                loss_avg, acc_avg = meter.avg()
+                ddp_print("Val epoch: [{:d}/{:d}][{:d}/{:d}]\tce_loss={:.4f}\ttop1_acc={:.4f}\tbatch_time={:6.3f}s"
+                          .format(epoch, args.epochs, i, n_iter, loss_avg, acc_avg, batch_times.avg), logger, rank)
+    loss_avg, acc_avg = meter.avg()
+    ddp_print("||==> Val epoch: [{:d}/{:d}]\tce_loss={:.4f}\ttop1_acc={:.4f}\tbatch_time={:6.3f}s"
+              .format(epoch, args.epochs, loss_avg, acc_avg, batch_times.avg), logger, rank)
+    if rank == 0 and writer is not None:
+        writer.add_scalar("Val_ce_loss", loss_avg, epoch)
+        writer.add_scalar("Val_top1_accuracy", acc_avg, epoch)
+    return acc_avg
+
+
+def _dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    return world, rank
+
+
+def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int):
+    use_amp = bool(getattr(args, "use_amp", False)) and dtype == torch.float16
+    sync_bn = bool(getattr(args, "sync_batchnorm", False))
+    common = dict(lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    if mode == "dp":
+        if engine == "native":
+            from ..parallel.dp import NativeDataParallelTrainer
+            ids = list(range(torch.cuda.device_count()))
+            return NativeDataParallelTrainer(model, ids, dtype=dtype, use_amp=use_amp, **common)
+        from .torch_trainer import TorchTrainer
+        return TorchTrainer(model, device, dtype=dtype, use_amp=use_amp, **common)
+    kw = dict(common, use_amp=use_amp, sync_bn=sync_bn, bucket_cap_mb=args.bucket_cap_mb,
+              first_bucket_mb=args.first_bucket_mb)
+    if engine == "native":
+        from .native_trainer import NativeTrainer
+        return NativeTrainer(model, device, dtype=dtype, **kw)
+    from .torch_trainer import TorchTrainer
+    return TorchTrainer(model, device, dtype=dtype, **kw)
+
+
+def main(mode: str, argv: Optional[list] = None) -> int:
+    args = cli.parse_args(mode, argv)
+    if args.use_gpus_flag and "HIP_VISIBLE_DEVICES" not in os.environ:
+        os.environ["HIP_VISIBLE_DEVICES"] = args.gpus
+    if args.seed is not None:
+        seed_everything(args.seed)
+        warnings.warn("You have chosen to seed training. Kernel selection is deterministic in this framework "
+                      "(no autotuning), so seeded runs are reproducible.")
+    args.outpath = args.outpath + "_" + args.arch
+    world, rank = (1, 0) if mode == "dp" else _dist_env()
+    local_rank = getattr(args, "local_rank", 0) if mode != "dp" else 0
+    if mode != "dp":
+        local_rank = int(os.environ.get("LOCAL_RANK", local_rank))
+        args.local_rank = local_rank
+    logger = writer = None
+    if rank == 0:
+        output_process(args.outpath, args.exist_policy)
+        logger = get_logger(args.outpath, cli.ENTRY_DEFAULTS[mode]["logger"])
+        if args.tensorboard:
+            writer = SummaryWriter(args.outpath)
+
+    on_gpu = torch.cuda.is_available()
+    distributed = mode != "dp" and world > 1
+    if on_gpu:
+        torch.cuda.set_device(local_rank if mode != "dp" else 0)
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    if distributed:
+        backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if on_gpu else "gloo")
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=device)
+        else:
+            dist.init_process_group(backend)
+    args.nprocs = world if mode != "dp" else max(1, torch.cuda.device_count() if on_gpu else 1)
+
+    if rank == 0:
+        write_settings(args)
+        logger.info(args)
+
+    if args.pretrained:
+        ddp_print("=> using pre-trained model: {}".format(args.arch), logger, rank)
+    else:
+        ddp_print("=> creating model: {}".format(args.arch), logger, rank)
+    model = registry.create(args.arch, pretrained=args.pretrained, pretrained_path=args.pretrained_path,
+                            num_classes=args.num_classes)
+    if mode == "ddp_amp":
+        if distributed and args.sync_batchnorm:
+            ddp_print("=> using sync BN", logger, rank)
+        else:
+            ddp_print("=> not use sync BN", logger, rank)
+    if mode != "dp":
+        args.batch_size = int(args.batch_size / args.nprocs)
+
+    dtype = resolve_precision(args, device)
+    engine = resolve_engine(args, device, dtype)
+    ddp_print("=> engine: {} | compute dtype: {} | device: {} | world: {}".format(engine, str(dtype).split(".")[-1],
+                                                                                device, world), logger, rank)
+    trainer = build_trainer(mode, model, args, device, dtype, engine, world)
+    optimizer = trainer.optimizer
+    lr_scheduler = build_scheduler(args.lr_scheduler, optimizer, args.step, args.gamma)
+    ddp_print("lr_scheduler: SGD MultiStepLR !!!", logger, rank)
+
+    train_loader, val_loader, train_sampler, val_sampler = build_loaders(args, world, rank, device, distributed,
+                                                                         args.batch_size)
+    best_acc1, best_acc1_index = 0.0, 0
+    start_epoch = args.start_epoch
+    if args.resume:
+        ck = load_checkpoint(args.resume)
+        trainer.model.load_state_dict(ck["state_dict"])
+        trainer.flat.refresh_shadow()
+        if hasattr(trainer, "executor"):
+            trainer.executor.update_derived()
+        if "optimizer" in ck:
+            optimizer.load_state_dict(ck["optimizer"])
+        if "scaler" in ck:
+            trainer.scaler.load_state_dict(ck["scaler"])
+        start_epoch = int(ck["epoch"])
+        best_acc1 = float(ck.get("best_acc1", 0.0))
+        best_acc1_index = int(ck.get("best_acc1_index", 0))
+        ddp_print("=> resumed from {} (epoch {})".format(args.resume, start_epoch), logger, rank)
+
+    if args.evaluate:
+        validate(val_loader, trainer, -1, args, logger, writer, rank, device)
+        _finish(writer, logger, distributed)
+        return 0
+
+    total_start = time.time()
+    for epoch in range(start_epoch, args.epochs):
+        if train_sampler is not None:
+            train_sampler.set_epoch(epoch)
+        if val_sampler is not None:
+            val_sampler.set_epoch(epoch)
+        epoch_start = time.time()
+        lr_scheduler.step(epoch)
+        train_epoch(train_loader, trainer, epoch, args, logger, writer, rank, device)
+        acc1 = validate(val_loader, trainer, epoch, args, logger, writer, rank, device)
+        is_best = acc1 > best_acc1
+        if is_best:
+            best_acc1_index = epoch
+            best_acc1 = acc1
+        epoch_end = time.time()
+        ddp_print("||==> Epoch=[{:d}/{:d}]\tbest_acc1={:.4f}\tbest_acc1_index={}\ttime_cost={:.4f}s"
+                  .format(epoch, args.epochs, best_acc1, best_acc1_index, epoch_end - epoch_start), logger, rank)
+        if rank == 0:
+            save_checkpoint(make_checkpoint_state(epoch + 1, args.arch, trainer.model, best_acc1, optimizer,
+                                                  trainer.scaler, lr_scheduler,
+                                                  extra={"best_acc1_index": best_acc1_index}),
+                            is_best, args.outpath)
+    total_end = time.time()
+    ddp_print("||==> total_time_cost={:.4f}s".format(total_end - total_start), logger, rank)
+    _finish(writer, logger, distributed)
+    return 0
+
+
+def _finish(writer, logger, distributed: bool) -> None:
+    if writer is not None:
+        writer.close()
+    close_logger(logger)
+    if distributed and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()

@@ -1,0 +1,97 @@
+"""Training step on stock PyTorch ops ("torch engine").
+
+This is the CPU reference execution path (BASELINE config 1, the numerics oracle of
+the tests) and the explicit ``--engine torch`` choice for architectures the native executor does not
+cover.  It shares everything else with the native path: the flat parameter/gradient storage, the
+gradient bucketer (here driven by autograd post-accumulate hooks), the fused-SGD semantics, the
+device-side loss scaler and the cross-rank metric reduction -- so DDP/SyncBN/AMP logic is exercised
+on CPU with the ``gloo`` backend exactly as on GPU with RCCL.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..amp.scaler import DeviceGradScaler
+from ..optim.flat import FlatBuffers, FlatParams
+from ..optim.sgd import FusedSGD
+from ..parallel.ddp import GradBucketer, broadcast_parameters, sync_buffers
+from ..parallel.syncbn import SyncBatchNorm
+from ..utils.meters import accuracy
+
+
+class TorchTrainer:
+    def __init__(self, model: nn.Module, device, dtype: torch.dtype = torch.float32, lr: float = 0.1,
+                 momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
+                 bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
+                 process_group=None, reduce_metrics: bool = True, channels_last: bool = True):
+        self.device = torch.device(device)
+        self.pg = process_group
+        self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
+        self.world = dist.get_world_size(process_group) if self.distributed else 1
+        if sync_bn and self.distributed:
+            model = SyncBatchNorm.convert_sync_batchnorm(model, process_group)
+        model = model.to(self.device)
+        if channels_last and self.device.type == "cuda":
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
+        self.dtype = dtype
+        self.flat = FlatParams(model, self.device, None)
+        self.buffers = FlatBuffers(model, self.device)
+        broadcast_parameters(self.flat, self.buffers, process_group)
+        self.bucketer = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
+        self.bucketer.register_autograd_hooks()
+        self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
+        self.scaler = DeviceGradScaler(self.device, enabled=use_amp and dtype == torch.float16)
+        self.broadcast_buffers = broadcast_buffers and self.distributed
+        self.reduce_metrics = reduce_metrics and self.distributed
+        self._steps = 0
+
+    def _autocast(self):
+        if self.dtype == torch.float32:
+            return contextlib.nullcontext()
+        return torch.autocast(self.device.type, dtype=self.dtype)
+
+    def _reduce(self, met):
+        if self.reduce_metrics:
+            dist.all_reduce(met, group=self.pg)
+            met.div_(self.world)
+        return met
+
+    def _inputs(self, images):
+        if self.device.type == "cuda":
+            images = images.contiguous(memory_format=torch.channels_last)
+        return images
+
+    def train_step(self, images, target):
+        self.model.train()
+        if self.broadcast_buffers and self._steps > 0:
+            sync_buffers(self.buffers, self.pg)
+        self.optimizer.zero_grad()
+        with self._autocast():
+            out = self.model(self._inputs(images))
+            loss = F.cross_entropy(out.float(), target)
+        acc = accuracy(out.detach().float(), target, 1)
+        met = self._reduce(torch.stack([loss.detach().float(), acc.float()]))
+        scale = self.scaler.scale_tensor
+        (loss * scale if scale is not None else loss).backward()
+        self.bucketer.finish()
+        self.scaler.unscale_check(self.flat.grad)
+        self.optimizer.step(grad_scale=self.bucketer.grad_scale(), loss_scale=scale, found_inf=self.scaler.found_inf)
+        self.scaler.update()
+        self._steps += 1
+        return out.detach().float(), met
+
+    @torch.no_grad()
+    def eval_step(self, images, target):
+        self.model.eval()
+        if self.broadcast_buffers and self._steps > 0:
+            sync_buffers(self.buffers, self.pg)
+        out = self.model(self._inputs(images)).float()  # validation runs without autocast (`:316-317`)
+        loss = F.cross_entropy(out, target)
+        acc = accuracy(out, target, 1)
+        return out, self._reduce(torch.stack([loss.float(), acc.float()]))

@@ -78,12 +78,13 @@ class ResNetExecutor:
 
     def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None,
-                 syncbn_group=None, wgrad_blocks: int = 2048):
+                 syncbn_group=None, wgrad_blocks: int = 512):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not isinstance(model, ResNet) or model.groups != 1:
             raise NotImplementedError("native executor supports torchvision-style ResNets with groups=1")
         self.C = native.C
+        self.n_slots = self.C.stat_slots()
         self.model = model
         self.flat = flat
         self.device = torch.device(device)
@@ -114,16 +115,27 @@ class ResNetExecutor:
                     d["ds_conv"] = None
                     d["ds_bn"] = None
                 self.blocks.append(d)
-        # stem weight as a padded [64][KP] matrix over the im2col columns (k = (r*7+s)*3+c)
+        # stem weight in "window" layout [Cout][R][32]: column j = s*4 + c of kernel row r (s < 7, c < 3),
+        # matching 8-pixel x 4-channel windows of the zero-padded NHWC4 image (no im2col)
         st = self.stem
-        self.stem_k = st.R * st.S * st.cin
-        self.stem_kp = (self.stem_k + 63) // 64 * 64
-        k = torch.arange(st.cout).view(-1, 1)
-        j = torch.arange(self.stem_kp).view(1, -1)
-        m = torch.where(j < self.stem_k, st.slot.offset + k * self.stem_k + j, torch.full_like(j, -1))
+        assert st.cin <= 4 and st.S <= 8, "window-mode stem needs Cin <= 4 and kernel width <= 8"
+        k = torch.arange(st.cout).view(-1, 1, 1)
+        r = torch.arange(st.R).view(1, -1, 1)
+        j = torch.arange(32).view(1, 1, -1)
+        s_, c_ = j // 4, j % 4
+        src = st.slot.offset + ((k * st.R + r) * st.S + s_) * st.cin + c_
+        m = torch.where((s_ < st.S) & (c_ < st.cin), src, torch.full_like(src, -1))
         self.stem_w_off = off[0]
         derived_maps.append(m.reshape(-1).to(torch.int32))
         off[0] += m.numel()
+        # stem weight-gradient scatter: [Cout][R/2 pairs][2][32] (wgrad window tile) -> KRSC [Cout][R][S][Cin]
+        self.stem_pairs = (st.R + 1) // 2
+        kk = torch.arange(st.cout).view(-1, 1, 1, 1)
+        rr = torch.arange(st.R).view(1, -1, 1, 1)
+        ss = torch.arange(st.S).view(1, 1, -1, 1)
+        cc = torch.arange(st.cin).view(1, 1, 1, -1)
+        self.stem_gidx = (kk * (self.stem_pairs * 64) + (rr // 2) * 64 + (rr % 2) * 32 + ss * 4 + cc).reshape(-1).to(
+            torch.int32).to(self.device)
         # fc: padded [NP][F] (forward) and its transpose [F][NP] (backward-data)
         fc = model.fc
         self.ncls, self.feat = fc.out_features, fc.in_features
@@ -183,15 +195,14 @@ class ResNetExecutor:
         M = N * P * Q
         sp = None
         if stats:
-            tiles = self.C.conv_m_tiles(M, bm)
-            sp = self._buf("stats", tiles * c.cout * 2, torch.float32)
+            sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64)
         self.C.conv_fwd(x, self._w(c) if w is None else w, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
-                        -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk)
-        return P, Q, sp, (self.C.conv_m_tiles(M, bm) if stats else 0)
+                        -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
+        return P, Q, sp, M
 
     def bn_train_finalize(self, bn: _BN, sp, tiles: int, count: int):
         C = bn.C
-        self.C.bn_partial_reduce(sp, tiles, C, 2, self._buf("bnred", 64 * C * 4, torch.float64), bn.sums)
+        self.C.bn_slot_sum(sp, C, 2, bn.sums)
         if self.syncbn_group is not None:
             import torch.distributed as dist
             dist.all_reduce(bn.sums, group=self.syncbn_group)
@@ -224,9 +235,10 @@ class ResNetExecutor:
                 continue
             wt = self.derived[doff:doff + dn]
             self.C.conv_fwd(dy, wt, dx, res, None, N, P, Q, c.cout, c.cin, T, U, Pm, Qm, 1, 1, ioff_h, ioff_w, -1, -1,
-                            H, W, c.st, c.st, ph, pw, bm, bn, bk)
+                            H, W, c.st, c.st, ph, pw, bm, bn, bk, 0)
 
-    def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None):
+    def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
+               win=False, dil=1):
         key = (cout, R, S, C, N * P * Q)
         plan = self._plans.get(key)
         if plan is None:
@@ -235,7 +247,8 @@ class ResNetExecutor:
         splits, pps = plan
         ldw = R * S * C
         ws = self._buf("ws", splits * cout * ldw, torch.float32)
-        self.C.conv_wgrad(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, st, pad, pad, 1, 1, ldw, splits, pps)
+        self.C.conv_wgrad(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, st, pad, pad, dil, dil, ldw, splits, pps, cs,
+                          win)
         self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, False)
 
     def bn_bwd(self, bn1: _BN, y1, g, out, count: int, bn2: Optional[_BN] = None, y2=None):
@@ -244,10 +257,10 @@ class ResNetExecutor:
         rows = g.numel() // C
         blocks = self.C.bn_bwd_reduce_blocks(rows, C)
         K = 4 if bn2 is not None else 2
-        part = self._buf("bnpart", blocks * C * K, torch.float32)
-        self.C.bn_bwd_reduce(g, out, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, part, blocks, rows, C)
+        slots = self._buf(("bnslots", C, K), self.n_slots * C * K, torch.float64)
+        self.C.bn_bwd_reduce(g, out, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows, C)
         sums = bn1.bsums[:C * K]
-        self.C.bn_partial_reduce(part, blocks, C, K, self._buf("bnred", 64 * C * 4, torch.float64), sums)
+        self.C.bn_slot_sum(slots, C, K, sums)
         if self.syncbn_group is not None:
             import torch.distributed as dist
             dist.all_reduce(sums, group=self.syncbn_group)
@@ -274,13 +287,18 @@ class ResNetExecutor:
         st = self.stem
         P0, Q0 = st.out_hw(H, W)
         saved = {"N": N, "H": H, "W": W}
-        # stem: im2col (fp32 NCHW -> 16-bit [N*P0*Q0][KP]) + GEMM with BN statistics
-        cols = self._buf("im2col", N * P0 * Q0 * self.stem_kp)
-        Cn.im2col(x32, cols, N, 3, H, W, st.R, st.S, st.st, st.pad, self.stem_kp)
+        # stem: zero-padded NHWC4 image + window-mode implicit GEMM with BN statistics (no im2col)
+        Hp = max(H + 2 * st.pad, 2 * (P0 - 1) + 2 * self.stem_pairs)
+        Wp = max(W + 2 * st.pad, (Q0 - 1) * st.st + 8)
+        xp = self._buf("stem_in", N * Hp * Wp * 4)
+        Cn.stem_pack(x32, xp, N, 3, H, W, st.pad, Hp, Wp)
         y0 = self._buf("y0", N * P0 * Q0 * st.cout)
-        wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * self.stem_kp]
-        _, _, sp, tiles = self.conv_fwd(st, cols, N, P0, Q0, y0, train, w=wst, cin=self.stem_kp, R=1, S=1, st=1,
-                                        pad=0)
+        wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * st.R * 32]
+        sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64) if train else None
+        bm, bn = _conv_tile(st.cout)
+        Cn.conv_fwd(xp, wst, y0, None, sp, N, Hp, Wp, 32, st.cout, st.R, 1, P0, Q0, st.st, st.st, 0, 0, 1, 0,
+                    P0, Q0, 1, 1, 0, 0, bm, bn, 32, 4)
+        tiles = N * P0 * Q0
         if train:
             self.bn_train_finalize(self.stem_bn, sp, tiles, N * P0 * Q0)
         else:
@@ -289,7 +307,7 @@ class ResNetExecutor:
         x = self._buf("act_in", N * H1 * W1 * st.cout)
         idx = self._buf("mp_idx", N * H1 * W1 * st.cout, torch.uint8)
         Cn.bn_relu_maxpool(y0, self.stem_bn.coef, x, idx, N, P0, Q0, st.cout)
-        saved.update(cols=cols, y0=y0, P0=P0, Q0=Q0, idx=idx, x0=x, H1=H1, W1=W1)
+        saved.update(xp=xp, Hp=Hp, Wp=Wp, y0=y0, P0=P0, Q0=Q0, idx=idx, x0=x, H1=H1, W1=W1)
         Hc, Wc, Cc = H1, W1, st.cout
         blk_saved = []
         for bi, b in enumerate(self.blocks):
@@ -338,7 +356,7 @@ class ResNetExecutor:
         wfc = self.derived[self.fc_w_off:self.fc_w_off + self.ncls_pad * self.feat]
         bm, bn = _conv_tile(self.ncls_pad)
         Cn.conv_fwd(feat, wfc, logits, None, None, N, 1, 1, self.feat, self.ncls_pad, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1,
-                    1, 1, 1, 1, 0, 0, bm, bn, 64)
+                    1, 1, 1, 1, 0, 0, bm, bn, 64, 0)
         saved.update(blocks=blk_saved, feat=feat, logits=logits, Hc=Hc, Wc=Wc, Cc=Cc)
         return saved
 
@@ -382,7 +400,7 @@ class ResNetExecutor:
         wt = self.derived[self.fc_wt_off:self.fc_wt_off + self.ncls_pad * self.feat]
         bm, bn = _conv_tile(self.feat)
         Cn.conv_fwd(dlog, wt, dfeat, None, None, N, 1, 1, self.ncls_pad, self.feat, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1,
-                    1, 1, 1, 1, 0, 0, bm, bn, 64)
+                    1, 1, 1, 1, 0, 0, bm, bn, 64, 0)
         Hc, Wc, Cc = saved["Hc"], saved["Wc"], saved["Cc"]
         g = self._buf("g_a", N * Hc * Wc * Cc)
         Cn.avgpool_bwd(dfeat, g, N, Hc * Wc, Cc, self.feat)
@@ -436,7 +454,7 @@ class ResNetExecutor:
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res)
             g = gnext
             gsel ^= 1
-        # stem: max-pool backward + ReLU mask -> BN backward -> weight gradient over im2col columns
+        # stem: max-pool backward + ReLU mask -> BN backward -> window-mode weight gradient
         st, sbn = self.stem, self.stem_bn
         P0, Q0 = saved["P0"], saved["Q0"]
         dz0 = self._buf("dz0", N * P0 * Q0 * st.cout)
@@ -444,6 +462,9 @@ class ResNetExecutor:
         self.bn_bwd(sbn, saved["y0"], dz0, None, N * P0 * Q0)
         dy0 = self._buf("dy0", dz0.numel())
         Cn.bn_bwd_apply(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
-        self._wgrad(st.cout, saved["cols"], dy0, N, P0, Q0, self.stem_kp, 1, 1, P0, Q0, 1, 0,
-                    self._g(st.slot), self.stem_k, rows=st.cout, cols=self.stem_k)
+        ldw = self.stem_pairs * 64
+        tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
+        self._wgrad(st.cout, saved["xp"], dy0, N, saved["Hp"], saved["Wp"], 64, self.stem_pairs, 1, P0, Q0, st.st, 0,
+                    tmp, ldw, cs=4, win=True, dil=2)
+        Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
         self.grad_ready(st.pid)

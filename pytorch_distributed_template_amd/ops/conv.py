@@ -70,14 +70,14 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
     bk = 64 if C % 64 == 0 else 32
     sp = None
     if stats:
-        tiles = native.C.conv_m_tiles(N * P * Q, bm)
-        sp = torch.empty(tiles * K * 2, dtype=torch.float32, device=x.device)
+        sp = torch.empty(native.C.stat_slots() * K * 2, dtype=torch.float64, device=x.device)
     native.C.conv_fwd(x, w, y, residual, sp, N, H, W, C, K, R, S, P, Q, stride, stride, -pad, -pad, 1, 1,
-                      P, Q, 1, 1, 0, 0, bm, bn, bk)
+                      P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
     if not stats:
         return y
-    part = sp.view(tiles, K, 2).double().sum(0)
-    return y, (part[:, 0], part[:, 1])
+    sums = torch.empty(2 * K, dtype=torch.float64, device=x.device)
+    native.C.bn_slot_sum(sp, K, 2, sums)
+    return y, (sums[:K], sums[K:])
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 1, pad: int = 0,
@@ -97,7 +97,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
         idx = dgrad_weight_index(K, C, R, S, rs, ss).to(w.device)
         wt = wflat[idx].contiguous() if idx.numel() else torch.empty(0, dtype=w.dtype, device=w.device)
         native.C.conv_fwd(dy, wt, dx, residual, None, N, P, Q, K, C, len(rs), len(ss), Pm, Qm, 1, 1, ioff_h, ioff_w,
-                          -1, -1, H, W, stride, stride, ph, pw, bm, bn, bk)
+                          -1, -1, H, W, stride, stride, ph, pw, bm, bn, bk, 0)
     return dx
 
 
@@ -109,7 +109,8 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int = 
     splits, pps = native.C.conv_wgrad_plan(K, R, S, C, N * P * Q, target_blocks)
     ldw = R * S * C
     ws = torch.empty(splits * K * ldw, dtype=torch.float32, device=x.device)
-    native.C.conv_wgrad(x, dy, ws, N, H, W, C, K, R, S, P, Q, stride, stride, pad, pad, 1, 1, ldw, splits, pps)
+    native.C.conv_wgrad(x, dy, ws, N, H, W, C, K, R, S, P, Q, stride, stride, pad, pad, 1, 1, ldw, splits, pps, 0,
+                        False)
     out = torch.empty(K * ldw, dtype=torch.float32, device=x.device)
     native.C.wgrad_reduce(ws, splits, K, ldw, ldw, K * ldw, out, ldw, 1.0, False)
     return out.view(K, R, S, C)

