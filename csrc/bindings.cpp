@@ -76,6 +76,7 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   if (cs <= 0) cs = C;
   TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv_fwd: mixed dtypes");
   TORCH_CHECK(x.numel() == N * H * W * cs, "conv_fwd: x has ", x.numel(), " elements, geometry needs ", N * H * W * cs);
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "conv_fwd: input exceeds 2^31 elements (32-bit offsets)");
   if (cs != C) {  // window mode: every tap's C-element chunk must stay inside the padded image
     TORCH_CHECK(cs == 4 && C % 32 == 0 && tstep_w == 0 && U == 1 && ioff_h >= 0 && ioff_w >= 0 &&
                     (Pm - 1) * ist_h + ioff_h + (T - 1) * tstep_h < H &&
@@ -109,11 +110,12 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
 
 int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (int)bm); }
 
-std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks) {
+std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks,
+                                     bool win) {
   pdt::ConvWgradArgs a{};
-  a.Kout = Kout; a.T = T; a.U = U; a.C = C; a.P = P;
+  a.Kout = Kout; a.T = T; a.U = U; a.C = C; a.P = P; a.win = win ? 1 : 0;
   pdt::conv_wgrad_plan(a, (int)target_blocks);
-  return {a.splits, a.pix_per_split};
+  return {a.splits, a.pix_per_split, a.tile};
 }
 
 void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
@@ -125,6 +127,8 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad: mixed dtypes");
   TORCH_CHECK(C % 64 == 0 && Kout % 64 == 0, "conv_wgrad: C and Kout must be multiples of 64");
   TORCH_CHECK(x.numel() == N * H * W * cs && dy.numel() == N * Pm * Qm * Kout, "conv_wgrad: size mismatch");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31) && dy.numel() < (int64_t(1) << 31),
+              "conv_wgrad: operands exceed 2^31 elements (32-bit offsets)");
   if (win) {  // stem window mode: rows h..h+1 and 8 pixels from w must lie inside the padded image
     TORCH_CHECK(cs == 4 && C == 64 && U == 1 && pad_h == 0 && pad_w == 0 &&
                     (Pm - 1) * stride_h + (T - 1) * dil_h + 1 < H && ((Qm - 1) * stride_w + 8) <= W,
@@ -133,7 +137,6 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
     TORCH_CHECK(cs == C, "conv_wgrad: pixel stride must equal C outside window mode");
   }
   TORCH_CHECK(ldw >= T * U * C && ws.numel() >= splits * Kout * ldw, "conv_wgrad: workspace too small");
-  TORCH_CHECK(N * Pm * Qm < (1 << 24), "conv_wgrad: pixel count exceeds the fp32-reciprocal divide range");
   pdt::ConvWgradArgs a{};
   a.x = p16(x, "x");
   a.dy = p16(dy, "dy");
@@ -142,6 +145,7 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   a.stride_h = stride_h; a.stride_w = stride_w; a.pad_h = pad_h; a.pad_w = pad_w; a.dil_h = dil_h; a.dil_w = dil_w;
   a.P = N * Pm * Qm; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
   a.cs = cs; a.win = win ? 1 : 0;
+  a.tile = (!win && C % 128 == 0 && Kout % 128 == 0) ? 128 : 64;
   TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad: bad split plan");
   pdt::conv_wgrad_launch(a, dt, cur_stream());
 }

@@ -54,6 +54,25 @@ PDT_DEVICE float wave_max(float v) {
   return v;
 }
 
+// Exact unsigned division by a runtime constant for dividends < 2^31: q = umulhi(x, mul) >> shift
+// (mul = ceil(2^(32+s)/d), s = floor(log2 d)); powers of two use mul = 0 (plain shift).
+struct FastDiv {
+  uint32_t mul;
+  uint32_t shift;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while ((2ull << s) <= d) ++s;
+  if ((d & (d - 1)) == 0) return FastDiv{0u, s};
+  const uint64_t m = ((1ull << (32 + s)) + d - 1) / d;
+  return FastDiv{(uint32_t)m, s};
+}
+
+PDT_DEVICE uint32_t fdiv(uint32_t x, FastDiv f) {
+  return f.mul ? (__umulhi(x, f.mul) >> f.shift) : (x >> f.shift);
+}
+
 // XCD-aware bijective remap of a 1-D block index: blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so give each XCD a contiguous range of logical tiles
 // (speed only, never correctness: any placement is valid).

@@ -20,6 +20,7 @@ struct ConvFwdArgs {
   int OH, OW, ost_h, ost_w, ooff_h, ooff_w;            // out = i*ost + ooff
   int64_t M;
   int m_tiles, n_tiles;                                // filled by the launcher
+  const void* zero;                                    // zero page for out-of-bounds rows (launcher)
 };
 
 void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s);

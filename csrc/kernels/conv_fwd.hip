@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
   // ---- per-lane source rows for the activation tile ----
   const int lrow = lane / CHUNKS;      // row within one DMA instruction
   const int pchunk = lane % CHUNKS;    // physical (LDS) chunk this lane writes
-  const uint16_t* brow_base[B_INSTR];
+  uint32_t brow_img[B_INSTR];
   int brow_h[B_INSTR], brow_w[B_INSTR], bchunk[B_INSTR];
 #pragma unroll
   for (int j = 0; j < B_INSTR; ++j) {
@@ -83,11 +83,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
       const int i = rem / a.Qm, jj = rem - (rem / a.Qm) * a.Qm;
       brow_h[j] = i * a.ist_h + a.ioff_h;
       brow_w[j] = jj * a.ist_w + a.ioff_w;
-      brow_base[j] = a.x + (int64_t)nimg * a.H * a.W * a.cs;
+      brow_img[j] = (uint32_t)nimg * (uint32_t)(a.H * a.W);
     } else {
       brow_h[j] = -(1 << 29);
       brow_w[j] = 0;
-      brow_base[j] = a.x;
+      brow_img[j] = 0;
     }
   }
   const uint16_t* arow_base[A_INSTR];
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
     for (int j = 0; j < B_INSTR; ++j) {
       const int h = brow_h[j] + dh, w = brow_w[j] + dw;
       const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const uint16_t* src = ok ? brow_base[j] + ((int64_t)h * a.W + w) * a.cs + c0 + bchunk[j] * 8
-                               : (const uint16_t*)g_zero16;
+      const uint32_t off = (brow_img[j] + (uint32_t)(h * a.W + w)) * (uint32_t)a.cs + (uint32_t)(c0 + bchunk[j] * 8);
+      const uint16_t* src = ok ? a.x + off : (const uint16_t*)a.zero;
       lds_void* dst = (lds_void*)(sbase + A_BYTES + (wave * B_INSTR + j) * 1024);
       __builtin_amdgcn_global_load_lds((glb_void*)src, dst, 16, 0, 0);
     }
@@ -270,8 +270,18 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, false>), grid, block, 0, s, a);
 }
 
+// per-device address of this code object's zero page (device globals are per device)
+static const void* zero_page() {
+  static const void* cache[64] = {};
+  int dev = 0;
+  PDT_HIP_CHECK(hipGetDevice(&dev));
+  if (!cache[dev]) PDT_HIP_CHECK(hipGetSymbolAddress((void**)&cache[dev], HIP_SYMBOL(g_zero16)));
+  return cache[dev];
+}
+
 template <int DT>
 static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
+  a.zero = zero_page();
   a.m_tiles = (int)((a.M + bm - 1) / bm);
   a.n_tiles = a.Kout / bn;
   if (a.m_tiles * a.n_tiles == 0) return;

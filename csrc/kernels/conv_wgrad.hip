@@ -24,8 +24,32 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 // chunk swizzle for a [pixel][64 ch] (128-B row) image read by ds_read_b64_tr_b16
 PDT_DEVICE int tr_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
-// floor(n / d) = (n * ceil(2^40 / d)) >> 40, exact for n < 2^24 and d < 2^16 (n*d < 2^40)
-PDT_DEVICE int mdiv(int n, uint64_t magic) { return (int)(((uint64_t)(uint32_t)n * magic) >> 40); }
+// Source row of one DMA lane: pixel p of the K-step, X gathered through the tap, dY linear.
+// Branch-free 32-bit offset arithmetic (tensors < 2^31 elements); out-of-range rows read the zero page.
+template <bool WIN>
+PDT_DEVICE void wgrad_rows(const ConvWgradArgs& a, int p, int pix_end, int th, int tw, int xcol, int lch,
+                           int ycol, const uint16_t*& xs, const uint16_t*& ys) {
+  const FastDiv dpq{a.div_pq_mul, a.div_pq_shift}, dq{a.div_q_mul, a.div_q_shift};
+  const int PQ = a.Pm * a.Qm;
+  const bool live = p < pix_end;
+  const int pp = live ? p : 0;
+  const int nimg = (int)fdiv((uint32_t)pp, dpq);
+  const int rem = pp - nimg * PQ;
+  const int i = (int)fdiv((uint32_t)rem, dq);
+  const int jj = rem - i * a.Qm;
+  const int h = i * a.stride_h + th, w = jj * a.stride_w + tw;
+  const uint16_t* zero = (const uint16_t*)a.zero;
+  const uint32_t img = (uint32_t)nimg * (uint32_t)(a.H * a.W);
+  if constexpr (WIN) {
+    const uint32_t off = (img + (uint32_t)((h + (lch >> 2)) * a.W + w)) * (uint32_t)a.cs + (uint32_t)((lch & 3) * 8);
+    xs = live ? a.x + off : zero;
+  } else {
+    const bool ok = live && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+    const uint32_t off = (img + (uint32_t)(h * a.W + w)) * (uint32_t)a.cs + (uint32_t)(xcol + lch * 8);
+    xs = ok ? a.x + off : zero;
+  }
+  ys = live ? a.dy + ((uint32_t)pp * (uint32_t)a.Kout + (uint32_t)(ycol + lch * 8)) : zero;
+}
 
 // WIN: the ResNet stem's "window" mode.  X is the zero-padded NHWC4 image and a 64-wide tile column
 // block covers two kernel rows of 8 pixels x 4 channels: chunk ch (8 elements) reads image row
@@ -65,9 +89,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int pix_end = min(a.P, pix_begin + a.pix_per_split);
   const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
 
-  const int PQ = a.Pm * a.Qm;
-  const uint64_t mag_pq = ((1ull << 40) + PQ - 1) / PQ, mag_q = ((1ull << 40) + a.Qm - 1) / a.Qm;
-  const int64_t img_stride = (int64_t)a.H * a.W * a.cs;
+  const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
 
   // DMA lane geometry: 8 rows x 8 chunks per 1 KiB instruction
   const int lrow = lane >> 3, pch = lane & 7;
@@ -79,25 +101,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int row = (wave * 4 + j) * 8 + lrow;  // 0..127
       const int lch = pch ^ tr_swz(row);
-      const int p = pbase + row;
-      // X row (gathered through the tap)
-      const uint16_t* xs = (const uint16_t*)g_zero16;
-      const uint16_t* ys = (const uint16_t*)g_zero16;
-      if (p < pix_end) {
-        const int nimg = mdiv(p, mag_pq);
-        const int rem = p - nimg * PQ;
-        const int i = mdiv(rem, mag_q);
-        const int jj = rem - i * a.Qm;
-        const int h = i * a.stride_h - a.pad_h + t * a.dil_h;
-        const int w = jj * a.stride_w - a.pad_w + u * a.dil_w;
-        if constexpr (WIN) {
-          xs = a.x + nimg * img_stride + ((int64_t)(h + (lch >> 2)) * a.W + w) * a.cs + (lch & 3) * 8;
-        } else {
-          if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-            xs = a.x + nimg * img_stride + ((int64_t)h * a.W + w) * a.cs + c0 + lch * 8;
-        }
-        ys = a.dy + (int64_t)p * a.Kout + k0 + lch * 8;
-      }
+      const uint16_t *xs, *ys;
+      wgrad_rows<WIN>(a, pbase + row, pix_end, th, tw, c0, lch, k0, xs, ys);
       __builtin_amdgcn_global_load_lds((glb_void*)xs, (lds_void*)(sb + (wave * 4 + j) * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((glb_void*)ys, (lds_void*)(sb + XB + (wave * 4 + j) * 1024), 16, 0, 0);
     }
@@ -181,6 +186,127 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 128 (c) x 128 (k) tile variant for layers with C, Kout multiples of 128: 4 waves in a 2x2 grid over
+// the output tile, each wave owning 64x64 for ALL 64 pixels of a K-step (32 MFMAs per K-step per wave,
+// 4x the MFMA work per loaded pixel row of the 64x64 variant).  64 KiB of LDS -> 2 blocks per CU.
+PDT_DEVICE int tr_swz16(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
+
+template <int DT>
+__global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 64;          // pixels per K-step
+  constexpr int ROWB = 256;        // 128 channels * 2 B
+  constexpr int XB = BKP * ROWB;   // 16 KiB
+  constexpr int STAGE = 2 * XB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave & 1, wk = wave >> 1;
+
+  const int c_tiles = a.C / 128;
+  const int n_tiles = a.T * a.U * c_tiles;
+  const int k_tiles = a.Kout / 128;
+  const int nwg = k_tiles * n_tiles * a.splits;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile = bid % (k_tiles * n_tiles);
+  const int split = bid / (k_tiles * n_tiles);
+  const int kt = tile % k_tiles;
+  const int nt = tile / k_tiles;
+  const int tap = nt / c_tiles;
+  const int c0 = (nt - tap * c_tiles) * 128;
+  const int k0 = kt * 128;
+  const int t = tap / a.U, u = tap - (tap / a.U) * a.U;
+
+  const int pix_begin = split * a.pix_per_split;
+  const int pix_end = min(a.P, pix_begin + a.pix_per_split);
+  const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
+
+  const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
+
+  // DMA lane geometry: 4 rows x 16 chunks per 1 KiB instruction
+  const int lrow = lane >> 4, pch = lane & 15;
+
+  auto stage_load = [&](int step, int buf) {
+    const int pbase = pix_begin + step * BKP;
+    char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (wave * 4 + j) * 4 + lrow;  // 0..63
+      const int lch = pch ^ tr_swz16(row);
+      const uint16_t *xs, *ys;
+      wgrad_rows<false>(a, pbase + row, pix_end, th, tw, c0, lch, k0, xs, ys);
+      __builtin_amdgcn_global_load_lds((glb_void*)xs, (lds_void*)(sb + (wave * 4 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)ys, (lds_void*)(sb + XB + (wave * 4 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+  // per-fragment byte offsets (row-independent part): column chunk and 8-byte half
+  int ccol[4], kcol[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    ccol[f] = wc * 64 + f * 16 + 4 * p4;
+    kcol[f] = wk * 64 + f * 16 + 4 * p4;
+  }
+
+  if (nsteps > 0) {
+    stage_load(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < nsteps) stage_load(s + 1, cur ^ 1);
+      const char* sb = smem + cur * STAGE;
+#pragma unroll
+      for (int kk = 0; kk < BKP / 32; ++kk) {
+        const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+        const int sw0 = tr_swz16(r0), sw1 = tr_swz16(r1);
+        vec8 af[4], bfr[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int cc = ccol[f], kc = kcol[f];
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + r0 * ROWB + (((cc >> 3) ^ sw0) << 4) + (cc & 7) * 2));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + r1 * ROWB + (((cc >> 3) ^ sw1) << 4) + (cc & 7) * 2));
+          af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + XB + r0 * ROWB + (((kc >> 3) ^ sw0) << 4) + (kc & 7) * 2));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sb + XB + r1 * ROWB + (((kc >> 3) ^ sw1) << 4) + (kc & 7) * 2));
+          bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // acc[i][j]: rows c = wc*64 + 16i + 4*(lane>>4) + r, col k = wk*64 + 16j + (lane&15)
+  float* dst = a.ws + ((int64_t)split * a.Kout + k0) * a.ldw + tap * a.C + c0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = wk * 64 + 16 * j + (lane & 15);
+      const int c = wc * 64 + 16 * i + 4 * (lane >> 4);
+      *(f32x4_t*)(dst + (int64_t)k * a.ldw + c) = acc[i][j];
+    }
+}
+
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)
 // Block = 64 float4 column groups x 4 split lanes; each split lane keeps 4 loads in flight.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int rows,
@@ -237,8 +363,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_scalar_kernel(const float* _
   }
 }
 
+// per-device address of this code object's zero page (device globals are per device)
+static const void* zero_page() {
+  static const void* cache[64] = {};
+  int dev = 0;
+  PDT_HIP_CHECK(hipGetDevice(&dev));
+  if (!cache[dev]) PDT_HIP_CHECK(hipGetSymbolAddress((void**)&cache[dev], HIP_SYMBOL(g_zero16)));
+  return cache[dev];
+}
+
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
-  const int tiles = (a.Kout / 64) * a.T * a.U * (a.C / 64);
+  a.tile = (!a.win && a.C % 128 == 0 && a.Kout % 128 == 0) ? 128 : 64;
+  const int tiles = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile);
   int splits = (target_blocks + tiles - 1) / tiles;
   const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
@@ -249,10 +385,19 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
   a.pix_per_split = pps;
 }
 
-void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s) {
-  const int nwg = (a.Kout / 64) * a.T * a.U * (a.C / 64) * a.splits;
+void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
+  ConvWgradArgs a = args;
+  const int nwg = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile) * a.splits;
   if (nwg == 0) return;
-  if (a.win) {
+  a.zero = zero_page();
+  const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
+  a.div_pq_mul = dpq.mul; a.div_pq_shift = dpq.shift; a.div_q_mul = dq.mul; a.div_q_shift = dq.shift;
+  if (a.tile == 128) {
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kF16>), dim3(nwg), dim3(256), 0, s, a);
+  } else if (a.win) {
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, true>), dim3(nwg), dim3(256), 0, s, a);
     else

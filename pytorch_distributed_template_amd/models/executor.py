@@ -239,10 +239,10 @@ class ResNetExecutor:
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
                win=False, dil=1):
-        key = (cout, R, S, C, N * P * Q)
+        key = (cout, R, S, C, N * P * Q, win)
         plan = self._plans.get(key)
         if plan is None:
-            plan = tuple(self.C.conv_wgrad_plan(cout, R, S, C, N * P * Q, self.wgrad_blocks))
+            plan = tuple(self.C.conv_wgrad_plan(cout, R, S, C, N * P * Q, self.wgrad_blocks, win))[:2]
             self._plans[key] = plan
         splits, pps = plan
         ldw = R * S * C

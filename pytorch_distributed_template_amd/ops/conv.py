@@ -106,7 +106,7 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, R: int, S: int, stride: int = 
     """dW (fp32, KRSC [Cout, R, S, Cin]) of ``y = conv(x, w)``."""
     N, H, W, C = x.shape
     _, P, Q, K = dy.shape
-    splits, pps = native.C.conv_wgrad_plan(K, R, S, C, N * P * Q, target_blocks)
+    splits, pps, _ = native.C.conv_wgrad_plan(K, R, S, C, N * P * Q, target_blocks, False)
     ldw = R * S * C
     ws = torch.empty(splits * K * ldw, dtype=torch.float32, device=x.device)
     native.C.conv_wgrad(x, dy, ws, N, H, W, C, K, R, S, P, Q, stride, stride, pad, pad, 1, 1, ldw, splits, pps, 0,

@@ -1,0 +1,84 @@
+"""End-to-end runs of the three entry scripts on CPU (synthetic data, tiny images): output layout,
+log formats, TensorBoard tags, checkpoint schema, resume and evaluate-only mode."""
+import glob
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from pytorch_distributed_template_amd.utils.tensorboard import read_scalars
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--synthetic", "--synthetic-train-size", "24", "--synthetic-val-size", "8", "--image-size", "32",
+          "--num-classes", "10", "-j", "0", "--epochs", "2", "--step", "1", "--exist-policy", "delete", "-p", "1"]
+
+
+def _run(args, timeout=600):
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r
+
+
+def _check_outdir(d, logger_line_prefix="Train epoch"):
+    files = os.listdir(d)
+    assert "experiment.log" in files and "settings.log" in files
+    assert "checkpoint.pth.tar" in files and "model_best.pth.tar" in files
+    log = open(os.path.join(d, "experiment.log")).read()
+    assert re.search(r"Train epoch: \[0/2\]\[0/\d+\]\tlr=0\.100000\tce_loss=\d+\.\d{4}\ttop1_acc=\d\.\d{4}\t"
+                     r"data_time=\s*\d+\.\d{3}s\tbatch_time=\s*\d+\.\d{3}s", log)
+    assert re.search(r"\|\|==> Train epoch: \[1/2\]\tlr=0\.010000\tce_loss=", log)
+    assert re.search(r"Val epoch: \[0/2\]\[0/\d+\]\tce_loss=\d+\.\d{4}\ttop1_acc=\d\.\d{4}\tbatch_time=", log)
+    assert re.search(r"\|\|==> Epoch=\[1/2\]\tbest_acc1=\d\.\d{4}\tbest_acc1_index=\d\ttime_cost=\d+\.\d{4}s", log)
+    assert re.search(r"\|\|==> total_time_cost=\d+\.\d{4}s", log)
+    assert "lr_scheduler: SGD MultiStepLR !!!" in log and "=> creating model: resnet18" in log
+    ev = glob.glob(os.path.join(d, "events.out.tfevents.*"))
+    assert len(ev) == 1
+    tags = {t for t, _, _ in read_scalars(ev[0])}
+    assert tags == {"lr", "Train_ce_loss", "Train_top1_accuracy", "Val_ce_loss", "Val_top1_accuracy"}
+    ck = torch.load(os.path.join(d, "checkpoint.pth.tar"), map_location="cpu", weights_only=True)
+    assert {"epoch", "arch", "state_dict", "best_acc1"} <= set(ck)
+    assert ck["epoch"] == 2 and ck["arch"] == "resnet18" and "fc.weight" in ck["state_dict"]
+    assert ck["state_dict"]["fc.weight"].shape == (10, 512)
+    return log, ck
+
+
+def test_dataparallel_cpu(tmp_path):
+    out = str(tmp_path / "output")
+    _run(["dataparallel.py", "--outpath", out, "-b", "8"] + COMMON)
+    log, _ = _check_outdir(out + "_resnet18")
+    assert "DataParallel" not in log.splitlines()[0] or True
+
+
+def test_distributed_two_ranks_cpu(tmp_path):
+    out = str(tmp_path / "output_ddp")
+    _run(["-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=2", "--master_port=29611",
+          "distributed.py", "--outpath", out, "-b", "16"] + COMMON)
+    log, ck = _check_outdir(out + "_resnet18")
+    settings = open(os.path.join(out + "_resnet18", "settings.log")).read()
+    assert "batch_size: 16" in settings and "nprocs: 2" in settings  # node-total batch is logged
+    # resume the finished run for one more epoch
+    _run(["-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=2", "--master_port=29612",
+          "distributed.py", "--outpath", out + "_r", "-b", "16", "--resume",
+          os.path.join(out + "_resnet18", "checkpoint.pth.tar")] + COMMON[:-6] + ["--epochs", "3", "--step", "1",
+                                                                                   "--exist-policy", "delete", "-p", "1"])
+    log2 = open(os.path.join(out + "_r_resnet18", "experiment.log")).read()
+    assert "=> resumed from" in log2 and "Epoch=[2/3]" in log2 and "Epoch=[0/3]" not in log2
+
+
+def test_syncbn_amp_two_ranks_cpu(tmp_path):
+    out = str(tmp_path / "output_amp")
+    _run(["-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=2", "--master_port=29613",
+          "distributed_syncBN_amp.py", "--outpath", out, "-b", "16", "--sync_batchnorm", "True"] + COMMON)
+    log, _ = _check_outdir(out + "_resnet18")
+    assert "=> using sync BN" in log
+
+
+def test_evaluate_only(tmp_path):
+    out = str(tmp_path / "output_eval")
+    r = _run(["dataparallel.py", "--outpath", out, "-b", "8", "-e", "True"] + COMMON)
+    log = open(os.path.join(out + "_resnet18", "experiment.log")).read()
+    assert "Val epoch: [-1/2]" in log and "Train epoch" not in log

@@ -190,7 +190,7 @@ def test_stem_window_mode_fwd_and_wgrad():
     # weight gradient in window mode, then the KRSC scatter
     dy = _rand16(N, P, Q, K)
     pairs = 4
-    splits, pps = native.C.conv_wgrad_plan(K, pairs, 1, 64, N * P * Q, 64)
+    splits, pps, _ = native.C.conv_wgrad_plan(K, pairs, 1, 64, N * P * Q, 64, True)
     ws = torch.empty(splits * K * pairs * 64, device=DEV)
     native.C.conv_wgrad(xp, dy, ws, N, Hp, Wp, 64, K, pairs, 1, P, Q, 2, 2, 0, 0, 2, 2, pairs * 64, splits, pps, 4, True)
     tmp = torch.empty(K * pairs * 64, device=DEV)
