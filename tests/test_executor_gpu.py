@@ -66,12 +66,15 @@ def test_train_step_matches_reference(arch, dtype):
         if ours > 1.5 * theirs + 0.02:
             bad.append((n, ours, theirs))
     assert not bad, bad[:5]
-    # running statistics follow the batch statistics like nn.BatchNorm2d
-    for (n, b), (n2, b2) in zip(model.named_buffers(), ref.named_buffers()):
-        if "running_var" in n:
-            assert _relnorm(b, b2) < 3e-2, n
-        elif "running_mean" in n:  # small means: judge against the spread of the channel statistics
-            assert ((b - b2).norm() / ref_scale(b2)).item() < 6e-2, n
+    # running statistics follow the batch statistics like nn.BatchNorm2d (judged against autocast too)
+    bad = []
+    for (n, b), (_, b2), (_, b3) in zip(model.named_buffers(), ref.named_buffers(), tb.named_buffers()):
+        if "running" in n:
+            scale = b2.float().norm().clamp_min(1e-3)
+            ours, theirs = ((b - b2).norm() / scale).item(), ((b3 - b2).norm() / scale).item()
+            if ours > 1.5 * theirs + 0.01:
+                bad.append((n, ours, theirs))
+    assert not bad, bad[:5]
 
 
 def test_eval_step_matches_reference():
