@@ -9,7 +9,9 @@
 #include <c10/hip/HIPGuard.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <optional>
+#include <vector>
 #include <stdexcept>
 #include <string>
 
@@ -109,6 +111,45 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
 }
 
 int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (int)bm); }
+
+// Backward-data of a (strided) conv in ONE launch: phases = [(ph, pw, T, U, ioff_h, ioff_w, woff), ...]
+// over dY [N,P,Q,K] -> dX [N,H,W,C] (+ residual), wt = concatenated per-phase [C][T][U][K] weights.
+void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
+                int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride, const std::vector<std::vector<int64_t>>& phases,
+                int64_t bm, int64_t bn, int64_t bk) {
+  const int dt = dt16(dy, "dy");
+  TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "conv_dgrad: mixed dtypes");
+  TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv_dgrad: size mismatch");
+  TORCH_CHECK(dy.numel() < (int64_t(1) << 31), "conv_dgrad: dY exceeds 2^31 elements");
+  TORCH_CHECK(!phases.empty() && phases.size() <= 4, "conv_dgrad: 1..4 phases");
+  TORCH_CHECK(K % bk == 0 && C % bn == 0, "conv_dgrad: K % bk / C % bn must be 0");
+  pdt::ConvFwdArgs a{};
+  a.x = p16(dy, "dy");
+  a.w = p16(wt, "wt");
+  a.y = p16(dx, "dx");
+  if (res.has_value()) {
+    TORCH_CHECK(res->numel() == dx.numel(), "conv_dgrad: residual size mismatch");
+    a.res = p16(*res, "res");
+  }
+  a.N = N; a.H = P; a.W = Q; a.C = K; a.cs = K; a.Kout = C;
+  a.ist_h = 1; a.ist_w = 1; a.tstep_h = -1; a.tstep_w = -1;
+  a.OH = H; a.OW = W; a.ost_h = stride; a.ost_w = stride;
+  a.nphase = (int)phases.size();
+  int64_t maxM = 0;
+  for (size_t i = 0; i < phases.size(); ++i) {
+    const auto& f = phases[i];
+    TORCH_CHECK(f.size() == 7, "conv_dgrad: phase = (ph, pw, T, U, ioff_h, ioff_w, woff)");
+    const int64_t ph = f[0], pw = f[1];
+    const int64_t Pm = (H - ph + stride - 1) / stride, Qm = (W - pw + stride - 1) / stride;
+    TORCH_CHECK(Pm > 0 && Qm > 0 && f[6] + C * f[2] * f[3] * K <= wt.numel(), "conv_dgrad: bad phase");
+    a.pooff_h[i] = (int)ph; a.pooff_w[i] = (int)pw; a.pT[i] = (int)f[2]; a.pU[i] = (int)f[3];
+    a.pioff_h[i] = (int)f[4]; a.pioff_w[i] = (int)f[5]; a.pwoff[i] = f[6];
+    a.pPm[i] = (int)Pm; a.pQm[i] = (int)Qm;
+    maxM = std::max(maxM, N * Pm * Qm);
+  }
+  a.M = maxM;
+  pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+}
 
 std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks,
                                      bool win) {
@@ -345,6 +386,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels of pytorch_distributed_template_amd";
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_m_tiles", &conv_m_tiles);
+  m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_reduce", &wgrad_reduce);

@@ -21,6 +21,11 @@ struct ConvFwdArgs {
   int64_t M;
   int m_tiles, n_tiles;                                // filled by the launcher
   const void* zero;                                    // zero page for out-of-bounds rows (launcher)
+  // Multi-phase launch (backward-data of strided convs): blockIdx.y selects a phase whose geometry
+  // overrides T, U, ioff, Pm, Qm, ooff and the weight offset.  nphase == 0: single-phase launch.
+  int nphase;
+  int pT[4], pU[4], pioff_h[4], pioff_w[4], pPm[4], pQm[4], pooff_h[4], pooff_w[4], pmt[4];
+  int64_t pwoff[4];
 };
 
 void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s);

@@ -34,7 +34,19 @@ template <int CHUNKS>
 PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
 template <int DT, int BM, int BN, int BK, int WAVES_N, bool STATS, bool RES>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
+  ConvFwdArgs a = args;
+  if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
+    const int ph = blockIdx.y;
+    a.T = args.pT[ph]; a.U = args.pU[ph];
+    a.ioff_h = args.pioff_h[ph]; a.ioff_w = args.pioff_w[ph];
+    a.Pm = args.pPm[ph]; a.Qm = args.pQm[ph];
+    a.ooff_h = args.pooff_h[ph]; a.ooff_w = args.pooff_w[ph];
+    a.m_tiles = args.pmt[ph];
+    a.M = (int64_t)a.N * a.Pm * a.Qm;
+    a.w = args.w + args.pwoff[ph];
+    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
+  }
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   constexpr int WAVES_M = 4 / WAVES_N;
@@ -258,7 +270,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs a) {
 // ----------------------------------------------------------------------------------------------
 template <int DT, int BM, int BN, int BK, int WAVES_N>
 static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
-  dim3 grid(a.m_tiles * a.n_tiles), block(256);
+  int gx = a.m_tiles * a.n_tiles;
+  if (a.nphase > 0) {
+    gx = 0;
+    for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
+  }
+  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(256);
   const bool st = a.stats != nullptr, rs = a.res != nullptr;
   if (st && rs)
     hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, true>), grid, block, 0, s, a);
@@ -284,7 +301,16 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   a.zero = zero_page();
   a.m_tiles = (int)((a.M + bm - 1) / bm);
   a.n_tiles = a.Kout / bn;
-  if (a.m_tiles * a.n_tiles == 0) return;
+  if (a.nphase > 0) {
+    int any = 0;
+    for (int p = 0; p < a.nphase; ++p) {
+      a.pmt[p] = (int)(((int64_t)a.N * a.pPm[p] * a.pQm[p] + bm - 1) / bm);
+      any |= a.pmt[p];
+    }
+    if (!any || a.n_tiles == 0) return;
+  } else if (a.m_tiles * a.n_tiles == 0) {
+    return;
+  }
 #define PDT_CFG(BM_, BN_, BK_, WN_)                                      \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
     launch_cfg<DT, BM_, BN_, BK_, WN_>(a, s);                            \

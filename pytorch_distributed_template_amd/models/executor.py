@@ -78,7 +78,7 @@ class ResNetExecutor:
 
     def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None,
-                 syncbn_group=None, wgrad_blocks: int = 512):
+                 syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not isinstance(model, ResNet) or model.groups != 1:
@@ -91,7 +91,8 @@ class ResNetExecutor:
         self.dtype = dtype
         self.grad_ready = grad_ready or (lambda pid: None)
         self.syncbn_group = syncbn_group
-        self.wgrad_blocks = wgrad_blocks
+        self.wgrad_blocks = wgrad_blocks  # split-K targets (tools/conv_bench.py sweep: 3x3 best ~2048, 1x1 ~512)
+        self.wgrad_blocks_1x1 = wgrad_blocks_1x1
         derived_maps: List[torch.Tensor] = []
         off = [0]
 
@@ -228,21 +229,17 @@ class ResNetExecutor:
             return
         bm, bn = _conv_tile(c.cin)
         bk = 64 if c.cout % 64 == 0 else 32
-        for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases:
-            Pm = (H - ph + c.st - 1) // c.st
-            Qm = (W - pw + c.st - 1) // c.st
-            if Pm <= 0 or Qm <= 0:
-                continue
-            wt = self.derived[doff:doff + dn]
-            self.C.conv_fwd(dy, wt, dx, res, None, N, P, Q, c.cout, c.cin, T, U, Pm, Qm, 1, 1, ioff_h, ioff_w, -1, -1,
-                            H, W, c.st, c.st, ph, pw, bm, bn, bk, 0)
+        phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
+                  if H - ph > 0 and W - pw > 0]
+        self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk)
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
                win=False, dil=1):
         key = (cout, R, S, C, N * P * Q, win)
         plan = self._plans.get(key)
         if plan is None:
-            plan = tuple(self.C.conv_wgrad_plan(cout, R, S, C, N * P * Q, self.wgrad_blocks, win))[:2]
+            target = self.wgrad_blocks if R * S > 1 else self.wgrad_blocks_1x1
+            plan = tuple(self.C.conv_wgrad_plan(cout, R, S, C, N * P * Q, target, win))[:2]
             self._plans[key] = plan
         splits, pps = plan
         ldw = R * S * C

@@ -1,8 +1,10 @@
 """Model registry by name (reference: `dataparallel.py:36-37` builds ``--arch`` choices from every
 lowercase callable in ``torchvision.models``; `:112-117` instantiates ``models.__dict__[arch]()``).
 
-torchvision is not available offline here, so the registry is ours: the ResNet family with
-torchvision-identical parameter names, shapes and initialisation.  ``pretrained=True`` loads weights
+torchvision is not available offline here, so the registry is ours, with torchvision-identical
+parameter names, shapes and initialisation: ResNet / ResNeXt / Wide-ResNet (native executor on GPU),
+AlexNet, VGG (with and without BN), SqueezeNet, DenseNet, MobileNetV2 and ShuffleNetV2 (stock-PyTorch
+engine).  ``pretrained=True`` loads weights
 from a LOCAL torchvision-format checkpoint (``--pretrained-path`` or ``$PDT_PRETRAINED_DIR/<arch>.pth``)
 with the safe ``weights_only`` loader -- the GPU box has no network.
 """
@@ -13,7 +15,7 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
-from . import resnet
+from . import classic, mobile, resnet
 
 _REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
     "resnet18": resnet.resnet18,
@@ -25,6 +27,15 @@ _REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
     "resnext101_32x8d": resnet.resnext101_32x8d,
     "wide_resnet50_2": resnet.wide_resnet50_2,
     "wide_resnet101_2": resnet.wide_resnet101_2,
+    "alexnet": classic.alexnet,
+    "vgg11": classic.vgg11, "vgg11_bn": classic.vgg11_bn, "vgg13": classic.vgg13, "vgg13_bn": classic.vgg13_bn,
+    "vgg16": classic.vgg16, "vgg16_bn": classic.vgg16_bn, "vgg19": classic.vgg19, "vgg19_bn": classic.vgg19_bn,
+    "squeezenet1_0": classic.squeezenet1_0, "squeezenet1_1": classic.squeezenet1_1,
+    "densenet121": mobile.densenet121, "densenet161": mobile.densenet161, "densenet169": mobile.densenet169,
+    "densenet201": mobile.densenet201,
+    "mobilenet_v2": mobile.mobilenet_v2,
+    "shufflenet_v2_x0_5": mobile.shufflenet_v2_x0_5, "shufflenet_v2_x1_0": mobile.shufflenet_v2_x1_0,
+    "shufflenet_v2_x1_5": mobile.shufflenet_v2_x1_5, "shufflenet_v2_x2_0": mobile.shufflenet_v2_x2_0,
 }
 
 

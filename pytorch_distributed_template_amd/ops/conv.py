@@ -90,14 +90,17 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
     bm, bn = conv_tile(C)
     bk = 64 if K % 64 == 0 else 32
     wflat = w.reshape(-1)
+    pieces, phases, off = [], [], 0
     for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(R, S, stride, pad):
-        Pm, Qm = (H - ph + stride - 1) // stride, (W - pw + stride - 1) // stride
-        if Pm <= 0 or Qm <= 0:
+        if H - ph <= 0 or W - pw <= 0:
             continue
         idx = dgrad_weight_index(K, C, R, S, rs, ss).to(w.device)
-        wt = wflat[idx].contiguous() if idx.numel() else torch.empty(0, dtype=w.dtype, device=w.device)
-        native.C.conv_fwd(dy, wt, dx, residual, None, N, P, Q, K, C, len(rs), len(ss), Pm, Qm, 1, 1, ioff_h, ioff_w,
-                          -1, -1, H, W, stride, stride, ph, pw, bm, bn, bk, 0)
+        if idx.numel():
+            pieces.append(wflat[idx])
+        phases.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, off])
+        off += idx.numel()
+    wt = torch.cat(pieces).contiguous() if pieces else torch.zeros(1, dtype=w.dtype, device=w.device)
+    native.C.conv_dgrad(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk)
     return dx
 
 

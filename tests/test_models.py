@@ -15,6 +15,24 @@ def test_param_counts(arch, nparams, ntensors):
     assert len(ps) == ntensors
 
 
+@pytest.mark.parametrize("arch,nparams", [
+    ("alexnet", 61100840), ("vgg11", 132863336), ("vgg16", 138357544), ("vgg16_bn", 138365992),
+    ("vgg19_bn", 143678248), ("squeezenet1_0", 1248424), ("squeezenet1_1", 1235496), ("densenet121", 7978856),
+    ("densenet161", 28681000), ("mobilenet_v2", 3504872), ("shufflenet_v2_x1_0", 2278604),
+    ("resnext50_32x4d", 25028904), ("wide_resnet50_2", 68883240)])
+def test_other_families_param_counts(arch, nparams):
+    """torchvision parameter counts (pins the exact architectures)."""
+    assert sum(p.numel() for p in registry.create(arch).parameters()) == nparams
+
+
+@pytest.mark.parametrize("arch", ["alexnet", "vgg11_bn", "squeezenet1_1", "densenet121", "mobilenet_v2",
+                                  "shufflenet_v2_x0_5"])
+def test_other_families_forward(arch):
+    m = registry.create(arch, num_classes=7).eval()
+    with torch.no_grad():
+        assert m(torch.randn(1, 3, 96 if arch != "alexnet" else 127, 96 if arch != "alexnet" else 127)).shape == (1, 7)
+
+
 def test_state_dict_keys():
     sd = registry.create("resnet18").state_dict()
     for k in ["conv1.weight", "bn1.weight", "bn1.running_mean", "bn1.num_batches_tracked", "layer1.0.conv1.weight",

@@ -1,0 +1,84 @@
+"""Per-layer conv kernel timing sweep (ResNet-18 shapes at B=1200) over tile configs.
+
+    python tools/conv_bench.py [--batch 1200] [--reps 5]
+
+Prints TFLOP/s for forward (each supported (BM, BN) tile), backward-data and weight-gradient
+(several split targets) of every distinct ResNet-18 conv shape.  Used to pick the per-shape tile table.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from pytorch_distributed_template_amd.ops import conv, native
+
+SHAPES = [  # H, Cin, Cout, k, stride
+    (56, 64, 64, 3, 1), (56, 64, 128, 3, 2), (28, 128, 128, 3, 1), (56, 64, 128, 1, 2),
+    (28, 128, 256, 3, 2), (14, 256, 256, 3, 1), (28, 128, 256, 1, 2), (14, 256, 512, 3, 2),
+    (7, 512, 512, 3, 1), (14, 256, 512, 1, 2),
+]
+FWD_TILES = [(128, 128), (256, 64), (128, 64), (64, 128)]
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1200)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    C = native.C
+    dev = "cuda"
+    res = []
+    for (H, ci, co, k, st) in SHAPES:
+        pad = k // 2
+        N = a.batch
+        P = (H + 2 * pad - k) // st + 1
+        x = torch.randn(N, H, H, ci, device=dev).to(torch.bfloat16)
+        w = (torch.randn(co, k, k, ci, device=dev) * 0.05).to(torch.bfloat16)
+        dy = torch.randn(N, P, P, co, device=dev).to(torch.bfloat16)
+        y = torch.empty(N, P, P, co, device=dev, dtype=torch.bfloat16)
+        flops = 2.0 * N * P * P * co * ci * k * k
+        row = {"shape": [H, ci, co, k, st]}
+        for (bm, bn) in FWD_TILES:
+            if co % bn:
+                continue
+            def f(bm=bm, bn=bn):
+                C.conv_fwd(x, w, y, None, None, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1,
+                           0, 0, bm, bn, 64, 0)
+            row[f"fwd_{bm}x{bn}"] = round(flops / timeit(f, a.reps) / 1e9, 1)
+        dx = torch.empty(N, H, H, ci, device=dev, dtype=torch.bfloat16)
+        pieces, phases, off = [], [], 0
+        for ph, pw, rs, ss, ih, iw in conv.dgrad_phases(k, k, st, pad):
+            idx = conv.dgrad_weight_index(co, ci, k, k, rs, ss).to(dev)
+            if idx.numel():
+                pieces.append(w.reshape(-1)[idx])
+            phases.append([ph, pw, len(rs), len(ss), ih, iw, off])
+            off += idx.numel()
+        wt = torch.cat(pieces).contiguous()
+        bm, bn = conv.conv_tile(ci)
+        row["dgrad"] = round(flops / timeit(lambda: C.conv_dgrad(dy, wt, dx, None, N, P, P, co, ci, H, H, st, phases,
+                                                                 bm, bn, 64), a.reps) / 1e9, 1)
+        for tb in (256, 512, 1024, 2048):
+            row[f"wgrad_{tb}"] = round(flops / timeit(lambda tb=tb: conv.conv_wgrad(x, dy, k, k, st, pad, tb), a.reps) / 1e9, 1)
+        print(json.dumps(row), flush=True)
+        res.append(row)
+        del x, w, dy, y
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -30,6 +30,10 @@ for stage in "$@"; do
       cd "${GRAFT_REPO_ROOT:-/root/repo}"
       tail -5 gpurun_out/prof.log
       [ $rc -eq 0 ] || { echo "prof failed rc=$rc"; exit $rc; } ;;
+    convbench)
+      timeout -k 10 600 python tools/conv_bench.py > gpurun_out/conv_bench.log 2>&1; rc=$?
+      cat gpurun_out/conv_bench.log | grep shape
+      [ $rc -eq 0 ] || { echo "conv_bench failed rc=$rc"; exit $rc; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
       tail -5 gpurun_out/smoke.log
