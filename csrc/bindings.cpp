@@ -78,7 +78,8 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   if (cs <= 0) cs = C;
   TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv_fwd: mixed dtypes");
   TORCH_CHECK(x.numel() == N * H * W * cs, "conv_fwd: x has ", x.numel(), " elements, geometry needs ", N * H * W * cs);
-  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "conv_fwd: input exceeds 2^31 elements (32-bit offsets)");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && w.numel() < (int64_t(1) << 30),
+              "conv_fwd: operands exceed 2 GiB (32-bit buffer offsets)");
   if (cs != C) {  // window mode: every tap's C-element chunk must stay inside the padded image
     TORCH_CHECK(cs == 4 && C % 32 == 0 && tstep_w == 0 && U == 1 && ioff_h >= 0 && ioff_w >= 0 &&
                     (Pm - 1) * ist_h + ioff_h + (T - 1) * tstep_h < H &&
@@ -120,7 +121,8 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res,
   const int dt = dt16(dy, "dy");
   TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "conv_dgrad: mixed dtypes");
   TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv_dgrad: size mismatch");
-  TORCH_CHECK(dy.numel() < (int64_t(1) << 31), "conv_dgrad: dY exceeds 2^31 elements");
+  TORCH_CHECK(dy.numel() < (int64_t(1) << 30) && wt.numel() < (int64_t(1) << 30),
+              "conv_dgrad: operands exceed 2 GiB (32-bit buffer offsets)");
   TORCH_CHECK(!phases.empty() && phases.size() <= 4, "conv_dgrad: 1..4 phases");
   TORCH_CHECK(K % bk == 0 && C % bn == 0, "conv_dgrad: K % bk / C % bn must be 0");
   pdt::ConvFwdArgs a{};
@@ -168,8 +170,8 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad: mixed dtypes");
   TORCH_CHECK(C % 64 == 0 && Kout % 64 == 0, "conv_wgrad: C and Kout must be multiples of 64");
   TORCH_CHECK(x.numel() == N * H * W * cs && dy.numel() == N * Pm * Qm * Kout, "conv_wgrad: size mismatch");
-  TORCH_CHECK(x.numel() < (int64_t(1) << 31) && dy.numel() < (int64_t(1) << 31),
-              "conv_wgrad: operands exceed 2^31 elements (32-bit offsets)");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30),
+              "conv_wgrad: operands exceed 2 GiB (32-bit buffer offsets)");
   if (win) {  // stem window mode: rows h..h+1 and 8 pixels from w must lie inside the padded image
     TORCH_CHECK(cs == 4 && C == 64 && U == 1 && pad_h == 0 && pad_w == 0 &&
                     (Pm - 1) * stride_h + (T - 1) * dil_h + 1 < H && ((Qm - 1) * stride_w + 8) <= W,

@@ -73,6 +73,19 @@ PDT_DEVICE uint32_t fdiv(uint32_t x, FastDiv f) {
   return f.mul ? (__umulhi(x, f.mul) >> f.shift) : (x >> f.shift);
 }
 
+// Raw buffer resource (stride 0): LDS-DMA through buffer_load ... lds.  A byte offset at or beyond
+// num_records reads zeros in hardware, which is how padding / tails are zero-filled (kOOB).
+typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr uint32_t kOOB = 0x80000000u;
+
+PDT_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+PDT_DEVICE void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds_dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
+}
+
 // XCD-aware bijective remap of a 1-D block index: blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so give each XCD a contiguous range of logical tiles
 // (speed only, never correctness: any placement is valid).

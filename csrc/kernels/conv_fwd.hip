@@ -16,7 +16,8 @@
 // lane's accumulator holds 4 consecutive output channels of one pixel (8-byte NHWC stores).
 //
 // Tiles are staged global->LDS with LDS-DMA (global_load_lds_dwordx4, 16 B/lane) into two LDS
-// buffers; out-of-bounds rows (padding, M tail) DMA from a zero page.  The LDS image is linear per
+// buffers (buffer_load ... lds); out-of-bounds rows (padding, M tail) read zeros through the buffer
+// resource range check.  The LDS image is linear per
 // wave-instruction and XOR-swizzled through the SOURCE address (chunk ^= (row>>1)&(chunks-1)), which
 // makes the ds_read_b128 fragment reads bank-conflict free.  Optional epilogues: residual add (used
 // to fuse the identity-gradient add of a residual block into dgrad) and per-channel BatchNorm
@@ -33,7 +34,7 @@ typedef __attribute__((address_space(1))) void glb_void;
 template <int CHUNKS>
 PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
-template <int DT, int BM, int BN, int BK, int WAVES_N, bool STATS, bool RES>
+template <int DT, int BM, int BN, int BK, int WAVES_N, bool STATS, bool RES, int STAGES>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   constexpr int A_BYTES = BN * ROWB;
   constexpr int STAGE = (BN + BM) * ROWB;
   static_assert(A_INSTR * RPI * 4 == BN && B_INSTR * RPI * 4 == BM, "tile/instr mismatch");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -79,58 +80,62 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   const int csteps = a.C / BK;
   const int ksteps = TU * csteps;
 
-  // ---- per-lane source rows for the activation tile ----
+  // ---- LDS-DMA sources: buffer resources over x and w; out-of-range byte offsets read zeros ----
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)a.Kout * TU * a.C * 2u);
+
+  // activation rows: per-lane (h0, w0) and byte offset of (image, h0, w0, chunk); the per-K-step
+  // tap/channel displacement is wave-uniform and added per step
   const int lrow = lane / CHUNKS;      // row within one DMA instruction
   const int pchunk = lane % CHUNKS;    // physical (LDS) chunk this lane writes
-  uint32_t brow_img[B_INSTR];
-  int brow_h[B_INSTR], brow_w[B_INSTR], bchunk[B_INSTR];
+  int brow_h[B_INSTR], brow_w[B_INSTR], brow_off[B_INSTR];
 #pragma unroll
   for (int j = 0; j < B_INSTR; ++j) {
     const int row = (wave * B_INSTR + j) * RPI + lrow;
     const int64_t m = m0 + row;
-    bchunk[j] = pchunk ^ swz<CHUNKS>(row);
+    const int bch = pchunk ^ swz<CHUNKS>(row);
     if (m < a.M) {
       const int nimg = (int)(m / PQ);
       const int rem = (int)(m - (int64_t)nimg * PQ);
       const int i = rem / a.Qm, jj = rem - (rem / a.Qm) * a.Qm;
       brow_h[j] = i * a.ist_h + a.ioff_h;
       brow_w[j] = jj * a.ist_w + a.ioff_w;
-      brow_img[j] = (uint32_t)nimg * (uint32_t)(a.H * a.W);
+      brow_off[j] = (((nimg * a.H + brow_h[j]) * a.W + brow_w[j]) * a.cs + bch * 8) * 2;
     } else {
       brow_h[j] = -(1 << 29);
       brow_w[j] = 0;
-      brow_img[j] = 0;
+      brow_off[j] = 0;
     }
   }
-  const uint16_t* arow_base[A_INSTR];
-  int achunk[A_INSTR];
+  uint32_t arow_off[A_INSTR];
 #pragma unroll
   for (int j = 0; j < A_INSTR; ++j) {
     const int row = (wave * A_INSTR + j) * RPI + lrow;
-    achunk[j] = pchunk ^ swz<CHUNKS>(row);
-    arow_base[j] = a.w + (int64_t)(n0 + row) * TU * a.C;
+    arow_off[j] = (uint32_t)(((n0 + row) * TU * a.C + (pchunk ^ swz<CHUNKS>(row)) * 8) * 2);
   }
 
-  auto stage_load = [&](int ks, int buf) {
-    const int tap = ks / csteps;
-    const int c0 = (ks - tap * csteps) * BK;
-    const int t = tap / a.U, u = tap - (tap / a.U) * a.U;
-    char* sbase = smem + buf * STAGE;
-#pragma unroll
-    for (int j = 0; j < A_INSTR; ++j) {
-      const uint16_t* src = arow_base[j] + tap * a.C + c0 + achunk[j] * 8;
-      lds_void* dst = (lds_void*)(sbase + (wave * A_INSTR + j) * 1024);
-      __builtin_amdgcn_global_load_lds((glb_void*)src, dst, 16, 0, 0);
+  // load cursor over (t, u, c0) in K-step order: advanced incrementally (no per-step divisions)
+  int cur_t = 0, cur_u = 0, cur_c = 0;
+  auto stage_load = [&](int buf) {
+    const int t = cur_t, u = cur_u, c0 = cur_c;
+    const int tap = t * a.U + u;
+    cur_c += BK;
+    if (cur_c == a.C) {
+      cur_c = 0;
+      if (++cur_u == a.U) { cur_u = 0; ++cur_t; }
     }
+    char* sbase = smem + buf * STAGE;
+    const uint32_t a_delta = (uint32_t)(tap * a.C + c0) * 2u;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j) buf_lds16(rw, sbase + (wave * A_INSTR + j) * 1024, arow_off[j] + a_delta);
     const int dh = t * a.tstep_h, dw = u * a.tstep_w;
+    const int b_delta = ((dh * a.W + dw) * a.cs + c0) * 2;
 #pragma unroll
     for (int j = 0; j < B_INSTR; ++j) {
       const int h = brow_h[j] + dh, w = brow_w[j] + dw;
       const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const uint32_t off = (brow_img[j] + (uint32_t)(h * a.W + w)) * (uint32_t)a.cs + (uint32_t)(c0 + bchunk[j] * 8);
-      const uint16_t* src = ok ? a.x + off : (const uint16_t*)a.zero;
-      lds_void* dst = (lds_void*)(sbase + A_BYTES + (wave * B_INSTR + j) * 1024);
-      __builtin_amdgcn_global_load_lds((glb_void*)src, dst, 16, 0, 0);
+      const uint32_t voff = ok ? (uint32_t)(brow_off[j] + b_delta) : kOOB;
+      buf_lds16(rx, sbase + A_BYTES + (wave * B_INSTR + j) * 1024, voff);
     }
   };
 
@@ -148,36 +153,65 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
 #pragma unroll
   for (int j = 0; j < FM; ++j) b_off[j] = A_BYTES + (wm * WM + j * 16 + fr) * ROWB;
 
-  if (ksteps > 0) {
-    stage_load(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int ks = 0; ks < ksteps; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < ksteps) stage_load(ks + 1, cur ^ 1);
-      const char* sb = smem + cur * STAGE;
+  auto compute_stage = [&](const char* sb) {
 #pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        vec8 af[FN], bfr[FM];
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      vec8 af[FN], bfr[FM];
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-          const int row = wn * WN + i * 16 + fr;
-          const int ch = (kk * 4 + fq) ^ swz<CHUNKS>(row);
-          af[i] = *(const vec8*)(sb + a_off[i] + ch * 16);
-        }
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-          const int row = wm * WM + j * 16 + fr;
-          const int ch = (kk * 4 + fq) ^ swz<CHUNKS>(row);
-          bfr[j] = *(const vec8*)(sb + b_off[j] + ch * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-          for (int j = 0; j < FM; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      for (int i = 0; i < FN; ++i) {
+        const int row = wn * WN + i * 16 + fr;
+        const int ch = (kk * 4 + fq) ^ swz<CHUNKS>(row);
+        af[i] = *(const vec8*)(sb + a_off[i] + ch * 16);
       }
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int row = wm * WM + j * 16 + fr;
+        const int ch = (kk * 4 + fq) ^ swz<CHUNKS>(row);
+        bfr[j] = *(const vec8*)(sb + b_off[j] + ch * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  if constexpr (STAGES == 2) {
+    if (ksteps > 0) {
+      stage_load(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      for (int ks = 0; ks < ksteps; ++ks) {
+        const int cur = ks & 1;
+        if (ks + 1 < ksteps) stage_load(cur ^ 1);
+        compute_stage(smem + cur * STAGE);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else {
+    // 3-stage LDS ring: two K-steps of LDS-DMA stay in flight; each iteration waits (counted vmcnt,
+    // never 0) only for the stage it is about to read, then a raw s_barrier publishes it to all waves.
+    // The buffer refilled in iteration ks was last read in iteration ks-1, which every wave finished
+    // before passing this iteration's barrier.
+    constexpr int PER_STAGE = A_INSTR + B_INSTR;  // LDS-DMA instructions per wave per stage
+    constexpr int WAIT_ONE = (PER_STAGE & 0xF) | ((PER_STAGE >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+    if (ksteps > 0) {
+      stage_load(0);
+      if (ksteps > 1) stage_load(1);
+      int buf = 0;
+      for (int ks = 0; ks < ksteps; ++ks) {
+        if (ks + 1 < ksteps)
+          __builtin_amdgcn_s_waitcnt(WAIT_ONE);  // stage ks landed, stage ks+1 may still be in flight
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (ks + 2 < ksteps) stage_load(buf == 0 ? 2 : buf - 1);
+        compute_stage(smem + buf * STAGE);
+        buf = buf == 2 ? 0 : buf + 1;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
   }
 
@@ -268,7 +302,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
 }
 
 // ----------------------------------------------------------------------------------------------
-template <int DT, int BM, int BN, int BK, int WAVES_N>
+template <int DT, int BM, int BN, int BK, int WAVES_N, int STAGES>
 static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
   int gx = a.m_tiles * a.n_tiles;
   if (a.nphase > 0) {
@@ -278,13 +312,13 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
   dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(256);
   const bool st = a.stats != nullptr, rs = a.res != nullptr;
   if (st && rs)
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, true, STAGES>), grid, block, 0, s, a);
   else if (st)
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, false>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, false, STAGES>), grid, block, 0, s, a);
   else if (rs)
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, true, STAGES>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, false>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, false, STAGES>), grid, block, 0, s, a);
 }
 
 // per-device address of this code object's zero page (device globals are per device)
@@ -311,17 +345,18 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   } else if (a.m_tiles * a.n_tiles == 0) {
     return;
   }
-#define PDT_CFG(BM_, BN_, BK_, WN_)                                      \
+#define PDT_CFG(BM_, BN_, BK_, WN_, ST_)                                 \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
-    launch_cfg<DT, BM_, BN_, BK_, WN_>(a, s);                            \
+    launch_cfg<DT, BM_, BN_, BK_, WN_, ST_>(a, s);                       \
     return;                                                              \
   }
-  PDT_CFG(128, 128, 64, 2)
-  PDT_CFG(256, 64, 64, 1)
-  PDT_CFG(128, 64, 64, 1)
-  PDT_CFG(128, 128, 32, 2)
-  PDT_CFG(256, 64, 32, 1)
-  PDT_CFG(64, 128, 64, 4)
+  // BK = 64 tiles: 2-stage ring; BK = 32 tiles: 3-stage ring (counted vmcnt, more latency hiding)
+  PDT_CFG(128, 128, 64, 2, 2)
+  PDT_CFG(256, 64, 64, 1, 2)
+  PDT_CFG(128, 64, 64, 1, 2)
+  PDT_CFG(128, 128, 32, 2, 3)
+  PDT_CFG(256, 64, 32, 1, 3)
+  PDT_CFG(64, 128, 64, 4, 2)
 #undef PDT_CFG
   pdt_hip_fail("conv_fwd: unsupported tile config", hipErrorInvalidValue, __FILE__, __LINE__);
 }

@@ -24,31 +24,28 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 // chunk swizzle for a [pixel][64 ch] (128-B row) image read by ds_read_b64_tr_b16
 PDT_DEVICE int tr_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
-// Source row of one DMA lane: pixel p of the K-step, X gathered through the tap, dY linear.
-// Branch-free 32-bit offset arithmetic (tensors < 2^31 elements); out-of-range rows read the zero page.
+// Byte offsets of one DMA lane's source rows for pixel p of the K-step: X gathered through the tap,
+// dY linear.  32-bit arithmetic; padding reads kOOB (zeros) and pixels past the end of the tensors land
+// beyond the buffers' num_records (zeros), so no per-lane "live" test is needed (splits are multiples
+// of the K-step).
 template <bool WIN>
-PDT_DEVICE void wgrad_rows(const ConvWgradArgs& a, int p, int pix_end, int th, int tw, int xcol, int lch,
-                           int ycol, const uint16_t*& xs, const uint16_t*& ys) {
+PDT_DEVICE void wgrad_rows(const ConvWgradArgs& a, int p, int th, int tw, int xcol, int lch, int ycol,
+                           uint32_t& xoff, uint32_t& yoff) {
   const FastDiv dpq{a.div_pq_mul, a.div_pq_shift}, dq{a.div_q_mul, a.div_q_shift};
   const int PQ = a.Pm * a.Qm;
-  const bool live = p < pix_end;
-  const int pp = live ? p : 0;
-  const int nimg = (int)fdiv((uint32_t)pp, dpq);
-  const int rem = pp - nimg * PQ;
+  const int nimg = (int)fdiv((uint32_t)p, dpq);
+  const int rem = p - nimg * PQ;
   const int i = (int)fdiv((uint32_t)rem, dq);
   const int jj = rem - i * a.Qm;
   const int h = i * a.stride_h + th, w = jj * a.stride_w + tw;
-  const uint16_t* zero = (const uint16_t*)a.zero;
-  const uint32_t img = (uint32_t)nimg * (uint32_t)(a.H * a.W);
   if constexpr (WIN) {
-    const uint32_t off = (img + (uint32_t)((h + (lch >> 2)) * a.W + w)) * (uint32_t)a.cs + (uint32_t)((lch & 3) * 8);
-    xs = live ? a.x + off : zero;
+    xoff = (uint32_t)((((nimg * a.H + h + (lch >> 2)) * a.W + w) * a.cs + (lch & 3) * 8) * 2);
   } else {
-    const bool ok = live && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-    const uint32_t off = (img + (uint32_t)(h * a.W + w)) * (uint32_t)a.cs + (uint32_t)(xcol + lch * 8);
-    xs = ok ? a.x + off : zero;
+    const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+    const uint32_t off = (uint32_t)((((nimg * a.H + h) * a.W + w) * a.cs + xcol + lch * 8) * 2);
+    xoff = ok ? off : kOOB;
   }
-  ys = live ? a.dy + ((uint32_t)pp * (uint32_t)a.Kout + (uint32_t)(ycol + lch * 8)) : zero;
+  yoff = (uint32_t)(p * a.Kout + ycol + lch * 8) * 2u;
 }
 
 // WIN: the ResNet stem's "window" mode.  X is the zero-padded NHWC4 image and a 64-wide tile column
@@ -90,6 +87,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
 
   const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
 
   // DMA lane geometry: 8 rows x 8 chunks per 1 KiB instruction
   const int lrow = lane >> 3, pch = lane & 7;
@@ -101,10 +100,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int row = (wave * 4 + j) * 8 + lrow;  // 0..127
       const int lch = pch ^ tr_swz(row);
-      const uint16_t *xs, *ys;
-      wgrad_rows<WIN>(a, pbase + row, pix_end, th, tw, c0, lch, k0, xs, ys);
-      __builtin_amdgcn_global_load_lds((glb_void*)xs, (lds_void*)(sb + (wave * 4 + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_void*)ys, (lds_void*)(sb + XB + (wave * 4 + j) * 1024), 16, 0, 0);
+      uint32_t xo, yo;
+      wgrad_rows<WIN>(a, pbase + row, th, tw, c0, lch, k0, xo, yo);
+      buf_lds16(rx, sb + (wave * 4 + j) * 1024, xo);
+      buf_lds16(ry, sb + XB + (wave * 4 + j) * 1024, yo);
     }
   };
 
@@ -226,6 +225,8 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
 
   const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
 
   // DMA lane geometry: 4 rows x 16 chunks per 1 KiB instruction
   const int lrow = lane >> 4, pch = lane & 15;
@@ -237,10 +238,10 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int row = (wave * 4 + j) * 4 + lrow;  // 0..63
       const int lch = pch ^ tr_swz16(row);
-      const uint16_t *xs, *ys;
-      wgrad_rows<false>(a, pbase + row, pix_end, th, tw, c0, lch, k0, xs, ys);
-      __builtin_amdgcn_global_load_lds((glb_void*)xs, (lds_void*)(sb + (wave * 4 + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_void*)ys, (lds_void*)(sb + XB + (wave * 4 + j) * 1024), 16, 0, 0);
+      uint32_t xo, yo;
+      wgrad_rows<false>(a, pbase + row, th, tw, c0, lch, k0, xo, yo);
+      buf_lds16(rx, sb + (wave * 4 + j) * 1024, xo);
+      buf_lds16(ry, sb + XB + (wave * 4 + j) * 1024, yo);
     }
   };
 

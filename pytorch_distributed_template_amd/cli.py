@@ -120,6 +120,11 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--resume", default="", metavar="PATH", help="resume from a checkpoint written by this framework")
     g.add_argument("--pretrained-path", default=None, help="local torchvision-format weights for --pretrained")
     g.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    g.add_argument("--dist-timeout", type=float, default=1800.0,
+                   help="collective timeout in seconds (a hung rank fails the job instead of hanging it)")
+    g.add_argument("--profile", default=False, type=str2bool, nargs="?", const=True,
+                   help="roctx ranges around train/eval steps (visible in rocprofv3 --marker-trace) and a "
+                        "per-epoch throughput line")
     g.add_argument("--use-gpus-flag", default=False, type=str2bool, nargs="?", const=True,
                    help="honour --gpus by setting HIP_VISIBLE_DEVICES (the reference ignores --gpus)")
     g.add_argument("--no-tensorboard", dest="tensorboard", action="store_false")

@@ -13,6 +13,7 @@ The printed running averages are identical either way.
 """
 from __future__ import annotations
 
+import datetime
 import os
 import random
 import time
@@ -30,6 +31,7 @@ from ..optim.lr import build_scheduler
 from ..utils.io import load_checkpoint, make_checkpoint_state, output_process, save_checkpoint, write_settings
 from ..utils.logging import close_logger, ddp_print, get_logger
 from ..utils.meters import AverageMeter, get_learning_rate
+from ..utils.profiling import roctx_range
 from ..utils.tensorboard import SummaryWriter
 
 NATIVE_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2")
@@ -92,15 +94,18 @@ def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, de
     if args.iters_per_epoch:
         n_iter = min(n_iter, args.iters_per_epoch)
     lr = get_learning_rate(trainer.optimizer)
-    end = time.time()
+    end = t_start = time.time()
+    seen = 0
     for i, (images, target) in enumerate(loader):
         if i >= n_iter:
             break
         data_times.update(time.time() - end)
         images = images.to(device, non_blocking=True)
         target = target.to(device, non_blocking=True)
-        _, met = trainer.train_step(images, target)
+        with roctx_range("train_step", args.profile):
+            _, met = trainer.train_step(images, target)
         meter.update(met, images.size(0))
+        seen += images.size(0)
         if args.strict_sync:
             if dist.is_initialized():
                 dist.barrier()
@@ -115,6 +120,10 @@ def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, de
     loss_avg, acc_avg = meter.avg()
     ddp_print("||==> Train epoch: [{:d}/{:d}]\tlr={:.6f}\tce_loss={:.4f}\ttop1_acc={:.4f}\tbatch_time={:6.3f}s"
               .format(epoch, args.epochs, lr, loss_avg, acc_avg, batch_times.avg), logger, rank)
+    if args.profile:
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        ddp_print("||==> Train throughput: {:.1f} img/s (node, {} ranks)".format(
+            seen * world / max(time.time() - t_start, 1e-9), world), logger, rank)
     if rank == 0 and writer is not None:
         writer.add_scalar("lr", lr, epoch)
         writer.add_scalar("Train_ce_loss", loss_avg, epoch)
@@ -135,7 +144,8 @@ def validate(loader, trainer, epoch: int, args, logger, writer, rank: int, devic
                 break
             images = images.to(device, non_blocking=True)
             target = target.to(device, non_blocking=True)
-            _, met = trainer.eval_step(images, target)
+            with roctx_range("eval_step", args.profile):
+                _, met = trainer.eval_step(images, target)
             meter.update(met, images.size(0))
             if args.strict_sync:
                 if dist.is_initialized():
@@ -212,10 +222,11 @@ def main(mode: str, argv: Optional[list] = None) -> int:
         device = torch.device("cpu")
     if distributed:
         backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if on_gpu else "gloo")
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         if backend == "nccl":
-            dist.init_process_group(backend, device_id=device)
+            dist.init_process_group(backend, device_id=device, timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     args.nprocs = world if mode != "dp" else max(1, torch.cuda.device_count() if on_gpu else 1)
 
     if rank == 0:

@@ -20,7 +20,7 @@ SHAPES = [  # H, Cin, Cout, k, stride
     (28, 128, 256, 3, 2), (14, 256, 256, 3, 1), (28, 128, 256, 1, 2), (14, 256, 512, 3, 2),
     (7, 512, 512, 3, 1), (14, 256, 512, 1, 2),
 ]
-FWD_TILES = [(128, 128), (256, 64), (128, 64), (64, 128)]
+FWD_TILES = [(128, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64), (256, 64, 32), (128, 128, 32)]
 
 
 def timeit(fn, reps):
@@ -53,13 +53,13 @@ def main():
         y = torch.empty(N, P, P, co, device=dev, dtype=torch.bfloat16)
         flops = 2.0 * N * P * P * co * ci * k * k
         row = {"shape": [H, ci, co, k, st]}
-        for (bm, bn) in FWD_TILES:
+        for (bm, bn, bk) in FWD_TILES:
             if co % bn:
                 continue
-            def f(bm=bm, bn=bn):
+            def f(bm=bm, bn=bn, bk=bk):
                 C.conv_fwd(x, w, y, None, None, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1,
-                           0, 0, bm, bn, 64, 0)
-            row[f"fwd_{bm}x{bn}"] = round(flops / timeit(f, a.reps) / 1e9, 1)
+                           0, 0, bm, bn, bk, 0)
+            row[f"fwd_{bm}x{bn}x{bk}"] = round(flops / timeit(f, a.reps) / 1e9, 1)
         dx = torch.empty(N, H, H, ci, device=dev, dtype=torch.bfloat16)
         pieces, phases, off = [], [], 0
         for ph, pw, rs, ss, ih, iw in conv.dgrad_phases(k, k, st, pad):
