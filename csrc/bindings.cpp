@@ -22,6 +22,7 @@
 #include "kernels/loss.h"
 #include "kernels/optim.h"
 #include "kernels/pool.h"
+#include "kernels/stem.h"
 
 void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line) {
   char buf[512];
@@ -80,11 +81,15 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   TORCH_CHECK(x.numel() == N * H * W * cs, "conv_fwd: x has ", x.numel(), " elements, geometry needs ", N * H * W * cs);
   TORCH_CHECK(x.numel() < (int64_t(1) << 30) && w.numel() < (int64_t(1) << 30),
               "conv_fwd: operands exceed 2 GiB (32-bit buffer offsets)");
+  int pair_skip = 0;
   if (cs != C) {  // window mode: every tap's C-element chunk must stay inside the padded image
-    TORCH_CHECK(cs == 4 && C % 32 == 0 && tstep_w == 0 && U == 1 && ioff_h >= 0 && ioff_w >= 0 &&
-                    (Pm - 1) * ist_h + ioff_h + (T - 1) * tstep_h < H &&
-                    ((Qm - 1) * ist_w + ioff_w) * cs + C <= W * cs,
+    // C == 32: one kernel row per tap; C == 64: two consecutive kernel rows per tap (BK must be 64)
+    const int rows = C == 64 ? 2 : 1;
+    TORCH_CHECK(cs == 4 && (C == 32 || (C == 64 && bk == 64)) && tstep_w == 0 && U == 1 && ioff_h >= 0 &&
+                    ioff_w >= 0 && (Pm - 1) * ist_h + ioff_h + (T - 1) * tstep_h + rows - 1 < H &&
+                    ((Qm - 1) * ist_w + ioff_w) * cs + 32 <= W * cs,
                 "conv_fwd: window-mode geometry leaves the padded image");
+    if (C == 64) pair_skip = (int)(W * cs - 32);
   }
   TORCH_CHECK(w.numel() == Kout * T * U * C, "conv_fwd: w size mismatch");
   TORCH_CHECK(y.numel() == N * OH * OW * Kout, "conv_fwd: y size mismatch");
@@ -105,10 +110,39 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
     a.stats = pd(*stats, "stats");
   }
   a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm; a.cs = cs;
+  a.pair_skip = pair_skip;
   a.ist_h = ist_h; a.ist_w = ist_w; a.ioff_h = ioff_h; a.ioff_w = ioff_w; a.tstep_h = tstep_h; a.tstep_w = tstep_w;
   a.OH = OH; a.OW = OW; a.ost_h = ost_h; a.ost_w = ost_w; a.ooff_h = ooff_h; a.ooff_w = ooff_w;
+  TORCH_CHECK(M < (int64_t(1) << 31), "conv_fwd: N*Pm*Qm must be < 2^31 (32-bit pixel indexing)");
   a.M = M;
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+}
+
+// ResNet stem forward (7x7/2, 3 -> 64) over the zero-padded NHWC4 image with window-row weights
+// [64][7][32]; optional fp64 BN statistics slots.
+void stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& stats, int64_t N, int64_t Hp, int64_t Wp,
+              int64_t P, int64_t Q, int64_t blocks_per_cu) {
+  const int dt = dt16(xp, "xp");
+  TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "stem_fwd: mixed dtypes");
+  TORCH_CHECK(xp.numel() == N * Hp * Wp * 4 && w.numel() == 64 * 7 * 32 && y.numel() == N * P * Q * 64,
+              "stem_fwd: size mismatch");
+  TORCH_CHECK(xp.numel() * 2 < (int64_t(1) << 31) && N * P * Q < (int64_t(1) << 31),
+              "stem_fwd: input exceeds 2 GiB / 2^31 pixels (32-bit offsets)");
+  TORCH_CHECK(pdt::stem_fwd_supported((int)Hp, (int)Wp, (int)P, (int)Q),
+              "stem_fwd: unsupported geometry (needs Q <= 112, 13*Wp*8 <= 24 KiB and a padded image that covers "
+              "every 7x7 window)");
+  pdt::StemFwdArgs a{};
+  a.x = p16(xp, "xp");
+  a.x_bytes = (uint32_t)(xp.numel() * 2);
+  a.w = p16(w, "w");
+  a.y = p16(y, "y");
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * 64 * 2, "stem_fwd: stats buffer too small");
+    a.stats = pd(*stats, "stats");
+  }
+  a.N = (int)N; a.Hp = (int)Hp; a.Wp = (int)Wp; a.P = (int)P; a.Q = (int)Q;
+  a.blocks_per_cu = (int)std::max<int64_t>(1, blocks_per_cu);
+  pdt::stem_fwd_launch(a, dt, cur_stream());
 }
 
 int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (int)bm); }
@@ -149,6 +183,7 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res,
     a.pPm[i] = (int)Pm; a.pQm[i] = (int)Qm;
     maxM = std::max(maxM, N * Pm * Qm);
   }
+  TORCH_CHECK(maxM < (int64_t(1) << 31), "conv_dgrad: N*Pm*Qm must be < 2^31 (32-bit pixel indexing)");
   a.M = maxM;
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
 }
@@ -285,6 +320,34 @@ void maxpool_bwd_relu(const Tensor& dp, const Tensor& idx, const Tensor& y, cons
                                N, H, W, C, cur_stream());
 }
 
+// Stem backward (max-pool bwd + ReLU mask + BN bwd) without the 112x112 dz tensor: reduce pass ...
+void stem_pool_bwd_reduce(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& slots,
+                          int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int dt = dt16(dp, "dp");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dt16(y, "y") == dt && dp.numel() == N * OH * OW * C && y.numel() == N * H * W * C &&
+                  idx.numel() == dp.numel() && C % 8 == 0 && C <= 2048 && coef.numel() >= 4 * C,
+              "stem_pool_bwd_reduce: bad sizes");
+  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * 2, "stem_pool_bwd_reduce: slots too small");
+  check_dev(idx, "idx");
+  pdt::stem_pool_bwd_reduce_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"),
+                                   pd(slots, "slots"), N, H, W, C, cur_stream());
+}
+
+// ... and apply pass writing dy = A*dz + B*y + C (bcoef from bn_bwd_finalize)
+void stem_pool_bwd_apply(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef,
+                         const Tensor& bcoef, Tensor& dy, int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int dt = dt16(dp, "dp");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dt16(y, "y") == dt && dt16(dy, "dy") == dt && dp.numel() == N * OH * OW * C &&
+                  y.numel() == N * H * W * C && dy.numel() == y.numel() && idx.numel() == dp.numel() &&
+                  C % 8 == 0 && coef.numel() >= 2 * C && bcoef.numel() >= 3 * C,
+              "stem_pool_bwd_apply: bad sizes");
+  check_dev(idx, "idx");
+  pdt::stem_pool_bwd_apply_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"),
+                                  pf(bcoef, "bcoef"), p16(dy, "dy"), N, H, W, C, cur_stream());
+}
+
 void avgpool_fwd(const Tensor& x, Tensor& feat, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
   const int dt = dt16(x, "x");
   TORCH_CHECK(x.numel() == N * HW * C && feat.numel() >= N * ldf && C % 8 == 0, "avgpool_fwd: bad sizes");
@@ -403,6 +466,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("bn_relu_maxpool", &bn_relu_maxpool);
   m.def("maxpool_bwd_relu", &maxpool_bwd_relu);
+  m.def("stem_fwd", &stem_fwd);
+  m.def("stem_fwd_supported", [](int64_t Hp, int64_t Wp, int64_t P, int64_t Q) {
+    return pdt::stem_fwd_supported((int)Hp, (int)Wp, (int)P, (int)Q);
+  });
+  m.def("stem_pool_bwd_reduce", &stem_pool_bwd_reduce);
+  m.def("stem_pool_bwd_apply", &stem_pool_bwd_apply);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("xent", &xent);

@@ -39,8 +39,16 @@ template <> struct E16<kF16> {
   }
 };
 
-// Zero bytes used as the global source for out-of-bounds LDS-DMA lanes (zero padding).
-static __device__ uint4 g_zero16[8];
+
+// Inclusive scan over each 16-lane DPP row (row_shr 1, 2, 4, 8 with zero fill): lane 15 of every row
+// ends with the sum of the row's 16 values.  Pure VALU (no LDS permute traffic).
+PDT_DEVICE float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
 
 PDT_DEVICE float wave_sum(float v) {
 #pragma unroll

@@ -15,17 +15,19 @@ struct ConvFwdArgs {
   double* stats;        // optional: [kStatSlots][Kout][2] fp64 (sum, sumsq) BN statistics (nullptr = none)
   int N, H, W, C, Kout, T, U;
   int cs;                                              // elements per input pixel (normally == C)
+  int pair_skip;  // window-pair mode (stem, BK=64): chunks 4..7 read the NEXT image row (+pair_skip elements)
   int Pm, Qm;                                          // GEMM-M sub-grid (M = N*Pm*Qm)
   int ist_h, ist_w, ioff_h, ioff_w, tstep_h, tstep_w;  // in = i*ist + ioff + t*tstep
   int OH, OW, ost_h, ost_w, ooff_h, ooff_w;            // out = i*ost + ooff
-  int64_t M;
+  int64_t M;                                           // < 2^31 (32-bit fast division of pixel indices)
   int m_tiles, n_tiles;                                // filled by the launcher
-  const void* zero;                                    // zero page for out-of-bounds rows (launcher)
+  uint32_t pq_mul, pq_shift, q_mul, q_shift;           // FastDiv by Pm*Qm and Qm (filled by the launcher)
   // Multi-phase launch (backward-data of strided convs): blockIdx.y selects a phase whose geometry
   // overrides T, U, ioff, Pm, Qm, ooff and the weight offset.  nphase == 0: single-phase launch.
   int nphase;
   int pT[4], pU[4], pioff_h[4], pioff_w[4], pPm[4], pQm[4], pooff_h[4], pooff_w[4], pmt[4];
   int64_t pwoff[4];
+  uint32_t ppq_mul[4], ppq_shift[4], pq1_mul[4], pq1_shift[4];
 };
 
 void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s);

@@ -8,7 +8,9 @@
 //   * linear layers:       a 1x1 "conv" over [B,1,1,K]
 // ``cs`` is the element stride between input pixels (== C, except for the ResNet stem's "window" mode,
 // where X is the zero-padded NHWC4 image and one 32-wide reduction chunk spans 8 pixels x 4 channels
-// of a kernel row, so the 7x7/2 stem runs with no im2col buffer).
+// of a kernel row, so the 7x7/2 stem runs with no im2col buffer).  With C == 64 ("window-pair" mode)
+// one 64-wide chunk covers TWO consecutive kernel rows (chunks 0..3 row h, chunks 4..7 row h+1), so the
+// stem runs 4 BK=64 steps instead of 7 BK=32 steps.
 // The generalised geometry is
 //   in_h  = i*ist_h + ioff_h + t*tstep_h      (t in [0,T)),  same for w / u
 //   out_h = i*ost_h + ooff_h
@@ -23,6 +25,8 @@
 // to fuse the identity-gradient add of a residual block into dgrad) and per-channel BatchNorm
 // statistics (sum, sum of squares of the rounded outputs), reduced per block and accumulated with
 // fp64 atomics into kStatSlots slot copies (so no separate statistics pass over the output).
+#include <cstdlib>
+
 #include "../common.h"
 #include "conv_fwd.h"
 
@@ -46,6 +50,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
     a.m_tiles = args.pmt[ph];
     a.M = (int64_t)a.N * a.Pm * a.Qm;
     a.w = args.w + args.pwoff[ph];
+    a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
+    a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
     if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
   }
   using E = E16<DT>;
@@ -76,6 +82,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   const int n0 = tile_n * BN;
 
   const int PQ = a.Pm * a.Qm;
+  const FastDiv fd_pq{a.pq_mul, a.pq_shift}, fd_q{a.q_mul, a.q_shift};
   const int TU = a.T * a.U;
   const int csteps = a.C / BK;
   const int ksteps = TU * csteps;
@@ -95,12 +102,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
     const int64_t m = m0 + row;
     const int bch = pchunk ^ swz<CHUNKS>(row);
     if (m < a.M) {
-      const int nimg = (int)(m / PQ);
-      const int rem = (int)(m - (int64_t)nimg * PQ);
-      const int i = rem / a.Qm, jj = rem - (rem / a.Qm) * a.Qm;
+      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
+      const int rem = (int)m - nimg * PQ;
+      const int i = (int)fdiv((uint32_t)rem, fd_q), jj = rem - i * a.Qm;
       brow_h[j] = i * a.ist_h + a.ioff_h;
       brow_w[j] = jj * a.ist_w + a.ioff_w;
-      brow_off[j] = (((nimg * a.H + brow_h[j]) * a.W + brow_w[j]) * a.cs + bch * 8) * 2;
+      const int pair = (CHUNKS == 8 && bch >= 4) ? a.pair_skip : 0;
+      brow_off[j] = (((nimg * a.H + brow_h[j]) * a.W + brow_w[j]) * a.cs + bch * 8 + pair) * 2;
     } else {
       brow_h[j] = -(1 << 29);
       brow_w[j] = 0;
@@ -226,9 +234,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   for (int j = 0; j < FM; ++j) {
     const int64_t m = m0 + wm * WM + j * 16 + fr;
     if (m < a.M) {
-      const int nimg = (int)(m / PQ);
-      const int rem = (int)(m - (int64_t)nimg * PQ);
-      const int i_ = rem / a.Qm, j_ = rem - (rem / a.Qm) * a.Qm;
+      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
+      const int rem = (int)m - nimg * PQ;
+      const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
       const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
       const int64_t obase = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
 #pragma unroll
@@ -321,33 +329,39 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, false, STAGES>), grid, block, 0, s, a);
 }
 
-// per-device address of this code object's zero page (device globals are per device)
-static const void* zero_page() {
-  static const void* cache[64] = {};
-  int dev = 0;
-  PDT_HIP_CHECK(hipGetDevice(&dev));
-  if (!cache[dev]) PDT_HIP_CHECK(hipGetSymbolAddress((void**)&cache[dev], HIP_SYMBOL(g_zero16)));
-  return cache[dev];
-}
-
 template <int DT>
 static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
-  a.zero = zero_page();
   a.m_tiles = (int)((a.M + bm - 1) / bm);
   a.n_tiles = a.Kout / bn;
+  {
+    const FastDiv f1 = make_fastdiv((uint32_t)(a.Pm * a.Qm)), f2 = make_fastdiv((uint32_t)a.Qm);
+    a.pq_mul = f1.mul; a.pq_shift = f1.shift; a.q_mul = f2.mul; a.q_shift = f2.shift;
+  }
   if (a.nphase > 0) {
     int any = 0;
     for (int p = 0; p < a.nphase; ++p) {
       a.pmt[p] = (int)(((int64_t)a.N * a.pPm[p] * a.pQm[p] + bm - 1) / bm);
       any |= a.pmt[p];
+      if (a.pPm[p] > 0 && a.pQm[p] > 0) {
+        const FastDiv f1 = make_fastdiv((uint32_t)(a.pPm[p] * a.pQm[p])), f2 = make_fastdiv((uint32_t)a.pQm[p]);
+        a.ppq_mul[p] = f1.mul; a.ppq_shift[p] = f1.shift; a.pq1_mul[p] = f2.mul; a.pq1_shift[p] = f2.shift;
+      }
     }
     if (!any || a.n_tiles == 0) return;
   } else if (a.m_tiles * a.n_tiles == 0) {
     return;
   }
+  // PDT_FWD_STAGES=2|3 forces the LDS ring depth (tuning sweeps); default: 2 for BK=64, 3 for BK=32
+  static const int force_stages = [] {
+    const char* e = getenv("PDT_FWD_STAGES");
+    return e ? atoi(e) : 0;
+  }();
 #define PDT_CFG(BM_, BN_, BK_, WN_, ST_)                                 \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
-    launch_cfg<DT, BM_, BN_, BK_, WN_, ST_>(a, s);                       \
+    if (force_stages == 5 - ST_)                                         \
+      launch_cfg<DT, BM_, BN_, BK_, WN_, 5 - ST_>(a, s);                 \
+    else                                                                 \
+      launch_cfg<DT, BM_, BN_, BK_, WN_, ST_>(a, s);                     \
     return;                                                              \
   }
   // BK = 64 tiles: 2-stage ring; BK = 32 tiles: 3-stage ring (counted vmcnt, more latency hiding)
@@ -356,6 +370,7 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   PDT_CFG(128, 64, 64, 1, 2)
   PDT_CFG(128, 128, 32, 2, 3)
   PDT_CFG(256, 64, 32, 1, 3)
+  PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
 #undef PDT_CFG
   pdt_hip_fail("conv_fwd: unsupported tile config", hipErrorInvalidValue, __FILE__, __LINE__);

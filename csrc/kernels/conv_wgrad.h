@@ -17,7 +17,6 @@ struct ConvWgradArgs {
   int win;             // stem window mode (see conv_wgrad.hip)
   int splits, pix_per_split;  // filled by conv_wgrad_plan
   int tile;                   // 64 or 128 (filled by conv_wgrad_plan)
-  const void* zero;           // 16+ zero bytes: DMA source for out-of-bounds rows (set by the launcher)
   uint32_t div_pq_mul, div_pq_shift, div_q_mul, div_q_shift;  // FastDiv of Pm*Qm and Qm (launcher)
 };
 

@@ -364,15 +364,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_scalar_kernel(const float* _
   }
 }
 
-// per-device address of this code object's zero page (device globals are per device)
-static const void* zero_page() {
-  static const void* cache[64] = {};
-  int dev = 0;
-  PDT_HIP_CHECK(hipGetDevice(&dev));
-  if (!cache[dev]) PDT_HIP_CHECK(hipGetSymbolAddress((void**)&cache[dev], HIP_SYMBOL(g_zero16)));
-  return cache[dev];
-}
-
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
   a.tile = (!a.win && a.C % 128 == 0 && a.Kout % 128 == 0) ? 128 : 64;
   const int tiles = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile);
@@ -390,7 +381,6 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   ConvWgradArgs a = args;
   const int nwg = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile) * a.splits;
   if (nwg == 0) return;
-  a.zero = zero_page();
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
   a.div_pq_mul = dpq.mul; a.div_pq_shift = dpq.shift; a.div_q_mul = dq.mul; a.div_q_shift = dq.shift;
   if (a.tile == 128) {

@@ -3,8 +3,13 @@
 //     112x112 post-ReLU tensor is never written.  The window argmax (0..8) is kept as uint8.
 //   * maxpool_bwd_relu: gather form of the max-pool backward (each input pixel collects from the
 //     <= 4 windows that selected it) fused with the ReLU mask recomputed from the BN input.
+//   * stem_pool_bwd_reduce / stem_pool_bwd_apply: the whole stem backward (max-pool backward, ReLU
+//     mask, BatchNorm backward) in two passes with no 112x112 intermediate: the reduce pass visits
+//     only the selected (argmax) elements through the pooled tensor; the apply pass gathers dz for
+//     each input pixel and writes dy = A*dz + B*y + C directly (SURVEY K9 + K7/K8 fused).
 //   * avgpool (global, HxW -> 1) forward and backward.
 #include "../common.h"
+#include "conv_fwd.h"
 #include "pool.h"
 
 namespace pdt {
@@ -146,6 +151,161 @@ void maxpool_bwd_relu_launch(int dtype, const uint16_t* dp, const uint8_t* idx, 
   else
     hipLaunchKernelGGL(maxpool_bwd_relu_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef, dz, N, H,
                        W, C, OH, OW);
+}
+
+// Stem backward, pass 1: per-channel sum(dz) and sum(dz * xhat) over the stem's conv output, visiting
+// only the elements each pooling window selected.  dz at an input element is the sum of the pooled
+// gradients of the windows that chose it, masked by ReLU; the sums are linear in dz, so they are
+// accumulated per window (no 112x112 dz tensor).  One thread per (pooled pixel, 8 channels).
+template <int DT>
+__global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(const uint16_t* __restrict__ dp,
+                                                                   const uint8_t* __restrict__ idx,
+                                                                   const uint16_t* __restrict__ y,
+                                                                   const float* __restrict__ coef,
+                                                                   double* __restrict__ slots, int N, int H, int W,
+                                                                   int C, int OH, int OW) {
+  using E = E16<DT>;
+  const int vpr = C / 8;
+  const int rpi = 256 / vpr;
+  const int cv = threadIdx.x % vpr, rl = threadIdx.x / vpr;
+  const int c0 = cv * 8;
+  float sc[8], sh[8], mu[8], is[8], s0[8], s1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = coef[c0 + e];
+    sh[e] = coef[C + c0 + e];
+    mu[e] = coef[2 * C + c0 + e];
+    is[e] = coef[3 * C + c0 + e];
+    s0[e] = 0.f;
+    s1[e] = 0.f;
+  }
+  const int64_t rows = (int64_t)N * OH * OW;
+  if (rl < rpi) {
+    for (int64_t r = (int64_t)blockIdx.x * rpi + rl; r < rows; r += (int64_t)gridDim.x * rpi) {
+      const int ow = (int)(r % OW);
+      const int64_t t = r / OW;
+      const int oh = (int)(t % OH);
+      const int n = (int)(t / OH);
+      const int64_t o = r * C + c0;
+      const uint2 ib = *(const uint2*)(idx + o);
+      const uint4 g = *(const uint4*)(dp + o);
+      const uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+      const uint16_t* ybase = y + ((int64_t)n * H * W) * C + c0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int pos = (int)((((e < 4) ? ib.x : ib.y) >> (8 * (e & 3))) & 0xff);
+        const int kh = pos / 3, kw = pos - 3 * (pos / 3);
+        const int h = oh * 2 - 1 + kh, w = ow * 2 - 1 + kw;  // always inside (argmax is a valid tap)
+        const float yv = E::to_f(ybase[((int64_t)h * W + w) * C + e]);
+        const float dz = (yv * sc[e] + sh[e] > 0.f) ? E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1)))) : 0.f;
+        s0[e] += dz;
+        s1[e] += dz * (yv - mu[e]) * is[e];
+      }
+    }
+  }
+  extern __shared__ float red[];  // [rpi][C][2]
+  if (rl < rpi) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[((int64_t)rl * C + c0 + e) * 2 + 0] = s0[e];
+      red[((int64_t)rl * C + c0 + e) * 2 + 1] = s1[e];
+    }
+  }
+  __syncthreads();
+  double* dst = slots + (int64_t)(blockIdx.x % kStatSlots) * C * 2;
+  for (int i = threadIdx.x; i < C * 2; i += 256) {
+    float t = 0.f;
+    for (int q = 0; q < rpi; ++q) t += red[(int64_t)q * C * 2 + i];
+    atomicAdd(dst + i, (double)t);
+  }
+}
+
+void stem_pool_bwd_reduce_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y,
+                                 const float* coef, double* slots, int N, int H, int W, int C, hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  PDT_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(double) * kStatSlots * C * 2, s));
+  const int rpi = 256 / (C / 8);
+  int64_t blocks = ((int64_t)N * OH * OW + rpi * 8 - 1) / (rpi * 8);
+  if (blocks > 4096) blocks = 4096;
+  const size_t smem = (size_t)rpi * C * 2 * sizeof(float);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel<kBF16>, dim3((int)blocks), dim3(256), smem, s, dp, idx, y, coef, slots,
+                       N, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel<kF16>, dim3((int)blocks), dim3(256), smem, s, dp, idx, y, coef, slots,
+                       N, H, W, C, OH, OW);
+}
+
+// Stem backward, pass 2: dy = A*dz + B*y + Cc at every conv-output element, with dz gathered from the
+// (<= 4) pooling windows that selected it and masked by ReLU (recomputed from y and the BN coefficients).
+template <int DT>
+__global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(const uint16_t* __restrict__ dp,
+                                                                  const uint8_t* __restrict__ idx,
+                                                                  const uint16_t* __restrict__ y,
+                                                                  const float* __restrict__ coef,
+                                                                  const float* __restrict__ bcoef,
+                                                                  uint16_t* __restrict__ dy, int N, int H, int W,
+                                                                  int C, int OH, int OW) {
+  using E = E16<DT>;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * H * W * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cv) * 8;
+    int64_t pix = v / cv;
+    const int w = (int)(pix % W);
+    pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int oh_lo = h / 2, oh_hi = (h + 1) / 2 < OH ? (h + 1) / 2 : OH - 1;
+    const int ow_lo = w / 2, ow_hi = (w + 1) / 2 < OW ? (w + 1) / 2 : OW - 1;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = h - (oh * 2 - 1);
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int kw = w - (ow * 2 - 1);
+        const uint32_t pos = (uint32_t)(kh * 3 + kw);
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+        const uint2 ib = *(const uint2*)(idx + o);
+        const uint4 g = *(const uint4*)(dp + o);
+        const uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t b = (((e < 4) ? ib.x : ib.y) >> (8 * (e & 3))) & 0xffu;
+          if (b == pos) acc[e] += E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1))));
+        }
+      }
+    }
+    const int64_t i = (((int64_t)n * H + h) * W + w) * C + c0;
+    const uint4 yy = *(const uint4*)(y + i);
+    const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
+    uint32_t o_[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t r[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int c = c0 + 2 * e + hh;
+        const float yv = E::to_f((uint16_t)(yw[e] >> (16 * hh)));
+        const float dz = yv * coef[c] + coef[C + c] > 0.f ? acc[2 * e + hh] : 0.f;
+        r[hh] = E::from_f(bcoef[c] * dz + bcoef[C + c] * yv + bcoef[2 * C + c]);
+      }
+      o_[e] = (uint32_t)r[0] | ((uint32_t)r[1] << 16);
+    }
+    *(uint4*)(dy + i) = make_uint4(o_[0], o_[1], o_[2], o_[3]);
+  }
+}
+
+void stem_pool_bwd_apply_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y,
+                                const float* coef, const float* bcoef, uint16_t* dy, int N, int H, int W, int C,
+                                hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(stem_pool_bwd_apply_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef,
+                       bcoef, dy, N, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(stem_pool_bwd_apply_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef,
+                       bcoef, dy, N, H, W, C, OH, OW);
 }
 
 // feat[n][c] = mean_{hw} x[n][hw][c]    (one thread per (n, 8 channels))

@@ -1,0 +1,229 @@
+// ResNet stem forward: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, as a persistent
+// row-tile MFMA kernel (stem row; the stem is torchvision's conv1, instantiated by
+// `dataparallel.py:112-117`).
+//
+// The stem's reduction is only 7 kernel rows x (8 pixels x 4 channels) = 224 long, so the generic
+// implicit-GEMM kernel spends most of each block on pipeline fill and epilogue (~200 TF/s measured).
+// This kernel is shaped around the stem's data reuse instead:
+//   * block tile = 4 consecutive output rows of one image (wave w owns output row oh0 + w, all Q <= 112
+//     columns as 7 groups of 16 pixels, all 64 output channels);
+//   * the 13 padded-image rows those 4 output rows read are ONE contiguous 24 KB range of the
+//     zero-padded NHWC4 image, so a tile's whole input is staged with 24 LDS-DMA instructions
+//     (buffer_load ... lds) into a 2-deep LDS ring: tile i+1 streams in while tile i computes;
+//   * an MFMA B fragment (8 consecutive K = 2 pixels x 4 channels of one kernel row) is one aligned
+//     16-byte ds_read at column 2*ow + 2*fq of the staged row: each quarter-wave reads 256 contiguous
+//     bytes (conflict-free), and the 4x overlap of neighbouring 7-wide windows costs no extra HBM/L2
+//     traffic;
+//   * the 64 x 224 weight matrix stays resident in LDS (rows padded to 464 B: conflict-free A reads);
+//   * K = 224 exactly (no padding to a tile multiple); blocks are persistent and each XCD walks a
+//     contiguous tile range;
+//   * BatchNorm statistics of the rounded outputs are reduced per tile (16-lane shuffles), accumulated
+//     in LDS across all of a block's tiles and reach the fp64 slot accumulators once per block.
+// Weight layout ("window rows"): w[cout][r][j], j = s*4 + c (kernel column s < 7, channel c < 3; zeros
+// elsewhere), i.e. [64][7][32].
+#include "../common.h"
+#include "conv_fwd.h"
+#include "stem.h"
+
+namespace pdt {
+
+namespace {
+
+constexpr int kCout = 64;
+constexpr int kRows = 7;                   // kernel rows
+constexpr int kWRow = kRows * 32 * 2;      // 448 B of weights per output channel
+constexpr int kWPitch = kWRow + 16;        // padded LDS pitch: 16-lane A reads hit distinct banks
+constexpr int kOutRows = 4;                // output rows per tile (one per wave)
+constexpr int kInRows = 2 * (kOutRows - 1) + kRows;  // 13 padded-image rows per tile
+constexpr int kStage = 24 * 1024;          // LDS bytes per staged tile (>= kInRows * Wp * 8)
+constexpr int kGroups = 7;                 // 16-pixel column groups per output row (Q <= 112)
+
+}  // namespace
+
+template <int DT, bool STATS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void stem_fwd_kernel(StemFwdArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  // ONE __shared__ object (a second one makes hipcc drain vmcnt(0) before every staged-tile read):
+  // [2 staged tiles][resident weights][per-wave BN partials (no cross-wave LDS atomic contention)]
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kStage + kCout * kWPitch + 4 * kCout * 2 * 4];
+  char* const wl = smem + 2 * kStage;
+  float(*const red)[kCout * 2] = (float(*)[kCout * 2])(smem + 2 * kStage + kCout * kWPitch);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- resident weights: 1792 16-byte chunks ----
+  {
+    const uint4* wg = (const uint4*)a.w;
+    for (int idx = tid; idx < kCout * (kWRow / 16); idx += 256) {
+      const int r = idx / (kWRow / 16), c = idx - r * (kWRow / 16);
+      *(uint4*)(wl + r * kWPitch + c * 16) = wg[idx];
+    }
+    for (int i = tid; i < 4 * kCout * 2; i += 256) (&red[0][0])[i] = 0.f;
+  }
+
+  // ---- tile schedule: tile = (image n, output rows 4*k .. 4*k+3); XCD x owns a contiguous range ----
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, lb = blockIdx.x >> 3;
+  const int per_x = G >> 3;  // host launches a multiple of 8 blocks
+  const int t_per = (a.tiles + 7) >> 3;
+  const int t_begin = xcd * t_per;
+  const int t_end = min(a.tiles, t_begin + t_per);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, a.x_bytes);
+  const FastDiv fd_tp{a.tp_mul, a.tp_shift};
+  const uint32_t row_bytes = (uint32_t)a.Wp * 8u;
+
+  auto tile_n_oh = [&](int t, int& n, int& oh0) {
+    n = (int)fdiv((uint32_t)t, fd_tp);
+    oh0 = (t - n * a.TP) * kOutRows;
+  };
+  // one tile's 13 input rows: contiguous bytes from row 2*oh0 of image n (6 wave-instructions/wave)
+  auto stage_tile = [&](int t, int buf) {
+    int n, oh0;
+    tile_n_oh(t, n, oh0);
+    const uint32_t base = (uint32_t)(n * a.Hp + 2 * oh0) * row_bytes;
+#pragma unroll
+    for (int i = 0; i < kStage / 4096; ++i) {
+      const int chunk = (i * 4 + wave) * 1024;
+      buf_lds16(rx, smem + buf * kStage + chunk, base + (uint32_t)chunk + (uint32_t)lane * 16u);
+    }
+  };
+
+  int t = t_begin + lb;
+  int buf = 0;
+  bool stores_behind = false;  // the previous epilogue issued >= kStoresBehind stores after the DMA
+  __syncthreads();             // resident weights visible to every wave
+  if (t < t_end) stage_tile(t, 0);
+  for (; t < t_end; t += per_x) {
+    // This wave's DMA of tile t was issued before the previous epilogue's stores; vector-memory ops
+    // retire in issue order, so a counted wait leaves those stores in flight.  Then a raw barrier
+    // (no vmcnt(0) drain): every wave's DMA landed and every wave finished reading the other buffer.
+    if (stores_behind)
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
+
+    f32x4_t acc[4][kGroups];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < kGroups; ++g) acc[i][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const char* sb = smem + buf * kStage + 2 * wave * row_bytes + (fr + fq) * 16;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      vec8 af[4], bf[kGroups];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const vec8*)(wl + (i * 16 + fr) * kWPitch + (r * 4 + fq) * 16);
+#pragma unroll
+      for (int g = 0; g < kGroups; ++g) bf[g] = *(const vec8*)(sb + r * row_bytes + g * 256);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) acc[i][g] = E::mfma16x16x32(af[i], bf[g], acc[i][g]);
+    }
+
+    // ---- epilogue: lane holds couts i*16 + 4*fq + r of pixel (oh, g*16 + fr) ----
+    int n, oh0;
+    tile_n_oh(t, n, oh0);
+    const int oh = oh0 + wave;
+    stores_behind = oh < a.P && a.Q == kGroups * 16;  // then 28 stores follow the next DMA
+    float csum[4][4], csq[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
+    if (oh < a.P) {
+      uint16_t* yrow = a.y + ((int64_t)(n * a.P + oh) * a.Q) * kCout + 4 * fq;
+#pragma unroll
+      for (int g = 0; g < kGroups; ++g) {
+        const int ow = g * 16 + fr;
+        if (ow < a.Q) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint16_t o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = E::from_f(acc[i][g][r]);
+            uint2 pk;
+            pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+            pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+            *(uint2*)(yrow + (int64_t)ow * kCout + i * 16) = pk;
+            if constexpr (STATS) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float q = E::to_f(o[r]);
+                csum[i][r] += q;
+                csq[i][r] += q * q;
+              }
+            }
+          }
+        }
+      }
+    }
+    if constexpr (STATS) {
+      // per-tile channel partials: reduce over the 16 pixel lanes (DPP row scan, no LDS traffic),
+      // accumulate in LDS (fp32) per wave
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          csum[i][r] = row16_sum(csum[i][r]);
+          csq[i][r] = row16_sum(csq[i][r]);
+        }
+      if (fr == 15) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = i * 16 + 4 * fq + r;
+            red[wave][c * 2 + 0] += csum[i][r];  // lanes fr == 15 of distinct fq own distinct c
+            red[wave][c * 2 + 1] += csq[i][r];
+          }
+      }
+    }
+    buf ^= 1;
+  }
+
+  if constexpr (STATS) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < kCout * 2) {
+      double* dst = a.stats + (int64_t)(blockIdx.x % kStatSlots) * kCout * 2;
+      atomicAdd(dst + tid, (double)(red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]));
+    }
+  }
+}
+
+bool stem_fwd_supported(int Hp, int Wp, int P, int Q) {
+  return Q <= kGroups * 16 && kInRows * Wp * 8 <= kStage && 2 * (Q - 1) + 8 <= Wp && 2 * (P - 1) + kRows <= Hp;
+}
+
+void stem_fwd_launch(StemFwdArgs a, int dtype, hipStream_t s) {
+  a.TP = (a.P + kOutRows - 1) / kOutRows;
+  a.tiles = a.N * a.TP;
+  const FastDiv f = make_fastdiv((uint32_t)a.TP);
+  a.tp_mul = f.mul; a.tp_shift = f.shift;
+  if (a.tiles == 0) return;
+  int dev = 0, cus = 256;
+  PDT_HIP_CHECK(hipGetDevice(&dev));
+  PDT_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  int G = cus * a.blocks_per_cu;
+  const int cap = (a.tiles + 7) / 8 * 8;
+  if (G > cap) G = cap;
+  G = (G + 7) / 8 * 8;
+  if (a.stats) PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * 2 * kStatSlots * kCout, s));
+  const bool st = a.stats != nullptr;
+#define PDT_STEM(DT_, ST_) hipLaunchKernelGGL((stem_fwd_kernel<DT_, ST_>), dim3(G), dim3(256), 0, s, a)
+  if (dtype == kBF16) {
+    if (st) PDT_STEM(kBF16, true); else PDT_STEM(kBF16, false);
+  } else {
+    if (st) PDT_STEM(kF16, true); else PDT_STEM(kF16, false);
+  }
+#undef PDT_STEM
+}
+
+}  // namespace pdt

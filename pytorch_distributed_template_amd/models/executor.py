@@ -20,6 +20,8 @@ weights and gradients.  Reference call sites mirror
 """
 from __future__ import annotations
 
+import os
+
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -93,6 +95,10 @@ class ResNetExecutor:
         self.syncbn_group = syncbn_group
         self.wgrad_blocks = wgrad_blocks  # split-K targets (tools/conv_bench.py sweep: 3x3 best ~2048, 1x1 ~512)
         self.wgrad_blocks_1x1 = wgrad_blocks_1x1
+        # generic-path stem tile (window mode, BK=32); PDT_STEM_TILE=BMxBN overrides (tuning)
+        stile = os.environ.get("PDT_STEM_TILE", "")
+        self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
+        self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         derived_maps: List[torch.Tensor] = []
         off = [0]
 
@@ -120,17 +126,20 @@ class ResNetExecutor:
         # matching 8-pixel x 4-channel windows of the zero-padded NHWC4 image (no im2col)
         st = self.stem
         assert st.cin <= 4 and st.S <= 8, "window-mode stem needs Cin <= 4 and kernel width <= 8"
+        self.stem_pairs = (st.R + 1) // 2  # the stem weight gradient works on kernel-row pairs
         k = torch.arange(st.cout).view(-1, 1, 1)
         r = torch.arange(st.R).view(1, -1, 1)
         j = torch.arange(32).view(1, 1, -1)
         s_, c_ = j // 4, j % 4
         src = st.slot.offset + ((k * st.R + r) * st.S + s_) * st.cin + c_
         m = torch.where((s_ < st.S) & (c_ < st.cin), src, torch.full_like(src, -1))
+        # dedicated persistent stem kernel (csrc/kernels/stem.hip) for the torchvision stem geometry
+        self.stem_kernel = (st.cout == 64 and st.R == 7 and st.S == 7 and st.st == 2 and st.pad == 3 and
+                            os.environ.get("PDT_STEM_KERNEL", "dedicated") == "dedicated")
         self.stem_w_off = off[0]
         derived_maps.append(m.reshape(-1).to(torch.int32))
         off[0] += m.numel()
         # stem weight-gradient scatter: [Cout][R/2 pairs][2][32] (wgrad window tile) -> KRSC [Cout][R][S][Cin]
-        self.stem_pairs = (st.R + 1) // 2
         kk = torch.arange(st.cout).view(-1, 1, 1, 1)
         rr = torch.arange(st.R).view(1, -1, 1, 1)
         ss = torch.arange(st.S).view(1, 1, -1, 1)
@@ -256,6 +265,12 @@ class ResNetExecutor:
         K = 4 if bn2 is not None else 2
         slots = self._buf(("bnslots", C, K), self.n_slots * C * K, torch.float64)
         self.C.bn_bwd_reduce(g, out, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows, C)
+        self._bn_bwd_finish(slots, count, bn1, bn2)
+
+    def _bn_bwd_finish(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None):
+        """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients."""
+        C = bn1.C
+        K = 4 if bn2 is not None else 2
         sums = bn1.bsums[:C * K]
         self.C.bn_slot_sum(slots, C, K, sums)
         if self.syncbn_group is not None:
@@ -292,9 +307,12 @@ class ResNetExecutor:
         y0 = self._buf("y0", N * P0 * Q0 * st.cout)
         wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * st.R * 32]
         sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64) if train else None
-        bm, bn = _conv_tile(st.cout)
-        Cn.conv_fwd(xp, wst, y0, None, sp, N, Hp, Wp, 32, st.cout, st.R, 1, P0, Q0, st.st, st.st, 0, 0, 1, 0,
-                    P0, Q0, 1, 1, 0, 0, bm, bn, 32, 4)
+        if self.stem_kernel and Cn.stem_fwd_supported(Hp, Wp, P0, Q0):
+            Cn.stem_fwd(xp, wst, y0, sp, N, Hp, Wp, P0, Q0, self.stem_blocks_per_cu)
+        else:  # generic implicit GEMM in window mode (one 32-wide K step per kernel row)
+            bm, bn = self.stem_tile
+            Cn.conv_fwd(xp, wst, y0, None, sp, N, Hp, Wp, 32, st.cout, st.R, 1, P0, Q0, st.st, st.st, 0, 0, 1, 0,
+                        P0, Q0, 1, 1, 0, 0, bm, bn, 32, 4)
         tiles = N * P0 * Q0
         if train:
             self.bn_train_finalize(self.stem_bn, sp, tiles, N * P0 * Q0)
@@ -451,14 +469,15 @@ class ResNetExecutor:
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res)
             g = gnext
             gsel ^= 1
-        # stem: max-pool backward + ReLU mask -> BN backward -> window-mode weight gradient
+        # stem: fused max-pool backward + ReLU mask + BN backward (two passes, no 112x112 dz tensor)
+        # -> window-mode weight gradient
         st, sbn = self.stem, self.stem_bn
         P0, Q0 = saved["P0"], saved["Q0"]
-        dz0 = self._buf("dz0", N * P0 * Q0 * st.cout)
-        Cn.maxpool_bwd_relu(g, saved["idx"], saved["y0"], sbn.coef, dz0, N, P0, Q0, st.cout)
-        self.bn_bwd(sbn, saved["y0"], dz0, None, N * P0 * Q0)
-        dy0 = self._buf("dy0", dz0.numel())
-        Cn.bn_bwd_apply(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
+        slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
+        Cn.stem_pool_bwd_reduce(g, saved["idx"], saved["y0"], sbn.coef, slots, N, P0, Q0, st.cout)
+        self._bn_bwd_finish(slots, N * P0 * Q0, sbn)
+        dy0 = self._buf("dy0", N * P0 * Q0 * st.cout)
+        Cn.stem_pool_bwd_apply(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
         ldw = self.stem_pairs * 64
         tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
         self._wgrad(st.cout, saved["xp"], dy0, N, saved["Hp"], saved["Wp"], 64, self.stem_pairs, 1, P0, Q0, st.st, 0,

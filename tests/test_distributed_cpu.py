@@ -150,13 +150,15 @@ def test_launcher_env_contract(tmp_path):
     script = tmp_path / "echo_env.py"
     script.write_text(
         "import os, sys\n"
-        "print('ENV', os.environ['RANK'], os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE'], os.environ['MASTER_PORT'],"
-        " [a for a in sys.argv[1:] if a.startswith('--local_rank')], sys.argv[-1], flush=True)\n")
+        "line = ' '.join(str(v) for v in ('ENV', os.environ['RANK'], os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE'],"
+        " os.environ['MASTER_PORT'], [a for a in sys.argv[1:] if a.startswith('--local_rank')], sys.argv[-1]))\n"
+        "open(os.path.join(os.path.dirname(__file__), 'env_%s.txt' % os.environ['RANK']), 'w').write(line)\n")
     r = subprocess.run([sys.executable, "-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=3",
                         "--master_port=23334", str(script), "last_arg"], cwd=ROOT, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr
-    lines = sorted(l for l in r.stdout.splitlines() if l.startswith("ENV"))
+    # each rank writes its own file: concurrent children's stdout lines may interleave
+    lines = sorted((tmp_path / f"env_{i}.txt").read_text() for i in range(3))
     assert len(lines) == 3
     for i, l in enumerate(lines):
         assert l.startswith(f"ENV {i} {i} 3 23334 ['--local_rank={i}'] last_arg")

@@ -26,8 +26,12 @@ def _run(args, timeout=600):
 def _check_outdir(d, logger_line_prefix="Train epoch"):
     files = os.listdir(d)
     assert "experiment.log" in files and "settings.log" in files
-    assert "checkpoint.pth.tar" in files and "model_best.pth.tar" in files
+    assert "checkpoint.pth.tar" in files
     log = open(os.path.join(d, "experiment.log")).read()
+    # model_best is written only when val top-1 strictly improves on 0 (reference `distributed.py:201`);
+    # a random tiny model on 8 synthetic images can stay at 0
+    best = max(float(v) for v in re.findall(r"best_acc1=(\d+\.\d+)", log))
+    assert ("model_best.pth.tar" in files) == (best > 0)
     assert re.search(r"Train epoch: \[0/2\]\[0/\d+\]\tlr=0\.100000\tce_loss=\d+\.\d{4}\ttop1_acc=\d\.\d{4}\t"
                      r"data_time=\s*\d+\.\d{3}s\tbatch_time=\s*\d+\.\d{3}s", log)
     assert re.search(r"\|\|==> Train epoch: \[1/2\]\tlr=0\.010000\tce_loss=", log)

@@ -187,6 +187,24 @@ def test_stem_window_mode_fwd_and_wgrad():
     xr = x.to(torch.bfloat16).float()
     ref = F.conv2d(xr, wk.to(torch.bfloat16).float().permute(0, 3, 1, 2), stride=2, padding=3)
     assert _rel(y.view(N, P, Q, K).permute(0, 3, 1, 2), ref) < 1e-2
+    # window-pair mode: one 64-wide K step covers kernel rows (2p, 2p+1); 4 steps with BK=64
+    wpair = torch.zeros(K, 8, 8, 4, device=DEV)
+    wpair[:, :7, :7, :3] = wk
+    wpair = wpair.reshape(K, 4 * 64).to(torch.bfloat16).contiguous()
+    for bm, bn in ((256, 64), (128, 64)):
+        y2 = torch.empty_like(y)
+        native.C.conv_fwd(xp, wpair, y2, None, None, N, Hp, Wp, 64, K, 4, 1, P, Q, 2, 2, 0, 0, 2, 0, P, Q, 1, 1, 0, 0,
+                          bm, bn, 64, 4)
+        assert _rel(y2.view(N, P, Q, K).permute(0, 3, 1, 2), ref) < 1e-2
+        # dedicated persistent stem kernel (register-fed B fragments, resident weights) with BN stats
+        ys = torch.empty_like(y)
+        stats = torch.zeros(native.C.stat_slots() * K * 2, dtype=torch.float64, device=DEV)
+        native.C.stem_fwd(xp, wwin, ys, stats, N, Hp, Wp, P, Q, 2)
+        assert _rel(ys.view(N, P, Q, K).permute(0, 3, 1, 2), ref) < 1e-2
+        st = stats.view(-1, K, 2).sum(0)
+        yf = ys.view(-1, K).float()
+        assert torch.allclose(st[:, 0].float(), yf.sum(0), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(st[:, 1].float(), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
     # weight gradient in window mode, then the KRSC scatter
     dy = _rand16(N, P, Q, K)
     pairs = 4
@@ -204,3 +222,69 @@ def test_stem_window_mode_fwd_and_wgrad():
     native.C.gather32(tmp, gidx, dw)
     refw = torch.nn.grad.conv2d_weight(xr, (K, 3, 7, 7), dy.float().permute(0, 3, 1, 2), stride=2, padding=3)
     assert _rel(dw.view(K, 7, 7, 3).permute(0, 3, 1, 2), refw) < 2e-3
+
+
+def test_stem_pool_backward_fused():
+    """Fused max-pool bwd + ReLU + BN bwd (reduce pass over argmax elements, apply pass) vs autograd fp32."""
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(8)
+    N, H, W, C = 3, 14, 13, 64
+    y = _rand16(N, H, W, C)
+    yf = y.float()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.2
+    mean = yf.mean((0, 1, 2))
+    var = yf.var((0, 1, 2), unbiased=False)
+    invstd = torch.rsqrt(var + 1e-5)
+    scale = gamma * invstd
+    coef = torch.cat([scale, beta - mean * scale, mean, invstd]).contiguous()
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=DEV)
+    idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=DEV)
+    native.C.bn_relu_maxpool(y, coef, out, idx, N, H, W, C)
+    dp = _rand16(N, OH, OW, C)
+    # reference: BN (batch stats) -> ReLU -> maxpool in fp32 autograd
+    xin = yf.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    g_ = gamma.clone().requires_grad_(True)
+    b_ = beta.clone().requires_grad_(True)
+    z = F.batch_norm(xin, None, None, g_, b_, training=True, eps=1e-5)
+    F.max_pool2d(torch.relu(z), 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
+    slots = torch.zeros(native.C.stat_slots() * C * 2, dtype=torch.float64, device=DEV)
+    native.C.stem_pool_bwd_reduce(dp, idx, y, coef, slots, N, H, W, C)
+    sums = torch.empty(2 * C, dtype=torch.float64, device=DEV)
+    native.C.bn_slot_sum(slots, C, 2, sums)
+    dgamma = torch.empty(C, device=DEV)
+    dbeta = torch.empty(C, device=DEV)
+    bcoef = torch.empty(3 * C, device=DEV)
+    native.C.bn_bwd_finalize(sums, float(N * H * W), coef, gamma, dgamma, dbeta, 1.0, bcoef)
+    assert _rel(dgamma, g_.grad) < 1e-2 and _rel(dbeta, b_.grad) < 1e-2
+    dy = torch.empty_like(y)
+    native.C.stem_pool_bwd_apply(dp, idx, y, coef, bcoef, dy, N, H, W, C)
+    assert _rel(dy.permute(0, 3, 1, 2), xin.grad) < 2e-2
+
+
+def test_stem_kernel_persistent_tiles():
+    """Stem kernel with more tiles than blocks (persistent loop + next-tile prefetch) vs F.conv2d."""
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(9)
+    N, H, W, K = 24, 112, 112, 64
+    x = torch.randn(N, 3, H, W, device=DEV)
+    w = torch.randn(K, 3, 7, 7, device=DEV) * 0.05
+    P, Q = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = max(H + 6, 2 * (P - 1) + 8), max(W + 6, 2 * (Q - 1) + 8)
+    xp = torch.empty(N * Hp * Wp * 4, dtype=torch.bfloat16, device=DEV)
+    native.C.stem_pack(x, xp, N, 3, H, W, 3, Hp, Wp)
+    wk = w.permute(0, 2, 3, 1)
+    wwin = torch.zeros(K, 7, 8, 4, device=DEV)
+    wwin[:, :, :7, :3] = wk
+    wwin = wwin.reshape(K, 7 * 32).to(torch.bfloat16).contiguous()
+    ys = torch.empty(N * P * Q * K, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(native.C.stat_slots() * K * 2, dtype=torch.float64, device=DEV)
+    native.C.stem_fwd(xp, wwin, ys, stats, N, Hp, Wp, P, Q, 1)
+    ref = F.conv2d(x.to(torch.bfloat16).float(), wk.to(torch.bfloat16).float().permute(0, 3, 1, 2), stride=2,
+                   padding=3)
+    assert _rel(ys.view(N, P, Q, K).permute(0, 3, 1, 2), ref) < 1e-2
+    st = stats.view(-1, K, 2).sum(0)
+    yf = ys.view(-1, K).double()
+    assert torch.allclose(st[:, 0], yf.sum(0), rtol=1e-4, atol=1e-1)
+    assert torch.allclose(st[:, 1], (yf * yf).sum(0), rtol=1e-4, atol=1e-1)

@@ -35,14 +35,52 @@ def timeit(fn, reps):
     return ev0.elapsed_time(ev1) / reps
 
 
+def stem_bench(C, N, reps):
+    """ResNet stem (7x7/2 over the zero-padded NHWC4 image): 1-row windows (BK=32) vs row pairs (BK=64)."""
+    dev = "cuda"
+    H = W = 224
+    P = Q = 112
+    Hp = Wp = 230
+    xp = (torch.randn(N * Hp * Wp * 4, device=dev) * 0.5).to(torch.bfloat16)
+    y = torch.empty(N * P * Q * 64, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(C.stat_slots() * 64 * 2, device=dev, dtype=torch.float64)
+    flops = 2.0 * N * P * Q * 64 * 147
+    row = {"shape": "stem"}
+    w1 = (torch.randn(64 * 7 * 32, device=dev) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(64 * 4 * 64, device=dev) * 0.05).to(torch.bfloat16)
+    for stats in (False, True):
+        sp = st if stats else None
+        tag = "_stats" if stats else ""
+        for (bm, bk) in ((256, 32), (128, 32)):
+            def f(bm=bm, bk=bk):
+                C.conv_fwd(xp, w1, y, None, sp, N, Hp, Wp, 32, 64, 7, 1, P, Q, 2, 2, 0, 0, 1, 0, P, Q, 1, 1, 0, 0,
+                           bm, 64, 32, 4)
+            row[f"row_{bm}x64x32{tag}"] = round(flops / timeit(f, reps) / 1e9, 1)
+        for bm in (256, 128):
+            def g(bm=bm):
+                C.conv_fwd(xp, w2, y, None, sp, N, Hp, Wp, 64, 64, 4, 1, P, Q, 2, 2, 0, 0, 2, 0, P, Q, 1, 1, 0, 0,
+                           bm, 64, 64, 4)
+            row[f"pair_{bm}x64x64{tag}"] = round(flops / timeit(g, reps) / 1e9, 1)
+        for bpc in (1, 2):
+            def h(bpc=bpc):
+                C.stem_fwd(xp, w1, y, sp, N, Hp, Wp, P, Q, bpc)
+            row[f"stemk_bpc{bpc}{tag}"] = round(flops / timeit(h, reps) / 1e9, 1)
+    row["note"] = "TF/s on the true 7x7x3 FLOPs"
+    print(json.dumps(row), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1200)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only-stem", action="store_true")
     a = ap.parse_args()
     C = native.C
     dev = "cuda"
     res = []
+    stem_bench(C, a.batch, a.reps)
+    if a.only_stem:
+        return
     for (H, ci, co, k, st) in SHAPES:
         pad = k // 2
         N = a.batch

@@ -34,6 +34,12 @@ for stage in "$@"; do
       timeout -k 10 600 python tools/conv_bench.py > gpurun_out/conv_bench.log 2>&1; rc=$?
       cat gpurun_out/conv_bench.log | grep shape
       [ $rc -eq 0 ] || { echo "conv_bench failed rc=$rc"; exit $rc; } ;;
+    stembench)
+      timeout -k 10 300 python tools/conv_bench.py --only-stem > gpurun_out/stem_bench.log 2>&1; rc=$?
+      [ $rc -eq 0 ] || { echo "stem bench failed rc=$rc"; exit $rc; }
+      PDT_FWD_STAGES=2 timeout -k 10 300 python tools/conv_bench.py --only-stem >> gpurun_out/stem_bench.log 2>&1; rc=$?
+      grep shape gpurun_out/stem_bench.log
+      [ $rc -eq 0 ] || { echo "stem bench (2-stage) failed rc=$rc"; exit $rc; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
       tail -5 gpurun_out/smoke.log
