@@ -149,9 +149,11 @@ int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (i
 
 // Backward-data of a (strided) conv in ONE launch: phases = [(ph, pw, T, U, ioff_h, ioff_w, woff), ...]
 // over dY [N,P,Q,K] -> dX [N,H,W,C] (+ residual), wt = concatenated per-phase [C][T][U][K] weights.
-void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
-                int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride, const std::vector<std::vector<int64_t>>& phases,
-                int64_t bm, int64_t bn, int64_t bk) {
+void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P,
+                     int64_t Q, int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride,
+                     const std::vector<std::vector<int64_t>>& phases, int64_t bm, int64_t bn, int64_t bk, int64_t bnb,
+                     const OptT& bn_y1, const OptT& bn_coef1, const OptT& bn_y2, const OptT& bn_coef2,
+                     const OptT& bn_out, const OptT& bn_slots) {
   const int dt = dt16(dy, "dy");
   TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "conv_dgrad: mixed dtypes");
   TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv_dgrad: size mismatch");
@@ -185,7 +187,35 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res,
   }
   TORCH_CHECK(maxM < (int64_t(1) << 31), "conv_dgrad: N*Pm*Qm must be < 2^31 (32-bit pixel indexing)");
   a.M = maxM;
+  if (bnb != 0) {
+    // fused BN-backward reduce of the BatchNorm that consumes dx (see conv_fwd.h)
+    TORCH_CHECK(bnb >= 1 && bnb <= 3, "conv_dgrad: bnb must be 0..3");
+    TORCH_CHECK(bn_y1.has_value() && bn_coef1.has_value() && bn_slots.has_value(), "conv_dgrad: bnb needs y1/coef1/slots");
+    TORCH_CHECK(bn_y1->numel() == dx.numel() && dt16(*bn_y1, "bn_y1") == dt && bn_coef1->numel() >= 4 * C,
+                "conv_dgrad: bn_y1 / bn_coef1 size");
+    TORCH_CHECK(bnb == 1 || (bn_out.has_value() && bn_out->numel() == dx.numel() && dt16(*bn_out, "bn_out") == dt),
+                "conv_dgrad: bnb 2/3 need the block output (ReLU mask)");
+    TORCH_CHECK(bnb != 3 || (bn_y2.has_value() && bn_coef2.has_value() && bn_y2->numel() == dx.numel() &&
+                             bn_coef2->numel() >= 4 * C),
+                "conv_dgrad: bnb 3 needs y2/coef2");
+    TORCH_CHECK((bnb == 1) == !res.has_value(), "conv_dgrad: bnb 1 runs without, 2/3 with the residual");
+    TORCH_CHECK(C % 4 == 0 && bn_slots->numel() >= pdt::kStatSlots * C * (bnb == 3 ? 4 : 2),
+                "conv_dgrad: bn_slots too small");
+    a.bnb = (int)bnb;
+    a.bn_y1 = p16(*bn_y1, "bn_y1");
+    a.bn_coef1 = pf(*bn_coef1, "bn_coef1");
+    if (bn_y2.has_value()) a.bn_y2 = p16(*bn_y2, "bn_y2");
+    if (bn_coef2.has_value()) a.bn_coef2 = pf(*bn_coef2, "bn_coef2");
+    if (bn_out.has_value()) a.bn_out = p16(*bn_out, "bn_out");
+    a.stats = pd(*bn_slots, "bn_slots");
+  }
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+}
+
+void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
+                int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride, const std::vector<std::vector<int64_t>>& phases,
+                int64_t bm, int64_t bn, int64_t bk) {
+  conv_dgrad_impl(dy, wt, dx, res, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk, 0, {}, {}, {}, {}, {}, {});
 }
 
 std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks,
@@ -452,6 +482,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_m_tiles", &conv_m_tiles);
   m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad_bn", &conv_dgrad_impl);
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_reduce", &wgrad_reduce);

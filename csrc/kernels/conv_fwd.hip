@@ -38,7 +38,7 @@ typedef __attribute__((address_space(1))) void glb_void;
 template <int CHUNKS>
 PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
-template <int DT, int BM, int BN, int BK, int WAVES_N, bool STATS, bool RES, int STAGES>
+template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, bool RES, int STAGES>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
@@ -224,11 +224,19 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   }
 
   // ---- epilogue: lane holds channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
-  float csum[FN][4], csq[FN][4];
+  // EPI: 0 plain | 1 forward BN statistics (sum, sumsq of the rounded outputs) | 2..4 BN-backward
+  // reduce of the consumer BatchNorm fused into this (backward-data) conv: the output written is
+  // dz = v * relu'(.), and per channel sum(dz), sum(dz * xhat) accumulate (2: ReLU mask recomputed from
+  // the BN input y1 and its forward coefficients; 3: mask = (block output > 0); 4: as 3 plus a second
+  // BN branch y2 sharing dz, e.g. a residual block's downsample BN).
+  constexpr int KS = EPI == 0 ? 0 : (EPI == 4 ? 3 : 2);  // accumulated quantities per channel
+  float sacc[FN][4][KS > 0 ? KS : 1];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < (KS > 0 ? KS : 1); ++k) sacc[i][r][k] = 0.f;
 
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
@@ -250,6 +258,30 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
           v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
           v[3] += E::to_f((uint16_t)(rr.y >> 16));
         }
+        float y1[4], y2[4];
+        if constexpr (EPI >= 2) {
+          const uint2 q1 = *(const uint2*)(a.bn_y1 + obase + n);
+          y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
+          y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
+          if constexpr (EPI == 2) {
+            const float4 sc = *(const float4*)(a.bn_coef1 + n), sh = *(const float4*)(a.bn_coef1 + a.Kout + n);
+            if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
+            if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
+            if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
+            if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
+          } else {
+            const uint2 qo = *(const uint2*)(a.bn_out + obase + n);
+            if (!(E::to_f((uint16_t)(qo.x & 0xffff)) > 0.f)) v[0] = 0.f;
+            if (!(E::to_f((uint16_t)(qo.x >> 16)) > 0.f)) v[1] = 0.f;
+            if (!(E::to_f((uint16_t)(qo.y & 0xffff)) > 0.f)) v[2] = 0.f;
+            if (!(E::to_f((uint16_t)(qo.y >> 16)) > 0.f)) v[3] = 0.f;
+          }
+          if constexpr (EPI == 4) {
+            const uint2 q2 = *(const uint2*)(a.bn_y2 + obase + n);
+            y2[0] = E::to_f((uint16_t)(q2.x & 0xffff)); y2[1] = E::to_f((uint16_t)(q2.x >> 16));
+            y2[2] = E::to_f((uint16_t)(q2.y & 0xffff)); y2[3] = E::to_f((uint16_t)(q2.y >> 16));
+          }
+        }
         uint16_t o[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = E::from_f(v[r]);
@@ -257,54 +289,74 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
         packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
         packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
         *(uint2*)(a.y + obase + n) = packed;
-        if constexpr (STATS) {
+        if constexpr (EPI == 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float q = E::to_f(o[r]);
-            csum[i][r] += q;
-            csq[i][r] += q * q;
+            sacc[i][r][0] += q;
+            sacc[i][r][1] += q * q;
+          }
+        } else if constexpr (EPI >= 2) {
+          const float4 mu = *(const float4*)(a.bn_coef1 + 2 * a.Kout + n);
+          const float4 is = *(const float4*)(a.bn_coef1 + 3 * a.Kout + n);
+          const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float dz = E::to_f(o[r]);
+            sacc[i][r][0] += dz;
+            sacc[i][r][1] += dz * (y1[r] - m1[r]) * i1[r];
+          }
+          if constexpr (EPI == 4) {
+            const float4 mu2 = *(const float4*)(a.bn_coef2 + 2 * a.Kout + n);
+            const float4 is2 = *(const float4*)(a.bn_coef2 + 3 * a.Kout + n);
+            const float m2[4] = {mu2.x, mu2.y, mu2.z, mu2.w}, i2[4] = {is2.x, is2.y, is2.z, is2.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sacc[i][r][2] += E::to_f(o[r]) * (y2[r] - m2[r]) * i2[r];
           }
         }
       }
     }
   }
 
-  if constexpr (STATS) {
-    // reduce over the 16 lanes (pixels) that share fq, then over the WAVES_M waves
+  if constexpr (KS > 0) {
+    // reduce over the 16 lanes (pixels) that share fq (DPP row scan: lane fr == 15 holds the total),
+    // then over the WAVES_M waves through LDS, then fp64 atomics into one of kStatSlots slot copies
+    // (by M tile: low per-address contention).  Slot layout [kStatSlots][Kout][KO].
+    constexpr int KO = EPI == 4 ? 4 : 2;  // stored quantities (EPI 4: sum dz is stored twice)
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          csum[i][r] += __shfl_xor(csum[i][r], o, 64);
-          csq[i][r] += __shfl_xor(csq[i][r], o, 64);
-        }
-      }
-    float* red = (float*)smem;  // [WAVES_M][BN][2]
+        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
+    float* red = (float*)smem;  // [WAVES_M][BN][KS]
     __syncthreads();
-    if (fr == 0) {
+    if (fr == 15) {
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int nl = wn * WN + i * 16 + 4 * fq + r;
-          red[(wm * BN + nl) * 2 + 0] = csum[i][r];
-          red[(wm * BN + nl) * 2 + 1] = csq[i][r];
+#pragma unroll
+          for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
         }
     }
     __syncthreads();
     if (tid < BN) {
-      float s = 0.f, q = 0.f;
+      float t[KS];
 #pragma unroll
-      for (int w = 0; w < WAVES_M; ++w) {
-        s += red[(w * BN + tid) * 2 + 0];
-        q += red[(w * BN + tid) * 2 + 1];
+      for (int k = 0; k < KS; ++k) t[k] = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) t[k] += red[(w * BN + tid) * KS + k];
+      double* dst = a.stats + ((int64_t)(tile_m % kStatSlots) * a.Kout + n0 + tid) * KO;
+      atomicAdd(dst, (double)t[0]);
+      atomicAdd(dst + 1, (double)t[1]);
+      if constexpr (EPI == 4) {
+        atomicAdd(dst + 2, (double)t[0]);
+        atomicAdd(dst + 3, (double)t[2]);
       }
-      // fp64 atomics into one of kStatSlots copies (by M tile) keep per-address contention low
-      double* dst = a.stats + ((int64_t)(tile_m % kStatSlots) * a.Kout + n0 + tid) * 2;
-      atomicAdd(dst, (double)s);
-      atomicAdd(dst + 1, (double)q);
     }
   }
 }
@@ -318,15 +370,24 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
   }
   dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(256);
-  const bool st = a.stats != nullptr, rs = a.res != nullptr;
-  if (st && rs)
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, true, STAGES>), grid, block, 0, s, a);
-  else if (st)
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, true, false, STAGES>), grid, block, 0, s, a);
-  else if (rs)
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, true, STAGES>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, false, false, STAGES>), grid, block, 0, s, a);
+  const bool rs = a.res != nullptr;
+  const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
+#define PDT_K(E_, R_) hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, E_, R_, STAGES>), grid, block, 0, s, a)
+  if (epi == 0) {
+    if (rs) PDT_K(0, true); else PDT_K(0, false);
+  } else if (epi == 1) {
+    if (rs) PDT_K(1, true); else PDT_K(1, false);
+  } else if constexpr (BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 16384) {
+    // fused BN-backward epilogues: only on the backward-data tiles (128x128x64, 256x64x64)
+    if (epi == 2 && !rs) PDT_K(2, false);
+    else if (epi == 3 && rs) PDT_K(3, true);
+    else if (epi == 4 && rs) PDT_K(4, true);
+    else pdt_hip_fail("conv_fwd: unsupported BN-backward epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
+  } else {
+    pdt_hip_fail("conv_fwd: BN-backward epilogue needs a 128x128x64 or 256x64x64 tile", hipErrorInvalidValue,
+                 __FILE__, __LINE__);
+  }
+#undef PDT_K
 }
 
 template <int DT>
@@ -377,7 +438,8 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
 }
 
 void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s) {
-  if (a.stats) PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * 2 * kStatSlots * a.Kout, s));
+  if (a.stats)
+    PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * (a.bnb == 3 ? 4 : 2) * kStatSlots * a.Kout, s));
   if (dtype == kBF16)
     launch_dt<kBF16>(a, bm, bn, bk, s);
   else

@@ -224,8 +224,11 @@ class ResNetExecutor:
         self.C.bn_eval_coef(self._p(bn.gslot), self._p(bn.bslot), bn.mod.running_mean, bn.mod.running_var,
                             bn.eps, bn.coef)
 
-    def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None):
-        """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``."""
+    def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None, bnb=None):
+        """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``.
+
+        ``bnb`` = (mode, y1, coef1, y2, coef2, out, slots): fuse the consuming BatchNorm's backward
+        reduce into the data-gradient epilogue (``dx`` then holds dz = dx * relu'; see conv_fwd.h)."""
         # --- wgrad
         if wgrad_geom is None:
             xg, Hx, Wx, Cx, R, S, st, pad = x, H, W, c.cin, c.R, c.S, c.st, c.pad
@@ -240,7 +243,11 @@ class ResNetExecutor:
         bk = 64 if c.cout % 64 == 0 else 32
         phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
                   if H - ph > 0 and W - pw > 0]
-        self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk)
+        if bnb is None:
+            self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk)
+        else:
+            self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk,
+                                 *bnb)
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
                win=False, dil=1):
@@ -420,6 +427,7 @@ class ResNetExecutor:
         g = self._buf("g_a", N * Hc * Wc * Cc)
         Cn.avgpool_bwd(dfeat, g, N, Hc * Wc, Cc, self.feat)
         gsel = 0
+        g_fused = None  # BN-backward sums of this block's output BN, produced by the previous dgrad epilogue
         for bi in range(len(self.blocks) - 1, -1, -1):
             b, rec = self.blocks[bi], saved["blocks"][bi]
             convs, bns = b["convs"], b["bns"]
@@ -429,13 +437,22 @@ class ResNetExecutor:
             x, Hin, Win, Cin = rec["x"], rec["H"], rec["W"], rec["C"]
             # block-output reduction: BN of the last conv (+ downsample BN) share dz = g * relu'(out)
             ds = b["ds_conv"] is not None
-            self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["out"], cnt, b["ds_bn"] if ds else None,
-                        rec["yd"] if ds else None)
+            dsbn = b["ds_bn"] if ds else None
+            if g_fused is not None:  # g already holds dz; sums are in the slots
+                self._bn_bwd_finish(g_fused, cnt, bns[-1], dsbn)
+                mask_src = None
+            else:
+                self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["out"], cnt, dsbn, rec["yd"] if ds else None)
+                mask_src = rec["out"]
             dy_last = self._buf("dy_a", rec["ys"][-1].numel())
             if ds:
                 dyd = self._buf("dy_b", rec["yd"].numel())
-                Cn.bn_bwd_apply(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy_last, rec["yd"], b["ds_bn"].bcoef,
+                Cn.bn_bwd_apply(g, mask_src, rec["ys"][-1], bns[-1].bcoef, dy_last, rec["yd"], dsbn.bcoef,
                                 dyd, None, convs[-1].cout)
+            elif g_fused is not None:
+                dz = g
+                Cn.bn_bwd_apply(g, None, rec["ys"][-1], bns[-1].bcoef, dy_last, None, None, None, None,
+                                convs[-1].cout)
             else:
                 dz = self._buf("dz_id", g.numel())
                 Cn.bn_bwd_apply(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy_last, None, None, None, dz,
@@ -456,17 +473,32 @@ class ResNetExecutor:
                 h, w, P, Q = rec["hw"][ci]
                 xin = rec["as"][ci - 1] if ci > 0 else x
                 if ci > 0:
+                    # dgrad epilogue applies the ReLU mask (recomputed from the BN input) and reduces the
+                    # inner BN's backward sums: da holds dz, no separate reduce pass
                     da = self._buf("da", N * h * w * c.cin)
-                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, da)
                     bnp = bns[ci - 1]
-                    a_prev = rec["as"][ci - 1]
-                    self.bn_bwd(bnp, rec["ys"][ci - 1], da, a_prev, N * h * w)
+                    yp = rec["ys"][ci - 1]
+                    slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, da, bnb=(1, yp, bnp.coef, None, None, None, slots))
+                    self._bn_bwd_finish(slots, N * h * w, bnp)
                     dname = "dy_c" if dname == "dy_a" else "dy_a"
-                    dyp = self._buf(dname, rec["ys"][ci - 1].numel())
-                    Cn.bn_bwd_apply(da, a_prev, rec["ys"][ci - 1], bnp.bcoef, dyp, None, None, None, None, c.cin)
+                    dyp = self._buf(dname, yp.numel())
+                    Cn.bn_bwd_apply(da, None, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
                     dy = dyp
+                elif bi > 0:
+                    # gnext is the previous block's output gradient: fuse that block's output-BN reduce
+                    # (ReLU mask from its output, one or two BN branches) into this dgrad's epilogue
+                    pb, prec = self.blocks[bi - 1], saved["blocks"][bi - 1]
+                    pds = pb["ds_conv"] is not None
+                    K = 4 if pds else 2
+                    slots = self._buf(("bnslots", c.cin, K), self.n_slots * c.cin * K, torch.float64)
+                    bnb = (3 if pds else 2, prec["ys"][-1], pb["bns"][-1].coef, prec["yd"] if pds else None,
+                           pb["ds_bn"].coef if pds else None, prec["out"], slots)
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, bnb=bnb)
+                    g_fused = slots
                 else:
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res)
+                    g_fused = None
             g = gnext
             gsel ^= 1
         # stem: fused max-pool backward + ReLU mask + BN backward (two passes, no 112x112 dz tensor)

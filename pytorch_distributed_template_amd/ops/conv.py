@@ -81,8 +81,11 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 1, pad: int = 0,
-               residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dX (NHWC, [N, H, W, Cin]) of ``y = conv(x, w)`` given dY ([N, P, Q, Cout])."""
+               residual: Optional[torch.Tensor] = None, bnb: Optional[tuple] = None) -> torch.Tensor:
+    """dX (NHWC, [N, H, W, Cin]) of ``y = conv(x, w)`` given dY ([N, P, Q, Cout]).
+
+    ``bnb = (mode, y1, coef1, y2, coef2, out, slots)`` fuses the consuming BatchNorm's backward reduce
+    into the epilogue (the result is then dz = dX * relu'; sums land in ``slots``)."""
     N, P, Q, K = dy.shape
     K2, R, S, C = w.shape
     assert K == K2
@@ -100,7 +103,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
         phases.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, off])
         off += idx.numel()
     wt = torch.cat(pieces).contiguous() if pieces else torch.zeros(1, dtype=w.dtype, device=w.device)
-    native.C.conv_dgrad(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk)
+    if bnb is None:
+        native.C.conv_dgrad(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk)
+    else:
+        native.C.conv_dgrad_bn(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk, *bnb)
     return dx
 
 

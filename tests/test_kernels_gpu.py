@@ -288,3 +288,49 @@ def test_stem_kernel_persistent_tiles():
     yf = ys.view(-1, K).double()
     assert torch.allclose(st[:, 0], yf.sum(0), rtol=1e-4, atol=1e-1)
     assert torch.allclose(st[:, 1], (yf * yf).sum(0), rtol=1e-4, atol=1e-1)
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 1, 1), (2, 15, 13, 128, 128, 3, 2, 1), (3, 14, 14, 256, 128, 1, 2, 0)])
+def test_conv_dgrad_fused_bn_backward(case, mode):
+    """dgrad epilogue with the consumer BN's backward reduce (ReLU mask + sum dz, sum dz*xhat) vs torch."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(11)
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    dy = _rand16(N, P, Q, K)
+    w = _rand16(K, R, R, C, scale=(1.0 / (K * R * R)) ** 0.5)
+    res = _rand16(N, H, W, C) if mode > 1 else None
+    plain = conv.conv_dgrad(dy, w, H, W, st, pad, residual=res).float()
+
+    def coef_for(y):
+        yf = y.float().view(-1, C)
+        mean, var = yf.mean(0), yf.var(0, unbiased=False)
+        invstd = torch.rsqrt(var + 1e-5)
+        scale = torch.rand(C, device=DEV) + 0.5
+        shift = torch.randn(C, device=DEV) * 0.3
+        return torch.cat([scale, shift, mean, invstd]).contiguous(), mean, invstd
+
+    y1 = _rand16(N, H, W, C)
+    coef1, m1, i1 = coef_for(y1)
+    y2 = _rand16(N, H, W, C) if mode == 3 else None
+    coef2, m2, i2 = coef_for(y2) if mode == 3 else (None, None, None)
+    out = torch.relu(_rand16(N, H, W, C)).to(torch.bfloat16) if mode > 1 else None
+    K_ = 4 if mode == 3 else 2
+    slots = torch.zeros(native.C.stat_slots() * C * K_, dtype=torch.float64, device=DEV)
+    dz = conv.conv_dgrad(dy, w, H, W, st, pad, residual=res, bnb=(mode, y1, coef1, y2, coef2, out, slots))
+    if mode == 1:
+        mask = (y1.float() * coef1[:C] + coef1[C:2 * C]) > 0
+    else:
+        mask = out.float() > 0
+    ref_dz = plain * mask
+    assert _rel(dz, ref_dz) < 1e-2
+    sums = slots.view(-1, C, K_).sum(0)
+    dzf = dz.float().view(-1, C).double()
+    x1 = ((y1.float() - m1) * i1).view(-1, C).double()
+    assert torch.allclose(sums[:, 0], dzf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sums[:, 1], (dzf * x1).sum(0), rtol=1e-3, atol=1e-2)
+    if mode == 3:
+        x2 = ((y2.float() - m2) * i2).view(-1, C).double()
+        assert torch.allclose(sums[:, 2], dzf.sum(0), rtol=1e-3, atol=1e-2)
+        assert torch.allclose(sums[:, 3], (dzf * x2).sum(0), rtol=1e-3, atol=1e-2)
