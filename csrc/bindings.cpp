@@ -258,6 +258,31 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   pdt::conv_wgrad_launch(a, dt, cur_stream());
 }
 
+// ResNet layer1 weight gradient (3x3/s1/p1, C = Kout = 64, W = 56): all 9 taps per block; writes
+// `blocks` fp32 partials [blocks][64][576] into ws and returns blocks (sum them with wgrad_reduce).
+int64_t wgrad_blocks_3x3c64() { return pdt::wgrad3x3_c64_blocks(); }
+
+bool wgrad_3x3c64_supported(int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t W, int64_t stride, int64_t pad) {
+  return pdt::wgrad3x3_c64_supported((int)C, (int)Kout, (int)T, (int)U, (int)W, (int)stride, (int)pad, 0);
+}
+
+int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W) {
+  const int dt = dt16(x, "x");
+  TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad_3x3c64: mixed dtypes");
+  TORCH_CHECK(pdt::wgrad3x3_c64_supported(64, 64, 3, 3, (int)W, 1, 1, 0), "conv_wgrad_3x3c64: needs W == 56");
+  TORCH_CHECK(x.numel() == N * H * W * 64 && dy.numel() == x.numel(), "conv_wgrad_3x3c64: size mismatch");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30), "conv_wgrad_3x3c64: operands exceed 2 GiB (32-bit buffer offsets)");
+  const int blocks = pdt::wgrad3x3_c64_blocks();
+  TORCH_CHECK(ws.numel() >= (int64_t)blocks * 64 * 576, "conv_wgrad_3x3c64: workspace too small");
+  pdt::ConvWgradArgs a{};
+  a.x = p16(x, "x");
+  a.dy = p16(dy, "dy");
+  a.ws = pf(ws, "ws");
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = 64; a.Kout = 64; a.T = 3; a.U = 3; a.ldw = 576;
+  pdt::wgrad3x3_c64_launch(a, blocks, dt, cur_stream());
+  return blocks;
+}
+
 void wgrad_reduce(const Tensor& ws, int64_t splits, int64_t rows, int64_t cols, int64_t ldw, int64_t split_stride,
                   Tensor& out, int64_t ldo, double scale, bool accumulate) {
   TORCH_CHECK(ws.numel() >= (splits - 1) * split_stride + (rows - 1) * ldw + cols, "wgrad_reduce: ws too small");
@@ -486,6 +511,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("wgrad_reduce", &wgrad_reduce);
+  m.def("wgrad_blocks_3x3c64", &wgrad_blocks_3x3c64);
+  m.def("wgrad_3x3c64_supported", &wgrad_3x3c64_supported);
+  m.def("conv_wgrad_3x3c64", &conv_wgrad_3x3c64);
   m.def("bn_slot_sum", &bn_slot_sum);
   m.def("stat_slots", &stat_slots);
   m.def("bn_finalize", &bn_finalize);

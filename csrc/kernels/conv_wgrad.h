@@ -22,6 +22,11 @@ struct ConvWgradArgs {
 
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks);
 void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s);
+// 3x3/s1/p1 C = Kout = 64, W = 56 specialisation: all 9 taps per block, persistent over 4-row tiles;
+// writes `blocks` fp32 partials [blocks][64][ldw] (ldw >= 576) for wgrad_reduce.
+bool wgrad3x3_c64_supported(int C, int Kout, int T, int U, int W, int stride, int pad, int win);
+int wgrad3x3_c64_blocks();
+void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s);
 void wgrad_reduce_launch(const float* ws, int splits, int rows, int cols, int ldw, int64_t split_stride,
                          float* out, int ldo, float scale, bool accumulate, hipStream_t s);
 

@@ -308,6 +308,168 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 weight gradient for C = Kout = 64 and W = 56 (ResNet layer1, the most
+// expensive weight gradients of ResNet-18/34), all 9 taps in one block.
+//
+// The 64x64-tile kernel above re-reads dY and X once per tap (32 FLOP per staged byte: L2/DMA bound).
+// Here a block tile is 4 output rows x 56 columns of one image: dY rows [4][56][64] and the X halo
+// [6][58][64] (rows h0-1 .. h0+4, columns -1 .. 56, zero padding through the buffer range check) are
+// staged ONCE per tile (72 KB, 2-deep LDS-DMA ring), and the 9 taps read shifted windows of the halo
+// (~230 FLOP per staged byte).  Waves split the 64 x 64 output quadrant-wise (32 k x 32 c x 9 taps,
+// 144 fp32 accumulators per lane).  A K-step = 32 pixels = column block j (8 px) of each of the 4
+// output rows, so every 8-pixel MFMA k-group stays inside one row and tap shifts are plain row offsets.
+// LDS rows are swizzled by (column bit 1, tile-row bit 0): conflict-free transposed reads for every
+// tap shift (tools/ simulation).  Blocks are persistent (one per CU); each writes one fp32 partial
+// [64][9*64] that wgrad_reduce sums.
+namespace {
+constexpr int kL1W = 56;                      // image width handled
+constexpr int kL1XP = kL1W + 2;               // halo row pitch (pixels)
+constexpr int kL1XRows = 6 * kL1XP;           // 348 halo pixels
+constexpr int kL1XBytes = 44 * 1024;          // 352 rows of 128 B (rows >= 348 read zeros)
+constexpr int kL1YBytes = 4 * kL1W * 128;     // 28 KB
+constexpr int kL1Stage = kL1XBytes + kL1YBytes;
+PDT_DEVICE int l1_swz(int row2d, int col) { return (((col >> 1) & 1) << 1) | ((row2d & 1) << 2); }
+}  // namespace
+
+template <int DT>
+__global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kL1Stage];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = wave & 1, chh = wave >> 1;  // this wave's k half and c half
+
+  const int TH = (a.H + 3) / 4;  // row tiles per image
+  const int tiles = a.N * TH;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, lb = blockIdx.x >> 3, per_x = G >> 3;
+  const int t_per = (tiles + 7) >> 3;
+  const int t_begin = xcd * t_per, t_end = min(tiles, t_begin + t_per);
+
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * kL1W * 128u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.N * a.H * kL1W * 128u);
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  // 72 DMA instructions per stage (44 X + 28 dY), 18 per wave
+  auto stage_tile = [&](int t, int buf) {
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    char* sb = smem + buf * kL1Stage;
+#pragma unroll
+    for (int m = 0; m < 18; ++m) {
+      const int ii = wave + 4 * m;
+      if (ii < 44) {
+        const int R = ii * 8 + lrow;
+        const int hr = R / kL1XP, wc = R - (R / kL1XP) * kL1XP;
+        const int h = h0 - 1 + hr, w = wc - 1;
+        const bool ok = R < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W;
+        const int ch = pch ^ l1_swz(hr, wc);
+        const uint32_t off = ok ? (uint32_t)((((n * a.H + h) * kL1W + w) * 64 + ch * 8) * 2) : kOOB;
+        buf_lds16(rx, sb + ii * 1024, off);
+      } else {
+        const int R = (ii - 44) * 8 + lrow;
+        const int r = R / kL1W, w = R - (R / kL1W) * kL1W;
+        const int h = h0 + r;
+        const int ch = pch ^ l1_swz(r, w);
+        const uint32_t off = h < a.H ? (uint32_t)((((n * a.H + h) * kL1W + w) * 64 + ch * 8) * 2) : kOOB;
+        buf_lds16(ry, sb + ii * 1024, off);
+      }
+    }
+  };
+
+  f32x4_t acc[9][2][2];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tp][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry: 16-lane group g <-> output row g of the K-step
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+  // fragment read: 16 channels [f*16, f*16+16) x 8 pixels (LDS rows R0+0..3 and R0+4..7)
+  auto frag = [&](const char* base, int row2d, int col, int f) -> vec8 {
+    const int e = f * 16 + 4 * p4;
+    const int ch = e >> 3, off = (e & 7) * 2;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(base + ((ch ^ l1_swz(row2d, col)) << 4) + off));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(base + 4 * 128 + ((ch ^ l1_swz(row2d, col + 4)) << 4) + off));
+    return __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  int t = t_begin + lb;
+  int buf = 0;
+  if (t < t_end) stage_tile(t, 0);
+  for (; t < t_end; t += per_x) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
+    const char* sx = smem + buf * kL1Stage;
+    const char* sy = sx + kL1XBytes;
+#pragma unroll 1
+    for (int j = 0; j < kL1W / 8; ++j) {
+      // A = dY^T (rows k): output row g, columns 8j + q (+4)
+      const int ycol = 8 * j + q;
+      const char* yb = sy + (g * kL1W + ycol) * 128;
+      vec8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = frag(yb, g, ycol, kh * 2 + i);
+#pragma unroll
+      for (int tr = 0; tr < 3; ++tr)
+#pragma unroll
+        for (int tu = 0; tu < 3; ++tu) {
+          // B = X (cols c): halo row g + tr, halo column 8j + tu + q (+4)
+          const int xcol = 8 * j + tu + q;
+          const char* xb = sx + ((g + tr) * kL1XP + xcol) * 128;
+          vec8 bf[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) bf[c] = frag(xb, g + tr, xcol, chh * 2 + c);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+              acc[tr * 3 + tu][i][c] = E::mfma16x16x32(af[i], bf[c], acc[tr * 3 + tu][i][c]);
+        }
+    }
+    buf ^= 1;
+  }
+
+  // partial dW[k][tap][c]: lane holds rows k = kb*16 + 4*(lane>>4) + r, column c = cb*16 + (lane&15)
+  float* dst = a.ws + (int64_t)blockIdx.x * 64 * a.ldw;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int k = (kh * 2 + i) * 16 + 4 * (lane >> 4);
+        const int cc = (chh * 2 + c) * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(int64_t)(k + r) * a.ldw + tp * 64 + cc] = acc[tp][i][c][r];
+      }
+}
+
+bool wgrad3x3_c64_supported(int C, int Kout, int T, int U, int W, int stride, int pad, int win) {
+  return !win && C == 64 && Kout == 64 && T == 3 && U == 3 && W == kL1W && stride == 1 && pad == 1;
+}
+
+int wgrad3x3_c64_blocks() {
+  int dev = 0, cus = 256;
+  PDT_HIP_CHECK(hipGetDevice(&dev));
+  PDT_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return (cus + 7) / 8 * 8;
+}
+
+void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s) {
+  if (dtype == kBF16)
+    hipLaunchKernelGGL((wgrad3x3_c64_kernel<kBF16>), dim3(blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((wgrad3x3_c64_kernel<kF16>), dim3(blocks), dim3(256), 0, s, a);
+}
+
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)
 // Block = 64 float4 column groups x 4 split lanes; each split lane keeps 4 loads in flight.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int rows,

@@ -99,6 +99,7 @@ class ResNetExecutor:
         stile = os.environ.get("PDT_STEM_TILE", "")
         self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
+        self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
         derived_maps: List[torch.Tensor] = []
         off = [0]
 
@@ -251,6 +252,13 @@ class ResNetExecutor:
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
                win=False, dil=1):
+        if not win and self.wgrad_l1 and self.C.wgrad_3x3c64_supported(C, cout, R, S, W, st, pad):
+            # ResNet layer1 3x3 convs: all 9 taps per block over staged 4-row tiles (csrc conv_wgrad.hip)
+            blocks = self.C.wgrad_blocks_3x3c64()
+            ws = self._buf("ws", blocks * 64 * 576, torch.float32)
+            self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W)
+            self.C.wgrad_reduce(ws, blocks, 64, 576, 576, 64 * 576, gout, ldo, 1.0, False)
+            return
         key = (cout, R, S, C, N * P * Q, win)
         plan = self._plans.get(key)
         if plan is None:

@@ -334,3 +334,20 @@ def test_conv_dgrad_fused_bn_backward(case, mode):
         x2 = ((y2.float() - m2) * i2).view(-1, C).double()
         assert torch.allclose(sums[:, 2], dzf.sum(0), rtol=1e-3, atol=1e-2)
         assert torch.allclose(sums[:, 3], (dzf * x2).sum(0), rtol=1e-3, atol=1e-2)
+
+
+def test_wgrad_3x3c64_all_taps():
+    """Layer1 weight-gradient kernel (9 taps per block, staged 4-row tiles, persistent) vs conv2d_weight."""
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(12)
+    N, H, W = 5, 22, 56   # H not a multiple of 4: partial last row tile
+    x = _rand16(N, H, W, 64)
+    dy = _rand16(N, H, W, 64)
+    blocks = native.C.wgrad_blocks_3x3c64()
+    ws = torch.empty(blocks * 64 * 576, device=DEV)
+    assert native.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W) == blocks
+    out = torch.empty(64 * 576, device=DEV)
+    native.C.wgrad_reduce(ws, blocks, 64, 576, 576, 64 * 576, out, 576, 1.0, False)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3), dy.float().permute(0, 3, 1, 2),
+                                      stride=1, padding=1)
+    assert _rel(out.view(64, 3, 3, 64).permute(0, 3, 1, 2), ref) < 2e-3

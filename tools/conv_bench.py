@@ -74,14 +74,18 @@ def main():
     ap.add_argument("--batch", type=int, default=1200)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only-stem", action="store_true")
+    ap.add_argument("--skip-stem", action="store_true")
+    ap.add_argument("--shapes", default="", help="comma-separated indices into SHAPES (default: all)")
     a = ap.parse_args()
     C = native.C
     dev = "cuda"
     res = []
-    stem_bench(C, a.batch, a.reps)
+    if not a.skip_stem:
+        stem_bench(C, a.batch, a.reps)
     if a.only_stem:
         return
-    for (H, ci, co, k, st) in SHAPES:
+    sel = [int(v) for v in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
+    for (H, ci, co, k, st) in [SHAPES[i] for i in sel]:
         pad = k // 2
         N = a.batch
         P = (H + 2 * pad - k) // st + 1
@@ -110,6 +114,15 @@ def main():
         bm, bn = conv.conv_tile(ci)
         row["dgrad"] = round(flops / timeit(lambda: C.conv_dgrad(dy, wt, dx, None, N, P, P, co, ci, H, H, st, phases,
                                                                  bm, bn, 64), a.reps) / 1e9, 1)
+        if C.wgrad_3x3c64_supported(ci, co, k, k, H, st, pad):
+            blocks = C.wgrad_blocks_3x3c64()
+            ws = torch.empty(blocks * 64 * 576, device=dev)
+            outw = torch.empty(64 * 576, device=dev)
+
+            def l1():
+                C.conv_wgrad_3x3c64(x, dy, ws, N, H, H)
+                C.wgrad_reduce(ws, blocks, 64, 576, 576, 64 * 576, outw, 576, 1.0, False)
+            row["wgrad_l1"] = round(flops / timeit(l1, a.reps) / 1e9, 1)
         for tb in (256, 512, 1024, 2048):
             row[f"wgrad_{tb}"] = round(flops / timeit(lambda tb=tb: conv.conv_wgrad(x, dy, k, k, st, pad, tb), a.reps) / 1e9, 1)
         print(json.dumps(row), flush=True)

@@ -40,6 +40,10 @@ for stage in "$@"; do
       PDT_FWD_STAGES=2 timeout -k 10 300 python tools/conv_bench.py --only-stem >> gpurun_out/stem_bench.log 2>&1; rc=$?
       grep shape gpurun_out/stem_bench.log
       [ $rc -eq 0 ] || { echo "stem bench (2-stage) failed rc=$rc"; exit $rc; } ;;
+    l1bench)
+      timeout -k 10 300 python tools/conv_bench.py --skip-stem --shapes 0 > gpurun_out/l1_bench.log 2>&1; rc=$?
+      grep shape gpurun_out/l1_bench.log
+      [ $rc -eq 0 ] || { echo "l1 bench failed rc=$rc"; exit $rc; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
       tail -5 gpurun_out/smoke.log
