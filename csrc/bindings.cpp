@@ -359,6 +359,7 @@ void bn_relu_maxpool(const Tensor& y, const Tensor& coef, Tensor& out, Tensor& i
   const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   TORCH_CHECK(y.numel() == N * H * W * C && out.numel() == N * OH * OW * C && idx.numel() == out.numel() && C % 8 == 0,
               "bn_relu_maxpool: bad sizes");
+  TORCH_CHECK(y.numel() < (int64_t(1) << 32), "bn_relu_maxpool: tensor exceeds 2^32 elements (32-bit indexing)");
   check_dev(idx, "idx");
   pdt::bn_relu_maxpool_launch(dt, p16(y, "y"), pf(coef, "coef"), p16(out, "out"), idx.data_ptr<uint8_t>(), N, H, W, C,
                               cur_stream());
@@ -398,6 +399,7 @@ void stem_pool_bwd_apply(const Tensor& dp, const Tensor& idx, const Tensor& y, c
                   y.numel() == N * H * W * C && dy.numel() == y.numel() && idx.numel() == dp.numel() &&
                   C % 8 == 0 && coef.numel() >= 2 * C && bcoef.numel() >= 3 * C,
               "stem_pool_bwd_apply: bad sizes");
+  TORCH_CHECK(y.numel() < (int64_t(1) << 32), "stem_pool_bwd_apply: tensor exceeds 2^32 elements (32-bit indexing)");
   check_dev(idx, "idx");
   pdt::stem_pool_bwd_apply_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"),
                                   pf(bcoef, "bcoef"), p16(dy, "dy"), N, H, W, C, cur_stream());

@@ -29,6 +29,7 @@
 
 #include "../common.h"
 #include "conv_fwd.h"
+#include "conv_l1.h"
 
 namespace pdt {
 
@@ -238,6 +239,23 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
 #pragma unroll
       for (int k = 0; k < (KS > 0 ? KS : 1); ++k) sacc[i][r][k] = 0.f;
 
+  // per-channel BN coefficients of the fused BN-backward epilogues, loaded once before any store (the
+  // stores could alias them as far as the compiler knows, which would force a reload per pixel)
+  float4 c_sc[EPI == 2 ? FN : 1], c_sh[EPI == 2 ? FN : 1], c_mu[EPI >= 2 ? FN : 1], c_is[EPI >= 2 ? FN : 1];
+
+  if constexpr (EPI >= 2) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * WN + i * 16 + 4 * fq;
+      if constexpr (EPI == 2) {
+        c_sc[i] = *(const float4*)(a.bn_coef1 + n);
+        c_sh[i] = *(const float4*)(a.bn_coef1 + a.Kout + n);
+      }
+      c_mu[i] = *(const float4*)(a.bn_coef1 + 2 * a.Kout + n);
+      c_is[i] = *(const float4*)(a.bn_coef1 + 3 * a.Kout + n);
+    }
+  }
+
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
     const int64_t m = m0 + wm * WM + j * 16 + fr;
@@ -264,7 +282,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
           y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
           y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
           if constexpr (EPI == 2) {
-            const float4 sc = *(const float4*)(a.bn_coef1 + n), sh = *(const float4*)(a.bn_coef1 + a.Kout + n);
+            const float4 sc = c_sc[i], sh = c_sh[i];
             if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
             if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
@@ -297,8 +315,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
             sacc[i][r][1] += q * q;
           }
         } else if constexpr (EPI >= 2) {
-          const float4 mu = *(const float4*)(a.bn_coef1 + 2 * a.Kout + n);
-          const float4 is = *(const float4*)(a.bn_coef1 + 3 * a.Kout + n);
+          const float4 mu = c_mu[i], is = c_is[i];
           const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -307,7 +324,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
             sacc[i][r][1] += dz * (y1[r] - m1[r]) * i1[r];
           }
           if constexpr (EPI == 4) {
-            const float4 mu2 = *(const float4*)(a.bn_coef2 + 2 * a.Kout + n);
+            const float4 mu2 = *(const float4*)(a.bn_coef2 + 2 * a.Kout + n);  // (not hoisted: registers)
             const float4 is2 = *(const float4*)(a.bn_coef2 + 3 * a.Kout + n);
             const float m2[4] = {mu2.x, mu2.y, mu2.z, mu2.w}, i2[4] = {is2.x, is2.y, is2.z, is2.w};
 #pragma unroll
@@ -438,6 +455,17 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
 }
 
 void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hipStream_t s) {
+  // ResNet layer1 geometry (3x3/s1/p1, 64 -> 64, W = 56): halo-reuse kernel (conv_l1.hip);
+  // PDT_CONV_L1=0 forces the generic path
+  static const bool l1_on = [] {
+    const char* e = getenv("PDT_CONV_L1");
+    return !(e && e[0] == '0');
+  }();
+  int flip = 0;
+  if (l1_on && conv_l1_eligible(a, &flip)) {
+    conv_l1_launch(a, flip, dtype, s);
+    return;
+  }
   if (a.stats)
     PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * (a.bnb == 3 ? 4 : 2) * kStatSlots * a.Kout, s));
   if (dtype == kBF16)

@@ -1,0 +1,352 @@
+// 3x3 / stride 1 / pad 1 convolution with 64 input and 64 output channels on 56-wide images (ResNet
+// layer1, the most expensive convolutions of ResNet-18/34), forward and backward-data.
+//
+// The generic implicit-GEMM kernel (conv_fwd.hip) streams a 256-pixel x 64-channel activation tile and
+// a weight tile per (tap, channel) K-step: every activation is fetched 9 times (once per tap) and the
+// L2 -> LDS stream, not the MFMAs, bounds it (~570 TF/s).  This kernel is built around the data reuse:
+//   * the whole weight tensor (64 x 9 x 64 bf16 = 72 KB) stays resident in LDS for the block's life;
+//   * a block tile is 4 output rows x 56 columns of one image; its input halo (6 rows x 58 columns x 64
+//     channels, zero padding from the buffer range check) is staged ONCE by LDS-DMA into a 2-deep ring
+//     (tile i+1 streams in while tile i computes) and all 9 taps read shifted windows of it;
+//   * MFMA B fragments (8 consecutive channels of one pixel) are single ds_read_b128s of the halo
+//     (rows XOR-swizzled by row & 7 with a matching lane -> pixel order: conflict-free);
+//     A fragments come from the resident weights (chunks swizzled by (cout >> 1) & 7);
+//   * persistent blocks (one per CU: 72 + 2 x 43.5 KB of LDS), XCD-contiguous tile ranges;
+//   * the epilogues of conv_fwd.hip: residual add, forward BN statistics, or the fused BN-backward
+//     reduce (ReLU mask from the BN input or from the block output), statistics accumulated in
+//     registers across all of a block's tiles.
+// Backward-data is the same convolution of dY with the transposed, 180-degree-rotated weights
+// ([C][3][3][K] with taps reversed): ``flip`` reads tap 8 - t of the derived dgrad weights.
+#include <type_traits>
+
+#include "../common.h"
+#include "conv_fwd.h"
+#include "conv_l1.h"
+
+namespace pdt {
+
+namespace {
+constexpr int kW = 56;                     // image width
+constexpr int kXP = kW + 2;                // halo row pitch (pixels)
+constexpr int kXRows = 6 * kXP;            // 348 halo pixels per tile
+constexpr int kStageB = kXRows * 128;      // 44544 B
+constexpr int kWB = 64 * 9 * 64 * 2;       // 73728 B of resident weights
+constexpr int kLds = kWB + 2 * kStageB;    // 162816 B (< 160 KiB)
+constexpr int kGroups = 4 * kW / 16;       // 14 groups of 16 pixels per tile
+
+// Halo row swizzle: 16-B chunk p of LDS row R holds logical chunk p ^ (R & 7).  ds_read_b128 serves a
+// wave in 4 groups of 16 lanes; each group reads chunk c for 8 pixels and chunk c ^ 1 for 8 others.
+// With the lane -> pixel map pix_of_lane() below, each set of 8 is 8 consecutive halo rows of one image
+// row (56 is a multiple of 8), so (R & 1, c ^ (R & 7)) is distinct across the whole group: conflict-free
+// for every tap shift (tools/lds_sim.py).
+PDT_DEVICE int hswz(int R) { return R & 7; }
+// MFMA column (lane & 15) -> pixel within a 16-pixel group: lanes {0-3, 12-15} -> pixels 0..7,
+// lanes 4..11 -> pixels 8..15 (matches the ds_read_b128 lane groups {0-3,12-15,20-27}, ...)
+PDT_DEVICE int pix_of_lane(int fr) { return fr < 4 ? fr : (fr >= 12 ? fr - 8 : fr + 4); }
+PDT_DEVICE int wswz(int co, int c) { return (c & ~7) | ((c & 7) ^ ((co >> 1) & 7)); }  // weight chunk
+}  // namespace
+
+template <int DT, int EPI, bool RES>
+__global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  __shared__ __attribute__((aligned(1024))) char smem[kLds];
+  char* const wl = smem;
+  char* const stage0 = smem + kWB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int TH = (a.H + 3) / 4;
+  const int tiles = a.N * TH;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, lb = blockIdx.x >> 3, per_x = G >> 3;
+  const int t_per = (tiles + 7) >> 3;
+  const int t_begin = xcd * t_per, t_end = min(tiles, t_begin + t_per);
+
+  const uint32_t img_bytes = (uint32_t)a.N * a.H * kW * 128u;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, img_bytes);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)kWB);
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  // ---- resident weights by LDS-DMA: 72 instructions of 8 rows x 8 chunks (18 per wave) ----
+  // LDS row co has 72 chunks; LDS chunk p of row co holds source chunk wswz(co, p) (an involution)
+#pragma unroll
+  for (int m = 0; m < 18; ++m) {
+    const int ii = wave + 4 * m;
+    const int L = ii * 64 + lrow * 8 + pch;  // LDS chunk index 0..4607
+    const int co = L / 72, p = L - co * 72;
+    buf_lds16(rw, wl + ii * 1024, (uint32_t)(co * 72 + wswz(co, p)) * 16u);
+  }
+
+  // ---- halo DMA: 348 rows of 128 B (44 instructions, 11 per wave; the last one half-masked) ----
+  auto stage_tile = [&](int t, int buf) {
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    char* sb = stage0 + buf * kStageB;
+#pragma unroll
+    for (int m = 0; m < 11; ++m) {
+      const int ii = wave + 4 * m;
+      const int R = ii * 8 + lrow;
+      if (R < kXRows) {
+        const int hr = R / kXP, wc = R - (R / kXP) * kXP;
+        const int h = h0 - 1 + hr, w = wc - 1;
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW;
+        const uint32_t off = ok ? (uint32_t)((((n * a.H + h) * kW + w) * 64 + (pch ^ hswz(R)) * 8) * 2) : kOOB;
+        buf_lds16(rx, sb + ii * 1024, off);
+      }
+    }
+  };
+
+  // pixel groups of this wave: 14 groups over 4 waves -> 4, 4, 3, 3
+  const int g0 = wave < 2 ? wave * 4 : 8 + (wave - 2) * 3;
+  const int ng = wave < 2 ? 4 : 3;
+  // per group: halo row (tap 0,0) of this lane's pixel
+  int R0[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int px = (g0 + j) * 16 + pix_of_lane(fr);
+    const int r = px / kW, w = px - (px / kW) * kW;
+    R0[j] = r * kXP + w;
+  }
+
+  constexpr int KS = EPI == 0 ? 1 : 2;
+  float sacc[4][4][KS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
+
+  // per-lane BN coefficients of the fused BN-backward epilogues (this lane's 16 channels never change;
+  // loading them once also keeps them from being re-fetched after every store)
+  float4 k_sc[EPI == 2 ? 4 : 1], k_sh[EPI == 2 ? 4 : 1], k_mu[EPI >= 2 ? 4 : 1], k_is[EPI >= 2 ? 4 : 1];
+  if constexpr (EPI >= 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c0 = i * 16 + 4 * fq;
+      if constexpr (EPI == 2) {
+        k_sc[i] = *(const float4*)(a.bn_coef1 + c0);
+        k_sh[i] = *(const float4*)(a.bn_coef1 + 64 + c0);
+      }
+      k_mu[i] = *(const float4*)(a.bn_coef1 + 128 + c0);
+      k_is[i] = *(const float4*)(a.bn_coef1 + 192 + c0);
+    }
+  }
+
+  int t = t_begin + lb;
+  int buf = 0;
+  if (t < t_end) stage_tile(t, 0);
+  for (; t < t_end; t += per_x) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and the weights, first time)
+    __syncthreads();
+    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
+    const char* sb = stage0 + buf * kStageB;
+
+    // epilogue operands (residual, BN input, block output) of this tile, loaded now so their latency
+    // hides under the MFMA loop (one block per CU: nothing else would cover an exposed epilogue)
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    int64_t obase[4];
+    bool pvalid[4];
+    uint2 pre_res[RES ? 4 : 1][RES ? 4 : 1], pre_y1[EPI >= 2 ? 4 : 1][EPI >= 2 ? 4 : 1];
+    uint2 pre_out[EPI == 3 ? 4 : 1][EPI == 3 ? 4 : 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int px = (g0 + j) * 16 + pix_of_lane(fr);
+      const int r = px / kW, w = px - (px / kW) * kW;
+      pvalid[j] = (j < ng) && (h0 + r < a.H);
+      obase[j] = ((int64_t)(n * a.H + h0 + r) * kW + w) * 64;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c0 = i * 16 + 4 * fq;
+        if constexpr (RES) pre_res[j][i] = pvalid[j] ? *(const uint2*)(a.res + obase[j] + c0) : make_uint2(0, 0);
+        if constexpr (EPI >= 2) pre_y1[j][i] = pvalid[j] ? *(const uint2*)(a.bn_y1 + obase[j] + c0) : make_uint2(0, 0);
+        if constexpr (EPI == 3) pre_out[j][i] = pvalid[j] ? *(const uint2*)(a.bn_out + obase[j] + c0) : make_uint2(0, 0);
+      }
+    }
+
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // 18 K-steps (9 taps x 2 channel halves), fully unrolled so the LDS reads of a step can be issued
+    // ahead of the previous step's MFMAs; the group count is a wave-uniform branch outside the loop
+    auto run = [&](auto NGc) {
+      constexpr int NG = decltype(NGc)::value;
+#pragma unroll
+      for (int st = 0; st < 18; ++st) {
+        const int tap = st >> 1, kk = st & 1;
+        const int tr = tap / 3, tu = tap % 3;
+        const int wtap = flip ? 8 - tap : tap;
+        const int dR = tr * kXP + tu;
+        vec8 af[4], bf[NG];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = i * 16 + fr;
+          const int c = wtap * 8 + kk * 4 + fq;
+          af[i] = *(const vec8*)(wl + co * 1152 + wswz(co, c) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+          const int R = R0[j] + dR;
+          bf[j] = *(const vec8*)(sb + R * 128 + (((kk * 4 + fq) ^ hswz(R)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NG; ++j) acc[i][j] = E::mfma16x16x32(af[i], bf[j], acc[i][j]);
+      }
+    };
+    if (ng == 4)
+      run(std::integral_constant<int, 4>{});
+    else
+      run(std::integral_constant<int, 3>{});
+
+    // ---- epilogue: lane holds couts n = i*16 + 4*fq + r of pixel (g0+j)*16 + fr ----
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!pvalid[j]) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c0 = i * 16 + 4 * fq;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (RES) {
+          const uint2 rr = pre_res[j][i];
+          v[0] += E::to_f((uint16_t)(rr.x & 0xffff));
+          v[1] += E::to_f((uint16_t)(rr.x >> 16));
+          v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
+          v[3] += E::to_f((uint16_t)(rr.y >> 16));
+        }
+        float y1[4];
+        if constexpr (EPI >= 2) {
+          const uint2 q1 = pre_y1[j][i];
+          y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
+          y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
+          if constexpr (EPI == 2) {
+            const float4 sc = k_sc[i], sh = k_sh[i];
+            if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
+            if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
+            if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
+            if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
+          } else {
+            const uint2 qo = pre_out[j][i];
+            if (!(E::to_f((uint16_t)(qo.x & 0xffff)) > 0.f)) v[0] = 0.f;
+            if (!(E::to_f((uint16_t)(qo.x >> 16)) > 0.f)) v[1] = 0.f;
+            if (!(E::to_f((uint16_t)(qo.y & 0xffff)) > 0.f)) v[2] = 0.f;
+            if (!(E::to_f((uint16_t)(qo.y >> 16)) > 0.f)) v[3] = 0.f;
+          }
+        }
+        uint16_t o[4];
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2) o[r2] = E::from_f(v[r2]);
+        uint2 packed;
+        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        *(uint2*)(a.y + obase[j] + c0) = packed;
+        if constexpr (EPI == 1) {
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2) {
+            const float q = E::to_f(o[r2]);
+            sacc[i][r2][0] += q;
+            sacc[i][r2][1] += q * q;
+          }
+        } else if constexpr (EPI >= 2) {
+          const float4 mu = k_mu[i], is = k_is[i];
+          const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2) {
+            const float dz = E::to_f(o[r2]);
+            sacc[i][r2][0] += dz;
+            sacc[i][r2][1] += dz * (y1[r2] - m1[r2]) * i1[r2];
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+  if constexpr (EPI > 0) {
+    // block totals: DPP row scan over the 16 pixel lanes, then the 4 waves through LDS (stage 0 is
+    // free once every wave passed the barrier below), fp64 atomics into slot blockIdx % kStatSlots
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* red = (float*)stage0;  // [4 waves][64][2]
+    if (fr == 15) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = i * 16 + 4 * fq + r;
+          red[(wave * 64 + c) * 2 + 0] = sacc[i][r][0];
+          red[(wave * 64 + c) * 2 + 1] = sacc[i][r][1];
+        }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const float s = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
+      atomicAdd(a.stats + (int64_t)(blockIdx.x % kStatSlots) * 128 + tid, (double)s);
+    }
+  }
+}
+
+bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
+  if (a.C != 64 || a.Kout != 64 || a.cs != 64 || a.W != kW || a.OW != kW || a.bnb == 3) return false;
+  if (a.nphase == 0) {
+    if (a.T == 3 && a.U == 3 && a.ist_h == 1 && a.ist_w == 1 && a.ioff_h == -1 && a.ioff_w == -1 &&
+        a.tstep_h == 1 && a.tstep_w == 1 && a.ost_h == 1 && a.ost_w == 1 && a.ooff_h == 0 && a.ooff_w == 0 &&
+        a.Pm == a.H && a.Qm == kW && a.OH == a.H) {
+      *flip = 0;
+      return true;
+    }
+    return false;
+  }
+  // single-phase backward-data of a stride-1 3x3 conv: in = i + 1 - t (taps flipped)
+  if (a.nphase == 1 && a.pT[0] == 3 && a.pU[0] == 3 && a.pioff_h[0] == 1 && a.pioff_w[0] == 1 &&
+      a.tstep_h == -1 && a.tstep_w == -1 && a.ist_h == 1 && a.ist_w == 1 && a.ost_h == 1 && a.ost_w == 1 &&
+      a.pooff_h[0] == 0 && a.pooff_w[0] == 0 && a.pPm[0] == a.H && a.pQm[0] == kW && a.OH == a.H) {
+    *flip = 1;
+    return true;
+  }
+  return false;
+}
+
+void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s) {
+  ConvFwdArgs a = args;
+  if (a.nphase == 1) a.w = args.w + args.pwoff[0];
+  int dev = 0, cus = 256;
+  PDT_HIP_CHECK(hipGetDevice(&dev));
+  PDT_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int tiles = a.N * ((a.H + 3) / 4);
+  int G = (cus + 7) / 8 * 8;
+  const int cap = (tiles + 7) / 8 * 8;
+  if (G > cap) G = cap;
+  const bool rs = a.res != nullptr;
+  const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
+  if (a.stats) PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * 2 * kStatSlots * 64, s));
+#define PDT_L1(DT_, E_, R_) hipLaunchKernelGGL((conv_l1_kernel<DT_, E_, R_>), dim3(G), dim3(256), 0, s, a, flip)
+#define PDT_L1_DT(DT_)                                                                                 \
+  if (epi == 0 && !rs) PDT_L1(DT_, 0, false);                                                          \
+  else if (epi == 0 && rs) PDT_L1(DT_, 0, true);                                                       \
+  else if (epi == 1 && !rs) PDT_L1(DT_, 1, false);                                                     \
+  else if (epi == 2 && !rs) PDT_L1(DT_, 2, false);                                                     \
+  else if (epi == 3 && rs) PDT_L1(DT_, 3, true);                                                       \
+  else pdt_hip_fail("conv_l1: unsupported epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
+  if (dtype == kBF16) {
+    PDT_L1_DT(kBF16)
+  } else {
+    PDT_L1_DT(kF16)
+  }
+#undef PDT_L1_DT
+#undef PDT_L1
+}
+
+}  // namespace pdt

@@ -26,14 +26,14 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
                                                               int N, int H, int W, int C, int OH, int OW) {
   using E = E16<DT>;
   const int cv = C / 8;
-  const int64_t total = (int64_t)N * OH * OW * cv;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(v % cv) * 8;
-    int64_t pix = v / cv;
-    const int ow = (int)(pix % OW);
-    pix /= OW;
-    const int oh = (int)(pix % OH);
-    const int n = (int)(pix / OH);
+  const uint32_t total = (uint32_t)N * OH * OW * cv;  // 32-bit index math (host checks sizes < 2^32)
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < total; v += gridDim.x * 256u) {
+    const uint32_t pixv = v / cv;
+    const int c0 = (int)(v - pixv * cv) * 8;
+    const int ow = (int)(pixv % OW);
+    const uint32_t t = pixv / OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
       for (int kw = 0; kw < 3; ++kw) {
         const int w = ow * 2 - 1 + kw;
         if ((unsigned)w >= (unsigned)W) continue;
-        const uint4 q = *(const uint4*)(y + (((int64_t)n * H + h) * W + w) * C + c0);
+        const uint4 q = *(const uint4*)(y + ((uint32_t)(n * H + h) * W + w) * C + c0);
         const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     uint32_t ow_[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) ow_[e] = (uint32_t)E::from_f(best[2 * e]) | ((uint32_t)E::from_f(best[2 * e + 1]) << 16);
-    const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+    const uint32_t o = pixv * C + c0;
     *(uint4*)(out + o) = make_uint4(ow_[0], ow_[1], ow_[2], ow_[3]);
     uint2 ib;
     ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
@@ -237,7 +237,10 @@ void stem_pool_bwd_reduce_launch(int dtype, const uint16_t* dp, const uint8_t* i
 }
 
 // Stem backward, pass 2: dy = A*dz + B*y + Cc at every conv-output element, with dz gathered from the
-// (<= 4) pooling windows that selected it and masked by ReLU (recomputed from y and the BN coefficients).
+// pooling windows that selected it and masked by ReLU (recomputed from y and the BN coefficients).
+// One thread per (pooled pixel (oh, ow), 8 channels) owns the 2x2 input block (2oh..2oh+1, 2ow..2ow+1):
+// exactly the windows (oh|oh+1, ow|ow+1) can select into it, so each window's argmax/gradient is read by
+// 4 threads (not 9) and all index math is 32-bit.
 template <int DT>
 __global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(const uint16_t* __restrict__ dp,
                                                                   const uint8_t* __restrict__ idx,
@@ -248,50 +251,73 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(const uint16_t
                                                                   int C, int OH, int OW) {
   using E = E16<DT>;
   const int cv = C / 8;
-  const int64_t total = (int64_t)N * H * W * cv;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)(v % cv) * 8;
-    int64_t pix = v / cv;
-    const int w = (int)(pix % W);
-    pix /= W;
-    const int h = (int)(pix % H);
-    const int n = (int)(pix / H);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int oh_lo = h / 2, oh_hi = (h + 1) / 2 < OH ? (h + 1) / 2 : OH - 1;
-    const int ow_lo = w / 2, ow_hi = (w + 1) / 2 < OW ? (w + 1) / 2 : OW - 1;
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      const int kh = h - (oh * 2 - 1);
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int kw = w - (ow * 2 - 1);
-        const uint32_t pos = (uint32_t)(kh * 3 + kw);
-        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+  const uint32_t total = (uint32_t)N * OH * OW * cv;
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < total; v += gridDim.x * 256u) {
+    const uint32_t pix = v / cv;
+    const int c0 = (int)(v - pix * cv) * 8;
+    const uint32_t ow = pix % OW, t = pix / OW;
+    const uint32_t oh = t % OH, n = t / OH;
+    float acc[2][2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[a][b][e] = 0.f;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const uint32_t wh = oh + dh, ww = ow + dw;
+        if (wh >= (uint32_t)OH || ww >= (uint32_t)OW) continue;
+        const uint32_t o = ((n * OH + wh) * OW + ww) * C + c0;
         const uint2 ib = *(const uint2*)(idx + o);
         const uint4 g = *(const uint4*)(dp + o);
         const uint32_t gw[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const uint32_t b = (((e < 4) ? ib.x : ib.y) >> (8 * (e & 3))) & 0xffu;
-          if (b == pos) acc[e] += E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1))));
+          const int pos = (int)((((e < 4) ? ib.x : ib.y) >> (8 * (e & 3))) & 0xffu);
+          const int kh = pos / 3, kw = pos - 3 * (pos / 3);
+          // selected input (2wh-1+kh, 2ww-1+kw) relative to this block's corner (2oh, 2ow)
+          const int rh = 2 * dh - 1 + kh, rw = 2 * dw - 1 + kw;
+          const float gv = E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1))));
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              if (rh == a && rw == b) acc[a][b][e] += gv;
         }
       }
+    float A[8], B[8], Cc[8], sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      A[e] = bcoef[c0 + e]; B[e] = bcoef[C + c0 + e]; Cc[e] = bcoef[2 * C + c0 + e];
+      sc[e] = coef[c0 + e]; sh[e] = coef[C + c0 + e];
     }
-    const int64_t i = (((int64_t)n * H + h) * W + w) * C + c0;
-    const uint4 yy = *(const uint4*)(y + i);
-    const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
-    uint32_t o_[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      uint16_t r[2];
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int c = c0 + 2 * e + hh;
-        const float yv = E::to_f((uint16_t)(yw[e] >> (16 * hh)));
-        const float dz = yv * coef[c] + coef[C + c] > 0.f ? acc[2 * e + hh] : 0.f;
-        r[hh] = E::from_f(bcoef[c] * dz + bcoef[C + c] * yv + bcoef[2 * C + c]);
+      for (int b = 0; b < 2; ++b) {
+        const uint32_t h = 2 * oh + a, w = 2 * ow + b;
+        if (h >= (uint32_t)H || w >= (uint32_t)W) continue;
+        const uint32_t i = ((n * H + h) * W + w) * C + c0;
+        const uint4 yy = *(const uint4*)(y + i);
+        const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
+        uint32_t o_[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint16_t r[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int c = 2 * e + hh;
+            const float yv = E::to_f((uint16_t)(yw[e] >> (16 * hh)));
+            const float dz = yv * sc[c] + sh[c] > 0.f ? acc[a][b][c] : 0.f;
+            r[hh] = E::from_f(A[c] * dz + B[c] * yv + Cc[c]);
+          }
+          o_[e] = (uint32_t)r[0] | ((uint32_t)r[1] << 16);
+        }
+        *(uint4*)(dy + i) = make_uint4(o_[0], o_[1], o_[2], o_[3]);
       }
-      o_[e] = (uint32_t)r[0] | ((uint32_t)r[1] << 16);
-    }
-    *(uint4*)(dy + i) = make_uint4(o_[0], o_[1], o_[2], o_[3]);
   }
 }
 
@@ -299,7 +325,7 @@ void stem_pool_bwd_apply_launch(int dtype, const uint16_t* dp, const uint8_t* id
                                 const float* coef, const float* bcoef, uint16_t* dy, int N, int H, int W, int C,
                                 hipStream_t s) {
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  const int64_t total = (int64_t)N * H * W * (C / 8);
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
   if (dtype == kBF16)
     hipLaunchKernelGGL(stem_pool_bwd_apply_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef,
                        bcoef, dy, N, H, W, C, OH, OW);

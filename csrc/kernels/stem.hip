@@ -14,7 +14,7 @@
 //     16-byte ds_read at column 2*ow + 2*fq of the staged row: each quarter-wave reads 256 contiguous
 //     bytes (conflict-free), and the 4x overlap of neighbouring 7-wide windows costs no extra HBM/L2
 //     traffic;
-//   * the 64 x 224 weight matrix stays resident in LDS (rows padded to 464 B: conflict-free A reads);
+//   * the 64 x 224 weight matrix stays resident in LDS (rows padded to 480 B: conflict-free A reads);
 //   * K = 224 exactly (no padding to a tile multiple); blocks are persistent and each XCD walks a
 //     contiguous tile range;
 //   * BatchNorm statistics of the rounded outputs are reduced per tile (16-lane shuffles), accumulated
@@ -32,7 +32,7 @@ namespace {
 constexpr int kCout = 64;
 constexpr int kRows = 7;                   // kernel rows
 constexpr int kWRow = kRows * 32 * 2;      // 448 B of weights per output channel
-constexpr int kWPitch = kWRow + 16;        // padded LDS pitch: 16-lane A reads hit distinct banks
+constexpr int kWPitch = kWRow + 32;        // padded LDS pitch: conflict-free A reads (tools/lds_sim.py)
 constexpr int kOutRows = 4;                // output rows per tile (one per wave)
 constexpr int kInRows = 2 * (kOutRows - 1) + kRows;  // 13 padded-image rows per tile
 constexpr int kStage = 24 * 1024;          // LDS bytes per staged tile (>= kInRows * Wp * 8)
