@@ -186,6 +186,117 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Stem ("window" mode) weight gradient: ALL FOUR kernel-row pairs of the 7x7 stem in one block.
+// The 64x64 kernel above runs one block per (pair, split) and so re-reads every dY tile 4 times; here a
+// block stages the dY tile once plus the 4 pair-windows of X (64 pixels x 128 B each, 40 KB per stage,
+// 2 stages -> 2 blocks per CU) and wave t owns pair t's 64 (window column) x 64 (cout) tile over the
+// whole pixel range of its split.  The partial tile goes out through LDS as coalesced float4 rows.
+template <int DT>
+__global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 64;         // pixels per K-step
+  constexpr int ROWB = 128;       // 64 elements * 2 B
+  constexpr int TB = BKP * ROWB;  // 8 KB per tile
+  constexpr int STAGE = 5 * TB;   // dY + 4 pair windows
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = kernel-row pair
+  const int split = blockIdx.x;
+  const int pix_begin = split * a.pix_per_split;
+  const int pix_end = min(a.P, pix_begin + a.pix_per_split);
+  const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
+  const int lrow = lane >> 3, pch = lane & 7;
+
+  // 40 DMA instructions per stage (8 dY + 4 x 8 X), 10 per wave
+  auto stage_load = [&](int step, int buf) {
+    const int pbase = pix_begin + step * BKP;
+    char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int m = 0; m < 10; ++m) {
+      const int ii = wave + 4 * m;
+      const int tile = ii >> 3;                 // 0 = dY, 1..4 = pair tile-1
+      const int row = (ii & 7) * 8 + lrow;      // pixel within the step
+      const int lch = pch ^ tr_swz(row);
+      const int th = (tile - 1) * a.dil_h - a.pad_h;
+      uint32_t xo, yo;
+      wgrad_rows<true>(a, pbase + row, th, 0, 0, lch, 0, xo, yo);
+      if (tile == 0)
+        buf_lds16(ry, sb + (ii & 7) * 1024, yo);
+      else
+        buf_lds16(rx, sb + tile * TB + (ii & 7) * 1024, xo);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+
+  if (nsteps > 0) {
+    stage_load(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+      const int cur = st & 1;
+      if (st + 1 < nsteps) stage_load(st + 1, cur ^ 1);
+      const char* sy = smem + cur * STAGE;
+      const char* sx = sy + (1 + wave) * TB;
+#pragma unroll
+      for (int kk = 0; kk < BKP / 32; ++kk) {
+        const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+        const int sw0 = tr_swz(r0), sw1 = tr_swz(r1);
+        vec8 af[4], bfr[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int col = f * 16 + 4 * p4;
+          const int ch = col >> 3, off = (col & 7) * 2;
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sx + r0 * ROWB + ((ch ^ sw0) << 4) + off));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sx + r1 * ROWB + ((ch ^ sw1) << 4) + off));
+          af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r0 * ROWB + ((ch ^ sw0) << 4) + off));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r1 * ROWB + ((ch ^ sw1) << 4) + off));
+          bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // acc[i][j]: rows (window column) c = 16i + 4*(lane>>4) + r, col k = 16j + (lane&15); transpose
+  // through LDS ([4 pairs][64 k][64 c]) and write ws[split][k][pair*64 + c] as float4 rows
+  float* red = (float*)smem;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 16 * j + (lane & 15);
+      const int c = 16 * i + 4 * (lane >> 4);
+      *(f32x4_t*)(red + (wave * 64 + k) * 64 + c) = acc[i][j];
+    }
+  __syncthreads();
+  float* dst = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int idx = (e * 256 + tid) * 4;  // 0..16383 over [k][pair][c]
+    const int k = idx >> 8, pc = idx & 255, pr = pc >> 6, c = pc & 63;
+    *(f32x4_t*)(dst + (int64_t)k * a.ldw + pc) = *(const f32x4_t*)(red + (pr * 64 + k) * 64 + c);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // 128 (c) x 128 (k) tile variant for layers with C, Kout multiples of 128: 4 waves in a 2x2 grid over
 // the output tile, each wave owning 64x64 for ALL 64 pixels of a K-step (32 MFMAs per K-step per wave,
 // 4x the MFMA work per loaded pixel row of the 64x64 variant).  64 KiB of LDS -> 2 blocks per CU.
@@ -550,6 +661,12 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16>), dim3(nwg), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad128_kernel<kF16>), dim3(nwg), dim3(256), 0, s, a);
+  } else if (a.win && a.T == 4 && a.U == 1 && a.C == 64 && a.Kout == 64 && a.ldw >= 256) {
+    // ResNet stem (4 kernel-row pairs): one block per split covers all pairs
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((wgrad_stem_kernel<kBF16>), dim3(a.splits), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((wgrad_stem_kernel<kF16>), dim3(a.splits), dim3(256), 0, s, a);
   } else if (a.win) {
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, true>), dim3(nwg), dim3(256), 0, s, a);
