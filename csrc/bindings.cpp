@@ -299,6 +299,34 @@ void bn_slot_sum(const Tensor& slots, int64_t C, int64_t K, Tensor& sums) {
 
 int64_t stat_slots() { return pdt::kStatSlots; }
 
+// slot sum + finalize in one launch (no SyncBN): slots [kStatSlots][C][2] -> coef (+ running stats), sums
+void bn_finalize_slots(const Tensor& slots, double count, const Tensor& gamma, const Tensor& beta, double eps,
+                       double momentum, Tensor& rm, Tensor& rv, Tensor& coef, Tensor& sums, bool update_running) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * 2 && coef.numel() >= 4 * C && sums.numel() >= 2 * C,
+              "bn_finalize_slots: bad sizes");
+  pdt::bn_finalize_slots_launch(pd(slots, "slots"), count, pf(gamma, "gamma"), pf(beta, "beta"), (float)eps,
+                                (float)momentum, pf(rm, "running_mean"), pf(rv, "running_var"), pf(coef, "coef"),
+                                pd(sums, "sums"), (int)C, update_running, cur_stream());
+}
+
+// slot sum + backward finalize for one (K = 2) or two (K = 4) BN branches, no SyncBN
+void bn_bwd_finalize_slots(const Tensor& slots, int64_t K, double count, const Tensor& coef1, const Tensor& gamma1,
+                           const OptT& dgamma1, const OptT& dbeta1, Tensor& bcoef1, const OptT& coef2,
+                           const OptT& gamma2, const OptT& dgamma2, const OptT& dbeta2, const OptT& bcoef2,
+                           double gscale) {
+  const int64_t C = gamma1.numel();
+  TORCH_CHECK((K == 2 || K == 4) && slots.numel() >= pdt::kStatSlots * C * K && bcoef1.numel() >= 3 * C,
+              "bn_bwd_finalize_slots: bad sizes");
+  TORCH_CHECK(K == 2 || (coef2.has_value() && gamma2.has_value() && bcoef2.has_value() && bcoef2->numel() >= 3 * C),
+              "bn_bwd_finalize_slots: K == 4 needs the second branch");
+  pdt::bn_bwd_finalize_slots_launch(pd(slots, "slots"), (int)K, count, pf(coef1, "coef1"), pf(gamma1, "gamma1"),
+                                    pfo(dgamma1, "dgamma1"), pfo(dbeta1, "dbeta1"), pf(bcoef1, "bcoef1"),
+                                    pfo(coef2, "coef2"), pfo(gamma2, "gamma2"), pfo(dgamma2, "dgamma2"),
+                                    pfo(dbeta2, "dbeta2"), pfo(bcoef2, "bcoef2"), (float)gscale, (int)C,
+                                    cur_stream());
+}
+
 void bn_finalize(const Tensor& sums, double count, const Tensor& gamma, const Tensor& beta, double eps, double momentum,
                  Tensor& rm, Tensor& rv, Tensor& coef, bool update_running) {
   const int64_t C = gamma.numel();
@@ -519,6 +547,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_slot_sum", &bn_slot_sum);
   m.def("stat_slots", &stat_slots);
   m.def("bn_finalize", &bn_finalize);
+  m.def("bn_finalize_slots", &bn_finalize_slots);
+  m.def("bn_bwd_finalize_slots", &bn_bwd_finalize_slots);
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_reduce_blocks", &bn_bwd_reduce_blocks);

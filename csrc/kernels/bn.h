@@ -4,6 +4,13 @@
 
 namespace pdt {
 void bn_slot_sum_launch(const double* slots, int C, int K, double* sums, hipStream_t s);
+void bn_finalize_slots_launch(const double* slots, double count, const float* gamma, const float* beta, float eps,
+                              float momentum, float* rm, float* rv, float* coef, double* sums, int C,
+                              bool update_running, hipStream_t s);
+void bn_bwd_finalize_slots_launch(const double* slots, int K, double count, const float* coef1, const float* gamma1,
+                                  float* dgamma1, float* dbeta1, float* bcoef1, const float* coef2,
+                                  const float* gamma2, float* dgamma2, float* dbeta2, float* bcoef2, float gscale,
+                                  int C, hipStream_t s);
 void bn_finalize_launch(const double* sums, double count, const float* gamma, const float* beta, float eps,
                         float momentum, float* rm, float* rv, float* coef, int C, bool update_running,
                         hipStream_t s);

@@ -59,6 +59,45 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, double count
   }
 }
 
+// Fused (no SyncBN) form of bn_slot_sum + bn_finalize: one thread per channel sums its kStatSlots fp64
+// slot copies and finalizes in place (one launch per BN layer instead of two).
+__global__ void bn_finalize_slots_kernel(const double* __restrict__ slots, double count,
+                                         const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                         float momentum, float* __restrict__ running_mean,
+                                         float* __restrict__ running_var, float* __restrict__ coef,
+                                         double* __restrict__ sums, int C, int update_running) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0, s1 = 0;
+  for (int g = 0; g < kStatSlots; ++g) {
+    s0 += slots[((int64_t)g * C + c) * 2];
+    s1 += slots[((int64_t)g * C + c) * 2 + 1];
+  }
+  sums[c] = s0;
+  sums[C + c] = s1;
+  const double mean = s0 / count;
+  double var = s1 / count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  coef[c] = sc;
+  coef[C + c] = beta[c] - (float)mean * sc;
+  coef[2 * C + c] = (float)mean;
+  coef[3 * C + c] = invstd;
+  if (update_running) {
+    const double unbiased = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+void bn_finalize_slots_launch(const double* slots, double count, const float* gamma, const float* beta, float eps,
+                              float momentum, float* rm, float* rv, float* coef, double* sums, int C,
+                              bool update_running, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_slots_kernel, dim3((C + 255) / 256), dim3(256), 0, s, slots, count, gamma, beta, eps,
+                     momentum, rm, rv, coef, sums, C, update_running ? 1 : 0);
+}
+
 // eval-mode coefficients from running statistics
 __global__ void bn_eval_coef_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                     const float* __restrict__ running_mean, const float* __restrict__ running_var,
@@ -278,6 +317,44 @@ void bn_bwd_finalize_launch(const double* sums, double count, const float* coef,
                             float* dbeta, float gscale, float* bcoef, int C, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, count, coef, gamma, dgamma,
                      dbeta, gscale, bcoef, C);
+}
+
+// Fused (no SyncBN) slot sum + backward finalize for one or two BN branches sharing dz
+// (slots [kStatSlots][C][K], K = 2 or 4: sum dz1, sum dz1*x1, sum dz2, sum dz2*x2).
+__device__ inline void bn_bwd_coef(double sdz, double sdzx, double count, float mean, float invstd, float gamma,
+                                   float* dgamma, float* dbeta, float gscale, float* bcoef, int C, int c) {
+  if (dgamma) dgamma[c] = (float)sdzx * gscale;
+  if (dbeta) dbeta[c] = (float)sdz * gscale;
+  const float A = gamma * invstd;
+  const float mdz = (float)(sdz / count), mdzx = (float)(sdzx / count);
+  bcoef[c] = A;
+  bcoef[C + c] = -A * invstd * mdzx;
+  bcoef[2 * C + c] = -A * mdz + A * invstd * mdzx * mean;
+}
+
+__global__ void bn_bwd_finalize_slots_kernel(const double* __restrict__ slots, int K, double count,
+                                             const float* __restrict__ coef1, const float* __restrict__ gamma1,
+                                             float* __restrict__ dgamma1, float* __restrict__ dbeta1,
+                                             float* __restrict__ bcoef1, const float* __restrict__ coef2,
+                                             const float* __restrict__ gamma2, float* __restrict__ dgamma2,
+                                             float* __restrict__ dbeta2, float* __restrict__ bcoef2, float gscale,
+                                             int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s[4] = {0, 0, 0, 0};
+  for (int g = 0; g < kStatSlots; ++g)
+    for (int k = 0; k < K; ++k) s[k] += slots[((int64_t)g * C + c) * K + k];
+  bn_bwd_coef(s[0], s[1], count, coef1[2 * C + c], coef1[3 * C + c], gamma1[c], dgamma1, dbeta1, gscale, bcoef1, C, c);
+  if (K == 4)
+    bn_bwd_coef(s[2], s[3], count, coef2[2 * C + c], coef2[3 * C + c], gamma2[c], dgamma2, dbeta2, gscale, bcoef2, C, c);
+}
+
+void bn_bwd_finalize_slots_launch(const double* slots, int K, double count, const float* coef1, const float* gamma1,
+                                  float* dgamma1, float* dbeta1, float* bcoef1, const float* coef2,
+                                  const float* gamma2, float* dgamma2, float* dbeta2, float* bcoef2, float gscale,
+                                  int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_slots_kernel, dim3((C + 255) / 256), dim3(256), 0, s, slots, K, count, coef1,
+                     gamma1, dgamma1, dbeta1, bcoef1, coef2, gamma2, dgamma2, dbeta2, bcoef2, gscale, C);
 }
 
 // dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad)

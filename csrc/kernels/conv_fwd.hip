@@ -39,8 +39,8 @@ typedef __attribute__((address_space(1))) void glb_void;
 template <int CHUNKS>
 PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
-template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, bool RES, int STAGES>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
+template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, bool RES, int STAGES, int NW>
+__global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
     const int ph = blockIdx.y;
@@ -57,18 +57,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
   }
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
-  constexpr int WAVES_M = 4 / WAVES_N;
+  constexpr int WAVES_M = NW / WAVES_N;
   constexpr int WN = BN / WAVES_N;
   constexpr int WM = BM / WAVES_M;
   constexpr int FN = WN / 16, FM = WM / 16;
   constexpr int ROWB = BK * 2;
   constexpr int CHUNKS = ROWB / 16;
   constexpr int RPI = 1024 / ROWB;               // rows per wave LDS-DMA instruction
-  constexpr int A_INSTR = BN / RPI / 4;          // weight-tile instructions per wave
-  constexpr int B_INSTR = BM / RPI / 4;          // activation-tile instructions per wave
+  constexpr int A_INSTR = BN / RPI / NW;         // weight-tile instructions per wave
+  constexpr int B_INSTR = BM / RPI / NW;         // activation-tile instructions per wave
   constexpr int A_BYTES = BN * ROWB;
   constexpr int STAGE = (BN + BM) * ROWB;
-  static_assert(A_INSTR * RPI * 4 == BN && B_INSTR * RPI * 4 == BM, "tile/instr mismatch");
+  static_assert(A_INSTR * RPI * NW == BN && B_INSTR * RPI * NW == BM, "tile/instr mismatch");
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
   const int tid = threadIdx.x;
@@ -379,22 +379,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvFwdArgs args) {
 }
 
 // ----------------------------------------------------------------------------------------------
-template <int DT, int BM, int BN, int BK, int WAVES_N, int STAGES>
+template <int DT, int BM, int BN, int BK, int WAVES_N, int STAGES, int NW>
 static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
   int gx = a.m_tiles * a.n_tiles;
   if (a.nphase > 0) {
     gx = 0;
     for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
   }
-  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(256);
+  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(NW * 64);
   const bool rs = a.res != nullptr;
   const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
-#define PDT_K(E_, R_) hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, E_, R_, STAGES>), grid, block, 0, s, a)
+#define PDT_K(E_, R_) hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, E_, R_, STAGES, NW>), grid, block, 0, s, a)
   if (epi == 0) {
     if (rs) PDT_K(0, true); else PDT_K(0, false);
   } else if (epi == 1) {
     if (rs) PDT_K(1, true); else PDT_K(1, false);
-  } else if constexpr (BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 16384) {
+  } else if constexpr (BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 4096 * NW) {
     // fused BN-backward epilogues: only on the backward-data tiles (128x128x64, 256x64x64)
     if (epi == 2 && !rs) PDT_K(2, false);
     else if (epi == 3 && rs) PDT_K(3, true);
@@ -434,14 +434,15 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
     const char* e = getenv("PDT_FWD_STAGES");
     return e ? atoi(e) : 0;
   }();
-#define PDT_CFG(BM_, BN_, BK_, WN_, ST_)                                 \
+#define PDT_CFGN(BM_, BN_, BK_, WN_, ST_, NW_)                          \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
     if (force_stages == 5 - ST_)                                         \
-      launch_cfg<DT, BM_, BN_, BK_, WN_, 5 - ST_>(a, s);                 \
+      launch_cfg<DT, BM_, BN_, BK_, WN_, 5 - ST_, NW_>(a, s);            \
     else                                                                 \
-      launch_cfg<DT, BM_, BN_, BK_, WN_, ST_>(a, s);                     \
+      launch_cfg<DT, BM_, BN_, BK_, WN_, ST_, NW_>(a, s);                \
     return;                                                              \
   }
+#define PDT_CFG(BM_, BN_, BK_, WN_, ST_) PDT_CFGN(BM_, BN_, BK_, WN_, ST_, 4)
   // BK = 64 tiles: 2-stage ring; BK = 32 tiles: 3-stage ring (counted vmcnt, more latency hiding)
   PDT_CFG(128, 128, 64, 2, 2)
   PDT_CFG(256, 64, 64, 1, 2)
@@ -450,7 +451,9 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   PDT_CFG(256, 64, 32, 1, 3)
   PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
+  PDT_CFGN(256, 128, 64, 2, 2, 8)  // 8 waves (4 x 2 of 64 x 64), 96 KB LDS: 25% less L2->LDS traffic per FLOP
 #undef PDT_CFG
+#undef PDT_CFGN
   pdt_hip_fail("conv_fwd: unsupported tile config", hipErrorInvalidValue, __FILE__, __LINE__);
 }
 

@@ -213,6 +213,10 @@ class ResNetExecutor:
 
     def bn_train_finalize(self, bn: _BN, sp, tiles: int, count: int):
         C = bn.C
+        if self.syncbn_group is None:  # slot sum + finalize in one launch
+            self.C.bn_finalize_slots(sp, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
+                                     bn.mod.running_mean, bn.mod.running_var, bn.coef, bn.sums, True)
+            return
         self.C.bn_slot_sum(sp, C, 2, bn.sums)
         if self.syncbn_group is not None:
             import torch.distributed as dist
@@ -286,6 +290,17 @@ class ResNetExecutor:
         """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients."""
         C = bn1.C
         K = 4 if bn2 is not None else 2
+        if self.syncbn_group is None:  # slot sum + finalize of both branches in one launch
+            self.C.bn_bwd_finalize_slots(
+                slots, K, float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot), self._g(bn1.bslot),
+                bn1.bcoef, bn2.coef if bn2 is not None else None, self._p(bn2.gslot) if bn2 is not None else None,
+                self._g(bn2.gslot) if bn2 is not None else None, self._g(bn2.bslot) if bn2 is not None else None,
+                bn2.bcoef if bn2 is not None else None, 1.0)
+            for b in (bn1, bn2):
+                if b is not None:
+                    self.grad_ready(b.gslot.index)
+                    self.grad_ready(b.bslot.index)
+            return
         sums = bn1.bsums[:C * K]
         self.C.bn_slot_sum(slots, C, K, sums)
         if self.syncbn_group is not None:
