@@ -125,6 +125,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--profile", default=False, type=str2bool, nargs="?", const=True,
                    help="roctx ranges around train/eval steps (visible in rocprofv3 --marker-trace) and a "
                         "per-epoch throughput line")
+    g.add_argument("--autotune", default=False, type=str2bool, nargs="?", const=True,
+                   help="time the candidate conv tile configs once per shape and keep the fastest (the analogue of "
+                        "the reference's cudnn.benchmark=True); off = the static per-shape table")
     g.add_argument("--use-gpus-flag", default=False, type=str2bool, nargs="?", const=True,
                    help="honour --gpus by setting HIP_VISIBLE_DEVICES (the reference ignores --gpus)")
     g.add_argument("--no-tensorboard", dest="tensorboard", action="store_false")

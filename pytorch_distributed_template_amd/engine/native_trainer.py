@@ -28,7 +28,7 @@ class NativeTrainer:
     def __init__(self, model, device, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1, momentum: float = 0.9,
                  weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
-                 process_group=None, reduce_metrics: bool = True):
+                 process_group=None, reduce_metrics: bool = True, autotune: bool = False):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -42,7 +42,7 @@ class NativeTrainer:
                                      enabled=self.distributed)
         self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
                                        syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed)
-                                       else None)
+                                       else None, autotune=autotune)
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executor.update_derived)
         # fp16 needs dynamic loss scaling; bf16 has fp32's exponent range and does not

@@ -80,7 +80,7 @@ class ResNetExecutor:
 
     def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None,
-                 syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512):
+                 syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512, autotune: bool = False):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not isinstance(model, ResNet) or model.groups != 1:
@@ -100,6 +100,8 @@ class ResNetExecutor:
         self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
+        self.autotune = autotune or os.environ.get("PDT_AUTOTUNE", "0") == "1"
+        self._tiles: Dict[tuple, Tuple[int, int]] = {}
         derived_maps: List[torch.Tensor] = []
         off = [0]
 
@@ -201,15 +203,46 @@ class ResNetExecutor:
         st = st or c.st
         pad = c.pad if pad is None else pad
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
-        bm, bn = _conv_tile(c.cout)
         bk = 64 if cin % 64 == 0 else 32
         M = N * P * Q
         sp = None
         if stats:
             sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64)
-        self.C.conv_fwd(x, self._w(c) if w is None else w, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
-                        -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
+        wt = self._w(c) if w is None else w
+
+        def launch(bm, bn):
+            self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
+                            -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
+        bm, bn = self._tile(("fwd", N, H, W, cin, c.cout, R, S, st, stats), c.cout, bk, launch)
+        launch(bm, bn)
         return P, Q, sp, M
+
+    # per-shape tile choice: the static table (ops.conv.conv_tile), or -- with autotune on, the analogue of
+    # the reference's cudnn.benchmark=True (`distributed.py:104`) -- the fastest candidate timed once per shape
+    _CANDIDATES = ((128, 128), (256, 64), (128, 64), (64, 128), (256, 128))
+
+    def _tile(self, key, n_dim, bk, launch, fused_epilogue: bool = False):
+        hit = self._tiles.get(key)
+        if hit is not None:
+            return hit
+        choice = _conv_tile(n_dim)
+        if self.autotune and bk == 64:
+            cands = [(bm, bn) for bm, bn in self._CANDIDATES if n_dim % bn == 0 and
+                     (not fused_epilogue or bm * bn in (16384, 32768))]
+            best = None
+            for bm, bn in cands:
+                launch(bm, bn)  # warm
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                launch(bm, bn)
+                e1.record()
+                e1.synchronize()
+                ms = e0.elapsed_time(e1)
+                if best is None or ms < best[0]:
+                    best = (ms, (bm, bn))
+            choice = best[1]
+        self._tiles[key] = choice
+        return choice
 
     def bn_train_finalize(self, bn: _BN, sp, tiles: int, count: int):
         C = bn.C
@@ -244,15 +277,19 @@ class ResNetExecutor:
         # --- dgrad
         if dx is None:
             return
-        bm, bn = _conv_tile(c.cin)
         bk = 64 if c.cout % 64 == 0 else 32
         phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
                   if H - ph > 0 and W - pw > 0]
-        if bnb is None:
-            self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk)
-        else:
-            self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk,
-                                 *bnb)
+
+        def launch(bm, bn):
+            if bnb is None:
+                self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk)
+            else:
+                self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn,
+                                     bk, *bnb)
+        key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, c.st, res is not None, bnb[0] if bnb else 0)
+        bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None)
+        launch(bm, bn)
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
                win=False, dil=1):

@@ -24,7 +24,8 @@ def _run(args, timeout=600, env_extra=None):
 
 
 @pytest.mark.parametrize("script,extra", [("distributed.py", []), ("dataparallel.py", []),
-                                          ("distributed_syncBN_amp.py", [])])
+                                          ("distributed_syncBN_amp.py", []),
+                                          ("distributed.py", ["--autotune", "--profile"])])
 def test_entry_scripts_native_gpu(tmp_path, script, extra):
     out = str(tmp_path / "out")
     _run([script, "--outpath", out] + COMMON + extra)

@@ -44,6 +44,10 @@ for stage in "$@"; do
       timeout -k 10 300 python tools/conv_bench.py --skip-stem --shapes 0 > gpurun_out/l1_bench.log 2>&1; rc=$?
       grep shape gpurun_out/l1_bench.log
       [ $rc -eq 0 ] || { echo "l1 bench failed rc=$rc"; exit $rc; } ;;
+    reftable)
+      timeout -k 10 600 python tools/reference_table.py --md gpurun_out/reference_table_1gpu.md > gpurun_out/reftable.log 2>&1; rc=$?
+      cat gpurun_out/reftable.log | grep mode
+      [ $rc -eq 0 ] || { echo "reference table failed rc=$rc"; exit $rc; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
       tail -5 gpurun_out/smoke.log
