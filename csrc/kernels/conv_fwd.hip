@@ -199,25 +199,38 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
       }
     }
   } else {
-    // 3-stage LDS ring: two K-steps of LDS-DMA stay in flight; each iteration waits (counted vmcnt,
-    // never 0) only for the stage it is about to read, then a raw s_barrier publishes it to all waves.
-    // The buffer refilled in iteration ks was last read in iteration ks-1, which every wave finished
-    // before passing this iteration's barrier.
+    // S-stage LDS ring (S = 3 or 4): S-2 K-steps of LDS-DMA stay in flight across every barrier; each
+    // iteration waits (counted vmcnt, never 0 while more are queued) only for the stage it is about to
+    // read, then a raw s_barrier publishes it to all waves.  The buffer refilled in iteration ks was last
+    // read in iteration ks-1, which every wave finished before passing this iteration's barrier.
+    // MFMA clusters run at raised wave priority (s_setprio) so the issue of the next DMA / reads
+    // interleaves with them instead of starving them.
+    constexpr int S = STAGES;
     constexpr int PER_STAGE = A_INSTR + B_INSTR;  // LDS-DMA instructions per wave per stage
-    constexpr int WAIT_ONE = (PER_STAGE & 0xF) | ((PER_STAGE >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+    auto wait_ahead = [&](int ahead) {             // vmcnt(ahead * PER_STAGE), immediate operands only
+      constexpr int W1 = PER_STAGE, W2 = 2 * PER_STAGE;
+      if (ahead >= 2)
+        __builtin_amdgcn_s_waitcnt((W2 & 0xF) | ((W2 >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+      else if (ahead == 1)
+        __builtin_amdgcn_s_waitcnt((W1 & 0xF) | ((W1 >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    static_assert(S <= 4, "wait_ahead covers at most two stages in flight");
     if (ksteps > 0) {
-      stage_load(0);
-      if (ksteps > 1) stage_load(1);
+#pragma unroll
+      for (int p = 0; p < S - 1; ++p)
+        if (p < ksteps) stage_load(p);
       int buf = 0;
       for (int ks = 0; ks < ksteps; ++ks) {
-        if (ks + 1 < ksteps)
-          __builtin_amdgcn_s_waitcnt(WAIT_ONE);  // stage ks landed, stage ks+1 may still be in flight
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int ahead = min(S - 2, ksteps - 1 - ks);
+        wait_ahead(ahead);
         __builtin_amdgcn_s_barrier();
-        if (ks + 2 < ksteps) stage_load(buf == 0 ? 2 : buf - 1);
+        if (ks + S - 1 < ksteps) stage_load(buf == 0 ? S - 1 : buf - 1);
+        __builtin_amdgcn_s_setprio(1);
         compute_stage(smem + buf * STAGE);
-        buf = buf == 2 ? 0 : buf + 1;
+        __builtin_amdgcn_s_setprio(0);
+        buf = buf == S - 1 ? 0 : buf + 1;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -394,7 +407,8 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     if (rs) PDT_K(0, true); else PDT_K(0, false);
   } else if (epi == 1) {
     if (rs) PDT_K(1, true); else PDT_K(1, false);
-  } else if constexpr (BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 4096 * NW) {
+  } else if constexpr ((BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 4096 * NW) ||
+                       (BM == 256 && BN == 256)) {
     // fused BN-backward epilogues: only on the backward-data tiles (128x128x64, 256x64x64)
     if (epi == 2 && !rs) PDT_K(2, false);
     else if (epi == 3 && rs) PDT_K(3, true);
@@ -436,8 +450,10 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   }();
 #define PDT_CFGN(BM_, BN_, BK_, WN_, ST_, NW_)                          \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
-    if (force_stages == 5 - ST_)                                         \
-      launch_cfg<DT, BM_, BN_, BK_, WN_, 5 - ST_, NW_>(a, s);            \
+    if (ST_ == 2 && force_stages == 3)                                   \
+      launch_cfg<DT, BM_, BN_, BK_, WN_, 3, NW_>(a, s);                  \
+    else if (ST_ == 3 && force_stages == 2)                              \
+      launch_cfg<DT, BM_, BN_, BK_, WN_, 2, NW_>(a, s);                  \
     else                                                                 \
       launch_cfg<DT, BM_, BN_, BK_, WN_, ST_, NW_>(a, s);                \
     return;                                                              \
@@ -452,6 +468,7 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
   PDT_CFGN(256, 128, 64, 2, 2, 8)  // 8 waves (4 x 2 of 64 x 64), 96 KB LDS: 25% less L2->LDS traffic per FLOP
+  PDT_CFGN(256, 256, 32, 4, 4, 8)  // 8 waves (2 x 4 of 128 x 64), 4-stage BK=32 ring (128 KB), 2 steps in flight
 #undef PDT_CFG
 #undef PDT_CFGN
   pdt_hip_fail("conv_fwd: unsupported tile config", hipErrorInvalidValue, __FILE__, __LINE__);

@@ -59,8 +59,9 @@ def out_hw(H: int, W: int, R: int, S: int, stride: int, pad: int) -> Tuple[int, 
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
-             residual: Optional[torch.Tensor] = None):
-    """y = conv(x, w) in NHWC/KRSC.  Returns ``y`` or ``(y, (sum, sumsq) per channel)`` with stats."""
+             residual: Optional[torch.Tensor] = None, tile: Optional[Tuple[int, int, int]] = None):
+    """y = conv(x, w) in NHWC/KRSC.  Returns ``y`` or ``(y, (sum, sumsq) per channel)`` with stats.
+    ``tile`` = (BM, BN, BK) overrides the per-shape table (tests / sweeps)."""
     N, H, W, C = x.shape
     K, R, S, C2 = w.shape
     assert C == C2
@@ -68,6 +69,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
     bm, bn = conv_tile(K)
     bk = 64 if C % 64 == 0 else 32
+    if tile is not None:
+        bm, bn, bk = tile
     sp = None
     if stats:
         sp = torch.empty(native.C.stat_slots() * K * 2, dtype=torch.float64, device=x.device)
@@ -81,7 +84,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 1, pad: int = 0,
-               residual: Optional[torch.Tensor] = None, bnb: Optional[tuple] = None) -> torch.Tensor:
+               residual: Optional[torch.Tensor] = None, bnb: Optional[tuple] = None,
+               tile: Optional[Tuple[int, int, int]] = None) -> torch.Tensor:
     """dX (NHWC, [N, H, W, Cin]) of ``y = conv(x, w)`` given dY ([N, P, Q, Cout]).
 
     ``bnb = (mode, y1, coef1, y2, coef2, out, slots)`` fuses the consuming BatchNorm's backward reduce
@@ -92,6 +96,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
     dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
     bm, bn = conv_tile(C)
     bk = 64 if K % 64 == 0 else 32
+    if tile is not None:
+        bm, bn, bk = tile
     wflat = w.reshape(-1)
     pieces, phases, off = [], [], 0
     for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(R, S, stride, pad):

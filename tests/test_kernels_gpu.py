@@ -353,3 +353,31 @@ def test_wgrad_3x3c64_all_taps():
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3), dy.float().permute(0, 3, 1, 2),
                                       stride=1, padding=1)
     assert _rel(out.view(64, 3, 3, 64).permute(0, 3, 1, 2), ref) < 2e-3
+
+
+TILES = [(128, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64), (256, 128, 64), (256, 256, 32),
+         (128, 128, 32), (256, 64, 32), (128, 64, 32)]
+
+
+@pytest.mark.parametrize("tile", TILES)
+def test_conv_tile_configs(tile):
+    """Every compiled tile config (ring depth, wave count) on a strided 3x3 with stats and a residual dgrad."""
+    from pytorch_distributed_template_amd.ops import conv
+    bm, bn, bk = tile
+    N, H, W, C, K = 2, 15, 13, 256, 256
+    torch.manual_seed(13)
+    x = _rand16(N, H, W, C)
+    w = _rand16(K, 3, 3, C, scale=(1.0 / (C * 9)) ** 0.5)
+    y, (s, ss) = conv.conv_fwd(x, w, 2, 1, stats=True, tile=tile)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=2, padding=1)
+    assert _rel(y, ref.permute(0, 2, 3, 1)) < 1e-2
+    yf = y.float().reshape(-1, K)
+    assert torch.allclose(s.float(), yf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(ss.float(), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+    P, Q = y.shape[1], y.shape[2]
+    dy = _rand16(N, P, Q, K)
+    res = _rand16(N, H, W, C)
+    dx = conv.conv_dgrad(dy, w, H, W, 2, 1, residual=res, tile=tile)
+    refx = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                      stride=2, padding=1).permute(0, 2, 3, 1) + res.float()
+    assert _rel(dx, refx) < 1e-2
