@@ -24,6 +24,10 @@
 #include "kernels/pool.h"
 #include "kernels/stem.h"
 
+namespace pdt_comm {
+void register_comm(pybind11::module& m);  // csrc/comm.cpp
+}
+
 void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line) {
   char buf[512];
   snprintf(buf, sizeof(buf), "%s failed: %s (%s:%d)", expr, hipGetErrorString(e), file, line);
@@ -533,6 +537,7 @@ void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  pdt_comm::register_comm(m);
   m.doc() = "gfx950 (MI355X) HIP kernels of pytorch_distributed_template_amd";
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_m_tiles", &conv_m_tiles);

@@ -120,6 +120,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--resume", default="", metavar="PATH", help="resume from a checkpoint written by this framework")
     g.add_argument("--pretrained-path", default=None, help="local torchvision-format weights for --pretrained")
     g.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    g.add_argument("--comm", default="torch", choices=["torch", "native"],
+                   help="collectives: torch.distributed (RCCL via c10d) or this framework's own RCCL communicator "
+                        "and C++ gradient bucketer")
     g.add_argument("--dist-timeout", type=float, default=1800.0,
                    help="collective timeout in seconds (a hung rank fails the job instead of hanging it)")
     g.add_argument("--profile", default=False, type=str2bool, nargs="?", const=True,

@@ -28,7 +28,8 @@ class NativeTrainer:
     def __init__(self, model, device, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1, momentum: float = 0.9,
                  weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
-                 process_group=None, reduce_metrics: bool = True, autotune: bool = False):
+                 process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
+                 force_comm: bool = False):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -38,28 +39,49 @@ class NativeTrainer:
         self.flat = FlatParams(model, self.device, dtype)
         self.buffers = FlatBuffers(model, self.device)
         broadcast_parameters(self.flat, self.buffers, process_group)
-        self.bucketer = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb,
-                                     enabled=self.distributed)
+        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
+        # collectives: torch.distributed (RCCL via c10d) or our own RCCL communicator + C++ bucketer
+        # (--comm native; force_comm exercises it on a single rank)
+        self.ncomm = None
+        if comm == "native" and (self.distributed or force_comm):
+            from ..parallel.comm import NativeBucketer, NativeComm
+            self.ncomm = NativeComm(self.device, process_group)
+            self.bucketer = NativeBucketer(layout, self.ncomm)
+        else:
+            self.bucketer = layout
         self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
                                        syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed)
-                                       else None, autotune=autotune)
+                                       else None, autotune=autotune,
+                                       syncbn_allreduce=self.ncomm.all_reduce if self.ncomm is not None else None)
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executor.update_derived)
         # fp16 needs dynamic loss scaling; bf16 has fp32's exponent range and does not
         self.scaler = DeviceGradScaler(self.device, enabled=use_amp and dtype == torch.float16)
-        self.broadcast_buffers = broadcast_buffers and self.distributed
-        self.reduce_metrics = reduce_metrics and self.distributed
+        self.broadcast_buffers = broadcast_buffers and (self.distributed or self.ncomm is not None)
+        self.reduce_metrics = reduce_metrics and (self.distributed or self.ncomm is not None)
         self._steps = 0
 
     def _reduce(self, met: torch.Tensor) -> torch.Tensor:
         if self.reduce_metrics:
-            dist.all_reduce(met, group=self.pg)
+            if self.ncomm is not None:
+                self.ncomm.all_reduce(met)
+            else:
+                dist.all_reduce(met, group=self.pg)
             met.div_(self.world)
         return met
 
+    def _sync_buffers(self) -> None:
+        if self.ncomm is not None:
+            if self.buffers.n_float:
+                self.ncomm.broadcast(self.buffers.fdata, 0)
+            if self.buffers.n_int:
+                self.ncomm.broadcast(self.buffers.idata, 0)
+        else:
+            sync_buffers(self.buffers, self.pg)
+
     def train_step(self, images: torch.Tensor, target: torch.Tensor):
         if self.broadcast_buffers and self._steps > 0:
-            sync_buffers(self.buffers, self.pg)
+            self._sync_buffers()
         logits, met = self.executor.train_step(images, target, loss_scale=self.scaler.scale_tensor,
                                                grad_div=float(images.shape[0]))
         if self.buffers.n_int:
@@ -76,6 +98,6 @@ class NativeTrainer:
     @torch.no_grad()
     def eval_step(self, images: torch.Tensor, target: torch.Tensor):
         if self.broadcast_buffers and self._steps > 0:
-            sync_buffers(self.buffers, self.pg)
+            self._sync_buffers()
         logits, met = self.executor.eval_step(images, target)
         return logits, self._reduce(met)

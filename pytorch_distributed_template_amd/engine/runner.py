@@ -187,7 +187,8 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
               first_bucket_mb=args.first_bucket_mb)
     if engine == "native":
         from .native_trainer import NativeTrainer
-        return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)), **kw)
+        return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)),
+                             comm=getattr(args, "comm", "torch"), **kw)
     from .torch_trainer import TorchTrainer
     return TorchTrainer(model, device, dtype=dtype, **kw)
 

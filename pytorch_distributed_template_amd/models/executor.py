@@ -80,7 +80,8 @@ class ResNetExecutor:
 
     def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None,
-                 syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512, autotune: bool = False):
+                 syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512, autotune: bool = False,
+                 syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not isinstance(model, ResNet) or model.groups != 1:
@@ -93,6 +94,12 @@ class ResNetExecutor:
         self.dtype = dtype
         self.grad_ready = grad_ready or (lambda pid: None)
         self.syncbn_group = syncbn_group
+        # SyncBN statistic all-reduce (fp64 sums): torch.distributed on syncbn_group, or a native RCCL
+        # communicator's all_reduce when one is given
+        if syncbn_group is not None:
+            import torch.distributed as dist
+            self.syncbn_world = dist.get_world_size(syncbn_group)
+            self._sync_sum = syncbn_allreduce or (lambda t: dist.all_reduce(t, group=syncbn_group))
         self.wgrad_blocks = wgrad_blocks  # split-K targets (tools/conv_bench.py sweep: 3x3 best ~2048, 1x1 ~512)
         self.wgrad_blocks_1x1 = wgrad_blocks_1x1
         # generic-path stem tile (window mode, BK=32); PDT_STEM_TILE=BMxBN overrides (tuning)
@@ -251,10 +258,8 @@ class ResNetExecutor:
                                      bn.mod.running_mean, bn.mod.running_var, bn.coef, bn.sums, True)
             return
         self.C.bn_slot_sum(sp, C, 2, bn.sums)
-        if self.syncbn_group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(bn.sums, group=self.syncbn_group)
-            count = count * dist.get_world_size(self.syncbn_group)
+        self._sync_sum(bn.sums)
+        count = count * self.syncbn_world
         self.C.bn_finalize(bn.sums, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
                            bn.mod.running_mean, bn.mod.running_var, bn.coef, True)
 
@@ -340,10 +345,8 @@ class ResNetExecutor:
             return
         sums = bn1.bsums[:C * K]
         self.C.bn_slot_sum(slots, C, K, sums)
-        if self.syncbn_group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(sums, group=self.syncbn_group)
-            count = count * dist.get_world_size(self.syncbn_group)
+        self._sync_sum(sums)
+        count = count * self.syncbn_world
         # sums layout: k*C + c for k in [sum dz1, sum dz1*x1, (sum dz2, sum dz2*x2)]
         self.C.bn_bwd_finalize(sums[:2 * C], float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot),
                                self._g(bn1.bslot), 1.0, bn1.bcoef)

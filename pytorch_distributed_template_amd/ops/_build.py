@@ -1,8 +1,9 @@
 """In-tree build of the native extension ``pytorch_distributed_template_amd/_C.so``.
 
 HIP kernels (``csrc/kernels/*.hip``) are compiled by ``hipcc --offload-arch=gfx950`` directly (no
-hipify, no CUDA sources, single target), the thin binding layer (``csrc/bindings.cpp``) by the host
-C++ compiler against the installed PyTorch headers, and everything is linked into one shared object
+hipify, no CUDA sources, single target), the thin binding layer (``csrc/bindings.cpp``) and the RCCL
+communicator / gradient bucketer (``csrc/comm.cpp``) by the host C++ compiler against the installed
+PyTorch headers, and everything is linked into one shared object
 that lives inside the package so it travels with the repository snapshot to the GPU box.
 
 Objects are rebuilt only when their source, any header under ``csrc/`` or the compile flags change.
@@ -95,10 +96,11 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         cmd = [hipcc] + hip_flags + ["-c", src, "-o", obj]
         jobs_list.append((src, obj, cmd, hashlib.sha1((" ".join(cmd) + hdr).encode()).hexdigest()))
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.o")
-    bcmd = [cxx] + cxx_flags + ["-c", bsrc, "-o", bobj]
-    jobs_list.append((bsrc, bobj, bcmd, hashlib.sha1((" ".join(bcmd) + hdr).encode()).hexdigest()))
+    for name in ("bindings.cpp", "comm.cpp"):  # host C++: op bindings; RCCL communicator + bucketer
+        bsrc = os.path.join(CSRC, name)
+        bobj = os.path.join(BUILD, name.replace(".cpp", ".o"))
+        bcmd = [cxx] + cxx_flags + ["-c", bsrc, "-o", bobj]
+        jobs_list.append((bsrc, bobj, bcmd, hashlib.sha1((" ".join(bcmd) + hdr).encode()).hexdigest()))
     if force:
         for _, obj, _, _ in jobs_list:
             if os.path.exists(obj):
@@ -111,7 +113,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     if any(changed) or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
         tmp = OUT + ".tmp"
         link = [cxx, "-shared", "-o", tmp] + objs + [
-            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            # RCCL: PyTorch's own copy (same soname), so the process holds a single RCCL instance
+            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lrccl",
             f"-L{os.path.join(ROCM, 'lib')}", "-lamdhip64", f"-Wl,-rpath,{tlib}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
         _run(link, verbose)
         os.replace(tmp, OUT)

@@ -1,0 +1,58 @@
+"""Native RCCL communicator and C++ gradient bucketer (csrc/comm.cpp) on one GPU.
+
+RCCL refuses two ranks on one device, so multi-rank numerics are covered by the torch.distributed path
+(test_distributed_cpu.py, test_training_gpu.py); here the native layer runs as a 1-rank communicator:
+collectives must be identities, stream ordering must hold (results read on the compute stream without
+host synchronisation), and a training step through the C++ bucketer must equal the default path.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_rccl_single_rank_collectives():
+    from pytorch_distributed_template_amd.parallel.comm import NativeComm
+    c = NativeComm(torch.device(DEV, 0))
+    assert c.world == 1 and c.rank == 0
+    x = torch.randn(1 << 20, device=DEV)
+    ref = x.clone()
+    x.mul_(2.0)  # enqueued on the compute stream; the collective must run after it
+    c.all_reduce(x)
+    assert torch.equal(x, ref * 2.0)
+    y = torch.arange(1000, device=DEV, dtype=torch.int64)
+    c.broadcast(y, 0)
+    assert torch.equal(y, torch.arange(1000, device=DEV, dtype=torch.int64))
+    out = torch.empty(4096, device=DEV, dtype=torch.bfloat16)
+    inp = torch.randn(4096, device=DEV).to(torch.bfloat16)
+    c.all_gather(inp, out)
+    assert torch.equal(out, inp)
+    m = torch.tensor([3.0, -1.0], device=DEV)
+    c.all_reduce(m, "max")
+    assert m.tolist() == [3.0, -1.0]
+    c.barrier()
+    c.check()
+
+
+def test_native_bucketer_step_matches_default():
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+
+    def one(comm):
+        torch.manual_seed(0)
+        model = registry.create("resnet18", num_classes=100)
+        tr = NativeTrainer(model, DEV, dtype=torch.bfloat16, comm=comm, force_comm=True, bucket_cap_mb=4.0)
+        g = torch.Generator(device=DEV).manual_seed(5)
+        x = torch.randn(16, 3, 64, 64, device=DEV, generator=g)
+        t = torch.randint(0, 100, (16,), device=DEV, generator=g)
+        for _ in range(2):
+            _, met = tr.train_step(x, t)
+        return tr, met
+
+    tn, mn = one("native")
+    assert tn.ncomm is not None and len(tn.bucketer.buckets) > 1
+    tt, mt = one("torch")
+    assert tt.ncomm is None
+    assert torch.equal(tn.flat.data, tt.flat.data)
+    assert torch.allclose(mn, mt)
