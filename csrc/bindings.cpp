@@ -528,6 +528,17 @@ void stem_pack(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, in
   pdt::stem_pack_launch(dt16(out, "out"), pf(x, "x"), p16(out, "out"), N, C, H, W, pad, Hp, Wp, cur_stream());
 }
 
+// uint8 NCHW pixels -> normalised, zero-padded NHWC4 16-bit stem input (v = x * scale[c] + shift[c])
+void stem_pack_u8(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t pad, int64_t Hp,
+                  int64_t Wp, const Tensor& scale, const Tensor& shift) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kByte, "stem_pack_u8: x must be uint8");
+  TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * Hp * Wp * 4 && C <= 4 && Hp >= H + 2 * pad &&
+                  Wp >= W + 2 * pad && scale.numel() >= C && shift.numel() >= C, "stem_pack_u8: bad sizes");
+  pdt::stem_pack_u8_launch(dt16(out, "out"), x.data_ptr<uint8_t>(), p16(out, "out"), N, C, H, W, pad, Hp, Wp,
+                           pf(scale, "scale"), pf(shift, "shift"), cur_stream());
+}
+
 void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
   check_dev(idx, "idx");
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == dst.numel(), "gather32: idx must be int32 like dst");
@@ -580,5 +591,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather16", &gather16);
   m.def("im2col", &im2col);
   m.def("stem_pack", &stem_pack);
+  m.def("stem_pack_u8", &stem_pack_u8);
   m.def("gather32", &gather32);
 }

@@ -14,5 +14,7 @@ void im2col_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H
                    int ldk, hipStream_t s);
 void stem_pack_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp, int Wp,
                       hipStream_t s);
+void stem_pack_u8_launch(int dtype, const uint8_t* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp,
+                         int Wp, const float* scale, const float* shift, hipStream_t s);
 void gather32_launch(const float* src, const int* idx, float* dst, int64_t n, hipStream_t s);
 }  // namespace pdt

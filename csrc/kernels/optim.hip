@@ -176,9 +176,13 @@ void im2col_launch(int dtype, const float* x, uint16_t* out, int N, int C, int H
 // Stem input: fp32 NCHW image batch -> zero-padded 16-bit NHWC4 image [N][H+2p][W+2p+ex][4]
 // (channel 3 and the border are zero).  The stem conv then reads 8-pixel x 4-channel windows of it
 // directly (window mode of conv_fwd / conv_wgrad): no im2col matrix.
-template <int DT>
-__global__ __launch_bounds__(256) void stem_pack_kernel(const float* __restrict__ x, uint16_t* __restrict__ out, int N,
-                                                        int C, int H, int W, int pad, int Hp, int Wp) {
+// TIN = float: x is already normalised; TIN = uint8_t: raw pixels, v = x * scale[c] + shift[c] (the
+// ImageNet Normalize of the data pipeline fused here, so batches cross PCIe as uint8 -- SURVEY K28)
+template <int DT, typename TIN>
+__global__ __launch_bounds__(256) void stem_pack_kernel(const TIN* __restrict__ x, uint16_t* __restrict__ out, int N,
+                                                        int C, int H, int W, int pad, int Hp, int Wp,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift) {
   using E = E16<DT>;
   const int64_t total = (int64_t)N * Hp * Wp;
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
@@ -189,7 +193,10 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const float* __restrict_
     const int h = hp - pad, w = wp - pad;
     uint16_t o[4] = {0, 0, 0, 0};
     if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
-      for (int c = 0; c < C && c < 4; ++c) o[c] = E::from_f(x[(((int64_t)n * C + c) * H + h) * W + w]);
+      for (int c = 0; c < C && c < 4; ++c) {
+        const float v = (float)x[(((int64_t)n * C + c) * H + h) * W + w];
+        o[c] = E::from_f(scale ? v * scale[c] + shift[c] : v);
+      }
     }
     uint2 q;
     q.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
@@ -202,9 +209,22 @@ void stem_pack_launch(int dtype, const float* x, uint16_t* out, int N, int C, in
                       hipStream_t s) {
   const int64_t total = (int64_t)N * Hp * Wp;
   if (dtype == kBF16)
-    hipLaunchKernelGGL(stem_pack_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W, pad, Hp, Wp);
+    hipLaunchKernelGGL((stem_pack_kernel<kBF16, float>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W,
+                       pad, Hp, Wp, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(stem_pack_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W, pad, Hp, Wp);
+    hipLaunchKernelGGL((stem_pack_kernel<kF16, float>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W,
+                       pad, Hp, Wp, nullptr, nullptr);
+}
+
+void stem_pack_u8_launch(int dtype, const uint8_t* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp,
+                         int Wp, const float* scale, const float* shift, hipStream_t s) {
+  const int64_t total = (int64_t)N * Hp * Wp;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL((stem_pack_kernel<kBF16, uint8_t>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H,
+                       W, pad, Hp, Wp, scale, shift);
+  else
+    hipLaunchKernelGGL((stem_pack_kernel<kF16, uint8_t>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H,
+                       W, pad, Hp, Wp, scale, shift);
 }
 
 __global__ __launch_bounds__(256) void gather32_kernel(const float* __restrict__ src, const int* __restrict__ idx,

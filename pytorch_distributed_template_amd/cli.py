@@ -120,6 +120,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--resume", default="", metavar="PATH", help="resume from a checkpoint written by this framework")
     g.add_argument("--pretrained-path", default=None, help="local torchvision-format weights for --pretrained")
     g.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    g.add_argument("--gpu-normalize", default="auto", choices=["auto", "on", "off"],
+                   help="ship uint8 images to the GPU and normalise there (fused into the native stem kernel); "
+                        "auto = on for the native engine, off otherwise")
     g.add_argument("--comm", default="torch", choices=["torch", "native"],
                    help="collectives: torch.distributed (RCCL via c10d) or this framework's own RCCL communicator "
                         "and C++ gradient bucketer")

@@ -66,11 +66,13 @@ class ImageFolder(Dataset):
 class SyntheticImageNet(Dataset):
     """Deterministic random images (standard-normal, i.e. already "normalised") and labels."""
 
-    def __init__(self, size: int = 1281167, image_size: int = 224, num_classes: int = 1000, seed: int = 0):
+    def __init__(self, size: int = 1281167, image_size: int = 224, num_classes: int = 1000, seed: int = 0,
+                 uint8: bool = False):
         self.size = size
         self.image_size = image_size
         self.num_classes = num_classes
         self.seed = seed
+        self.uint8 = uint8  # raw-pixel samples (the gpu_normalize pipeline)
 
     def __len__(self) -> int:
         return self.size
@@ -78,6 +80,9 @@ class SyntheticImageNet(Dataset):
     def __getitem__(self, index: int):
         g = torch.Generator()
         g.manual_seed(self.seed * 1000003 + index)
-        img = torch.randn(3, self.image_size, self.image_size, generator=g)
+        if self.uint8:
+            img = torch.randint(0, 256, (3, self.image_size, self.image_size), generator=g, dtype=torch.uint8)
+        else:
+            img = torch.randn(3, self.image_size, self.image_size, generator=g)
         target = int(torch.randint(0, self.num_classes, (1,), generator=g).item())
         return img, target

@@ -18,7 +18,7 @@ from torch.utils.data import DataLoader
 
 from .datasets import ImageFolder, SyntheticImageNet
 from .sampler import DistributedSampler
-from .transforms import train_transform, val_transform
+from .transforms import normalize_on_device, train_transform, val_transform
 
 
 class DeviceSyntheticLoader:
@@ -67,10 +67,13 @@ class DeviceSyntheticLoader:
 class DevicePrefetcher:
     """Wrap a host DataLoader: batch i+1 is copied to the device on a side stream during step i."""
 
-    def __init__(self, loader, device):
+    def __init__(self, loader, device, normalize_uint8: bool = False):
         self.loader = loader
         self.device = torch.device(device)
         self.stream = torch.cuda.Stream(device=self.device)
+        # uint8 batches: keep them uint8 (the native engine normalises inside its stem kernel) or
+        # normalise on the side stream (torch engine)
+        self.normalize_uint8 = normalize_uint8
 
     def __len__(self) -> int:
         return len(self.loader)
@@ -82,7 +85,10 @@ class DevicePrefetcher:
     def _copy(self, batch):
         x, t = batch
         with torch.cuda.stream(self.stream):
-            return x.to(self.device, non_blocking=True), t.to(self.device, non_blocking=True)
+            x = x.to(self.device, non_blocking=True)
+            if self.normalize_uint8 and x.dtype == torch.uint8:
+                x = normalize_on_device(x)
+            return x, t.to(self.device, non_blocking=True)
 
     def __iter__(self):
         it = iter(self.loader)
@@ -110,6 +116,10 @@ def build_loaders(args, world: int, rank: int, device, distributed: bool, batch_
     process count for DDP, `distributed.py:143`; DataParallel uses the node-total batch)."""
     device = torch.device(device)
     on_gpu = device.type == "cuda"
+    # gpu_normalize: samples stay uint8 on the host and cross PCIe as uint8 (K28); "native" keeps them
+    # uint8 on the device too (fused into the stem kernel), "torch" normalises after the copy
+    gpu_norm = getattr(args, "gpu_normalize_mode", "off") if on_gpu else "off"
+    u8 = gpu_norm in ("native", "torch")
     if args.synthetic and on_gpu:
         tr = DeviceSyntheticLoader(args.synthetic_train_size, batch_size, world, rank, device, args.image_size,
                                    args.num_classes, seed=args.seed or 0)
@@ -117,11 +127,11 @@ def build_loaders(args, world: int, rank: int, device, distributed: bool, batch_
                                    args.num_classes, seed=(args.seed or 0) + 1, pool=2)
         return tr, va, tr, va
     if args.synthetic:
-        train_ds = SyntheticImageNet(args.synthetic_train_size, args.image_size, args.num_classes, seed=0)
-        val_ds = SyntheticImageNet(args.synthetic_val_size, args.image_size, args.num_classes, seed=1)
+        train_ds = SyntheticImageNet(args.synthetic_train_size, args.image_size, args.num_classes, seed=0, uint8=u8)
+        val_ds = SyntheticImageNet(args.synthetic_val_size, args.image_size, args.num_classes, seed=1, uint8=u8)
     else:
-        train_ds = ImageFolder(os.path.join(args.data, "train"), train_transform(args.image_size))
-        val_ds = ImageFolder(os.path.join(args.data, "val"), val_transform(args.image_size))
+        train_ds = ImageFolder(os.path.join(args.data, "train"), train_transform(args.image_size, gpu_normalize=u8))
+        val_ds = ImageFolder(os.path.join(args.data, "val"), val_transform(args.image_size, gpu_normalize=u8))
     if distributed:
         train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
         val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank)
@@ -136,5 +146,7 @@ def build_loaders(args, world: int, rank: int, device, distributed: bool, batch_
         val_loader = DataLoader(val_ds, batch_size=batch_size, shuffle=False, num_workers=args.workers,
                                 pin_memory=on_gpu, persistent_workers=args.workers > 0)
     if on_gpu:
-        train_loader, val_loader = DevicePrefetcher(train_loader, device), DevicePrefetcher(val_loader, device)
+        nz = gpu_norm == "torch"
+        train_loader = DevicePrefetcher(train_loader, device, normalize_uint8=nz)
+        val_loader = DevicePrefetcher(val_loader, device, normalize_uint8=nz)
     return train_loader, val_loader, train_sampler, val_sampler

@@ -254,6 +254,11 @@ def main(mode: str, argv: Optional[list] = None) -> int:
                                                                                 device, world), logger, rank)
     trainer = build_trainer(mode, model, args, device, dtype, engine, world)
     optimizer = trainer.optimizer
+    gn = getattr(args, "gpu_normalize", "off")
+    if device.type != "cuda" or gn == "off" or (gn == "auto" and engine != "native"):
+        args.gpu_normalize_mode = "off"
+    else:
+        args.gpu_normalize_mode = "native" if engine == "native" else "torch"
     lr_scheduler = build_scheduler(args.lr_scheduler, optimizer, args.step, args.gamma)
     ddp_print("lr_scheduler: SGD MultiStepLR !!!", logger, rank)
 

@@ -107,6 +107,11 @@ class ResNetExecutor:
         self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
+        # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
+        from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
+        std = torch.tensor(IMAGENET_STD)
+        self.norm_scale = (1.0 / (255.0 * std)).to(self.device)
+        self.norm_shift = (-torch.tensor(IMAGENET_MEAN) / std).to(self.device)
         self.autotune = autotune or os.environ.get("PDT_AUTOTUNE", "0") == "1"
         self._tiles: Dict[tuple, Tuple[int, int]] = {}
         derived_maps: List[torch.Tensor] = []
@@ -363,8 +368,8 @@ class ResNetExecutor:
         Cn = self.C
         N = images.shape[0]
         assert images.dim() == 4 and images.shape[1] == 3, "expected NCHW images"
-        x32 = images if images.dtype == torch.float32 else images.float()
-        x32 = x32.contiguous()
+        u8 = images.dtype == torch.uint8  # raw pixels: ImageNet Normalize fused into the stem packing
+        x32 = images.contiguous() if u8 or images.dtype == torch.float32 else images.float().contiguous()
         H, W = images.shape[2], images.shape[3]
         st = self.stem
         P0, Q0 = st.out_hw(H, W)
@@ -373,7 +378,10 @@ class ResNetExecutor:
         Hp = max(H + 2 * st.pad, 2 * (P0 - 1) + 2 * self.stem_pairs)
         Wp = max(W + 2 * st.pad, (Q0 - 1) * st.st + 8)
         xp = self._buf("stem_in", N * Hp * Wp * 4)
-        Cn.stem_pack(x32, xp, N, 3, H, W, st.pad, Hp, Wp)
+        if u8:
+            Cn.stem_pack_u8(x32, xp, N, 3, H, W, st.pad, Hp, Wp, self.norm_scale, self.norm_shift)
+        else:
+            Cn.stem_pack(x32, xp, N, 3, H, W, st.pad, Hp, Wp)
         y0 = self._buf("y0", N * P0 * Q0 * st.cout)
         wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * st.R * 32]
         sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64) if train else None

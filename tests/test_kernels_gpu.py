@@ -381,3 +381,21 @@ def test_conv_tile_configs(tile):
     refx = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
                                       stride=2, padding=1).permute(0, 2, 3, 1) + res.float()
     assert _rel(dx, refx) < 1e-2
+
+
+def test_stem_pack_u8_fused_normalize():
+    """uint8 pixels normalised inside the stem packing == host-style Normalize then packing."""
+    from pytorch_distributed_template_amd.data.transforms import IMAGENET_MEAN, IMAGENET_STD, normalize_on_device
+    from pytorch_distributed_template_amd.ops import native
+    N, H, W, pad = 3, 20, 18, 3
+    Hp, Wp = H + 2 * pad + 2, W + 2 * pad + 2
+    x8 = torch.randint(0, 256, (N, 3, H, W), device=DEV, dtype=torch.uint8)
+    ref = torch.empty(N * Hp * Wp * 4, dtype=torch.bfloat16, device=DEV)
+    native.C.stem_pack(normalize_on_device(x8).contiguous(), ref, N, 3, H, W, pad, Hp, Wp)
+    out = torch.empty_like(ref)
+    std = torch.tensor(IMAGENET_STD)
+    scale = (1.0 / (255.0 * std)).to(DEV)
+    shift = (-torch.tensor(IMAGENET_MEAN) / std).to(DEV)
+    native.C.stem_pack_u8(x8, out, N, 3, H, W, pad, Hp, Wp, scale, shift)
+    assert (out.float() - ref.float()).abs().max().item() < 2e-2
+    assert out.view(N, Hp, Wp, 4)[:, :, :, 3].abs().max().item() == 0  # 4th channel and padding stay zero
