@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--sync-bn", action="store_true")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--graph", action="store_true", help="replay the training step as a captured HIP graph")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -54,7 +55,8 @@ def main():
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     model = registry.create(args.arch)
     tr = NativeTrainer(model, dev, dtype=dtype, lr=0.1, momentum=0.9, weight_decay=1e-4,
-                       use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb)
+                       use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb,
+                       graph=args.graph)
     B = args.batch_per_gpu
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)

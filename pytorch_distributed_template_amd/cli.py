@@ -123,6 +123,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--gpu-normalize", default="auto", choices=["auto", "on", "off"],
                    help="ship uint8 images to the GPU and normalise there (fused into the native stem kernel); "
                         "auto = on for the native engine, off otherwise")
+    g.add_argument("--graph", default=False, type=str2bool, nargs="?", const=True,
+                   help="capture the whole native training step in a HIP graph and replay it (single process; "
+                        "pays off when small batches make the step launch-bound)")
     g.add_argument("--comm", default="torch", choices=["torch", "native"],
                    help="collectives: torch.distributed (RCCL via c10d) or this framework's own RCCL communicator "
                         "and C++ gradient bucketer")

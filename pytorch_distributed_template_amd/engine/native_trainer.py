@@ -29,7 +29,7 @@ class NativeTrainer:
                  weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
-                 force_comm: bool = False):
+                 force_comm: bool = False, graph: bool = False):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -60,6 +60,10 @@ class NativeTrainer:
         self.broadcast_buffers = broadcast_buffers and (self.distributed or self.ncomm is not None)
         self.reduce_metrics = reduce_metrics and (self.distributed or self.ncomm is not None)
         self._steps = 0
+        # whole-step HIP graph (launch-bound small batches): single-process only, collectives stay eager
+        self.use_graph = graph and not self.distributed and self.ncomm is None
+        self._graphs = {}
+        self._graph_warm = 0
 
     def _reduce(self, met: torch.Tensor) -> torch.Tensor:
         if self.reduce_metrics:
@@ -80,6 +84,38 @@ class NativeTrainer:
             sync_buffers(self.buffers, self.pg)
 
     def train_step(self, images: torch.Tensor, target: torch.Tensor):
+        if self.use_graph:
+            return self._graphed_step(images, target)
+        return self._train_step_eager(images, target)
+
+    def _graphed_step(self, images: torch.Tensor, target: torch.Tensor):
+        """Replay one captured training step (forward, loss, backward, SGD, scaler update) as a HIP graph.
+
+        Two eager warm-up steps settle every lazily created buffer and per-shape kernel choice (and the
+        momentum initialisation of the first SGD step); the graph is keyed by input shape / dtype and the
+        learning rate (a kernel argument), so an LR-schedule change captures a new graph."""
+        key = (tuple(images.shape), images.dtype, float(self.optimizer.lr))
+        ent = self._graphs.get(key)
+        if ent is None:
+            if self._graph_warm < 2:
+                self._graph_warm += 1
+                return self._train_step_eager(images, target)
+            sx, st = images.clone(), target.clone()
+            g = torch.cuda.CUDAGraph()
+            steps, sc = self._steps, self.optimizer.step_count
+            with torch.cuda.graph(g):
+                out = self._train_step_eager(sx, st)
+            self._steps, self.optimizer.step_count = steps, sc  # capture does not run the step
+            ent = self._graphs[key] = (g, sx, st, out)
+        g, sx, st, out = ent
+        sx.copy_(images)
+        st.copy_(target)
+        g.replay()
+        self._steps += 1
+        self.optimizer.step_count += 1
+        return out
+
+    def _train_step_eager(self, images: torch.Tensor, target: torch.Tensor):
         if self.broadcast_buffers and self._steps > 0:
             self._sync_buffers()
         logits, met = self.executor.train_step(images, target, loss_scale=self.scaler.scale_tensor,

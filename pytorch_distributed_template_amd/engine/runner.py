@@ -188,7 +188,7 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
     if engine == "native":
         from .native_trainer import NativeTrainer
         return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)),
-                             comm=getattr(args, "comm", "torch"), **kw)
+                             comm=getattr(args, "comm", "torch"), graph=bool(getattr(args, "graph", False)), **kw)
     from .torch_trainer import TorchTrainer
     return TorchTrainer(model, device, dtype=dtype, **kw)
 
