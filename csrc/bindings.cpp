@@ -67,6 +67,15 @@ float* pf(const Tensor& t, const char* name) {
 }
 float* pfo(const OptT& t, const char* name) { return t.has_value() ? pf(*t, name) : nullptr; }
 
+// ReLU bitmask (bit e of byte v = element 8v+e > 0) of a 16-bit activation with `n` elements
+uint8_t* pmask(const OptT& t, int64_t n, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_dev(*t, name);
+  TORCH_CHECK(t->scalar_type() == at::kByte, name, ": expected a uint8 bitmask");
+  TORCH_CHECK(n % 8 == 0 && t->numel() == n / 8, name, ": bitmask must hold numel/8 bytes");
+  return t->data_ptr<uint8_t>();
+}
+
 double* pd(const Tensor& t, const char* name) {
   check_dev(t, name);
   TORCH_CHECK(t.scalar_type() == at::kDouble, name, ": expected float64");
@@ -157,7 +166,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
                      int64_t Q, int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride,
                      const std::vector<std::vector<int64_t>>& phases, int64_t bm, int64_t bn, int64_t bk, int64_t bnb,
                      const OptT& bn_y1, const OptT& bn_coef1, const OptT& bn_y2, const OptT& bn_coef2,
-                     const OptT& bn_out, const OptT& bn_slots) {
+                     const OptT& bn_mask, const OptT& bn_slots) {
   const int dt = dt16(dy, "dy");
   TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "conv_dgrad: mixed dtypes");
   TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv_dgrad: size mismatch");
@@ -197,8 +206,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     TORCH_CHECK(bn_y1.has_value() && bn_coef1.has_value() && bn_slots.has_value(), "conv_dgrad: bnb needs y1/coef1/slots");
     TORCH_CHECK(bn_y1->numel() == dx.numel() && dt16(*bn_y1, "bn_y1") == dt && bn_coef1->numel() >= 4 * C,
                 "conv_dgrad: bn_y1 / bn_coef1 size");
-    TORCH_CHECK(bnb == 1 || (bn_out.has_value() && bn_out->numel() == dx.numel() && dt16(*bn_out, "bn_out") == dt),
-                "conv_dgrad: bnb 2/3 need the block output (ReLU mask)");
+    TORCH_CHECK(bnb == 1 || bn_mask.has_value(), "conv_dgrad: bnb 2/3 need the block output's ReLU bitmask");
     TORCH_CHECK(bnb != 3 || (bn_y2.has_value() && bn_coef2.has_value() && bn_y2->numel() == dx.numel() &&
                              bn_coef2->numel() >= 4 * C),
                 "conv_dgrad: bnb 3 needs y2/coef2");
@@ -210,7 +218,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     a.bn_coef1 = pf(*bn_coef1, "bn_coef1");
     if (bn_y2.has_value()) a.bn_y2 = p16(*bn_y2, "bn_y2");
     if (bn_coef2.has_value()) a.bn_coef2 = pf(*bn_coef2, "bn_coef2");
-    if (bn_out.has_value()) a.bn_out = p16(*bn_out, "bn_out");
+    a.bn_mask = pmask(bn_mask, dx.numel(), "bn_mask");
     a.stats = pd(*bn_slots, "bn_slots");
   }
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
@@ -347,24 +355,25 @@ void bn_eval_coef(const Tensor& gamma, const Tensor& beta, const Tensor& rm, con
 }
 
 void bn_apply(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& rcoef, Tensor& out, int64_t C,
-              int64_t resmode, bool relu) {
+              int64_t resmode, bool relu, const OptT& mask) {
   const int dt = dt16(y, "y");
   TORCH_CHECK(C % 8 == 0 && y.numel() % C == 0 && out.numel() == y.numel(), "bn_apply: bad sizes");
   if (resmode != 0) TORCH_CHECK(res.has_value() && res->numel() == y.numel(), "bn_apply: residual missing/mismatch");
   if (resmode == 2) TORCH_CHECK(rcoef.has_value(), "bn_apply: residual coefficients missing");
+  TORCH_CHECK(!mask.has_value() || (resmode != 0 && relu), "bn_apply: the ReLU bitmask is built for residual block outputs");
   pdt::bn_apply_launch(dt, p16(y, "y"), pf(coef, "coef"), p16o(res, "res"), pfo(rcoef, "rcoef"), p16(out, "out"),
-                       y.numel(), C, (int)resmode, relu, cur_stream());
+                       pmask(mask, y.numel(), "mask"), y.numel(), C, (int)resmode, relu, cur_stream());
 }
 
 int64_t bn_bwd_reduce_blocks(int64_t rows, int64_t C) { return pdt::bn_bwd_reduce_blocks(rows, (int)C); }
 
-void bn_bwd_reduce(const Tensor& g, const OptT& out, const Tensor& y1, const Tensor& coef1, const OptT& y2,
+void bn_bwd_reduce(const Tensor& g, const OptT& mask, const Tensor& y1, const Tensor& coef1, const OptT& y2,
                    const OptT& coef2, Tensor& slots, int64_t blocks, int64_t rows, int64_t C) {
   const int dt = dt16(g, "g");
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && g.numel() == rows * C && y1.numel() == rows * C, "bn_bwd_reduce: bad sizes");
   const int K = y2.has_value() ? 4 : 2;
   TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K, "bn_bwd_reduce: slots too small");
-  pdt::bn_bwd_reduce_launch(dt, p16(g, "g"), p16o(out, "out"), p16(y1, "y1"), pf(coef1, "coef1"), p16o(y2, "y2"),
+  pdt::bn_bwd_reduce_launch(dt, p16(g, "g"), pmask(mask, g.numel(), "mask"), p16(y1, "y1"), pf(coef1, "coef1"), p16o(y2, "y2"),
                             pfo(coef2, "coef2"), pd(slots, "slots"), (int)blocks, rows, (int)C, cur_stream());
 }
 
@@ -376,11 +385,11 @@ void bn_bwd_finalize(const Tensor& sums, double count, const Tensor& coef, const
                               pfo(dbeta, "dbeta"), (float)gscale, pf(bcoef, "bcoef"), C, cur_stream());
 }
 
-void bn_bwd_apply(const Tensor& g, const OptT& out, const Tensor& y1, const Tensor& b1, Tensor& dy1, const OptT& y2,
+void bn_bwd_apply(const Tensor& g, const OptT& mask, const Tensor& y1, const Tensor& b1, Tensor& dy1, const OptT& y2,
                   const OptT& b2, const OptT& dy2, const OptT& dz, int64_t C) {
   const int dt = dt16(g, "g");
   TORCH_CHECK(C % 8 == 0 && g.numel() % C == 0 && dy1.numel() == g.numel(), "bn_bwd_apply: bad sizes");
-  pdt::bn_bwd_apply_launch(dt, p16(g, "g"), p16o(out, "out"), p16(y1, "y1"), pf(b1, "b1"), p16(dy1, "dy1"),
+  pdt::bn_bwd_apply_launch(dt, p16(g, "g"), pmask(mask, g.numel(), "mask"), p16(y1, "y1"), pf(b1, "b1"), p16(dy1, "dy1"),
                            p16o(y2, "y2"), pfo(b2, "b2"), p16m(dy2, "dy2"), p16m(dz, "dz"), g.numel(), C, cur_stream());
 }
 

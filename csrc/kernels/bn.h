@@ -17,14 +17,14 @@ void bn_finalize_launch(const double* sums, double count, const float* gamma, co
 void bn_eval_coef_launch(const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
                          float* coef, int C, hipStream_t s);
 void bn_apply_launch(int dtype, const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef,
-                     uint16_t* out, int64_t n, int C, int resmode, bool relu, hipStream_t s);
+                     uint16_t* out, uint8_t* mask, int64_t n, int C, int resmode, bool relu, hipStream_t s);
 int bn_bwd_reduce_blocks(int64_t rows, int C);
-void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* coef1,
+void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint8_t* mask, const uint16_t* y1, const float* coef1,
                           const uint16_t* y2, const float* coef2, double* slots, int blocks, int64_t rows, int C,
                           hipStream_t s);
 void bn_bwd_finalize_launch(const double* sums, double count, const float* coef, const float* gamma, float* dgamma,
                             float* dbeta, float gscale, float* bcoef, int C, hipStream_t s);
-void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* b1,
+void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint8_t* mask, const uint16_t* y1, const float* b1,
                          uint16_t* dy1, const uint16_t* y2, const float* b2, uint16_t* dy2, uint16_t* dz_out, int64_t n,
                          int C, hipStream_t s);
 }  // namespace pdt

@@ -125,12 +125,14 @@ void bn_eval_coef_launch(const float* gamma, const float* beta, const float* rm,
 }
 
 // -------------------------------------------------------------------------------------------------
-// out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift
-template <int DT, int RESMODE, bool RELU>
+// out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift.
+// WM: also write the ReLU bitmask (bit e of mask[v] = out[8v+e] > 0) that the backward reads instead of
+// re-reading the 16-bit block output (1 bit instead of 16 per element).
+template <int DT, int RESMODE, bool RELU, bool WM>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                        const uint16_t* __restrict__ res,
                                                        const float* __restrict__ rcoef, uint16_t* __restrict__ out,
-                                                       int64_t n8, int C) {
+                                                       uint8_t* __restrict__ mask, int64_t n8, int C) {
   using E = E16<DT>;
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
     const int c0 = (int)((v * 8) % C);
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
     uint32_t rw[4];
     if constexpr (RESMODE != 0) { rw[0] = rr.x; rw[1] = rr.y; rw[2] = rr.z; rw[3] = rr.w; }
-    uint32_t ow[4];
+    uint32_t ow[4], bits = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float o2[2];
@@ -154,8 +156,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
         o2[h] = val;
       }
       ow[e] = (uint32_t)E::from_f(o2[0]) | ((uint32_t)E::from_f(o2[1]) << 16);
+      // the mask tests the ROUNDED output, exactly what a 16-bit re-read would see
+      if constexpr (WM) bits |= ((ow[e] & 0x7fffu) != 0 && !(ow[e] & 0x8000u) ? 1u : 0u) << (2 * e) |
+                                ((ow[e] & 0x7fff0000u) != 0 && !(ow[e] & 0x80000000u) ? 1u : 0u) << (2 * e + 1);
     }
     ((uint4*)out)[v] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    if constexpr (WM) mask[v] = (uint8_t)bits;
   }
 }
 
@@ -167,33 +173,35 @@ static int ew_blocks(int64_t n) {
 
 template <int DT>
 static void bn_apply_dt(const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef, uint16_t* out,
-                        int64_t n, int C, int resmode, bool relu, hipStream_t s) {
+                        uint8_t* mask, int64_t n, int C, int resmode, bool relu, hipStream_t s) {
   const int64_t n8 = n / 8;
   dim3 g(ew_blocks(n8)), b(256);
-#define PDT_AP(RM, RL)                                                                          \
-  if (resmode == RM && relu == RL) {                                                            \
-    hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL>), g, b, 0, s, y, coef, res, rcoef, out, n8, C); \
-    return;                                                                                     \
+  const bool wm = mask != nullptr;
+#define PDT_AP(RM, RL, WM)                                                                                  \
+  if (resmode == RM && relu == RL && wm == WM) {                                                            \
+    hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL, WM>), g, b, 0, s, y, coef, res, rcoef, out, mask, n8, C); \
+    return;                                                                                                 \
   }
-  PDT_AP(0, true) PDT_AP(1, true) PDT_AP(2, true) PDT_AP(0, false) PDT_AP(1, false) PDT_AP(2, false)
+  PDT_AP(0, true, false) PDT_AP(1, true, false) PDT_AP(2, true, false) PDT_AP(0, false, false)
+  PDT_AP(1, false, false) PDT_AP(2, false, false) PDT_AP(1, true, true) PDT_AP(2, true, true)
 #undef PDT_AP
 }
 
 void bn_apply_launch(int dtype, const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef,
-                     uint16_t* out, int64_t n, int C, int resmode, bool relu, hipStream_t s) {
+                     uint16_t* out, uint8_t* mask, int64_t n, int C, int resmode, bool relu, hipStream_t s) {
   if (dtype == kBF16)
-    bn_apply_dt<kBF16>(y, coef, res, rcoef, out, n, C, resmode, relu, s);
+    bn_apply_dt<kBF16>(y, coef, res, rcoef, out, mask, n, C, resmode, relu, s);
   else
-    bn_apply_dt<kF16>(y, coef, res, rcoef, out, n, C, resmode, relu, s);
+    bn_apply_dt<kF16>(y, coef, res, rcoef, out, mask, n, C, resmode, relu, s);
 }
 
 // -------------------------------------------------------------------------------------------------
-// Backward reduce.  dz = g * (out > 0) (mask optional).  For branch b in {1,2}:
+// Backward reduce.  dz = g * mask (ReLU bitmask of the block output, optional).  For branch b in {1,2}:
 //   part[blk][c][2b-2] += dz ; part[blk][c][2b-1] += dz * (y_b - mean_b) * invstd_b
 // Each thread owns 8 consecutive channels of a row; rows are strided over the grid.
 template <int DT, bool MASK, int NBR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
-                                                            const uint16_t* __restrict__ out,
+                                                            const uint8_t* __restrict__ mask,
                                                             const uint16_t* __restrict__ y1,
                                                             const float* __restrict__ coef1,
                                                             const uint16_t* __restrict__ y2,
@@ -222,8 +230,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       const int64_t off = r * C + c0;
       const uint4 gv = *(const uint4*)(g + off);
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
-      uint32_t ow[4] = {0, 0, 0, 0};
-      if constexpr (MASK) { const uint4 ov = *(const uint4*)(out + off); ow[0] = ov.x; ow[1] = ov.y; ow[2] = ov.z; ow[3] = ov.w; }
+      uint32_t mb = 0xffu;
+      if constexpr (MASK) mb = mask[off >> 3];
       const uint4 y1v = *(const uint4*)(y1 + off);
       const uint32_t y1w[4] = {y1v.x, y1v.y, y1v.z, y1v.w};
       uint32_t y2w[4] = {0, 0, 0, 0};
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       for (int e = 0; e < 8; ++e) {
         const int sh = 16 * (e & 1);
         float dz = E::to_f((uint16_t)(gw[e >> 1] >> sh));
-        if constexpr (MASK) dz = E::to_f((uint16_t)(ow[e >> 1] >> sh)) > 0.f ? dz : 0.f;
+        if constexpr (MASK) dz = (mb >> e) & 1u ? dz : 0.f;
         const float x1 = (E::to_f((uint16_t)(y1w[e >> 1] >> sh)) - m1[e]) * i1[e];
         s[0][e] += dz;
         s[1][e] += dz * x1;
@@ -269,7 +277,7 @@ int bn_bwd_reduce_blocks(int64_t rows, int C) {
   return (int)(b < 1 ? 1 : b);
 }
 
-void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* coef1,
+void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint8_t* out, const uint16_t* y1, const float* coef1,
                           const uint16_t* y2, const float* coef2, double* slots, int blocks, int64_t rows, int C,
                           hipStream_t s) {
   const int rpi = 256 / (C / 8);
@@ -360,7 +368,7 @@ void bn_bwd_finalize_slots_launch(const double* slots, int K, double count, cons
 // dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad)
 template <int DT, bool MASK, int NBR, bool WDZ>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ g,
-                                                           const uint16_t* __restrict__ out,
+                                                           const uint8_t* __restrict__ mask,
                                                            const uint16_t* __restrict__ y1,
                                                            const float* __restrict__ b1, uint16_t* __restrict__ dy1,
                                                            const uint16_t* __restrict__ y2,
@@ -371,8 +379,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
     const int c0 = (int)((v * 8) % C);
     const uint4 gv = ((const uint4*)g)[v];
     const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
-    uint32_t ow[4] = {0, 0, 0, 0};
-    if constexpr (MASK) { const uint4 ov = ((const uint4*)out)[v]; ow[0] = ov.x; ow[1] = ov.y; ow[2] = ov.z; ow[3] = ov.w; }
+    uint32_t mb = 0xffu;
+    if constexpr (MASK) mb = mask[v];
     const uint4 y1v = ((const uint4*)y1)[v];
     const uint32_t y1w[4] = {y1v.x, y1v.y, y1v.z, y1v.w};
     uint32_t y2w[4] = {0, 0, 0, 0};
@@ -385,7 +393,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
       for (int h = 0; h < 2; ++h) {
         const int c = c0 + 2 * e + h;
         float dz = E::to_f((uint16_t)(gw[e] >> (16 * h)));
-        if constexpr (MASK) dz = E::to_f((uint16_t)(ow[e] >> (16 * h))) > 0.f ? dz : 0.f;
+        if constexpr (MASK) dz = (mb >> (2 * e + h)) & 1u ? dz : 0.f;
         rz[h] = E::from_f(dz);
         r1[h] = E::from_f(b1[c] * dz + b1[C + c] * E::to_f((uint16_t)(y1w[e] >> (16 * h))) + b1[2 * C + c]);
         if constexpr (NBR == 2)
@@ -401,7 +409,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   }
 }
 
-void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint16_t* out, const uint16_t* y1, const float* b1,
+void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint8_t* out, const uint16_t* y1, const float* b1,
                          uint16_t* dy1, const uint16_t* y2, const float* b2, uint16_t* dy2, uint16_t* dz_out, int64_t n,
                          int C, hipStream_t s) {
   const int64_t n8 = n / 8;

@@ -15,13 +15,14 @@ struct ConvFwdArgs {
   double* stats;        // optional: [kStatSlots][Kout][2] fp64 (sum, sumsq) BN statistics (nullptr = none);
                         // with bnb != 0: [kStatSlots][Kout][2 or 4] BN-backward sums (sum dz, sum dz*xhat ...)
   // Fused BN-backward reduce (backward-data use): 0 none | 1 mask from bn_y1 * coef1 (inner BN + ReLU)
-  // | 2 mask from bn_out > 0 (block output ReLU) | 3 as 2 with a second BN branch bn_y2 / bn_coef2.
+  // | 2 mask from bn_mask (ReLU bitmask of the block output, bit e of byte v = element 8v+e > 0)
+  // | 3 as 2 with a second BN branch bn_y2 / bn_coef2.
   int bnb;
   const uint16_t* bn_y1;
   const float* bn_coef1;  // forward coefficients [scale | shift | mean | invstd] x Kout
   const uint16_t* bn_y2;
   const float* bn_coef2;
-  const uint16_t* bn_out;
+  const uint8_t* bn_mask;
   int N, H, W, C, Kout, T, U;
   int cs;                                              // elements per input pixel (normally == C)
   int pair_skip;  // window-pair mode (stem, BK=64): chunks 4..7 read the NEXT image row (+pair_skip elements)

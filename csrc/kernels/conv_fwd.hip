@@ -301,11 +301,11 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint2 qo = *(const uint2*)(a.bn_out + obase + n);
-            if (!(E::to_f((uint16_t)(qo.x & 0xffff)) > 0.f)) v[0] = 0.f;
-            if (!(E::to_f((uint16_t)(qo.x >> 16)) > 0.f)) v[1] = 0.f;
-            if (!(E::to_f((uint16_t)(qo.y & 0xffff)) > 0.f)) v[2] = 0.f;
-            if (!(E::to_f((uint16_t)(qo.y >> 16)) > 0.f)) v[3] = 0.f;
+            const uint32_t mb = (uint32_t)a.bn_mask[(obase + n) >> 3] >> (n & 4);
+            if (!(mb & 1u)) v[0] = 0.f;
+            if (!(mb & 2u)) v[1] = 0.f;
+            if (!(mb & 4u)) v[2] = 0.f;
+            if (!(mb & 8u)) v[3] = 0.f;
           }
           if constexpr (EPI == 4) {
             const uint2 q2 = *(const uint2*)(a.bn_y2 + obase + n);

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
     int64_t obase[4];
     bool pvalid[4];
     uint2 pre_res[RES ? 4 : 1][RES ? 4 : 1], pre_y1[EPI >= 2 ? 4 : 1][EPI >= 2 ? 4 : 1];
-    uint2 pre_out[EPI == 3 ? 4 : 1][EPI == 3 ? 4 : 1];
+    uint32_t pre_m[EPI == 3 ? 4 : 1][EPI == 3 ? 4 : 1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int px = (g0 + j) * 16 + pix_of_lane(fr);
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
         const int c0 = i * 16 + 4 * fq;
         if constexpr (RES) pre_res[j][i] = pvalid[j] ? *(const uint2*)(a.res + obase[j] + c0) : make_uint2(0, 0);
         if constexpr (EPI >= 2) pre_y1[j][i] = pvalid[j] ? *(const uint2*)(a.bn_y1 + obase[j] + c0) : make_uint2(0, 0);
-        if constexpr (EPI == 3) pre_out[j][i] = pvalid[j] ? *(const uint2*)(a.bn_out + obase[j] + c0) : make_uint2(0, 0);
+        if constexpr (EPI == 3) pre_m[j][i] = pvalid[j] ? (uint32_t)a.bn_mask[(obase[j] + c0) >> 3] >> (c0 & 4) : 0u;
       }
     }
 
@@ -232,11 +232,11 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint2 qo = pre_out[j][i];
-            if (!(E::to_f((uint16_t)(qo.x & 0xffff)) > 0.f)) v[0] = 0.f;
-            if (!(E::to_f((uint16_t)(qo.x >> 16)) > 0.f)) v[1] = 0.f;
-            if (!(E::to_f((uint16_t)(qo.y & 0xffff)) > 0.f)) v[2] = 0.f;
-            if (!(E::to_f((uint16_t)(qo.y >> 16)) > 0.f)) v[3] = 0.f;
+            const uint32_t mb = pre_m[j][i];
+            if (!(mb & 1u)) v[0] = 0.f;
+            if (!(mb & 2u)) v[1] = 0.f;
+            if (!(mb & 4u)) v[2] = 0.f;
+            if (!(mb & 8u)) v[3] = 0.f;
           }
         }
         uint16_t o[4];

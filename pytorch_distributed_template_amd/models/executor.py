@@ -275,7 +275,7 @@ class ResNetExecutor:
     def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None, bnb=None):
         """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``.
 
-        ``bnb`` = (mode, y1, coef1, y2, coef2, out, slots): fuse the consuming BatchNorm's backward
+        ``bnb`` = (mode, y1, coef1, y2, coef2, out_mask, slots): fuse the consuming BatchNorm's backward
         reduce into the data-gradient epilogue (``dx`` then holds dz = dx * relu'; see conv_fwd.h)."""
         # --- wgrad
         if wgrad_geom is None:
@@ -323,14 +323,14 @@ class ResNetExecutor:
                           win)
         self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, False)
 
-    def bn_bwd(self, bn1: _BN, y1, g, out, count: int, bn2: Optional[_BN] = None, y2=None):
+    def bn_bwd(self, bn1: _BN, y1, g, out_mask, count: int, bn2: Optional[_BN] = None, y2=None):
         """Reduce pass + finalize (dgamma/dbeta into grad buffer).  Returns nothing; coefficients in bcoef."""
         C = bn1.C
         rows = g.numel() // C
         blocks = self.C.bn_bwd_reduce_blocks(rows, C)
         K = 4 if bn2 is not None else 2
         slots = self._buf(("bnslots", C, K), self.n_slots * C * K, torch.float64)
-        self.C.bn_bwd_reduce(g, out, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows, C)
+        self.C.bn_bwd_reduce(g, out_mask, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows, C)
         self._bn_bwd_finish(slots, count, bn1, bn2)
 
     def _bn_bwd_finish(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None):
@@ -419,13 +419,15 @@ class ResNetExecutor:
                 rec["hw"].append((h, w, P, Q))
                 if ci < nconv - 1:
                     a = self._buf(("a", bi, ci), N * P * Q * c.cout)
-                    Cn.bn_apply(y, bn.coef, None, None, a, c.cout, 0, True)
+                    Cn.bn_apply(y, bn.coef, None, None, a, c.cout, 0, True, None)
                     rec["as"].append(a)
                     cur, h, w = a, P, Q
                 else:
                     h, w = P, Q
             cl, bnl = b["convs"][-1], b["bns"][-1]
             out = self._buf(("out", bi), N * h * w * cl.cout)
+            # backward reads the block output's ReLU as a bitmask (1 bit/element instead of 16)
+            om = self._buf(("omask", bi), N * h * w * cl.cout // 8, torch.uint8) if train else None
             if b["ds_conv"] is not None:
                 dc, dbn = b["ds_conv"], b["ds_bn"]
                 yd = self._buf(("yd", bi), N * h * w * dc.cout)
@@ -434,11 +436,11 @@ class ResNetExecutor:
                     self.bn_train_finalize(dbn, sp, tiles, N * h * w)
                 else:
                     self.bn_eval(dbn)
-                Cn.bn_apply(rec["ys"][-1], bnl.coef, yd, dbn.coef, out, cl.cout, 2, True)
+                Cn.bn_apply(rec["ys"][-1], bnl.coef, yd, dbn.coef, out, cl.cout, 2, True, om)
                 rec["yd"] = yd
             else:
-                Cn.bn_apply(rec["ys"][-1], bnl.coef, x, None, out, cl.cout, 1, True)
-            rec["out"] = out
+                Cn.bn_apply(rec["ys"][-1], bnl.coef, x, None, out, cl.cout, 1, True, om)
+            rec["out"], rec["omask"] = out, om
             blk_saved.append(rec)
             x, Hc, Wc, Cc = out, h, w, cl.cout
         # head: global average pool -> fc (1x1 GEMM over the padded class dimension)
@@ -513,8 +515,8 @@ class ResNetExecutor:
                 self._bn_bwd_finish(g_fused, cnt, bns[-1], dsbn)
                 mask_src = None
             else:
-                self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["out"], cnt, dsbn, rec["yd"] if ds else None)
-                mask_src = rec["out"]
+                self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["omask"], cnt, dsbn, rec["yd"] if ds else None)
+                mask_src = rec["omask"]
             dy_last = self._buf("dy_a", rec["ys"][-1].numel())
             if ds:
                 dyd = self._buf("dy_b", rec["yd"].numel())
@@ -526,7 +528,7 @@ class ResNetExecutor:
                                 convs[-1].cout)
             else:
                 dz = self._buf("dz_id", g.numel())
-                Cn.bn_bwd_apply(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy_last, None, None, None, dz,
+                Cn.bn_bwd_apply(g, rec["omask"], rec["ys"][-1], bns[-1].bcoef, dy_last, None, None, None, dz,
                                 convs[-1].cout)
             # gradient w.r.t. the block input accumulates in g_next
             gnext = self._buf("g_b" if gsel == 0 else "g_a", N * Hin * Win * Cin)
@@ -564,7 +566,7 @@ class ResNetExecutor:
                     K = 4 if pds else 2
                     slots = self._buf(("bnslots", c.cin, K), self.n_slots * c.cin * K, torch.float64)
                     bnb = (3 if pds else 2, prec["ys"][-1], pb["bns"][-1].coef, prec["yd"] if pds else None,
-                           pb["ds_bn"].coef if pds else None, prec["out"], slots)
+                           pb["ds_bn"].coef if pds else None, prec["omask"], slots)
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, bnb=bnb)
                     g_fused = slots
                 else:

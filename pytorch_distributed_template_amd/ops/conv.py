@@ -83,13 +83,22 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
     return y, (sums[:K], sums[K:])
 
 
+def pack_relu_mask(out: torch.Tensor) -> torch.Tensor:
+    """ReLU bitmask of a 16-bit activation: bit e of byte v is ``out.flatten()[8v + e] > 0`` (the layout
+    ``bn_apply(..., mask)`` writes and the backward kernels read)."""
+    bits = (out.reshape(-1, 8) > 0).to(torch.int32)
+    w = (1 << torch.arange(8, device=out.device, dtype=torch.int32))
+    return (bits * w).sum(1).to(torch.uint8)
+
+
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 1, pad: int = 0,
                residual: Optional[torch.Tensor] = None, bnb: Optional[tuple] = None,
                tile: Optional[Tuple[int, int, int]] = None) -> torch.Tensor:
     """dX (NHWC, [N, H, W, Cin]) of ``y = conv(x, w)`` given dY ([N, P, Q, Cout]).
 
-    ``bnb = (mode, y1, coef1, y2, coef2, out, slots)`` fuses the consuming BatchNorm's backward reduce
-    into the epilogue (the result is then dz = dX * relu'; sums land in ``slots``)."""
+    ``bnb = (mode, y1, coef1, y2, coef2, out_mask, slots)`` fuses the consuming BatchNorm's backward
+    reduce into the epilogue (the result is then dz = dX * relu'; sums land in ``slots``); ``out_mask`` is
+    the block output's ReLU bitmask (:func:`pack_relu_mask`, modes 2/3)."""
     N, P, Q, K = dy.shape
     K2, R, S, C = w.shape
     assert K == K2

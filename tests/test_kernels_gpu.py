@@ -320,7 +320,8 @@ def test_conv_dgrad_fused_bn_backward(case, mode):
     out = torch.relu(_rand16(N, H, W, C)).to(torch.bfloat16) if mode > 1 else None
     K_ = 4 if mode == 3 else 2
     slots = torch.zeros(native.C.stat_slots() * C * K_, dtype=torch.float64, device=DEV)
-    dz = conv.conv_dgrad(dy, w, H, W, st, pad, residual=res, bnb=(mode, y1, coef1, y2, coef2, out, slots))
+    om = conv.pack_relu_mask(out) if mode > 1 else None
+    dz = conv.conv_dgrad(dy, w, H, W, st, pad, residual=res, bnb=(mode, y1, coef1, y2, coef2, om, slots))
     if mode == 1:
         mask = (y1.float() * coef1[:C] + coef1[C:2 * C]) > 0
     else:
@@ -399,3 +400,38 @@ def test_stem_pack_u8_fused_normalize():
     native.C.stem_pack_u8(x8, out, N, 3, H, W, pad, Hp, Wp, scale, shift)
     assert (out.float() - ref.float()).abs().max().item() < 2e-2
     assert out.view(N, Hp, Wp, 4)[:, :, :, 3].abs().max().item() == 0  # 4th channel and padding stay zero
+
+
+@pytest.mark.parametrize("resmode", [1, 2])
+def test_bn_apply_relu_bitmask_and_masked_backward(resmode):
+    """bn_apply writes the block output's ReLU bitmask; bn_bwd_reduce / bn_bwd_apply mask with it."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    torch.manual_seed(5)
+    rows, C = 3000, 128
+    y = _rand16(rows, C)
+    res = _rand16(rows, C)
+    coef = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3,
+                      torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5]).contiguous()
+    rcoef = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3]).contiguous()
+    out = torch.empty_like(y)
+    mask = torch.empty(rows * C // 8, dtype=torch.uint8, device=DEV)
+    native.C.bn_apply(y, coef, res, rcoef if resmode == 2 else None, out, C, resmode, True, mask)
+    r = res.float() if resmode == 1 else res.float() * rcoef[:C] + rcoef[C:]
+    ref = torch.relu(y.float() * coef[:C] + coef[C:2 * C] + r)
+    assert _rel(out, ref) < 1e-2
+    assert torch.equal(mask, conv.pack_relu_mask(out))
+    g = _rand16(rows, C)
+    dz_ref = g.float() * (out.float() > 0)
+    slots = torch.zeros(native.C.stat_slots() * C * 2, dtype=torch.float64, device=DEV)
+    native.C.bn_bwd_reduce(g, mask, y, coef, None, None, slots, native.C.bn_bwd_reduce_blocks(rows, C), rows, C)
+    sums = slots.view(-1, C, 2).sum(0)
+    xhat = (y.float() - coef[2 * C:3 * C]) * coef[3 * C:]
+    assert torch.allclose(sums[:, 0], dz_ref.double().sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sums[:, 1], (dz_ref * xhat).double().sum(0), rtol=1e-3, atol=1e-2)
+    b1 = torch.randn(3 * C, device=DEV)
+    dy1 = torch.empty_like(y)
+    dz = torch.empty_like(y)
+    native.C.bn_bwd_apply(g, mask, y, b1, dy1, None, None, None, dz, C)
+    assert torch.equal(dz.float(), dz_ref.to(dz.dtype).float())
+    ref1 = b1[:C] * dz_ref + b1[C:2 * C] * y.float() + b1[2 * C:]
+    assert _rel(dy1, ref1) < 1e-2
