@@ -39,6 +39,169 @@ typedef __attribute__((address_space(1))) void glb_void;
 template <int CHUNKS>
 PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
+// Shared epilogue of the implicit-GEMM conv kernels: the wave's accumulators acc[i][j] hold output
+// channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m = m0 + wm*WM + j*16 + fr.
+template <int DT, int EPI, bool RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M>
+PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int64_t m0, int n0, int tile_m, int wn,
+                              int wm, int tid, int lane, char* smem) {
+  using E = E16<DT>;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int PQ = a.Pm * a.Qm;
+  const FastDiv fd_pq{a.pq_mul, a.pq_shift}, fd_q{a.q_mul, a.q_shift};
+  // ---- epilogue: lane holds channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
+  // EPI: 0 plain | 1 forward BN statistics (sum, sumsq of the rounded outputs) | 2..4 BN-backward
+  // reduce of the consumer BatchNorm fused into this (backward-data) conv: the output written is
+  // dz = v * relu'(.), and per channel sum(dz), sum(dz * xhat) accumulate (2: ReLU mask recomputed from
+  // the BN input y1 and its forward coefficients; 3: mask = (block output > 0); 4: as 3 plus a second
+  // BN branch y2 sharing dz, e.g. a residual block's downsample BN).
+  constexpr int KS = EPI == 0 ? 0 : (EPI == 4 ? 3 : 2);  // accumulated quantities per channel
+  float sacc[FN][4][KS > 0 ? KS : 1];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < (KS > 0 ? KS : 1); ++k) sacc[i][r][k] = 0.f;
+
+  // per-channel BN coefficients of the fused BN-backward epilogues, loaded once before any store (the
+  // stores could alias them as far as the compiler knows, which would force a reload per pixel)
+  float4 c_sc[EPI == 2 ? FN : 1], c_sh[EPI == 2 ? FN : 1], c_mu[EPI >= 2 ? FN : 1], c_is[EPI >= 2 ? FN : 1];
+
+  if constexpr (EPI >= 2) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * WN + i * 16 + 4 * fq;
+      if constexpr (EPI == 2) {
+        c_sc[i] = *(const float4*)(a.bn_coef1 + n);
+        c_sh[i] = *(const float4*)(a.bn_coef1 + a.Kout + n);
+      }
+      c_mu[i] = *(const float4*)(a.bn_coef1 + 2 * a.Kout + n);
+      c_is[i] = *(const float4*)(a.bn_coef1 + 3 * a.Kout + n);
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int64_t m = m0 + wm * WM + j * 16 + fr;
+    if (m < a.M) {
+      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
+      const int rem = (int)m - nimg * PQ;
+      const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
+      const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
+      const int64_t obase = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + 4 * fq;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (RES) {
+          const uint2 rr = *(const uint2*)(a.res + obase + n);
+          v[0] += E::to_f((uint16_t)(rr.x & 0xffff));
+          v[1] += E::to_f((uint16_t)(rr.x >> 16));
+          v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
+          v[3] += E::to_f((uint16_t)(rr.y >> 16));
+        }
+        float y1[4], y2[4];
+        if constexpr (EPI >= 2) {
+          const uint2 q1 = *(const uint2*)(a.bn_y1 + obase + n);
+          y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
+          y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
+          if constexpr (EPI == 2) {
+            const float4 sc = c_sc[i], sh = c_sh[i];
+            if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
+            if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
+            if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
+            if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
+          } else {
+            const uint32_t mb = (uint32_t)a.bn_mask[(obase + n) >> 3] >> (n & 4);
+            if (!(mb & 1u)) v[0] = 0.f;
+            if (!(mb & 2u)) v[1] = 0.f;
+            if (!(mb & 4u)) v[2] = 0.f;
+            if (!(mb & 8u)) v[3] = 0.f;
+          }
+          if constexpr (EPI == 4) {
+            const uint2 q2 = *(const uint2*)(a.bn_y2 + obase + n);
+            y2[0] = E::to_f((uint16_t)(q2.x & 0xffff)); y2[1] = E::to_f((uint16_t)(q2.x >> 16));
+            y2[2] = E::to_f((uint16_t)(q2.y & 0xffff)); y2[3] = E::to_f((uint16_t)(q2.y >> 16));
+          }
+        }
+        uint16_t o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = E::from_f(v[r]);
+        uint2 packed;
+        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        *(uint2*)(a.y + obase + n) = packed;
+        if constexpr (EPI == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float q = E::to_f(o[r]);
+            sacc[i][r][0] += q;
+            sacc[i][r][1] += q * q;
+          }
+        } else if constexpr (EPI >= 2) {
+          const float4 mu = c_mu[i], is = c_is[i];
+          const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float dz = E::to_f(o[r]);
+            sacc[i][r][0] += dz;
+            sacc[i][r][1] += dz * (y1[r] - m1[r]) * i1[r];
+          }
+          if constexpr (EPI == 4) {
+            const float4 mu2 = *(const float4*)(a.bn_coef2 + 2 * a.Kout + n);  // (not hoisted: registers)
+            const float4 is2 = *(const float4*)(a.bn_coef2 + 3 * a.Kout + n);
+            const float m2[4] = {mu2.x, mu2.y, mu2.z, mu2.w}, i2[4] = {is2.x, is2.y, is2.z, is2.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sacc[i][r][2] += E::to_f(o[r]) * (y2[r] - m2[r]) * i2[r];
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (KS > 0) {
+    // reduce over the 16 lanes (pixels) that share fq (DPP row scan: lane fr == 15 holds the total),
+    // then over the WAVES_M waves through LDS, then fp64 atomics into one of kStatSlots slot copies
+    // (by M tile: low per-address contention).  Slot layout [kStatSlots][Kout][KO].
+    constexpr int KO = EPI == 4 ? 4 : 2;  // stored quantities (EPI 4: sum dz is stored twice)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
+    float* red = (float*)smem;  // [WAVES_M][BN][KS]
+    __syncthreads();
+    if (fr == 15) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * WN + i * 16 + 4 * fq + r;
+#pragma unroll
+          for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
+        }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float t[KS];
+#pragma unroll
+      for (int k = 0; k < KS; ++k) t[k] = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) t[k] += red[(w * BN + tid) * KS + k];
+      double* dst = a.stats + ((int64_t)(tile_m % kStatSlots) * a.Kout + n0 + tid) * KO;
+      atomicAdd(dst, (double)t[0]);
+      atomicAdd(dst + 1, (double)t[1]);
+      if constexpr (EPI == 4) {
+        atomicAdd(dst + 2, (double)t[0]);
+        atomicAdd(dst + 3, (double)t[2]);
+      }
+    }
+  }
+}
+
 template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, bool RES, int STAGES, int NW>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
@@ -237,158 +400,267 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
     }
   }
 
-  // ---- epilogue: lane holds channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
-  // EPI: 0 plain | 1 forward BN statistics (sum, sumsq of the rounded outputs) | 2..4 BN-backward
-  // reduce of the consumer BatchNorm fused into this (backward-data) conv: the output written is
-  // dz = v * relu'(.), and per channel sum(dz), sum(dz * xhat) accumulate (2: ReLU mask recomputed from
-  // the BN input y1 and its forward coefficients; 3: mask = (block output > 0); 4: as 3 plus a second
-  // BN branch y2 sharing dz, e.g. a residual block's downsample BN).
-  constexpr int KS = EPI == 0 ? 0 : (EPI == 4 ? 3 : 2);  // accumulated quantities per channel
-  float sacc[FN][4][KS > 0 ? KS : 1];
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+}
+
+// ----------------------------------------------------------------------------------------------
+// "Ping-pong" implicit-GEMM conv: 8 waves, one workgroup per CU, BK = 64, two LDS buffers.
+//
+// The 2-stage kernel above waits vmcnt(0) + barrier every K-step; with its DMA in flight only for one
+// K-step the MFMA pipe idles whenever both waves of a SIMD wait at once (PMC: 42-46 % MFMA busy).
+// Here every K-step runs as 4 phases, each a LOAD segment (LDS fragment reads + the next DMA piece)
+// and a COMPUTE segment (16 MFMAs) separated by workgroup barriers, and waves 4-7 start one barrier
+// late, so on every SIMD one wave computes while its partner loads.  The DMA of K-step k+1 is issued
+// in four pieces during K-step k and waited with COUNTED vmcnt (never 0 in the loop), each piece
+// having 2-4 phases to land.
+//
+// Geometry: tile BM pixels x BN output channels; each wave owns 128 pixels x 64 channels (8 x 4
+// MFMA 16x16 fragments, 128 fp32 accumulators per lane).  BN = 256: waves 2 (px) x 4 (ch), 64 KB per
+// LDS buffer; BN = 128: BM = 512, waves 4 x 2, 80 KB per buffer (2 x 80 KB = the whole 160 KB LDS).
+// The operand images are split in halves: X half h holds, for every pixel group g of 128, pixels
+// g*128 + h*64 .. +64; W half h holds channels g*64 + h*32 .. +32.  Phase p reads (X half, W half):
+//   p1: X0 (8 b128) + W0 (4)   compute X0 x W0
+//   p2: W1 (4)                 compute X0 x W1
+//   p3: X1 (8)                 compute X1 x W1
+//   p4: -                      compute X1 x W0
+// and issues the DMA of the next K-step's X0, W0, W1, X1 (in that order).  A half is refilled four
+// phases after its last read (WAR safe for both wave groups) and read 3-4 phases after its DMA
+// (RAW: each wave waits for its own pieces with a counted vmcnt before a barrier the readers pass).
+template <int N>
+PDT_DEVICE void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <int DT, int BM, int BN, int EPI, bool RES>
+__global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
+  ConvFwdArgs a = args;
+  if (args.nphase > 0) {  // multi-phase launch (strided backward-data): this block's phase geometry
+    const int ph = blockIdx.y;
+    a.T = args.pT[ph]; a.U = args.pU[ph];
+    a.ioff_h = args.pioff_h[ph]; a.ioff_w = args.pioff_w[ph];
+    a.Pm = args.pPm[ph]; a.Qm = args.pQm[ph];
+    a.ooff_h = args.pooff_h[ph]; a.ooff_w = args.pooff_w[ph];
+    a.m_tiles = args.pmt[ph];
+    a.M = (int64_t)a.N * a.Pm * a.Qm;
+    a.w = args.w + args.pwoff[ph];
+    a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
+    a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
+    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
+  }
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int NW = 8, WN = 64, WM = 128;
+  constexpr int WAVES_N = BN / WN, WAVES_M = NW / WAVES_N;
+  static_assert(WAVES_N * WAVES_M == NW && WAVES_M * WM == BM, "pp tile geometry");
+  constexpr int FN = 4, FM = 8;           // channel / pixel fragments per wave
+  constexpr int ROWB = 128;               // 64 16-bit elements per LDS row
+  constexpr int XH = (BM / 2) * ROWB;     // bytes of one X half
+  constexpr int WH = (BN / 2) * ROWB;     // bytes of one W half
+  constexpr int NX = XH / 1024 / NW;      // DMA instructions per wave per X half
+  constexpr int NWI = WH / 1024 / NW;     // ... per W half
+  static_assert(NX * 1024 * NW == XH && NWI * 1024 * NW == WH, "pp DMA split");
+  constexpr int BUF = 2 * XH + 2 * WH;
+  constexpr int OX0 = 0, OX1 = XH, OW0 = 2 * XH, OW1 = 2 * XH + WH;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;  // waves w and w+4 share a SIMD: they run one barrier apart
+  const int wn = wave % WAVES_N, wm = wave / WAVES_N;
+
+  const int nwg = a.m_tiles * a.n_tiles;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile_m = bid / a.n_tiles, tile_n = bid % a.n_tiles;
+  const int64_t m0 = (int64_t)tile_m * BM;
+  const int n0 = tile_n * BN;
+
+  const int PQ = a.Pm * a.Qm;
+  const FastDiv fd_pq{a.pq_mul, a.pq_shift}, fd_q{a.q_mul, a.q_shift};
+  const int TU = a.T * a.U;
+  const int csteps = a.C >> 6;
+  const int ksteps = TU * csteps;
+
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)a.Kout * TU * a.C * 2u);
+
+  // DMA lane geometry: 8 rows x 8 chunks of 16 B per 1 KiB instruction; the source chunk is XOR
+  // swizzled by the LDS row so the ds_read_b128 fragment reads are conflict free
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  // X rows: packed (h << 16 | w & 0xffff) input position and byte offset, per half and instruction
+  int xhw[2][NX], xoff[2][NX];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int hr = (wave * NX + j) * 8 + lrow;  // row of the half image
+      const int64_t m = m0 + (hr >> 6) * 128 + h * 64 + (hr & 63);
+      const int bch = pchunk ^ ((hr >> 1) & 7);
+      if (m < a.M) {
+        const int nimg = (int)fdiv((uint32_t)m, fd_pq);
+        const int rem = (int)m - nimg * PQ;
+        const int i = (int)fdiv((uint32_t)rem, fd_q), jj = rem - i * a.Qm;
+        const int ih = i * a.ist_h + a.ioff_h, iw = jj * a.ist_w + a.ioff_w;
+        xhw[h][j] = (ih << 16) | (iw & 0xffff);
+        xoff[h][j] = (((nimg * a.H + ih) * a.W + iw) * a.cs + bch * 8) * 2;
+      } else {
+        xhw[h][j] = (int)0xC0000000;  // h = -16384: always out of range
+        xoff[h][j] = 0;
+      }
+    }
+  uint32_t woff[2][NWI];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < NWI; ++j) {
+      const int hr = (wave * NWI + j) * 8 + lrow;
+      const int n = n0 + (hr >> 5) * 64 + h * 32 + (hr & 31);
+      woff[h][j] = (uint32_t)((n * TU * a.C + (pchunk ^ ((hr >> 1) & 7)) * 8) * 2);
+    }
+
+  // K-step cursor (tap, channel block) of the K-step whose DMA is being issued
+  int cur_t = 0, cur_u = 0, cur_c = 0;
+  uint32_t s_adelta = 0;
+  int s_dh = 0, s_dw = 0, s_bdelta = 0;
+  auto advance = [&]() {  // latch the cursor's K-step deltas, then step the cursor
+    s_adelta = (uint32_t)((cur_t * a.U + cur_u) * a.C + cur_c) * 2u;
+    s_dh = cur_t * a.tstep_h;
+    s_dw = cur_u * a.tstep_w;
+    s_bdelta = ((s_dh * a.W + s_dw) * a.cs + cur_c) * 2;
+    cur_c += 64;
+    if (cur_c == a.C) {
+      cur_c = 0;
+      if (++cur_u == a.U) { cur_u = 0; ++cur_t; }
+    }
+  };
+  auto dma_x = [&](char* buf, int h) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int ih = (xhw[h][j] >> 16) + s_dh, iw = (int)(short)(xhw[h][j] & 0xffff) + s_dw;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      buf_lds16(rx, buf + (h ? OX1 : OX0) + (wave * NX + j) * 1024, ok ? (uint32_t)(xoff[h][j] + s_bdelta) : kOOB);
+    }
+  };
+  auto dma_w = [&](char* buf, int h) {
+#pragma unroll
+    for (int j = 0; j < NWI; ++j)
+      buf_lds16(rw, buf + (h ? OW1 : OW0) + (wave * NWI + j) * 1024, woff[h][j] + s_adelta);
+  };
+
+  f32x4_t acc[FN][FM];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int k = 0; k < (KS > 0 ? KS : 1); ++k) sacc[i][r][k] = 0.f;
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // per-channel BN coefficients of the fused BN-backward epilogues, loaded once before any store (the
-  // stores could alias them as far as the compiler knows, which would force a reload per pixel)
-  float4 c_sc[EPI == 2 ? FN : 1], c_sh[EPI == 2 ? FN : 1], c_mu[EPI >= 2 ? FN : 1], c_is[EPI >= 2 ? FN : 1];
-
-  if constexpr (EPI >= 2) {
+  const int fr = lane & 15, fq = lane >> 4;
+  // fragment rows within the half images (the swizzle depends on the row only through bits 1..3,
+  // which fr determines: every fragment base is a multiple of 16)
+  const int xrow0 = wm * 64 + fr, wrow0 = wn * 32 + fr;
+  const int sw = (fr >> 1) & 7;
+  vec8 xs[4][2], w0r[2][2], w1r[2][2];
+  auto read_x = [&](const char* base) {
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int n = n0 + wn * WN + i * 16 + 4 * fq;
-      if constexpr (EPI == 2) {
-        c_sc[i] = *(const float4*)(a.bn_coef1 + n);
-        c_sh[i] = *(const float4*)(a.bn_coef1 + a.Kout + n);
-      }
-      c_mu[i] = *(const float4*)(a.bn_coef1 + 2 * a.Kout + n);
-      c_is[i] = *(const float4*)(a.bn_coef1 + 3 * a.Kout + n);
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        xs[f][kk] = *(const vec8*)(base + (xrow0 + f * 16) * ROWB + (((kk * 4 + fq) ^ sw) << 4));
+  };
+  auto read_w = [&](vec8 (&wr)[2][2], const char* base) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        wr[f][kk] = *(const vec8*)(base + (wrow0 + f * 16) * ROWB + (((kk * 4 + fq) ^ sw) << 4));
+  };
+  auto mma = [&](const vec8 (&wr)[2][2], int xh, int wh) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f2 = 0; f2 < 2; ++f2)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          acc[wh * 2 + f2][xh * 4 + f] = E::mfma16x16x32(wr[f2][kk], xs[f][kk], acc[wh * 2 + f2][xh * 4 + f]);
+  };
+  auto compute = [&](const vec8 (&wr)[2][2], int xh, int wh) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mma(wr, xh, wh);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (ksteps > 0) {
+    // prologue: all of K-step 0, then wait for its X0 / W0 (W1 and X1 may still fly)
+    advance();
+    dma_x(smem, 0);
+    dma_w(smem, 0);
+    dma_w(smem, 1);
+    dma_x(smem, 1);
+    vm_wait<NWI + NX>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const char* cb = smem + (ks & 1) * BUF;
+      char* nb = smem + ((ks + 1) & 1) * BUF;
+      const bool more = ks + 1 < ksteps;
+      if (more) advance();
+      // phase 1: DMA X0(k+1); wait W1(k); read X0, W0; compute X0 x W0
+      if (more) { dma_x(nb, 0); vm_wait<2 * NX>(); } else { vm_wait<NX>(); }
+      read_x(cb + OX0);
+      read_w(w0r, cb + OW0);
+      compute(w0r, 0, 0);
+      // phase 2: DMA W0(k+1); wait X1(k); read W1; compute X0 x W1
+      if (more) { dma_w(nb, 0); vm_wait<NX + NWI>(); } else { vm_wait<0>(); }
+      read_w(w1r, cb + OW1);
+      compute(w1r, 0, 1);
+      // phase 3: DMA W1(k+1); read X1; compute X1 x W1
+      if (more) dma_w(nb, 1);
+      read_x(cb + OX1);
+      compute(w1r, 1, 1);
+      // phase 4: DMA X1(k+1); wait X0(k+1), W0(k+1); compute X1 x W0
+      if (more) { dma_x(nb, 1); vm_wait<NWI + NX>(); }
+      compute(w0r, 1, 0);
     }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave groups
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 
-#pragma unroll
-  for (int j = 0; j < FM; ++j) {
-    const int64_t m = m0 + wm * WM + j * 16 + fr;
-    if (m < a.M) {
-      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
-      const int rem = (int)m - nimg * PQ;
-      const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
-      const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
-      const int64_t obase = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
-#pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + 4 * fq;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (RES) {
-          const uint2 rr = *(const uint2*)(a.res + obase + n);
-          v[0] += E::to_f((uint16_t)(rr.x & 0xffff));
-          v[1] += E::to_f((uint16_t)(rr.x >> 16));
-          v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
-          v[3] += E::to_f((uint16_t)(rr.y >> 16));
-        }
-        float y1[4], y2[4];
-        if constexpr (EPI >= 2) {
-          const uint2 q1 = *(const uint2*)(a.bn_y1 + obase + n);
-          y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
-          y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
-          if constexpr (EPI == 2) {
-            const float4 sc = c_sc[i], sh = c_sh[i];
-            if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
-            if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
-            if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
-            if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
-          } else {
-            const uint32_t mb = (uint32_t)a.bn_mask[(obase + n) >> 3] >> (n & 4);
-            if (!(mb & 1u)) v[0] = 0.f;
-            if (!(mb & 2u)) v[1] = 0.f;
-            if (!(mb & 4u)) v[2] = 0.f;
-            if (!(mb & 8u)) v[3] = 0.f;
-          }
-          if constexpr (EPI == 4) {
-            const uint2 q2 = *(const uint2*)(a.bn_y2 + obase + n);
-            y2[0] = E::to_f((uint16_t)(q2.x & 0xffff)); y2[1] = E::to_f((uint16_t)(q2.x >> 16));
-            y2[2] = E::to_f((uint16_t)(q2.y & 0xffff)); y2[3] = E::to_f((uint16_t)(q2.y >> 16));
-          }
-        }
-        uint16_t o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = E::from_f(v[r]);
-        uint2 packed;
-        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-        *(uint2*)(a.y + obase + n) = packed;
-        if constexpr (EPI == 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float q = E::to_f(o[r]);
-            sacc[i][r][0] += q;
-            sacc[i][r][1] += q * q;
-          }
-        } else if constexpr (EPI >= 2) {
-          const float4 mu = c_mu[i], is = c_is[i];
-          const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float dz = E::to_f(o[r]);
-            sacc[i][r][0] += dz;
-            sacc[i][r][1] += dz * (y1[r] - m1[r]) * i1[r];
-          }
-          if constexpr (EPI == 4) {
-            const float4 mu2 = *(const float4*)(a.bn_coef2 + 2 * a.Kout + n);  // (not hoisted: registers)
-            const float4 is2 = *(const float4*)(a.bn_coef2 + 3 * a.Kout + n);
-            const float m2[4] = {mu2.x, mu2.y, mu2.z, mu2.w}, i2[4] = {is2.x, is2.y, is2.z, is2.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sacc[i][r][2] += E::to_f(o[r]) * (y2[r] - m2[r]) * i2[r];
-          }
-        }
-      }
-    }
-  }
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+}
 
-  if constexpr (KS > 0) {
-    // reduce over the 16 lanes (pixels) that share fq (DPP row scan: lane fr == 15 holds the total),
-    // then over the WAVES_M waves through LDS, then fp64 atomics into one of kStatSlots slot copies
-    // (by M tile: low per-address contention).  Slot layout [kStatSlots][Kout][KO].
-    constexpr int KO = EPI == 4 ? 4 : 2;  // stored quantities (EPI 4: sum dz is stored twice)
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
-    float* red = (float*)smem;  // [WAVES_M][BN][KS]
-    __syncthreads();
-    if (fr == 15) {
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int nl = wn * WN + i * 16 + 4 * fq + r;
-#pragma unroll
-          for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
-        }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float t[KS];
-#pragma unroll
-      for (int k = 0; k < KS; ++k) t[k] = 0.f;
-#pragma unroll
-      for (int w = 0; w < WAVES_M; ++w)
-#pragma unroll
-        for (int k = 0; k < KS; ++k) t[k] += red[(w * BN + tid) * KS + k];
-      double* dst = a.stats + ((int64_t)(tile_m % kStatSlots) * a.Kout + n0 + tid) * KO;
-      atomicAdd(dst, (double)t[0]);
-      atomicAdd(dst + 1, (double)t[1]);
-      if constexpr (EPI == 4) {
-        atomicAdd(dst + 2, (double)t[0]);
-        atomicAdd(dst + 3, (double)t[2]);
-      }
-    }
+template <int DT, int BM, int BN>
+static void launch_pp(const ConvFwdArgs& a, hipStream_t s) {
+  int gx = a.m_tiles * a.n_tiles;
+  if (a.nphase > 0) {
+    gx = 0;
+    for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
   }
+  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(512);
+  const bool rs = a.res != nullptr;
+  const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
+#define PDT_K(E_, R_) hipLaunchKernelGGL((conv_pp_kernel<DT, BM, BN, E_, R_>), grid, block, 0, s, a)
+  if (epi == 0) {
+    if (rs) PDT_K(0, true); else PDT_K(0, false);
+  } else if (epi == 1) {
+    if (rs) PDT_K(1, true); else PDT_K(1, false);
+  } else if (epi == 2 && !rs) {
+    PDT_K(2, false);
+  } else if (epi == 3 && rs) {
+    PDT_K(3, true);
+  } else if (epi == 4 && rs) {
+    PDT_K(4, true);
+  } else {
+    pdt_hip_fail("conv_pp: unsupported epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
+  }
+#undef PDT_K
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -467,6 +739,8 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   PDT_CFG(256, 64, 32, 1, 3)
   PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
+  if (bk == 64 && bm == 256 && bn == 256 && a.C % 64 == 0) { launch_pp<DT, 256, 256>(a, s); return; }
+  if (bk == 64 && bm == 512 && bn == 128 && a.C % 64 == 0) { launch_pp<DT, 512, 128>(a, s); return; }
   PDT_CFGN(256, 128, 64, 2, 2, 8)  // 8 waves (4 x 2 of 64 x 64), 96 KB LDS: 25% less L2->LDS traffic per FLOP
   PDT_CFGN(256, 256, 32, 4, 4, 8)  // 8 waves (2 x 4 of 128 x 64), 4-stage BK=32 ring (128 KB), 2 steps in flight
 #undef PDT_CFG

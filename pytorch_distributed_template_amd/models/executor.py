@@ -225,22 +225,22 @@ class ResNetExecutor:
         def launch(bm, bn):
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
                             -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
-        bm, bn = self._tile(("fwd", N, H, W, cin, c.cout, R, S, st, stats), c.cout, bk, launch)
+        bm, bn = self._tile(("fwd", N, H, W, cin, c.cout, R, S, st, stats), c.cout, bk, launch, kdim=cin * R * S)
         launch(bm, bn)
         return P, Q, sp, M
 
     # per-shape tile choice: the static table (ops.conv.conv_tile), or -- with autotune on, the analogue of
     # the reference's cudnn.benchmark=True (`distributed.py:104`) -- the fastest candidate timed once per shape
-    _CANDIDATES = ((128, 128), (256, 64), (128, 64), (64, 128), (256, 128))
+    _CANDIDATES = ((128, 128), (256, 64), (128, 64), (64, 128), (256, 128), (256, 256), (512, 128))
 
-    def _tile(self, key, n_dim, bk, launch, fused_epilogue: bool = False):
+    def _tile(self, key, n_dim, bk, launch, fused_epilogue: bool = False, kdim: int = 0):
         hit = self._tiles.get(key)
         if hit is not None:
             return hit
-        choice = _conv_tile(n_dim)
+        choice = _conv_tile(n_dim, kdim if bk == 64 else 0)
         if self.autotune and bk == 64:
             cands = [(bm, bn) for bm, bn in self._CANDIDATES if n_dim % bn == 0 and
-                     (not fused_epilogue or bm * bn in (16384, 32768))]
+                     (not fused_epilogue or bm * bn in (16384, 32768, 65536))]
             best = None
             for bm, bn in cands:
                 launch(bm, bn)  # warm
@@ -298,7 +298,7 @@ class ResNetExecutor:
                 self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn,
                                      bk, *bnb)
         key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, c.st, res is not None, bnb[0] if bnb else 0)
-        bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None)
+        bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
         launch(bm, bn)
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,

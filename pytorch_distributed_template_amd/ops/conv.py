@@ -19,8 +19,16 @@ import torch
 from . import native
 
 
-def conv_tile(cout: int) -> Tuple[int, int]:
-    """(BM, BN) tile of the implicit-GEMM kernel for a given GEMM-N (output channels)."""
+def conv_tile(cout: int, kdim: int = 0) -> Tuple[int, int]:
+    """(BM, BN) tile of the implicit-GEMM kernel for a given GEMM-N (output channels) and GEMM-K
+    (reduction length ``Cin*R*S``; 0 = unknown).
+
+    Long reductions over >= 256 channels go to the 8-wave ping-pong kernel (256x256, one workgroup per
+    CU, counted-vmcnt DMA pipeline: +10-25 % over the 2-stage 128x128 kernel on ResNet layer3/4 shapes,
+    tools/conv_bench.py); short ones (1x1 convs: 1-4 K-steps) stay on the 2-stage kernel, whose
+    prologue/epilogue is cheaper."""
+    if cout % 256 == 0 and kdim >= 512 and kdim % 64 == 0:
+        return 256, 256
     if cout % 128 == 0:
         return 128, 128
     return 256, 64
@@ -67,7 +75,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
     assert C == C2
     P, Q = out_hw(H, W, R, S, stride, pad)
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
-    bm, bn = conv_tile(K)
+    bm, bn = conv_tile(K, C * R * S)
     bk = 64 if C % 64 == 0 else 32
     if tile is not None:
         bm, bn, bk = tile
@@ -103,7 +111,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
     K2, R, S, C = w.shape
     assert K == K2
     dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
-    bm, bn = conv_tile(C)
+    bm, bn = conv_tile(C, K * R * S)
     bk = 64 if K % 64 == 0 else 32
     if tile is not None:
         bm, bn, bk = tile

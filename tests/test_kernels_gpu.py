@@ -357,7 +357,8 @@ def test_wgrad_3x3c64_all_taps():
 
 
 TILES = [(128, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64), (256, 128, 64), (256, 256, 32),
-         (128, 128, 32), (256, 64, 32), (128, 64, 32)]
+         (128, 128, 32), (256, 64, 32), (128, 64, 32), (256, 256, 64), (512, 128, 64)]
+PP_TILES = [(256, 256, 64), (512, 128, 64)]  # 8-wave ping-pong kernel (conv_pp_kernel)
 
 
 @pytest.mark.parametrize("tile", TILES)
@@ -435,3 +436,52 @@ def test_bn_apply_relu_bitmask_and_masked_backward(resmode):
     assert torch.equal(dz.float(), dz_ref.to(dz.dtype).float())
     ref1 = b1[:C] * dz_ref + b1[C:2 * C] * y.float() + b1[2 * C:]
     assert _rel(dy1, ref1) < 1e-2
+
+
+@pytest.mark.parametrize("tile", PP_TILES)
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_conv_pp_long_k_and_fused_bn_backward(tile, mode):
+    """Ping-pong kernel over many K-steps and several (partial) M tiles: forward with stats, and
+    backward-data with every fused BN-backward epilogue (mode 0 = plain dgrad with residual)."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    N, H, W, C, K = 5, 14, 14, 256, 256
+    torch.manual_seed(21 + mode)
+    x = _rand16(N, H, W, C)
+    w = _rand16(K, 3, 3, C, scale=(1.0 / (C * 9)) ** 0.5)
+    y, (s, ss) = conv.conv_fwd(x, w, 1, 1, stats=True, tile=tile)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2
+    yf = y.float().reshape(-1, K)
+    assert torch.allclose(s.float(), yf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(ss.float(), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+    dy = _rand16(N, H, W, K)
+    res = _rand16(N, H, W, C) if mode != 1 else None
+    plain = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                       padding=1).permute(0, 2, 3, 1)
+    if res is not None:
+        plain = plain + res.float()
+    if mode == 0:
+        dx = conv.conv_dgrad(dy, w, H, W, 1, 1, residual=res, tile=tile)
+        assert _rel(dx, plain) < 1e-2
+        return
+    y1 = _rand16(N, H, W, C)
+    yf1 = y1.float().view(-1, C)
+    m1, i1 = yf1.mean(0), torch.rsqrt(yf1.var(0, unbiased=False) + 1e-5)
+    coef1 = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3, m1, i1]).contiguous()
+    y2 = _rand16(N, H, W, C) if mode == 3 else None
+    coef2 = coef1 if mode == 3 else None
+    out = torch.relu(_rand16(N, H, W, C)) if mode > 1 else None
+    om = conv.pack_relu_mask(out) if mode > 1 else None
+    K_ = 4 if mode == 3 else 2
+    slots = torch.zeros(native.C.stat_slots() * C * K_, dtype=torch.float64, device=DEV)
+    dz = conv.conv_dgrad(dy, w, H, W, 1, 1, residual=res, bnb=(mode, y1, coef1, y2, coef2, om, slots), tile=tile)
+    mask = ((y1.float() * coef1[:C] + coef1[C:2 * C]) > 0) if mode == 1 else (out.float() > 0)
+    assert _rel(dz, plain * mask) < 1e-2
+    sums = slots.view(-1, C, K_).sum(0)
+    dzf = dz.float().view(-1, C).double()
+    x1 = ((y1.float() - m1) * i1).view(-1, C).double()
+    assert torch.allclose(sums[:, 0], dzf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sums[:, 1], (dzf * x1).sum(0), rtol=1e-3, atol=1e-2)
+    if mode == 3:
+        x2 = ((y2.float() - m1) * i1).view(-1, C).double()
+        assert torch.allclose(sums[:, 3], (dzf * x2).sum(0), rtol=1e-3, atol=1e-2)

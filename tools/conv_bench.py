@@ -20,7 +20,7 @@ SHAPES = [  # H, Cin, Cout, k, stride
     (28, 128, 256, 3, 2), (14, 256, 256, 3, 1), (28, 128, 256, 1, 2), (14, 256, 512, 3, 2),
     (7, 512, 512, 3, 1), (14, 256, 512, 1, 2),
 ]
-FWD_TILES = [(128, 128, 64), (256, 256, 32), (256, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64),
+FWD_TILES = [(256, 256, 64), (512, 128, 64), (128, 128, 64), (256, 256, 32), (256, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64),
              (256, 64, 32), (128, 128, 32)]
 
 
@@ -112,9 +112,10 @@ def main():
             phases.append([ph, pw, len(rs), len(ss), ih, iw, off])
             off += idx.numel()
         wt = torch.cat(pieces).contiguous()
-        bm, bn = conv.conv_tile(ci)
-        row["dgrad"] = round(flops / timeit(lambda: C.conv_dgrad(dy, wt, dx, None, N, P, P, co, ci, H, H, st, phases,
-                                                                 bm, bn, 64), a.reps) / 1e9, 1)
+        dts = [conv.conv_tile(ci)] + [t for t in ((256, 256), (512, 128), (128, 128)) if ci % t[1] == 0]
+        for bm, bn in dict.fromkeys(dts):
+            row[f"dgrad_{bm}x{bn}"] = round(flops / timeit(lambda: C.conv_dgrad(dy, wt, dx, None, N, P, P, co, ci, H, H,
+                                                                           st, phases, bm, bn, 64), a.reps) / 1e9, 1)
         if C.wgrad_3x3c64_supported(ci, co, k, k, H, st, pad):
             blocks = C.wgrad_blocks_3x3c64()
             ws = torch.empty(blocks * 64 * 576, device=dev)
