@@ -27,6 +27,12 @@
 namespace pdt_comm {
 void register_comm(pybind11::module& m);  // csrc/comm.cpp
 }
+namespace pdt_store {
+void register_store(pybind11::module& m);  // csrc/store.cpp
+}
+namespace pdt_dp {
+void register_dp(pybind11::module& m);  // csrc/dp_group.cpp
+}
 
 void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line) {
   char buf[512];
@@ -558,6 +564,8 @@ void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pdt_comm::register_comm(m);
+  pdt_store::register_store(m);
+  pdt_dp::register_dp(m);
   m.doc() = "gfx950 (MI355X) HIP kernels of pytorch_distributed_template_amd";
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_m_tiles", &conv_m_tiles);

@@ -96,7 +96,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         cmd = [hipcc] + hip_flags + ["-c", src, "-o", obj]
         jobs_list.append((src, obj, cmd, hashlib.sha1((" ".join(cmd) + hdr).encode()).hexdigest()))
-    for name in ("bindings.cpp", "comm.cpp"):  # host C++: op bindings; RCCL communicator + bucketer
+    # host C++: op bindings; RCCL communicator + bucketer; TCP rendezvous store; single-process DP group
+    for name in ("bindings.cpp", "comm.cpp", "store.cpp", "dp_group.cpp"):
         bsrc = os.path.join(CSRC, name)
         bobj = os.path.join(BUILD, name.replace(".cpp", ".o"))
         bcmd = [cxx] + cxx_flags + ["-c", bsrc, "-o", bobj]

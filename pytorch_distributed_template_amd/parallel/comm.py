@@ -11,12 +11,14 @@ X1-X9; `distributed.py:124,144`).
 from __future__ import annotations
 
 import itertools
+import os
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..ops import native
+from .store import NativeStore
 
 _COUNTER = itertools.count()
 
@@ -24,13 +26,21 @@ _COUNTER = itertools.count()
 class NativeComm:
     """A process-group-like wrapper over :class:`_C.Communicator`."""
 
-    def __init__(self, device: torch.device, process_group=None):
+    def __init__(self, device: torch.device, process_group=None, store=None):
+        """The RCCL unique id travels through ``store``: c10d's store when torch.distributed is up,
+        otherwise (or when given) our native TCP store (:class:`~.store.NativeStore`, env://)."""
         self.device = torch.device(device)
-        if dist.is_initialized():
-            self.rank = dist.get_rank(process_group)
-            self.world = dist.get_world_size(process_group)
+        key = f"pdt_rccl_uid_{next(_COUNTER)}"
+        if store is None and dist.is_initialized():
             store = dist.distributed_c10d._get_default_store()
-            key = f"pdt_rccl_uid_{next(_COUNTER)}"
+        elif store is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            store = NativeStore.from_env()
+        if store is not None:
+            if isinstance(store, NativeStore):
+                self.rank, self.world = store.rank, store.world
+            else:
+                self.rank = dist.get_rank(process_group)
+                self.world = dist.get_world_size(process_group)
             if self.rank == 0:
                 uid = native.C.rccl_unique_id()
                 store.set(key, uid)
@@ -39,6 +49,7 @@ class NativeComm:
         else:
             self.rank, self.world = 0, 1
             uid = native.C.rccl_unique_id()
+        self.store = store
         self.comm = native.C.Communicator(bytes(uid), self.world, self.rank, self.device.index or 0)
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> None:

@@ -9,10 +9,12 @@ Reference semantics (``nn.DataParallel``) kept here:
 * BatchNorm running statistics come from GPU 0's replica only (other replicas' updates are discarded).
 
 MI355X-native mechanics: replicas are :class:`ResNetExecutor` instances (one per device, each with
-its own 16-bit weight shadow), the weight broadcast moves the 16-bit shadow (half the bytes of the
-fp32 parameters) with ``torch.cuda.comm.broadcast_coalesced`` (RCCL), gradients are reduced with
-``torch.cuda.comm.reduce_add_coalesced`` (RCCL) into GPU 0's flat gradient buffer, and all devices run
-concurrently because every launch is asynchronous on its device's stream.
+its own 16-bit weight shadow).  Collectives go through our single-process RCCL device group
+(csrc/dp_group.cpp: ``ncclCommInitAll`` over the visible GPUs, one grouped call per collective on each
+device's current stream): the per-forward weight broadcast moves the 16-bit shadow (half the bytes of
+the fp32 parameters) and the BN buffers from GPU 0 over xGMI, and gradients are reduce-added in place
+into GPU 0's flat gradient buffer.  All devices run concurrently because every launch is asynchronous on
+its device's stream; no host synchronisation is needed anywhere in the step.
 """
 from __future__ import annotations
 
@@ -20,7 +22,6 @@ import copy
 from typing import List
 
 import torch
-import torch.cuda.comm as comm
 
 from ..amp.scaler import DeviceGradScaler
 from ..models.executor import ResNetExecutor
@@ -50,14 +51,18 @@ class NativeDataParallelTrainer:
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executors[0].update_derived)
         self.scaler = DeviceGradScaler(self.devices[0], enabled=use_amp and dtype == torch.float16)
+        self.group = None
+        if len(self.devices) > 1:
+            from ..ops import native
+            self.group = native.C.DeviceGroup(self.device_ids)
 
     def _replicate(self) -> None:
         if len(self.devices) == 1:
             return
-        outs = comm.broadcast_coalesced([self.flat.shadow, self.buffers[0].fdata], self.devices)
+        self.group.broadcast([f.shadow for f in self.flats], 0)
+        if self.buffers[0].n_float:
+            self.group.broadcast([b.fdata for b in self.buffers], 0)
         for i in range(1, len(self.devices)):
-            self.flats[i].shadow.copy_(outs[i][0])
-            self.buffers[i].fdata.copy_(outs[i][1])
             with torch.cuda.device(self.devices[i]):
                 self.executors[i].update_derived()
 
@@ -85,9 +90,8 @@ class NativeDataParallelTrainer:
                 logits, met = ex.train_step(x, t, loss_scale=ls, grad_div=float(B))
             outs.append(logits)
             mets.append(met.to(self.devices[0]) * (x.shape[0] / B))
-        if len(self.devices) > 1:
-            summed = comm.reduce_add_coalesced([f.grad for f in self.flats], destination=self.device_ids[0])
-            self.flat.grad.copy_(summed[0])
+        if self.group is not None:
+            self.group.reduce([f.grad for f in self.flats], 0)  # in place into GPU 0's flat gradient
         self.scaler.unscale_check(self.flat.grad)
         self.optimizer.step(grad_scale=1.0, loss_scale=scale, found_inf=self.scaler.found_inf)
         self.scaler.update()

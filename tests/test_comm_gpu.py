@@ -83,3 +83,40 @@ def test_graphed_training_step_matches_eager():
     assert len(tg._graphs) == 2 and tg.optimizer.step_count == te.optimizer.step_count == 6
     assert torch.allclose(mg, me, rtol=1e-3, atol=1e-3)
     assert ((tg.flat.data - te.flat.data).norm() / te.flat.data.norm()).item() < 1e-4
+
+
+def test_device_group_single_process_collectives():
+    """Single-process DP collectives (csrc/dp_group.cpp, ncclCommInitAll) on the visible device(s):
+    broadcast from the root, in-place reduce-add into the root, all-reduce; ordered on the current
+    stream behind earlier compute without host synchronisation."""
+    from pytorch_distributed_template_amd.ops import native
+    n = torch.cuda.device_count()
+    g = native.C.DeviceGroup(list(range(n)))
+    assert g.size == n
+    xs = []
+    for d in range(n):
+        with torch.cuda.device(d):
+            xs.append(torch.full((1 << 16,), float(d + 1), device=f"cuda:{d}"))
+    with torch.cuda.device(0):
+        xs[0].mul_(3.0)  # compute-stream work the collective must follow
+    g.reduce(xs, 0)
+    assert torch.allclose(xs[0], torch.full_like(xs[0], 3.0 + sum(range(2, n + 1))))
+    g.broadcast(xs, 0)
+    for x in xs:
+        assert torch.equal(x.cpu(), xs[0].cpu())
+    g.all_reduce(xs)
+    assert torch.allclose(xs[0], torch.full_like(xs[0], n * (3.0 + sum(range(2, n + 1)))))
+
+
+def test_native_comm_over_native_tcp_store():
+    """The native communicator rendezvousing through our C++ TCP store instead of c10d's."""
+    from pytorch_distributed_template_amd.parallel.comm import NativeComm
+    from pytorch_distributed_template_amd.parallel.store import NativeStore
+    st = NativeStore("127.0.0.1", 0, 0, 1)
+    c = NativeComm(torch.device(DEV, 0), store=st)
+    assert c.world == 1 and c.rank == 0
+    x = torch.randn(4096, device=DEV)
+    ref = x.clone()
+    c.all_reduce(x)
+    assert torch.equal(x, ref)
+    c.barrier()
