@@ -437,6 +437,19 @@ void stem_pool_bwd_reduce(const Tensor& dp, const Tensor& idx, const Tensor& y, 
                                    pd(slots, "slots"), N, H, W, C, cur_stream());
 }
 
+// pass 1 from the pooled output alone (mask = out > 0, BN input recovered from out)
+void stem_pool_bwd_reduce_out(const Tensor& dp, const Tensor& out, const Tensor& coef, Tensor& slots, int64_t N,
+                              int64_t H, int64_t W, int64_t C) {
+  const int dt = dt16(dp, "dp");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dt16(out, "out") == dt && dp.numel() == N * OH * OW * C && out.numel() == dp.numel() && C % 8 == 0 &&
+                  C <= 2048 && coef.numel() >= 4 * C,
+              "stem_pool_bwd_reduce_out: bad sizes");
+  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * 2, "stem_pool_bwd_reduce_out: slots too small");
+  pdt::stem_pool_bwd_reduce_out_launch(dt, p16(dp, "dp"), p16(out, "out"), pf(coef, "coef"), pd(slots, "slots"), N, H,
+                                       W, C, cur_stream());
+}
+
 // ... and apply pass writing dy = A*dz + B*y + C (bcoef from bn_bwd_finalize)
 void stem_pool_bwd_apply(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef,
                          const Tensor& bcoef, Tensor& dy, int64_t N, int64_t H, int64_t W, int64_t C) {
@@ -595,6 +608,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return pdt::stem_fwd_supported((int)Hp, (int)Wp, (int)P, (int)Q);
   });
   m.def("stem_pool_bwd_reduce", &stem_pool_bwd_reduce);
+  m.def("stem_pool_bwd_reduce_out", &stem_pool_bwd_reduce_out);
   m.def("stem_pool_bwd_apply", &stem_pool_bwd_apply);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

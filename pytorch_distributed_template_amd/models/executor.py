@@ -579,7 +579,8 @@ class ResNetExecutor:
         st, sbn = self.stem, self.stem_bn
         P0, Q0 = saved["P0"], saved["Q0"]
         slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
-        Cn.stem_pool_bwd_reduce(g, saved["idx"], saved["y0"], sbn.coef, slots, N, P0, Q0, st.cout)
+        # BN-backward sums from the pooled output alone (ReLU mask = out > 0, BN input recovered from out)
+        Cn.stem_pool_bwd_reduce_out(g, saved["x0"], sbn.coef, slots, N, P0, Q0, st.cout)
         self._bn_bwd_finish(slots, N * P0 * Q0, sbn)
         dy0 = self._buf("dy0", N * P0 * Q0 * st.cout)
         Cn.stem_pool_bwd_apply(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)

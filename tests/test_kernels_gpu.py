@@ -259,6 +259,13 @@ def test_stem_pool_backward_fused():
     bcoef = torch.empty(3 * C, device=DEV)
     native.C.bn_bwd_finalize(sums, float(N * H * W), coef, gamma, dgamma, dbeta, 1.0, bcoef)
     assert _rel(dgamma, g_.grad) < 1e-2 and _rel(dbeta, b_.grad) < 1e-2
+    # the same sums from the pooled output alone
+    slots2 = torch.zeros_like(slots)
+    native.C.stem_pool_bwd_reduce_out(dp, out, coef, slots2, N, H, W, C)
+    sums2 = torch.empty(2 * C, dtype=torch.float64, device=DEV)
+    native.C.bn_slot_sum(slots2, C, 2, sums2)
+    assert torch.allclose(sums2[:C], sums[:C], rtol=1e-4, atol=1e-3)
+    assert torch.allclose(sums2[C:], sums[C:], rtol=2e-2, atol=2e-2)
     dy = torch.empty_like(y)
     native.C.stem_pool_bwd_apply(dp, idx, y, coef, bcoef, dy, N, H, W, C)
     assert _rel(dy.permute(0, 3, 1, 2), xin.grad) < 2e-2
