@@ -41,7 +41,7 @@ PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
 // Shared epilogue of the implicit-GEMM conv kernels: the wave's accumulators acc[i][j] hold output
 // channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m = m0 + wm*WM + j*16 + fr.
-template <int DT, int EPI, bool RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M>
+template <int DT, int EPI, bool RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_>
 PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int64_t m0, int n0, int tile_m, int wn,
                               int wm, int tid, int lane, char* smem) {
   using E = E16<DT>;
@@ -63,96 +63,137 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
 #pragma unroll
       for (int k = 0; k < (KS > 0 ? KS : 1); ++k) sacc[i][r][k] = 0.f;
 
-  // per-channel BN coefficients of the fused BN-backward epilogues, loaded once before any store (the
-  // stores could alias them as far as the compiler knows, which would force a reload per pixel)
-  float4 c_sc[EPI == 2 ? FN : 1], c_sh[EPI == 2 ? FN : 1], c_mu[EPI >= 2 ? FN : 1], c_is[EPI >= 2 ? FN : 1];
-
+  // Per-channel BN coefficients of the fused BN-backward epilogues, staged once per block in LDS (free after
+  // the main loop; placed behind the statistics scratch) and read back as float4 per channel fragment:
+  // registers would cost 32-64 VGPRs per lane, global reloads would be serialised behind the stores.
+  // Layout [quantity][BN]: 0 scale, 1 shift, 2 mean, 3 invstd (branch 1); 4 mean, 5 invstd (branch 2).
+  constexpr int RED_BYTES = WAVES_M * BN * 3 * 4;
+  float* cf = (float*)(smem + RED_BYTES);
   if constexpr (EPI >= 2) {
-#pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int n = n0 + wn * WN + i * 16 + 4 * fq;
-      if constexpr (EPI == 2) {
-        c_sc[i] = *(const float4*)(a.bn_coef1 + n);
-        c_sh[i] = *(const float4*)(a.bn_coef1 + a.Kout + n);
+    for (int c = tid; c < BN; c += NW_ * 64) {
+      const int n = n0 + c;
+      cf[0 * BN + c] = a.bn_coef1[n];
+      cf[1 * BN + c] = a.bn_coef1[a.Kout + n];
+      cf[2 * BN + c] = a.bn_coef1[2 * a.Kout + n];
+      cf[3 * BN + c] = a.bn_coef1[3 * a.Kout + n];
+      if constexpr (EPI == 4) {
+        cf[4 * BN + c] = a.bn_coef2[2 * a.Kout + n];
+        cf[5 * BN + c] = a.bn_coef2[3 * a.Kout + n];
       }
-      c_mu[i] = *(const float4*)(a.bn_coef1 + 2 * a.Kout + n);
-      c_is[i] = *(const float4*)(a.bn_coef1 + 3 * a.Kout + n);
     }
+    __syncthreads();
   }
+  auto coef4 = [&](int q, int i) { return *(const float4*)(cf + q * BN + wn * WN + i * 16 + 4 * fq); };
 
+  // Two-phase chunks of JC pixel fragments: every epilogue operand load of the chunk (residual, BN input(s),
+  // ReLU mask) is issued before any arithmetic or store, so the chunk pays ONE memory latency instead of
+  // one per (pixel fragment, channel fragment) -- the stores could alias the operands as far as the
+  // compiler knows, so it would not hoist them itself.  Out-of-range pixels (M tail) load from pixel 0.
+  constexpr bool LY1 = EPI >= 2, LY2 = EPI == 4, LM = EPI == 3 || EPI == 4;
+  // registers per pixel fragment of hoisted operands; chunk size keeps them within the budget left
+  // beside the accumulators (FN*FM*4) so no variant spills or loses occupancy
+  constexpr int PER_J = FN * (2 * RES + 2 * LY1 + 2 * LY2 + LM);
+  constexpr int BUDGET = FN * FM * 4 >= 128 ? 64 : 96;
+  constexpr int JC = PER_J == 0 ? FM
+                     : (8 * PER_J <= BUDGET && FM % 8 == 0) ? 8
+                     : (4 * PER_J <= BUDGET && FM % 4 == 0) ? 4
+                     : (2 * PER_J <= BUDGET && FM % 2 == 0) ? 2 : 1;
+  static_assert(FM % JC == 0, "epilogue chunking");
 #pragma unroll
-  for (int j = 0; j < FM; ++j) {
-    const int64_t m = m0 + wm * WM + j * 16 + fr;
-    if (m < a.M) {
-      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
-      const int rem = (int)m - nimg * PQ;
+  for (int jc = 0; jc < FM; jc += JC) {
+    int64_t obase[JC];
+    bool valid[JC];
+#pragma unroll
+    for (int jj = 0; jj < JC; ++jj) {
+      const int64_t m = m0 + wm * WM + (jc + jj) * 16 + fr;
+      valid[jj] = m < a.M;
+      const int mm = valid[jj] ? (int)m : 0;
+      const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
+      const int rem = mm - nimg * PQ;
       const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
       const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
-      const int64_t obase = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+      obase[jj] = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+    }
+    uint2 p_res[RES ? JC : 1][RES ? FN : 1], p_y1[LY1 ? JC : 1][LY1 ? FN : 1], p_y2[LY2 ? JC : 1][LY2 ? FN : 1];
+    uint32_t p_m[LM ? JC : 1][LM ? FN : 1];
+#pragma unroll
+    for (int jj = 0; jj < JC; ++jj)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int64_t o = obase[jj] + n0 + wn * WN + i * 16 + 4 * fq;
+        if constexpr (RES) p_res[jj][i] = *(const uint2*)(a.res + o);
+        if constexpr (LY1) p_y1[jj][i] = *(const uint2*)(a.bn_y1 + o);
+        if constexpr (LY2) p_y2[jj][i] = *(const uint2*)(a.bn_y2 + o);
+        if constexpr (LM) p_m[jj][i] = (uint32_t)a.bn_mask[o >> 3] >> ((int)o & 4);
+      }
+#pragma unroll
+    for (int jj = 0; jj < JC; ++jj) {
+      if (!valid[jj]) continue;
+      const int j = jc + jj;
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int n = n0 + wn * WN + i * 16 + 4 * fq;
+        const int64_t o = obase[jj] + n;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if constexpr (RES) {
-          const uint2 rr = *(const uint2*)(a.res + obase + n);
+          const uint2 rr = p_res[jj][i];
           v[0] += E::to_f((uint16_t)(rr.x & 0xffff));
           v[1] += E::to_f((uint16_t)(rr.x >> 16));
           v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
           v[3] += E::to_f((uint16_t)(rr.y >> 16));
         }
         float y1[4], y2[4];
-        if constexpr (EPI >= 2) {
-          const uint2 q1 = *(const uint2*)(a.bn_y1 + obase + n);
+        if constexpr (LY1) {
+          const uint2 q1 = p_y1[jj][i];
           y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
           y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
           if constexpr (EPI == 2) {
-            const float4 sc = c_sc[i], sh = c_sh[i];
+            const float4 sc = coef4(0, i), sh = coef4(1, i);
             if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
             if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint32_t mb = (uint32_t)a.bn_mask[(obase + n) >> 3] >> (n & 4);
+            const uint32_t mb = p_m[jj][i];
             if (!(mb & 1u)) v[0] = 0.f;
             if (!(mb & 2u)) v[1] = 0.f;
             if (!(mb & 4u)) v[2] = 0.f;
             if (!(mb & 8u)) v[3] = 0.f;
           }
-          if constexpr (EPI == 4) {
-            const uint2 q2 = *(const uint2*)(a.bn_y2 + obase + n);
-            y2[0] = E::to_f((uint16_t)(q2.x & 0xffff)); y2[1] = E::to_f((uint16_t)(q2.x >> 16));
-            y2[2] = E::to_f((uint16_t)(q2.y & 0xffff)); y2[3] = E::to_f((uint16_t)(q2.y >> 16));
-          }
         }
-        uint16_t o[4];
+        if constexpr (LY2) {
+          const uint2 q2 = p_y2[jj][i];
+          y2[0] = E::to_f((uint16_t)(q2.x & 0xffff)); y2[1] = E::to_f((uint16_t)(q2.x >> 16));
+          y2[2] = E::to_f((uint16_t)(q2.y & 0xffff)); y2[3] = E::to_f((uint16_t)(q2.y >> 16));
+        }
+        uint16_t ov[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = E::from_f(v[r]);
+        for (int r = 0; r < 4; ++r) ov[r] = E::from_f(v[r]);
         uint2 packed;
-        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-        *(uint2*)(a.y + obase + n) = packed;
+        packed.x = (uint32_t)ov[0] | ((uint32_t)ov[1] << 16);
+        packed.y = (uint32_t)ov[2] | ((uint32_t)ov[3] << 16);
+        *(uint2*)(a.y + o) = packed;
         if constexpr (EPI == 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float q = E::to_f(o[r]);
+            const float q = E::to_f(ov[r]);
             sacc[i][r][0] += q;
             sacc[i][r][1] += q * q;
           }
         } else if constexpr (EPI >= 2) {
-          const float4 mu = c_mu[i], is = c_is[i];
+          const float4 mu = coef4(2, i), is = coef4(3, i);
           const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float dz = E::to_f(o[r]);
+            const float dz = E::to_f(ov[r]);
             sacc[i][r][0] += dz;
             sacc[i][r][1] += dz * (y1[r] - m1[r]) * i1[r];
           }
           if constexpr (EPI == 4) {
-            const float4 mu2 = *(const float4*)(a.bn_coef2 + 2 * a.Kout + n);  // (not hoisted: registers)
-            const float4 is2 = *(const float4*)(a.bn_coef2 + 3 * a.Kout + n);
+            const float4 mu2 = coef4(4, i), is2 = coef4(5, i);
             const float m2[4] = {mu2.x, mu2.y, mu2.z, mu2.w}, i2[4] = {is2.x, is2.y, is2.z, is2.w};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sacc[i][r][2] += E::to_f(o[r]) * (y2[r] - m2[r]) * i2[r];
+            for (int r = 0; r < 4; ++r) sacc[i][r][2] += E::to_f(ov[r]) * (y2[r] - m2[r]) * i2[r];
           }
         }
       }
@@ -400,7 +441,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
     }
   }
 
-  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -633,7 +674,7 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
     __builtin_amdgcn_s_barrier();
   }
 
-  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
 }
 
 template <int DT, int BM, int BN>
