@@ -61,18 +61,44 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, double count
 
 // Fused (no SyncBN) form of bn_slot_sum + bn_finalize: one thread per channel sums its kStatSlots fp64
 // slot copies and finalizes in place (one launch per BN layer instead of two).
-__global__ void bn_finalize_slots_kernel(const double* __restrict__ slots, double count,
+// Slot totals for 64 channels per 256-thread block: 4 thread quarters each sum 16 of the kStatSlots slot
+// copies (16 independent loads in flight per thread instead of a 64-long serial chain), combined in LDS.
+// Returns true in the threads (quarter 0) that hold the totals of a valid channel c.
+template <int K>
+__device__ inline bool slot_sum_block(const double* __restrict__ slots, int C, double (&s)[K], int& c) {
+  static_assert(kStatSlots == 64, "slot_sum_block splits 64 slots in 4 quarters");
+  __shared__ double part[3][64][K];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  c = blockIdx.x * 64 + cl;
+#pragma unroll
+  for (int k = 0; k < K; ++k) s[k] = 0.0;
+  if (c < C) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+#pragma unroll
+      for (int k = 0; k < K; ++k) s[k] += slots[((int64_t)(q * 16 + g) * C + c) * K + k];
+  }
+  if (q > 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) part[q - 1][cl][k] = s[k];
+  __syncthreads();
+  if (q != 0) return false;
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int k = 0; k < K; ++k) s[k] += part[p][cl][k];
+  return c < C;
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_slots_kernel(const double* __restrict__ slots, double count,
                                          const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                                          float momentum, float* __restrict__ running_mean,
                                          float* __restrict__ running_var, float* __restrict__ coef,
                                          double* __restrict__ sums, int C, int update_running) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s0 = 0, s1 = 0;
-  for (int g = 0; g < kStatSlots; ++g) {
-    s0 += slots[((int64_t)g * C + c) * 2];
-    s1 += slots[((int64_t)g * C + c) * 2 + 1];
-  }
+  double sv[2];
+  int c;
+  if (!slot_sum_block<2>(slots, C, sv, c)) return;
+  const double s0 = sv[0], s1 = sv[1];
   sums[c] = s0;
   sums[C + c] = s1;
   const double mean = s0 / count;
@@ -94,7 +120,7 @@ __global__ void bn_finalize_slots_kernel(const double* __restrict__ slots, doubl
 void bn_finalize_slots_launch(const double* slots, double count, const float* gamma, const float* beta, float eps,
                               float momentum, float* rm, float* rv, float* coef, double* sums, int C,
                               bool update_running, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_slots_kernel, dim3((C + 255) / 256), dim3(256), 0, s, slots, count, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_slots_kernel, dim3((C + 63) / 64), dim3(256), 0, s, slots, count, gamma, beta, eps,
                      momentum, rm, rv, coef, sums, C, update_running ? 1 : 0);
 }
 
@@ -340,20 +366,19 @@ __device__ inline void bn_bwd_coef(double sdz, double sdzx, double count, float 
   bcoef[2 * C + c] = -A * mdz + A * invstd * mdzx * mean;
 }
 
-__global__ void bn_bwd_finalize_slots_kernel(const double* __restrict__ slots, int K, double count,
+template <int K>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_slots_kernel(const double* __restrict__ slots, double count,
                                              const float* __restrict__ coef1, const float* __restrict__ gamma1,
                                              float* __restrict__ dgamma1, float* __restrict__ dbeta1,
                                              float* __restrict__ bcoef1, const float* __restrict__ coef2,
                                              const float* __restrict__ gamma2, float* __restrict__ dgamma2,
                                              float* __restrict__ dbeta2, float* __restrict__ bcoef2, float gscale,
                                              int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s[4] = {0, 0, 0, 0};
-  for (int g = 0; g < kStatSlots; ++g)
-    for (int k = 0; k < K; ++k) s[k] += slots[((int64_t)g * C + c) * K + k];
+  double s[K];
+  int c;
+  if (!slot_sum_block<K>(slots, C, s, c)) return;
   bn_bwd_coef(s[0], s[1], count, coef1[2 * C + c], coef1[3 * C + c], gamma1[c], dgamma1, dbeta1, gscale, bcoef1, C, c);
-  if (K == 4)
+  if constexpr (K == 4)
     bn_bwd_coef(s[2], s[3], count, coef2[2 * C + c], coef2[3 * C + c], gamma2[c], dgamma2, dbeta2, gscale, bcoef2, C, c);
 }
 
@@ -361,8 +386,12 @@ void bn_bwd_finalize_slots_launch(const double* slots, int K, double count, cons
                                   float* dgamma1, float* dbeta1, float* bcoef1, const float* coef2,
                                   const float* gamma2, float* dgamma2, float* dbeta2, float* bcoef2, float gscale,
                                   int C, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_slots_kernel, dim3((C + 255) / 256), dim3(256), 0, s, slots, K, count, coef1,
-                     gamma1, dgamma1, dbeta1, bcoef1, coef2, gamma2, dgamma2, dbeta2, bcoef2, gscale, C);
+  if (K == 4)
+    hipLaunchKernelGGL(bn_bwd_finalize_slots_kernel<4>, dim3((C + 63) / 64), dim3(256), 0, s, slots, count, coef1,
+                       gamma1, dgamma1, dbeta1, bcoef1, coef2, gamma2, dgamma2, dbeta2, bcoef2, gscale, C);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_slots_kernel<2>, dim3((C + 63) / 64), dim3(256), 0, s, slots, count, coef1,
+                       gamma1, dgamma1, dbeta1, bcoef1, coef2, gamma2, dgamma2, dbeta2, bcoef2, gscale, C);
 }
 
 // dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad)
