@@ -271,7 +271,7 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   a.stride_h = stride_h; a.stride_w = stride_w; a.pad_h = pad_h; a.pad_w = pad_w; a.dil_h = dil_h; a.dil_w = dil_w;
   a.P = N * Pm * Qm; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
   a.cs = cs; a.win = win ? 1 : 0;
-  a.tile = (!win && C % 128 == 0 && Kout % 128 == 0) ? 128 : 64;
+  a.tile = pdt::wgrad_tile((int)C, (int)Kout, win ? 1 : 0);
   TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad: bad split plan");
   pdt::conv_wgrad_launch(a, dt, cur_stream());
 }

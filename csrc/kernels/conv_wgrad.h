@@ -16,10 +16,11 @@ struct ConvWgradArgs {
   int cs;              // elements per pixel of x (== C except in window mode)
   int win;             // stem window mode (see conv_wgrad.hip)
   int splits, pix_per_split;  // filled by conv_wgrad_plan
-  int tile;                   // 64 or 128 (filled by conv_wgrad_plan)
+  int tile;                   // 64, 128 or 256 (filled by conv_wgrad_plan)
   uint32_t div_pq_mul, div_pq_shift, div_q_mul, div_q_shift;  // FastDiv of Pm*Qm and Qm (launcher)
 };
 
+int wgrad_tile(int C, int Kout, int win);  // 256 (ping-pong), 128 or 64
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks);
 void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s);
 // 3x3/s1/p1 C = Kout = 64, W = 56 specialisation: all 9 taps per block, persistent over 4-row tiles;

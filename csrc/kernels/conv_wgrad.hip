@@ -12,6 +12,8 @@
 // K-step and a full 64x64 accumulator; the waves are summed through LDS at the end and each block
 // writes one fp32 partial tile.  Partials over the split-K axis are summed by wgrad_reduce, which
 // writes (and scales) straight into the fp32 gradient buffer (the DDP bucket view).
+#include <cstdlib>
+
 #include "../common.h"
 #include "conv_wgrad.h"
 
@@ -420,6 +422,189 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// 256 (c) x 256 (k) ping-pong weight-gradient kernel for layers with C, Kout multiples of 256 (ResNet
+// layer3/4, ResNet-50 stages 2-4): the schedule of conv_pp_kernel (conv_fwd.hip) on the wgrad GEMM.
+// 8 waves as 2 (c) x 4 (k), each owning 128 c x 64 k (128 fp32 accumulators), one workgroup per CU,
+// 64-pixel K-steps in 4 phases of 16 MFMAs; waves 4-7 run one barrier behind waves 0-3 so that on
+// every SIMD one wave computes while its partner reads fragments / issues DMA.
+// The X and dY images of a K-step are split in halves by channel (X half h: c = g*128 + h*64 .. +64
+// for g = 0, 1; dY half h: k = g*64 + h*32 .. +32 for g = 0..3), each [64 px][128 ch] (256-B rows,
+// tr_swz16-swizzled for conflict-free ds_read_b64_tr_b16).  Phase p reads (X half, dY half):
+//   p1: X0 + Y0, compute X0 x Y0;  p2: Y1, X0 x Y1;  p3: X1, X1 x Y1;  p4: -, X1 x Y0
+// and issues the next K-step's X0, Y0, Y1, X1 DMA with the counted-vmcnt discipline of conv_pp_kernel.
+template <int N>
+PDT_DEVICE void wg_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <int DT>
+__global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 64, ROWB = 256;
+  constexpr int HALF = BKP * ROWB;          // 16 KiB per half image
+  constexpr int BUF = 4 * HALF;             // X0 X1 Y0 Y1
+  constexpr int OX0 = 0, OX1 = HALF, OY0 = 2 * HALF, OY1 = 3 * HALF;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;              // waves w and w+4 share a SIMD
+  const int wx = wave & 1, wy = wave >> 1;  // 2 (c) x 4 (k)
+
+  const int c_tiles = a.C / 256, k_tiles = a.Kout / 256;
+  const int n_tiles = a.T * a.U * c_tiles;
+  const int nwg = k_tiles * n_tiles * a.splits;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile = bid % (k_tiles * n_tiles);
+  const int split = bid / (k_tiles * n_tiles);
+  const int kt = tile % k_tiles, nt = tile / k_tiles;
+  const int tap = nt / c_tiles;
+  const int c0 = (nt - tap * c_tiles) * 256, k0 = kt * 256;
+  const int t = tap / a.U, u = tap - (tap / a.U) * a.U;
+  const int pix_begin = split * a.pix_per_split;
+  const int pix_end = min(a.P, pix_begin + a.pix_per_split);
+  const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
+  const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
+
+  // DMA lane geometry: 4 pixel rows x 16 chunks per 1 KiB instruction, 2 instructions per wave per half
+  const int lrow = lane >> 4, pch = lane & 15;
+  int drow[2], lch[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    drow[j] = (wave * 2 + j) * 4 + lrow;
+    lch[j] = pch ^ tr_swz16(drow[j]);
+  }
+  // image column (8-channel chunk) -> channel within the tile, half 0 (half 1 adds 64 / 32)
+  int xcol[2], ycol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = lch[j] * 8;
+    xcol[j] = c0 + (col >> 6) * 128 + (col & 63);
+    ycol[j] = k0 + (col >> 5) * 64 + (col & 31);
+  }
+  uint32_t xo[2], yo[2];
+  auto offsets = [&](int step) {  // source offsets of this lane's two rows for K-step `step`
+    const int pbase = pix_begin + step * BKP;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint32_t x_, y_;
+      wgrad_rows<false>(a, pbase + drow[j], th, tw, xcol[j] - lch[j] * 8, lch[j], ycol[j] - lch[j] * 8, x_, y_);
+      xo[j] = x_;
+      yo[j] = y_;
+    }
+  };
+  auto dma_x = [&](char* buf, int h) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      buf_lds16(rx, buf + (h ? OX1 : OX0) + (wave * 2 + j) * 1024, xo[j] == kOOB ? kOOB : xo[j] + h * 128u);
+  };
+  auto dma_y = [&](char* buf, int h) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) buf_lds16(ry, buf + (h ? OY1 : OY0) + (wave * 2 + j) * 1024, yo[j] + h * 64u);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry (see conv_wgrad128_kernel): rows r0 / r0+4 of each 32-pixel group
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+  vec8 xs[4][2], y0r[2][2], y1r[2][2];
+  // The transposed LDS reads are issued through inline asm: the ds_read_tr builtin carries no memory
+  // operand, so the compiler would wait vmcnt(0) (every in-flight LDS-DMA) before each of them and
+  // de-pipeline the loop.  Their completion is waited explicitly (lgkmcnt(0)) at the top of each compute
+  // segment, after the barrier.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto frag = [&](const char* base, int cc, int kk) {
+    const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+    const uint32_t a0 = lds0 + (uint32_t)(base - smem) + r0 * ROWB + (((cc >> 3) ^ tr_swz16(r0)) << 4) + (cc & 7) * 2;
+    const uint32_t a1 = lds0 + (uint32_t)(base - smem) + r1 * ROWB + (((cc >> 3) ^ tr_swz16(r1)) << 4) + (cc & 7) * 2;
+    s16x4_t lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1));
+    return __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto read_x = [&](const char* base) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) xs[f][kk] = frag(base, wx * 64 + f * 16 + 4 * p4, kk);
+  };
+  auto read_y = [&](vec8 (&yr)[2][2], const char* base) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) yr[f][kk] = frag(base, wy * 32 + f * 16 + 4 * p4, kk);
+  };
+  auto compute = [&](const vec8 (&yr)[2][2], int xh, int yh) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f2 = 0; f2 < 2; ++f2)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          acc[xh * 4 + f][yh * 2 + f2] = E::mfma16x16x32(xs[f][kk], yr[f2][kk], acc[xh * 4 + f][yh * 2 + f2]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (nsteps > 0) {
+    offsets(0);
+    dma_x(smem, 0);
+    dma_y(smem, 0);
+    dma_y(smem, 1);
+    dma_x(smem, 1);
+    wg_vm_wait<4>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();
+    for (int ks = 0; ks < nsteps; ++ks) {
+      const char* cb = smem + (ks & 1) * BUF;
+      char* nb = smem + ((ks + 1) & 1) * BUF;
+      const bool more = ks + 1 < nsteps;
+      if (more) offsets(ks + 1);
+      if (more) { dma_x(nb, 0); wg_vm_wait<4>(); } else { wg_vm_wait<2>(); }
+      read_x(cb + OX0);
+      read_y(y0r, cb + OY0);
+      compute(y0r, 0, 0);
+      if (more) { dma_y(nb, 0); wg_vm_wait<4>(); } else { wg_vm_wait<0>(); }
+      read_y(y1r, cb + OY1);
+      compute(y1r, 0, 1);
+      if (more) dma_y(nb, 1);
+      read_x(cb + OX1);
+      compute(y1r, 1, 1);
+      if (more) { dma_x(nb, 1); wg_vm_wait<4>(); }
+      compute(y0r, 1, 0);
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+  // acc[i][j]: c = wx*128 + 16i + 4*(lane>>4) + r (i = xh*4 + f), k = wy*64 + 16j + (lane&15)
+  float* dst = a.ws + ((int64_t)split * a.Kout + k0) * a.ldw + tap * a.C + c0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = wy * 64 + 16 * j + (lane & 15);
+      const int c = wx * 128 + 16 * i + 4 * (lane >> 4);
+      *(f32x4_t*)(dst + (int64_t)k * a.ldw + c) = acc[i][j];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 weight gradient for C = Kout = 64 and W = 56 (ResNet layer1, the most
 // expensive weight gradients of ResNet-18/34), all 9 taps in one block.
 //
@@ -637,10 +822,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce_scalar_kernel(const float* _
   }
 }
 
+int wgrad_tile(int C, int Kout, int win) {
+  // PDT_WGRAD_PP=0 disables the 256x256 ping-pong kernel (A/B sweeps)
+  static const bool pp_on = [] {
+    const char* e = getenv("PDT_WGRAD_PP");
+    return !(e && e[0] == '0');
+  }();
+  if (!win && pp_on && C % 256 == 0 && Kout % 256 == 0) return 256;
+  return (!win && C % 128 == 0 && Kout % 128 == 0) ? 128 : 64;
+}
+
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
-  a.tile = (!a.win && a.C % 128 == 0 && a.Kout % 128 == 0) ? 128 : 64;
+  a.tile = wgrad_tile(a.C, a.Kout, a.win);
   const int tiles = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile);
   int splits = (target_blocks + tiles - 1) / tiles;
+  if (a.tile == 256) {
+    // one 8-wave block per CU: aim at whole rounds of the CU count (a 2.1-round grid runs 3 rounds)
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return n > 0 ? n : 256;
+    }();
+    const int goal = target_blocks / 4 > cus ? (target_blocks / 4) / cus * cus : cus;
+    splits = goal / tiles > 0 ? goal / tiles : 1;
+  }
   const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
   int pps = (a.P + splits - 1) / splits;
@@ -656,7 +862,12 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
   a.div_pq_mul = dpq.mul; a.div_pq_shift = dpq.shift; a.div_q_mul = dq.mul; a.div_q_shift = dq.shift;
-  if (a.tile == 128) {
+  if (a.tile == 256) {
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad_pp_kernel<kBF16>), dim3(nwg), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_pp_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
+  } else if (a.tile == 128) {
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16>), dim3(nwg), dim3(256), 0, s, a);
     else

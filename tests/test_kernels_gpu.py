@@ -492,3 +492,21 @@ def test_conv_pp_long_k_and_fused_bn_backward(tile, mode):
     if mode == 3:
         x2 = ((y2.float() - m1) * i1).view(-1, C).double()
         assert torch.allclose(sums[:, 3], (dzf * x2).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", [(6, 14, 14, 256, 256, 3, 1, 1), (4, 15, 13, 256, 512, 3, 2, 1),
+                                  (5, 14, 14, 512, 256, 1, 2, 0)])
+@pytest.mark.parametrize("target", [64, 1024])
+def test_conv_wgrad_pp_256(case, target):
+    """256x256 ping-pong weight-gradient kernel (C, Kout multiples of 256) over several splits vs torch."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    N, H, W, C, K, R, st, pad = case
+    torch.manual_seed(31)
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    assert native.C.conv_wgrad_plan(K, R, R, C, N * P * Q, target, False)[2] == 256
+    x = _rand16(N, H, W, C)
+    dy = _rand16(N, P, Q, K)
+    dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=target)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
+                                      stride=st, padding=pad).permute(0, 2, 3, 1)
+    assert _rel(dw, ref) < 2e-3
