@@ -94,6 +94,20 @@ PDT_DEVICE void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds_dst, uint32_t voff
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_dst, 16, voff, 0, 0, 0);
 }
 
+// The same LDS-DMA issued through inline asm: identical instruction, but invisible to the compiler's
+// waitcnt pass, which otherwise drains EVERY in-flight LDS-DMA (s_waitcnt vmcnt(0)) in front of any
+// ds_read_b64_tr_b16 (the transposed-read builtins carry no memory operand, so they may alias any
+// pending DMA) -- that silently serialises a "prefetch next stage, compute current stage" loop.
+// Callers order these DMAs themselves: an explicit (counted) s_waitcnt vmcnt + barrier before the
+// first read of a staged buffer.
+PDT_DEVICE void buf_lds16_asm(__amdgpu_buffer_rsrc_t r, void* lds_dst, uint32_t voff) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_void_t*)lds_dst;  // LDS byte address (wave-uniform)
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0v), "v"(voff), "s"(r)
+               : "m0");
+}
+
 // XCD-aware bijective remap of a 1-D block index: blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so give each XCD a contiguous range of logical tiles
 // (speed only, never correctness: any placement is valid).

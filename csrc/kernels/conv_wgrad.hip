@@ -104,8 +104,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       const int lch = pch ^ tr_swz(row);
       uint32_t xo, yo;
       wgrad_rows<WIN>(a, pbase + row, th, tw, c0, lch, k0, xo, yo);
-      buf_lds16(rx, sb + (wave * 4 + j) * 1024, xo);
-      buf_lds16(ry, sb + XB + (wave * 4 + j) * 1024, yo);
+      buf_lds16_asm(rx, sb + (wave * 4 + j) * 1024, xo);
+      buf_lds16_asm(ry, sb + XB + (wave * 4 + j) * 1024, yo);
     }
   };
 
@@ -227,9 +227,9 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
       uint32_t xo, yo;
       wgrad_rows<true>(a, pbase + row, th, 0, 0, lch, 0, xo, yo);
       if (tile == 0)
-        buf_lds16(ry, sb + (ii & 7) * 1024, yo);
+        buf_lds16_asm(ry, sb + (ii & 7) * 1024, yo);
       else
-        buf_lds16(rx, sb + tile * TB + (ii & 7) * 1024, xo);
+        buf_lds16_asm(rx, sb + tile * TB + (ii & 7) * 1024, xo);
     }
   };
 
@@ -353,8 +353,8 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
       const int lch = pch ^ tr_swz16(row);
       uint32_t xo, yo;
       wgrad_rows<false>(a, pbase + row, th, tw, c0, lch, k0, xo, yo);
-      buf_lds16(rx, sb + (wave * 4 + j) * 1024, xo);
-      buf_lds16(ry, sb + XB + (wave * 4 + j) * 1024, yo);
+      buf_lds16_asm(rx, sb + (wave * 4 + j) * 1024, xo);
+      buf_lds16_asm(ry, sb + XB + (wave * 4 + j) * 1024, yo);
     }
   };
 
@@ -432,6 +432,8 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
 // tr_swz16-swizzled for conflict-free ds_read_b64_tr_b16).  Phase p reads (X half, dY half):
 //   p1: X0 + Y0, compute X0 x Y0;  p2: Y1, X0 x Y1;  p3: X1, X1 x Y1;  p4: -, X1 x Y0
 // and issues the next K-step's X0, Y0, Y1, X1 DMA with the counted-vmcnt discipline of conv_pp_kernel.
+// The DMA goes through buf_lds16_asm (common.h): with the builtin form the compiler drains the whole
+// DMA pipeline (vmcnt(0)) before every transposed read.
 template <int N>
 PDT_DEVICE void wg_vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -500,11 +502,11 @@ __global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
   auto dma_x = [&](char* buf, int h) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      buf_lds16(rx, buf + (h ? OX1 : OX0) + (wave * 2 + j) * 1024, xo[j] == kOOB ? kOOB : xo[j] + h * 128u);
+      buf_lds16_asm(rx, buf + (h ? OX1 : OX0) + (wave * 2 + j) * 1024, xo[j] == kOOB ? kOOB : xo[j] + h * 128u);
   };
   auto dma_y = [&](char* buf, int h) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) buf_lds16(ry, buf + (h ? OY1 : OY0) + (wave * 2 + j) * 1024, yo[j] + h * 64u);
+    for (int j = 0; j < 2; ++j) buf_lds16_asm(ry, buf + (h ? OY1 : OY0) + (wave * 2 + j) * 1024, yo[j] + h * 64u);
   };
 
   f32x4_t acc[8][4];
@@ -516,18 +518,12 @@ __global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
   // transposed-read lane geometry (see conv_wgrad128_kernel): rows r0 / r0+4 of each 32-pixel group
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
   vec8 xs[4][2], y0r[2][2], y1r[2][2];
-  // The transposed LDS reads are issued through inline asm: the ds_read_tr builtin carries no memory
-  // operand, so the compiler would wait vmcnt(0) (every in-flight LDS-DMA) before each of them and
-  // de-pipeline the loop.  Their completion is waited explicitly (lgkmcnt(0)) at the top of each compute
-  // segment, after the barrier.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   auto frag = [&](const char* base, int cc, int kk) {
     const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
-    const uint32_t a0 = lds0 + (uint32_t)(base - smem) + r0 * ROWB + (((cc >> 3) ^ tr_swz16(r0)) << 4) + (cc & 7) * 2;
-    const uint32_t a1 = lds0 + (uint32_t)(base - smem) + r1 * ROWB + (((cc >> 3) ^ tr_swz16(r1)) << 4) + (cc & 7) * 2;
-    s16x4_t lo, hi;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1));
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(base + r0 * ROWB + (((cc >> 3) ^ tr_swz16(r0)) << 4) + (cc & 7) * 2));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(base + r1 * ROWB + (((cc >> 3) ^ tr_swz16(r1)) << 4) + (cc & 7) * 2));
     return __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto read_x = [&](const char* base) {
@@ -545,7 +541,6 @@ __global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
   auto compute = [&](const vec8 (&yr)[2][2], int xh, int yh) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -663,14 +658,14 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
         const bool ok = R < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W;
         const int ch = pch ^ l1_swz(hr, wc);
         const uint32_t off = ok ? (uint32_t)((((n * a.H + h) * kL1W + w) * 64 + ch * 8) * 2) : kOOB;
-        buf_lds16(rx, sb + ii * 1024, off);
+        buf_lds16_asm(rx, sb + ii * 1024, off);
       } else {
         const int R = (ii - 44) * 8 + lrow;
         const int r = R / kL1W, w = R - (R / kL1W) * kL1W;
         const int h = h0 + r;
         const int ch = pch ^ l1_swz(r, w);
         const uint32_t off = h < a.H ? (uint32_t)((((n * a.H + h) * kL1W + w) * 64 + ch * 8) * 2) : kOOB;
-        buf_lds16(ry, sb + ii * 1024, off);
+        buf_lds16_asm(ry, sb + ii * 1024, off);
       }
     }
   };
@@ -844,8 +839,10 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
         n = 256;
       return n > 0 ? n : 256;
     }();
-    const int goal = target_blocks / 4 > cus ? (target_blocks / 4) / cus * cus : cus;
-    splits = goal / tiles > 0 ? goal / tiles : 1;
+    // one full round: each block then streams ~130 K-steps (ResNet-18 layer3/4), amortising its prologue
+    // and its 256 KB fp32 partial; measured faster than two rounds (tools/conv_bench.py wgrad_256 column)
+    (void)target_blocks;
+    splits = cus / tiles > 0 ? cus / tiles : 1;
   }
   const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
