@@ -137,10 +137,24 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
 
   int t = t_begin + lb;
   int buf = 0;
+  // Stores this wave issued in the previous tile's epilogue: they are the only vector-memory operations
+  // younger than the halo DMA of the tile about to be computed, and vmcnt retires in issue order, so
+  // vmcnt(n_st) proves the DMA landed without also waiting out the store latency (vmcnt(0) here used to
+  // expose ~1-2 us of store drain per tile: one wave per SIMD, nothing else to cover it).  Full tiles
+  // only (exactly 4 stores per pixel group with any valid lane); otherwise n_st = 0 (wait for all).
+  int n_st = 0;
   if (t < t_end) stage_tile(t, 0);
   for (; t < t_end; t += per_x) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and the weights, first time)
-    __syncthreads();
+    if (n_st == 16)
+      __builtin_amdgcn_s_waitcnt((16 & 0xF) | ((16 >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+    else if (n_st == 12)
+      __builtin_amdgcn_s_waitcnt((12 & 0xF) | ((12 >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (and the weights, first time)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
     if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
     const char* sb = stage0 + buf * kStageB;
 
@@ -206,6 +220,10 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
       run(std::integral_constant<int, 3>{});
 
     // ---- epilogue: lane holds couts n = i*16 + 4*fq + r of pixel (g0+j)*16 + fr ----
+    n_st = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) n_st += __builtin_amdgcn_ballot_w64(pvalid[j]) != 0 ? 4 : 0;
+    if (n_st != 4 * ng) n_st = 0;  // partial tile: no counted wait next time
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!pvalid[j]) continue;
