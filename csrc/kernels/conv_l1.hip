@@ -190,28 +190,37 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
     // ahead of the previous step's MFMAs; the group count is a wave-uniform branch outside the loop
     auto run = [&](auto NGc) {
       constexpr int NG = decltype(NGc)::value;
-#pragma unroll
-      for (int st = 0; st < 18; ++st) {
+      // Fragments of step st+1 are read while step st's MFMAs run: an explicit register double buffer,
+      // pinned with scheduling barriers (left alone, hipcc sinks each ds_read to ~3 MFMAs before its use,
+      // which exposes the LDS latency on every fragment -- one wave per SIMD, nothing else covers it).
+      vec8 af[2][4], bf[2][NG];
+      auto load = [&](int st, int sl) {
         const int tap = st >> 1, kk = st & 1;
         const int tr = tap / 3, tu = tap % 3;
         const int wtap = flip ? 8 - tap : tap;
         const int dR = tr * kXP + tu;
-        vec8 af[4], bf[NG];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int co = i * 16 + fr;
           const int c = wtap * 8 + kk * 4 + fq;
-          af[i] = *(const vec8*)(wl + co * 1152 + wswz(co, c) * 16);
+          af[sl][i] = *(const vec8*)(wl + co * 1152 + wswz(co, c) * 16);
         }
 #pragma unroll
         for (int j = 0; j < NG; ++j) {
           const int R = R0[j] + dR;
-          bf[j] = *(const vec8*)(sb + R * 128 + (((kk * 4 + fq) ^ hswz(R)) << 4));
+          bf[sl][j] = *(const vec8*)(sb + R * 128 + (((kk * 4 + fq) ^ hswz(R)) << 4));
         }
+      };
+      load(0, 0);
+#pragma unroll
+      for (int st = 0; st < 18; ++st) {
+        if (st + 1 < 18) load(st + 1, (st + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < NG; ++j) acc[i][j] = E::mfma16x16x32(af[i], bf[j], acc[i][j]);
+          for (int j = 0; j < NG; ++j) acc[i][j] = E::mfma16x16x32(af[st & 1][i], bf[st & 1][j], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     };
     if (ng == 4)
