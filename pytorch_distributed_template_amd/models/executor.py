@@ -92,7 +92,19 @@ class ResNetExecutor:
         self.flat = flat
         self.device = torch.device(device)
         self.dtype = dtype
-        self.grad_ready = grad_ready or (lambda pid: None)
+        self._user_grad_ready = grad_ready or (lambda pid: None)
+        # Weight gradients run on a side HIP stream, concurrently with the rest of the backward chain
+        # (dgrad -> BN-backward passes of the earlier layers): the compute-bound wgrad kernels overlap the
+        # memory-bound elementwise passes.  Ordering: the side stream waits for the main stream before
+        # each wgrad (its dY is ready); a main-stream write to a buffer a pending wgrad still reads waits
+        # for that wgrad (_buf); gradient-bucket all-reduces are launched from the side stream after it
+        # caught up with the main stream (so they see both streams' gradient writes); the main stream joins
+        # the side stream at the end of backward.  PDT_WGRAD_STREAM=0 runs everything on one stream.
+        self.side = None
+        if self.device.type == "cuda" and os.environ.get("PDT_WGRAD_STREAM", "1") != "0":
+            self.side = torch.cuda.Stream(device=self.device)
+        self._on_side = False
+        self._pending_reads: Dict[int, "torch.cuda.Event"] = {}
         self.syncbn_group = syncbn_group
         # SyncBN statistic all-reduce (fp64 sums): torch.distributed on syncbn_group, or a native RCCL
         # communicator's all_reduce when one is given
@@ -195,7 +207,44 @@ class ResNetExecutor:
         if t is None or t.numel() < numel:
             t = torch.empty(numel, dtype=dtype, device=self.device)
             self._bufs[k] = t
+        if self._pending_reads:  # the caller is about to overwrite it: wait for side-stream readers
+            ev = self._pending_reads.pop(t.data_ptr(), None)
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
         return t[:numel]
+
+    def grad_ready(self, pid: int) -> None:
+        """Forward a parameter's gradient readiness to the bucketer; with the side stream, from the side
+        stream after it caught up with the main stream (see __init__)."""
+        if self.side is None or self._on_side:
+            self._user_grad_ready(pid)
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            self._user_grad_ready(pid)
+
+    def _side_wgrad(self, reads: torch.Tensor, fn) -> None:
+        """Run ``fn`` (a weight gradient + its grad_ready) on the side stream behind the main stream's work
+        so far; later main-stream writes to ``reads`` wait for it."""
+        if self.side is None:
+            fn()
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            self._on_side = True
+            try:
+                fn()
+            finally:
+                self._on_side = False
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        reads.record_stream(self.side)  # the allocator must not recycle it before the side stream read it
+        self._pending_reads[reads.data_ptr()] = ev
+
+    def _join_side(self) -> None:
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self._pending_reads.clear()
 
     def _w(self, c: _Conv) -> torch.Tensor:
         s = c.slot
@@ -282,8 +331,10 @@ class ResNetExecutor:
             xg, Hx, Wx, Cx, R, S, st, pad = x, H, W, c.cin, c.R, c.S, c.st, c.pad
         else:
             xg, Hx, Wx, Cx, R, S, st, pad = wgrad_geom
-        self._wgrad(c.cout, xg, dy, N, Hx, Wx, Cx, R, S, P, Q, st, pad, self._g(c.slot), R * S * Cx)
-        self.grad_ready(c.pid)
+        def wg():
+            self._wgrad(c.cout, xg, dy, N, Hx, Wx, Cx, R, S, P, Q, st, pad, self._g(c.slot), R * S * Cx)
+            self.grad_ready(c.pid)
+        self._side_wgrad(dy, wg)
         # --- dgrad
         if dx is None:
             return
@@ -488,9 +539,11 @@ class ResNetExecutor:
         # fc: bias grad (column sums), weight grad (1x1 wgrad over the batch), data grad
         Cn.colsum(dlog, N, self.ncls_pad, self.ncls, self._g(self.fcb_slot), 1.0)
         self.grad_ready(self.fcb_slot.index)
-        self._wgrad(self.ncls_pad, saved["feat"], dlog, N, 1, 1, self.feat, 1, 1, 1, 1, 1, 0,
-                    self._g(self.fc_slot), self.feat, rows=self.ncls, cols=self.feat)
-        self.grad_ready(self.fc_slot.index)
+        def fc_wg():
+            self._wgrad(self.ncls_pad, saved["feat"], dlog, N, 1, 1, self.feat, 1, 1, 1, 1, 1, 0,
+                        self._g(self.fc_slot), self.feat, rows=self.ncls, cols=self.feat)
+            self.grad_ready(self.fc_slot.index)
+        self._side_wgrad(dlog, fc_wg)
         dfeat = self._buf("dfeat", N * self.feat)
         wt = self.derived[self.fc_wt_off:self.fc_wt_off + self.ncls_pad * self.feat]
         bm, bn = _conv_tile(self.feat)
@@ -585,8 +638,12 @@ class ResNetExecutor:
         dy0 = self._buf("dy0", N * P0 * Q0 * st.cout)
         Cn.stem_pool_bwd_apply(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
         ldw = self.stem_pairs * 64
-        tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
-        self._wgrad(st.cout, saved["xp"], dy0, N, saved["Hp"], saved["Wp"], 64, self.stem_pairs, 1, P0, Q0, st.st, 0,
-                    tmp, ldw, cs=4, win=True, dil=2)
-        Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
-        self.grad_ready(st.pid)
+
+        def stem_wg():
+            tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
+            self._wgrad(st.cout, saved["xp"], dy0, N, saved["Hp"], saved["Wp"], 64, self.stem_pairs, 1, P0, Q0,
+                        st.st, 0, tmp, ldw, cs=4, win=True, dil=2)
+            Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
+            self.grad_ready(st.pid)
+        self._side_wgrad(dy0, stem_wg)
+        self._join_side()
