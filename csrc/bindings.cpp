@@ -276,6 +276,45 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   pdt::conv_wgrad_launch(a, dt, cur_stream());
 }
 
+// ResNet stem weight gradient with its dY computed in-kernel (max-pool backward + ReLU mask + BN-backward
+// apply from the pooled gradient dp, the argmax idx, the conv output y0 and the BN coefficients): the
+// window-mode conv_wgrad above without the [P][64] dY tensor.  x: padded NHWC4 image [N][Hp][Wp][4].
+void conv_wgrad_stem_fused(const Tensor& x, const Tensor& dp, const Tensor& idx, const Tensor& y0, const Tensor& coef,
+                           const Tensor& bcoef, Tensor& ws, int64_t N, int64_t Hp, int64_t Wp, int64_t pairs,
+                           int64_t Pm, int64_t Qm, int64_t stride, int64_t dil, int64_t ldw, int64_t splits,
+                           int64_t pix_per_split) {
+  const int dt = dt16(x, "x");
+  const int64_t OH = (Pm - 1) / 2 + 1, OW = (Qm - 1) / 2 + 1;  // 3x3/2 pad-1 max-pool output
+  TORCH_CHECK(dt16(dp, "dp") == dt && dt16(y0, "y0") == dt, "conv_wgrad_stem_fused: mixed dtypes");
+  TORCH_CHECK(x.numel() == N * Hp * Wp * 4 && y0.numel() == N * Pm * Qm * 64 && dp.numel() == N * OH * OW * 64 &&
+                  idx.numel() == dp.numel() && coef.numel() >= 2 * 64 && bcoef.numel() >= 3 * 64,
+              "conv_wgrad_stem_fused: size mismatch");
+  TORCH_CHECK(Qm % 2 == 0, "conv_wgrad_stem_fused: the conv output width must be even (pixel pairs)");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && y0.numel() < (int64_t(1) << 31),
+              "conv_wgrad_stem_fused: operands exceed 32-bit offsets");
+  TORCH_CHECK(pairs == 4 && ldw >= 256 && ws.numel() >= splits * 64 * ldw, "conv_wgrad_stem_fused: needs 4 row pairs");
+  TORCH_CHECK((Pm - 1) * stride + (pairs - 1) * dil + 1 < Hp && ((Qm - 1) * stride + 8) <= Wp,
+              "conv_wgrad_stem_fused: window-mode geometry leaves the padded image");
+  check_dev(idx, "idx");
+  pdt::ConvWgradArgs a{};
+  a.x = p16(x, "x");
+  a.dy = nullptr;
+  a.ws = pf(ws, "ws");
+  a.N = N; a.H = Hp; a.W = Wp; a.C = 64; a.Kout = 64; a.T = pairs; a.U = 1; a.Pm = Pm; a.Qm = Qm;
+  a.stride_h = stride; a.stride_w = stride; a.pad_h = 0; a.pad_w = 0; a.dil_h = dil; a.dil_w = dil;
+  a.P = N * Pm * Qm; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
+  a.cs = 4; a.win = 1;
+  a.tile = pdt::wgrad_tile(64, 64, 1);
+  TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad_stem_fused: bad split plan");
+  a.f_y = p16(y0, "y0");
+  a.f_dp = p16(dp, "dp");
+  a.f_idx = idx.data_ptr<uint8_t>();
+  a.f_coef = pf(coef, "coef");
+  a.f_bcoef = pf(bcoef, "bcoef");
+  a.f_OH = (int)OH; a.f_OW = (int)OW;
+  pdt::conv_wgrad_launch(a, dt, cur_stream());
+}
+
 // ResNet layer1 weight gradient (3x3/s1/p1, C = Kout = 64, W = 56): all 9 taps per block; writes
 // `blocks` fp32 partials [blocks][64][576] into ws and returns blocks (sum them with wgrad_reduce).
 int64_t wgrad_blocks_3x3c64() { return pdt::wgrad3x3_c64_blocks(); }
@@ -586,6 +625,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bn", &conv_dgrad_impl);
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad_stem_fused", &conv_wgrad_stem_fused);
   m.def("wgrad_reduce", &wgrad_reduce);
   m.def("wgrad_blocks_3x3c64", &wgrad_blocks_3x3c64);
   m.def("wgrad_3x3c64_supported", &wgrad_3x3c64_supported);

@@ -18,6 +18,15 @@ struct ConvWgradArgs {
   int splits, pix_per_split;  // filled by conv_wgrad_plan
   int tile;                   // 64, 128 or 256 (filled by conv_wgrad_plan)
   uint32_t div_pq_mul, div_pq_shift, div_q_mul, div_q_shift;  // FastDiv of Pm*Qm and Qm (launcher)
+  // stem only (f_y != nullptr): dY computed in-kernel from the 3x3/2 max-pool backward + ReLU + BN backward
+  // (dy unused).  f_y: conv output [P][64]; f_dp / f_idx: pooled gradient and argmax [N][f_OH][f_OW][64];
+  // f_coef: BN forward scale, shift; f_bcoef: backward apply A, B, C (64 each)
+  const uint16_t* f_y = nullptr;
+  const uint16_t* f_dp = nullptr;
+  const uint8_t* f_idx = nullptr;
+  const float* f_coef = nullptr;
+  const float* f_bcoef = nullptr;
+  int f_OH = 0, f_OW = 0;
 };
 
 int wgrad_tile(int C, int Kout, int win);  // 256 (ping-pong), 128 or 64

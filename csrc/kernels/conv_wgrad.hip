@@ -193,7 +193,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
 // block stages the dY tile once plus the 4 pair-windows of X (64 pixels x 128 B each, 40 KB per stage,
 // 2 stages -> 2 blocks per CU) and wave t owns pair t's 64 (window column) x 64 (cout) tile over the
 // whole pixel range of its split.  The partial tile goes out through LDS as coalesced float4 rows.
-template <int DT>
+//
+// FUSE: the stem's whole backward tail in this kernel -- dY is never materialised.  Instead of a dY DMA,
+// every K-step's 64 x 64 dY tile is computed from the pooled gradient, the max-pool argmax, the conv
+// output y0 and the BatchNorm coefficients (max-pool backward + ReLU mask + BN-backward apply:
+// dY = A * relu'(sc*y0 + sh) * dz + B * y0 + C) and written to LDS.  A thread owns 8 channels of a
+// horizontal pixel pair (2s, 2s+1) of one conv-output row h: the pair's dz gathers from at most 4
+// pooling windows (rows h>>1 and, for odd h, h>>1 + 1; columns s and s+1).  The loads of step st+1 are
+// issued before step st's MFMAs and consumed after them, so they hide behind the matrix work.  This
+// removes the 1.9 GB dY write and re-read of ResNet-18 at B = 1200 (the separate apply pass).
+template <int DT, bool FUSE>
 __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -213,12 +222,13 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
   const int lrow = lane >> 3, pch = lane & 7;
 
-  // 40 DMA instructions per stage (8 dY + 4 x 8 X), 10 per wave
+  // 40 DMA instructions per stage (8 dY + 4 x 8 X), 10 per wave (FUSE: the 8 dY ones are replaced by
+  // dy_load / dy_store below; m < 2 <=> tile 0)
   auto stage_load = [&](int step, int buf) {
     const int pbase = pix_begin + step * BKP;
     char* sb = smem + buf * STAGE;
 #pragma unroll
-    for (int m = 0; m < 10; ++m) {
+    for (int m = FUSE ? 2 : 0; m < 10; ++m) {
       const int ii = wave + 4 * m;
       const int tile = ii >> 3;                 // 0 = dY, 1..4 = pair tile-1
       const int row = (ii & 7) * 8 + lrow;      // pixel within the step
@@ -240,13 +250,98 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
 
+  // ---- FUSE: dY tile rows 2*pr, 2*pr + 1 (a pixel pair), channels 8*c8 .. 8*c8 + 7 of this thread
+  const int pr = tid >> 3, c8 = tid & 7;
+  float fA[8], fB[8], fC[8], fsc[8], fsh[8];
+  uint4 fy[2], fg[4];
+  uint2 fi[4];
+  int fkh = 0;
+  bool fok = false;
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c8 * 8 + e;
+      fA[e] = a.f_bcoef[c]; fB[e] = a.f_bcoef[64 + c]; fC[e] = a.f_bcoef[128 + c];
+      fsc[e] = a.f_coef[c]; fsh[e] = a.f_coef[64 + c];
+    }
+  }
+  // issue the global loads of step `step`'s dY inputs (y0 of the pair, argmax + gradient of 4 windows)
+  auto dy_load = [&](int step) {
+    const int p0 = pix_begin + step * BKP + 2 * pr;
+    fok = p0 < a.P;  // P is even (Qm even), so the pair is all-in or all-out
+    const int p = fok ? p0 : 0;
+    const FastDiv dpq{a.div_pq_mul, a.div_pq_shift}, dq{a.div_q_mul, a.div_q_shift};
+    const int nimg = (int)fdiv((uint32_t)p, dpq);
+    const int rem = p - nimg * (a.Pm * a.Qm);
+    const int h = (int)fdiv((uint32_t)rem, dq), w = rem - h * a.Qm;  // w even
+    const int oh = h >> 1, s = w >> 1;
+    fkh = h & 1 ? 2 : 1;                        // kernel row of window oh that selects row h
+    const bool okb = (h & 1) && oh + 1 < a.f_OH;  // window oh+1 (kernel row 0) covers odd h
+    const bool oks = s + 1 < a.f_OW;             // window column s+1 (kernel column 0) covers w+1
+    fy[0] = *(const uint4*)(a.f_y + (uint32_t)p * 64u + c8 * 8);
+    fy[1] = *(const uint4*)(a.f_y + (uint32_t)(p + 1) * 64u + c8 * 8);
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const int wr = oh + (wi >> 1), wc = s + (wi & 1);
+      const bool ok = ((wi >> 1) == 0 || okb) && ((wi & 1) == 0 || oks);
+      const uint32_t o = (((uint32_t)nimg * a.f_OH + (ok ? wr : oh)) * a.f_OW + (ok ? wc : s)) * 64u + c8 * 8;
+      fi[wi] = *(const uint2*)(a.f_idx + o);
+      fg[wi] = *(const uint4*)(a.f_dp + o);
+      if (!ok) fi[wi] = make_uint2(0xffffffffu, 0xffffffffu);  // argmax 255 matches no tap
+    }
+  };
+  // finish step's dY (max-pool backward, ReLU mask, BN-backward apply) into LDS buffer `buf`
+  auto dy_store = [&](int buf) {
+    char* sy = smem + buf * STAGE;
+    uint32_t ov[2][4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int sh = 16 * (e & 1);
+      auto pos = [&](int wi) { return (int)(((e < 4 ? fi[wi].x : fi[wi].y) >> (8 * (e & 3))) & 0xffu); };
+      auto grd = [&](int wi) {
+        const uint32_t gw[4] = {fg[wi].x, fg[wi].y, fg[wi].z, fg[wi].w};
+        return E::to_f((uint16_t)(gw[e >> 1] >> sh));
+      };
+      // window (oh, s) selects (h, w) with tap (fkh, 1) and (h, w+1) with (fkh, 2); (oh, s+1) selects
+      // (h, w+1) with (fkh, 0); (oh+1, s): (h, w) with (0, 1), (h, w+1) with (0, 2); (oh+1, s+1): (h, w+1)
+      // with (0, 0)
+      const int p0 = pos(0), p1 = pos(1), p2 = pos(2), p3 = pos(3);
+      const float g0 = grd(0), g1 = grd(1), g2 = grd(2), g3 = grd(3);
+      float dz0 = 0.f, dz1 = 0.f;
+      if (p0 == fkh * 3 + 1) dz0 += g0;
+      if (p2 == 1) dz0 += g2;
+      if (p0 == fkh * 3 + 2) dz1 += g0;
+      if (p1 == fkh * 3) dz1 += g1;
+      if (p2 == 2) dz1 += g2;
+      if (p3 == 0) dz1 += g3;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t yw[4] = {fy[q].x, fy[q].y, fy[q].z, fy[q].w};
+        const float yv = E::to_f((uint16_t)(yw[e >> 1] >> sh));
+        const float dz = yv * fsc[e] + fsh[e] > 0.f ? (q ? dz1 : dz0) : 0.f;
+        const uint32_t r = fok ? (uint32_t)E::from_f(fA[e] * dz + fB[e] * yv + fC[e]) : 0u;
+        if (e & 1) ov[q][e >> 1] |= r << 16; else ov[q][e >> 1] = r;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int row = 2 * pr + q;
+      *(uint4*)(sy + row * ROWB + ((c8 ^ tr_swz(row)) << 4)) = make_uint4(ov[q][0], ov[q][1], ov[q][2], ov[q][3]);
+    }
+  };
+
   if (nsteps > 0) {
+    if constexpr (FUSE) dy_load(0);
     stage_load(0, 0);
+    if constexpr (FUSE) dy_store(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int st = 0; st < nsteps; ++st) {
       const int cur = st & 1;
-      if (st + 1 < nsteps) stage_load(st + 1, cur ^ 1);
+      if (st + 1 < nsteps) {
+        if constexpr (FUSE) dy_load(st + 1);
+        stage_load(st + 1, cur ^ 1);
+      }
       const char* sy = smem + cur * STAGE;
       const char* sx = sy + (1 + wave) * TB;
 #pragma unroll
@@ -271,6 +366,12 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+      if constexpr (FUSE) {
+        if (st + 1 < nsteps) {
+          __builtin_amdgcn_sched_barrier(0);  // keep the dY math (and its load wait) behind the MFMAs
+          dy_store(cur ^ 1);
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -871,10 +972,16 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad128_kernel<kF16>), dim3(nwg), dim3(256), 0, s, a);
   } else if (a.win && a.T == 4 && a.U == 1 && a.C == 64 && a.Kout == 64 && a.ldw >= 256) {
     // ResNet stem (4 kernel-row pairs): one block per split covers all pairs
-    if (dtype == kBF16)
-      hipLaunchKernelGGL((wgrad_stem_kernel<kBF16>), dim3(a.splits), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((wgrad_stem_kernel<kF16>), dim3(a.splits), dim3(256), 0, s, a);
+    if (a.f_y != nullptr) {
+      if (dtype == kBF16)
+        hipLaunchKernelGGL((wgrad_stem_kernel<kBF16, true>), dim3(a.splits), dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((wgrad_stem_kernel<kF16, true>), dim3(a.splits), dim3(256), 0, s, a);
+    } else if (dtype == kBF16) {
+      hipLaunchKernelGGL((wgrad_stem_kernel<kBF16, false>), dim3(a.splits), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((wgrad_stem_kernel<kF16, false>), dim3(a.splits), dim3(256), 0, s, a);
+    }
   } else if (a.win) {
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, true>), dim3(nwg), dim3(256), 0, s, a);

@@ -119,6 +119,8 @@ class ResNetExecutor:
         self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
+        # stem backward: weight gradient with in-kernel dY (PDT_STEM_FUSED=0: separate apply pass + wgrad)
+        self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -635,15 +637,35 @@ class ResNetExecutor:
         # BN-backward sums from the pooled output alone (ReLU mask = out > 0, BN input recovered from out)
         Cn.stem_pool_bwd_reduce_out(g, saved["x0"], sbn.coef, slots, N, P0, Q0, st.cout)
         self._bn_bwd_finish(slots, N * P0 * Q0, sbn)
-        dy0 = self._buf("dy0", N * P0 * Q0 * st.cout)
-        Cn.stem_pool_bwd_apply(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
         ldw = self.stem_pairs * 64
+        if self.stem_fused and self.stem_pairs == 4 and Q0 % 2 == 0:
+            # the stem weight gradient computes its dY tiles itself (max-pool backward + ReLU + BN-backward
+            # apply from g / argmax / y0): the 112x112 dY is never written or re-read
+            def stem_wg():
+                tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
+                key = (st.cout, self.stem_pairs, 1, 64, N * P0 * Q0, True)
+                plan = self._plans.get(key)
+                if plan is None:
+                    plan = tuple(Cn.conv_wgrad_plan(st.cout, self.stem_pairs, 1, 64, N * P0 * Q0, self.wgrad_blocks,
+                                                    True))[:2]
+                    self._plans[key] = plan
+                splits, pps = plan
+                ws = self._buf("ws", splits * st.cout * ldw, torch.float32)
+                Cn.conv_wgrad_stem_fused(saved["xp"], g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, ws, N,
+                                         saved["Hp"], saved["Wp"], self.stem_pairs, P0, Q0, st.st, 2, ldw, splits, pps)
+                Cn.wgrad_reduce(ws, splits, st.cout, ldw, ldw, st.cout * ldw, tmp, ldw, 1.0, False)
+                Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
+                self.grad_ready(st.pid)
+            self._side_wgrad(g, stem_wg)
+        else:
+            dy0 = self._buf("dy0", N * P0 * Q0 * st.cout)
+            Cn.stem_pool_bwd_apply(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
 
-        def stem_wg():
-            tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
-            self._wgrad(st.cout, saved["xp"], dy0, N, saved["Hp"], saved["Wp"], 64, self.stem_pairs, 1, P0, Q0,
-                        st.st, 0, tmp, ldw, cs=4, win=True, dil=2)
-            Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
-            self.grad_ready(st.pid)
-        self._side_wgrad(dy0, stem_wg)
+            def stem_wg():
+                tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
+                self._wgrad(st.cout, saved["xp"], dy0, N, saved["Hp"], saved["Wp"], 64, self.stem_pairs, 1, P0, Q0,
+                            st.st, 0, tmp, ldw, cs=4, win=True, dil=2)
+                Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
+                self.grad_ready(st.pid)
+            self._side_wgrad(dy0, stem_wg)
         self._join_side()

@@ -271,6 +271,73 @@ def test_stem_pool_backward_fused():
     assert _rel(dy.permute(0, 3, 1, 2), xin.grad) < 2e-2
 
 
+@pytest.mark.parametrize("geom", [(2, 29, 28), (3, 28, 36)])
+def test_stem_wgrad_fused_dy(geom):
+    """Stem weight gradient with dY computed in-kernel (max-pool bwd + ReLU + BN-bwd apply) vs the two-pass
+    path (stem_pool_bwd_apply -> window-mode conv_wgrad) and vs an fp32 autograd reference.  The second
+    geometry has an even conv-output height and a pooled width whose last window column is out of range
+    for the last pixel pair (boundary windows), both have a partial last K-step."""
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(9)
+    N, H, W = geom
+    K = C = 64
+    P, Q = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = max(H + 6, 2 * (P - 1) + 8), max(W + 6, 2 * (Q - 1) + 8)
+    x = torch.randn(N, 3, H, W, device=DEV)
+    xp = torch.empty(N * Hp * Wp * 4, dtype=torch.bfloat16, device=DEV)
+    native.C.stem_pack(x, xp, N, 3, H, W, 3, Hp, Wp)
+    y = _rand16(N, P, Q, C)  # stands in for the stem conv output
+    yf = y.float()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.2
+    mean = yf.mean((0, 1, 2))
+    invstd = torch.rsqrt(yf.var((0, 1, 2), unbiased=False) + 1e-5)
+    scale = gamma * invstd
+    coef = torch.cat([scale, beta - mean * scale, mean, invstd]).contiguous()
+    OH, OW = (P - 1) // 2 + 1, (Q - 1) // 2 + 1
+    out = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=DEV)
+    idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=DEV)
+    native.C.bn_relu_maxpool(y, coef, out, idx, N, P, Q, C)
+    dp = _rand16(N, OH, OW, C)
+    slots = torch.zeros(native.C.stat_slots() * C * 2, dtype=torch.float64, device=DEV)
+    native.C.stem_pool_bwd_reduce_out(dp, out, coef, slots, N, P, Q, C)
+    sums = torch.empty(2 * C, dtype=torch.float64, device=DEV)
+    native.C.bn_slot_sum(slots, C, 2, sums)
+    dgamma, dbeta, bcoef = torch.empty(C, device=DEV), torch.empty(C, device=DEV), torch.empty(3 * C, device=DEV)
+    native.C.bn_bwd_finalize(sums, float(N * P * Q), coef, gamma, dgamma, dbeta, 1.0, bcoef)
+    pairs, ldw = 4, 256
+    splits, pps, _ = native.C.conv_wgrad_plan(K, pairs, 1, 64, N * P * Q, 64, True)
+    # two-pass path
+    dy = torch.empty_like(y)
+    native.C.stem_pool_bwd_apply(dp, idx, y, coef, bcoef, dy, N, P, Q, C)
+    ws = torch.empty(splits * K * ldw, device=DEV)
+    native.C.conv_wgrad(xp, dy, ws, N, Hp, Wp, 64, K, pairs, 1, P, Q, 2, 2, 0, 0, 2, 2, ldw, splits, pps, 4, True)
+    t1 = torch.empty(K * ldw, device=DEV)
+    native.C.wgrad_reduce(ws, splits, K, ldw, ldw, K * ldw, t1, ldw, 1.0, False)
+    # fused path
+    ws2 = torch.full_like(ws, float("nan"))
+    native.C.conv_wgrad_stem_fused(xp, dp, idx, y, coef, bcoef, ws2, N, Hp, Wp, pairs, P, Q, 2, 2, ldw, splits, pps)
+    t2 = torch.empty(K * ldw, device=DEV)
+    native.C.wgrad_reduce(ws2, splits, K, ldw, ldw, K * ldw, t2, ldw, 1.0, False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(t2).all()
+    assert _rel(t2, t1) < 2e-3
+    # fp32 reference: autograd through BN -> ReLU -> max-pool gives dY, conv2d_weight gives dW
+    xin = yf.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    z = F.batch_norm(xin, None, None, gamma, beta, training=True, eps=1e-5)
+    F.max_pool2d(torch.relu(z), 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
+    xr = x.to(torch.bfloat16).float()
+    refw = torch.nn.grad.conv2d_weight(xr, (K, 3, 7, 7), xin.grad, stride=2, padding=3)
+    kk = torch.arange(K).view(-1, 1, 1, 1)
+    rr = torch.arange(7).view(1, -1, 1, 1)
+    ss = torch.arange(7).view(1, 1, -1, 1)
+    cc = torch.arange(3).view(1, 1, 1, -1)
+    gidx = (kk * ldw + (rr // 2) * 64 + (rr % 2) * 32 + ss * 4 + cc).reshape(-1).to(torch.int32).to(DEV)
+    dw = torch.empty(K * 7 * 7 * 3, device=DEV)
+    native.C.gather32(t2, gidx, dw)
+    assert _rel(dw.view(K, 7, 7, 3).permute(0, 3, 1, 2), refw) < 3e-2
+
+
 def test_stem_kernel_persistent_tiles():
     """Stem kernel with more tiles than blocks (persistent loop + next-tile prefetch) vs F.conv2d."""
     from pytorch_distributed_template_amd.ops import native
