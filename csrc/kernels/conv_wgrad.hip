@@ -255,8 +255,8 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
   float fA[8], fB[8], fC[8], fsc[8], fsh[8];
   uint4 fy[2], fg[4];
   uint2 fi[4];
-  int fkh = 0;
-  bool fok = false;
+  int fkh = 0, fv = 0;  // fv: bit wi = window wi exists (applied in dy_store: a select right after the
+  bool fok = false;     // loads would make the wave wait for them before the MFMAs)
   if constexpr (FUSE) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -287,12 +287,13 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
       const uint32_t o = (((uint32_t)nimg * a.f_OH + (ok ? wr : oh)) * a.f_OW + (ok ? wc : s)) * 64u + c8 * 8;
       fi[wi] = *(const uint2*)(a.f_idx + o);
       fg[wi] = *(const uint4*)(a.f_dp + o);
-      if (!ok) fi[wi] = make_uint2(0xffffffffu, 0xffffffffu);  // argmax 255 matches no tap
     }
+    fv = 1 | (okb ? 4 : 0) | (oks ? 2 : 0) | (okb && oks ? 8 : 0);
   };
   // finish step's dY (max-pool backward, ReLU mask, BN-backward apply) into LDS buffer `buf`
   auto dy_store = [&](int buf) {
     char* sy = smem + buf * STAGE;
+    const uint32_t keep = fok ? 0xffffffffu : 0u;  // pixels past the end: zero rows (branch-free)
     uint32_t ov[2][4];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
       // window (oh, s) selects (h, w) with tap (fkh, 1) and (h, w+1) with (fkh, 2); (oh, s+1) selects
       // (h, w+1) with (fkh, 0); (oh+1, s): (h, w) with (0, 1), (h, w+1) with (0, 2); (oh+1, s+1): (h, w+1)
       // with (0, 0)
-      const int p0 = pos(0), p1 = pos(1), p2 = pos(2), p3 = pos(3);
+      const int p0 = pos(0), p1 = fv & 2 ? pos(1) : 255, p2 = fv & 4 ? pos(2) : 255, p3 = fv & 8 ? pos(3) : 255;
       const float g0 = grd(0), g1 = grd(1), g2 = grd(2), g3 = grd(3);
       float dz0 = 0.f, dz1 = 0.f;
       if (p0 == fkh * 3 + 1) dz0 += g0;
@@ -319,29 +320,34 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
         const uint32_t yw[4] = {fy[q].x, fy[q].y, fy[q].z, fy[q].w};
         const float yv = E::to_f((uint16_t)(yw[e >> 1] >> sh));
         const float dz = yv * fsc[e] + fsh[e] > 0.f ? (q ? dz1 : dz0) : 0.f;
-        const uint32_t r = fok ? (uint32_t)E::from_f(fA[e] * dz + fB[e] * yv + fC[e]) : 0u;
+        const uint32_t r = (uint32_t)E::from_f(__builtin_fmaf(fA[e], dz, __builtin_fmaf(fB[e], yv, fC[e])));
         if (e & 1) ov[q][e >> 1] |= r << 16; else ov[q][e >> 1] = r;
       }
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int row = 2 * pr + q;
-      *(uint4*)(sy + row * ROWB + ((c8 ^ tr_swz(row)) << 4)) = make_uint4(ov[q][0], ov[q][1], ov[q][2], ov[q][3]);
+      *(uint4*)(sy + row * ROWB + ((c8 ^ tr_swz(row)) << 4)) =
+          make_uint4(ov[q][0] & keep, ov[q][1] & keep, ov[q][2] & keep, ov[q][3] & keep);
     }
   };
 
+  // FUSE schedule: step st+1's dY inputs are loaded at the end of step st-1 (after that step's dY tile
+  // was stored), so they have all of step st (DMA issue + MFMAs) to arrive; step st ends with one
+  // vmcnt(0) covering both the X-tile DMA and those loads, then stores the dY tile of st+1 and issues
+  // the loads of st+2.  One register set suffices and no load is waited for ahead of the MFMAs.
   if (nsteps > 0) {
     if constexpr (FUSE) dy_load(0);
     stage_load(0, 0);
-    if constexpr (FUSE) dy_store(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (FUSE) {
+      dy_store(0);
+      if (nsteps > 1) dy_load(1);
+    }
     __syncthreads();
     for (int st = 0; st < nsteps; ++st) {
       const int cur = st & 1;
-      if (st + 1 < nsteps) {
-        if constexpr (FUSE) dy_load(st + 1);
-        stage_load(st + 1, cur ^ 1);
-      }
+      if (st + 1 < nsteps) stage_load(st + 1, cur ^ 1);
       const char* sy = smem + cur * STAGE;
       const char* sx = sy + (1 + wave) * TB;
 #pragma unroll
@@ -367,13 +373,15 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
       }
+      if constexpr (FUSE) __builtin_amdgcn_sched_barrier(0);  // the wait stays behind the last MFMA
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (FUSE) {
         if (st + 1 < nsteps) {
-          __builtin_amdgcn_sched_barrier(0);  // keep the dY math (and its load wait) behind the MFMAs
+          __builtin_amdgcn_sched_barrier(0);  // keep the dY math behind the MFMAs and the wait
           dy_store(cur ^ 1);
+          if (st + 2 < nsteps) dy_load(st + 2);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   }

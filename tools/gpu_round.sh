@@ -30,6 +30,14 @@ for stage in "$@"; do
       cd "${GRAFT_REPO_ROOT:-/root/repo}"
       tail -5 gpurun_out/prof.log
       [ $rc -eq 0 ] || { echo "prof failed rc=$rc"; exit $rc; } ;;
+    profserial)
+      # one stream (PDT_WGRAD_STREAM=0) so per-kernel durations are not inflated by concurrency
+      cd /tmp && export TMPDIR=/tmp
+      PDT_WGRAD_STREAM=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/profs" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/profs.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      tail -2 gpurun_out/profs.log
+      [ $rc -eq 0 ] || { echo "prof failed rc=$rc"; exit $rc; } ;;
     convbench)
       timeout -k 10 600 python tools/conv_bench.py > gpurun_out/conv_bench.log 2>&1; rc=$?
       cat gpurun_out/conv_bench.log | grep shape
