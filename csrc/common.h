@@ -108,6 +108,23 @@ PDT_DEVICE void buf_lds16_asm(__amdgpu_buffer_rsrc_t r, void* lds_dst, uint32_t 
                : "m0");
 }
 
+// Global loads through inline asm, for kernels that count their vector-memory operations themselves
+// (mixed with buf_lds16_asm): the compiler neither waits for them nor knows they are in flight, so the
+// caller MUST s_waitcnt before any use -- with the loaded values as "+v" operands of that wait asm, so
+// the uses cannot be scheduled ahead of it.
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+PDT_DEVICE u32x4v gload16_asm(const void* p) {
+  u32x4v v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+PDT_DEVICE u32x2v gload8_asm(const void* p) {
+  u32x2v v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+
 // XCD-aware bijective remap of a 1-D block index: blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so give each XCD a contiguous range of logical tiles
 // (speed only, never correctness: any placement is valid).

@@ -250,11 +250,30 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
 
+  // FUSE: the 8 X-tile DMAs of a wave cover only two pixel rows (wave*8 + lrow and (wave+4)*8 + lrow),
+  // once per kernel-row pair; the pairs differ by a constant image-row offset, so the pixel decode runs
+  // twice per step instead of once per DMA.  Same rows / LDS slots as stage_load's m = 2..9.
+  const uint32_t pair_step = (uint32_t)a.dil_h * a.W * a.cs * 2u;
+  auto stage_load_x = [&](int step, int buf) {
+    const int pbase = pix_begin + step * BKP;
+    char* sb = smem + buf * STAGE;
+    const int ra = wave * 8 + lrow, rb = ra + 32;
+    const int lch = pch ^ tr_swz(ra);  // == pch ^ tr_swz(rb): the swizzle reads row bits 1 and 3
+    uint32_t xa, xb, unused;
+    wgrad_rows<true>(a, pbase + ra, -a.pad_h, 0, 0, lch, 0, xa, unused);
+    wgrad_rows<true>(a, pbase + rb, -a.pad_h, 0, 0, lch, 0, xb, unused);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      buf_lds16_asm(rx, sb + (1 + t) * TB + wave * 1024, xa + t * pair_step);
+      buf_lds16_asm(rx, sb + (1 + t) * TB + (wave + 4) * 1024, xb + t * pair_step);
+    }
+  };
+
   // ---- FUSE: dY tile rows 2*pr, 2*pr + 1 (a pixel pair), channels 8*c8 .. 8*c8 + 7 of this thread
   const int pr = tid >> 3, c8 = tid & 7;
   float fA[8], fB[8], fC[8], fsc[8], fsh[8];
-  uint4 fy[2], fg[4];
-  uint2 fi[4];
+  u32x4v fy[2], fg[4];  // loaded through inline asm (gload*_asm): invisible to the compiler's waitcnt pass,
+  u32x2v fi[4];         // waited for by FUSE_WAIT, which also carries them as operands (see the loop)
   int fkh = 0, fv = 0;  // fv: bit wi = window wi exists (applied in dy_store: a select right after the
   bool fok = false;     // loads would make the wave wait for them before the MFMAs)
   if constexpr (FUSE) {
@@ -278,15 +297,15 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
     fkh = h & 1 ? 2 : 1;                        // kernel row of window oh that selects row h
     const bool okb = (h & 1) && oh + 1 < a.f_OH;  // window oh+1 (kernel row 0) covers odd h
     const bool oks = s + 1 < a.f_OW;             // window column s+1 (kernel column 0) covers w+1
-    fy[0] = *(const uint4*)(a.f_y + (uint32_t)p * 64u + c8 * 8);
-    fy[1] = *(const uint4*)(a.f_y + (uint32_t)(p + 1) * 64u + c8 * 8);
+    fy[0] = gload16_asm(a.f_y + (uint32_t)p * 64u + c8 * 8);
+    fy[1] = gload16_asm(a.f_y + (uint32_t)(p + 1) * 64u + c8 * 8);
 #pragma unroll
     for (int wi = 0; wi < 4; ++wi) {
       const int wr = oh + (wi >> 1), wc = s + (wi & 1);
       const bool ok = ((wi >> 1) == 0 || okb) && ((wi & 1) == 0 || oks);
       const uint32_t o = (((uint32_t)nimg * a.f_OH + (ok ? wr : oh)) * a.f_OW + (ok ? wc : s)) * 64u + c8 * 8;
-      fi[wi] = *(const uint2*)(a.f_idx + o);
-      fg[wi] = *(const uint4*)(a.f_dp + o);
+      fi[wi] = gload8_asm(a.f_idx + o);
+      fg[wi] = gload16_asm(a.f_dp + o);
     }
     fv = 1 | (okb ? 4 : 0) | (oks ? 2 : 0) | (okb && oks ? 8 : 0);
   };
@@ -336,18 +355,40 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
   // was stored), so they have all of step st (DMA issue + MFMAs) to arrive; step st ends with one
   // vmcnt(0) covering both the X-tile DMA and those loads, then stores the dY tile of st+1 and issues
   // the loads of st+2.  One register set suffices and no load is waited for ahead of the MFMAs.
+  // The dY-input loads are asm (the compiler would wait vmcnt(0) for them, draining the X-tile DMA
+  // too); FUSE_WAIT(n) waits for all but the n youngest vector-memory ops and takes the loaded
+  // registers as in/out operands, so no use of them can be scheduled ahead of it.  Per step st the
+  // queue is [loads(st+1): 10][DMA(st+1): 8] at the dY store (vmcnt(8): the DMA stays in flight under
+  // the dY math), then [DMA(st+1): 8][loads(st+2): 10] before the barrier (vmcnt(10)).
+#define FUSE_WAIT(n)                                                                                   \
+  asm volatile("s_waitcnt vmcnt(" #n ")"                                                               \
+               : "+v"(fy[0]), "+v"(fy[1]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]), "+v"(fi[3]), "+v"(fg[0]), \
+                 "+v"(fg[1]), "+v"(fg[2]), "+v"(fg[3])                                                 \
+               :                                                                                       \
+               : "memory")
   if (nsteps > 0) {
-    if constexpr (FUSE) dy_load(0);
-    stage_load(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (FUSE) {
+      dy_load(0);
+      stage_load_x(0, 0);
+    } else {
+      stage_load(0, 0);
+    }
+    if constexpr (FUSE) {
+      FUSE_WAIT(0);
       dy_store(0);
       if (nsteps > 1) dy_load(1);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     for (int st = 0; st < nsteps; ++st) {
       const int cur = st & 1;
-      if (st + 1 < nsteps) stage_load(st + 1, cur ^ 1);
+      if (st + 1 < nsteps) {
+        if constexpr (FUSE)
+          stage_load_x(st + 1, cur ^ 1);
+        else
+          stage_load(st + 1, cur ^ 1);
+      }
       const char* sy = smem + cur * STAGE;
       const char* sx = sy + (1 + wave) * TB;
 #pragma unroll
@@ -373,18 +414,28 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
       }
-      if constexpr (FUSE) __builtin_amdgcn_sched_barrier(0);  // the wait stays behind the last MFMA
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (FUSE) {
+        __builtin_amdgcn_sched_barrier(0);  // the waits and the dY math stay behind the last MFMA
         if (st + 1 < nsteps) {
-          __builtin_amdgcn_sched_barrier(0);  // keep the dY math behind the MFMAs and the wait
+          FUSE_WAIT(8);
+          __builtin_amdgcn_sched_barrier(0);
           dy_store(cur ^ 1);
-          if (st + 2 < nsteps) dy_load(st + 2);
+          if (st + 2 < nsteps) {
+            dy_load(st + 2);
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
     }
   }
+#undef FUSE_WAIT
   // acc[i][j]: rows (window column) c = 16i + 4*(lane>>4) + r, col k = 16j + (lane&15); transpose
   // through LDS ([4 pairs][64 k][64 c]) and write ws[split][k][pair*64 + c] as float4 rows
   float* red = (float*)smem;
