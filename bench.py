@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--graph", action="store_true", help="replay the training step as a captured HIP graph")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, the benchmark) or gloo (multi-rank rehearsal on fewer GPUs than ranks)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -47,10 +49,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":  # rehearsal: ranks may share a GPU
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     torch.manual_seed(0)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     model = registry.create(args.arch)

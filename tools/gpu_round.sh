@@ -60,6 +60,20 @@ for stage in "$@"; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
       tail -5 gpurun_out/smoke.log
       [ $rc -eq 0 ] || { echo "smoke failed rc=$rc"; exit $rc; } ;;
+    rehearse2)
+      # 2 DDP ranks sharing the one GPU over gloo: exercises the world>1 native-trainer path
+      # (bucketer, buffer broadcast, metric all-reduce, side-stream ordering) without a second GPU
+      timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --batch-per-gpu 256 \
+        > gpurun_out/rehearse2.log 2>&1; rc=$?
+      grep metric gpurun_out/rehearse2.log
+      [ $rc -eq 0 ] || { tail -30 gpurun_out/rehearse2.log; echo "rehearse2 failed rc=$rc"; exit $rc; } ;;
+    rehearse2sbn)
+      timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29612 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --batch-per-gpu 256 \
+        --sync-bn --dtype fp16 > gpurun_out/rehearse2sbn.log 2>&1; rc=$?
+      grep metric gpurun_out/rehearse2sbn.log
+      [ $rc -eq 0 ] || { tail -30 gpurun_out/rehearse2sbn.log; echo "rehearse2sbn failed rc=$rc"; exit $rc; } ;;
   esac
 done
 echo "ALL DONE"
