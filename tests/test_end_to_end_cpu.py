@@ -86,3 +86,28 @@ def test_evaluate_only(tmp_path):
     r = _run(["dataparallel.py", "--outpath", out, "-b", "8", "-e", "True"] + COMMON)
     log = open(os.path.join(out + "_resnet18", "experiment.log")).read()
     assert "Val epoch: [-1/2]" in log and "Train epoch" not in log
+
+
+def test_two_simulated_nodes_cpu(tmp_path):
+    """2 "nodes" x 2 ranks on localhost (SURVEY §4 layer 2): two launchers with --nnodes 2 --node_rank r
+    rendezvous on one master; only global rank 0 writes the output directory."""
+    out = str(tmp_path / "output_2n")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="1")
+    procs = []
+    for node in (0, 1):
+        cmd = [sys.executable, "-m", "pytorch_distributed_template_amd.launch", "--nnodes=2", f"--node_rank={node}",
+               "--nproc_per_node=2", "--master_addr=127.0.0.1", "--master_port=29617", "distributed.py",
+               "--outpath", out, "-b", "16"] + COMMON
+        procs.append(subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    for p in procs:
+        o, _ = p.communicate(timeout=600)
+        outs.append(o)
+        assert p.returncode == 0, o[-3000:]
+    log, _ = _check_outdir(out + "_resnet18")
+    assert "world: 4" in log
+    settings = open(os.path.join(out + "_resnet18", "settings.log")).read()
+    assert "nprocs: 4" in settings
+    # node 1 hosts global ranks 2, 3: no rank-0 duties there
+    assert "Train epoch" not in outs[1]
