@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--graph", action="store_true", help="replay the training step as a captured HIP graph")
+    ap.add_argument("--autotune", action="store_true", help="time every conv tile candidate once per shape")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the benchmark) or gloo (multi-rank rehearsal on fewer GPUs than ranks)")
     args = ap.parse_args()
@@ -63,7 +64,7 @@ def main():
     model = registry.create(args.arch)
     tr = NativeTrainer(model, dev, dtype=dtype, lr=0.1, momentum=0.9, weight_decay=1e-4,
                        use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb,
-                       graph=args.graph)
+                       graph=args.graph, autotune=args.autotune)
     B = args.batch_per_gpu
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -77,6 +78,9 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    if args.autotune and rank == 0:
+        for k, v in tr.executor._tiles.items():
+            print("tile", k, v, file=sys.stderr)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -60,6 +60,10 @@ for stage in "$@"; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
       tail -5 gpurun_out/smoke.log
       [ $rc -eq 0 ] || { echo "smoke failed rc=$rc"; exit $rc; } ;;
+    autotune)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 --autotune > gpurun_out/bench_autotune.log 2>&1; rc=$?
+      grep metric gpurun_out/bench_autotune.log
+      [ $rc -eq 0 ] || { echo "autotune bench failed rc=$rc"; exit $rc; } ;;
     rehearse2)
       # 2 DDP ranks sharing the one GPU over gloo: exercises the world>1 native-trainer path
       # (bucketer, buffer broadcast, metric all-reduce, side-stream ordering) without a second GPU
