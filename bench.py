@@ -101,7 +101,8 @@ def main():
     value = world * B * args.steps / el
     if rank == 0:
         print(json.dumps({
-            "metric": "images/sec (node) ResNet-18 DDP bs=1200/GPU at 1/2/4/8 MI355X",
+            "metric": "images/sec (node) ResNet-18 DDP bs=1200/GPU at 1/2/4/8 MI355X" if args.arch == "resnet18"
+            else f"images/sec (node) {args.arch} DDP bs={B}/GPU",
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / REF_IMG_PER_S, 3), "dtype": args.dtype, "data": "synthetic",
