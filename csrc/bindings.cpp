@@ -172,7 +172,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
                      int64_t Q, int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride,
                      const std::vector<std::vector<int64_t>>& phases, int64_t bm, int64_t bn, int64_t bk, int64_t bnb,
                      const OptT& bn_y1, const OptT& bn_coef1, const OptT& bn_y2, const OptT& bn_coef2,
-                     const OptT& bn_mask, const OptT& bn_slots) {
+                     const OptT& bn_mask, const OptT& bn_slots, int64_t res_phase) {
   const int dt = dt16(dy, "dy");
   TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "conv_dgrad: mixed dtypes");
   TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv_dgrad: size mismatch");
@@ -184,10 +184,20 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
   a.x = p16(dy, "dy");
   a.w = p16(wt, "wt");
   a.y = p16(dx, "dx");
+  TORCH_CHECK(res_phase < (int64_t)phases.size() && (res_phase < 0 || res.has_value()), "conv_dgrad: bad res_phase");
   if (res.has_value()) {
-    TORCH_CHECK(res->numel() == dx.numel(), "conv_dgrad: residual size mismatch");
+    if (res_phase >= 0) {  // compact residual of one phase: [N * Pm * Qm][C] of that phase
+      const auto& f = phases[res_phase];
+      TORCH_CHECK(f.size() == 7, "conv_dgrad: phase = (ph, pw, T, U, ioff_h, ioff_w, woff)");
+      const int64_t Pm = (H - f[0] + stride - 1) / stride, Qm = (W - f[1] + stride - 1) / stride;
+      TORCH_CHECK(res->numel() == N * Pm * Qm * C, "conv_dgrad: compact residual size mismatch");
+    } else {
+      TORCH_CHECK(res->numel() == dx.numel(), "conv_dgrad: residual size mismatch");
+    }
+    TORCH_CHECK(dt16(*res, "res") == dt, "conv_dgrad: residual dtype");
     a.res = p16(*res, "res");
   }
+  a.res_phase = (int)res_phase;
   a.N = N; a.H = P; a.W = Q; a.C = K; a.cs = K; a.Kout = C;
   a.ist_h = 1; a.ist_w = 1; a.tstep_h = -1; a.tstep_w = -1;
   a.OH = H; a.OW = W; a.ost_h = stride; a.ost_w = stride;
@@ -233,7 +243,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
 void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
                 int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride, const std::vector<std::vector<int64_t>>& phases,
                 int64_t bm, int64_t bn, int64_t bk) {
-  conv_dgrad_impl(dy, wt, dx, res, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk, 0, {}, {}, {}, {}, {}, {});
+  conv_dgrad_impl(dy, wt, dx, res, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk, 0, {}, {}, {}, {}, {}, {}, -1);
 }
 
 std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks,

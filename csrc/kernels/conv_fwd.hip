@@ -99,9 +99,12 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
                      : (4 * PER_J <= BUDGET && FM % 4 == 0) ? 4
                      : (2 * PER_J <= BUDGET && FM % 2 == 0) ? 2 : 1;
   static_assert(FM % JC == 0, "epilogue chunking");
+  // compact per-phase residual (see ConvFwdArgs::res_phase): absent on the other phases (block-uniform)
+  const bool has_res = RES && a.res != nullptr;
+  const bool res_compact = RES && a.res_phase >= 0;
 #pragma unroll
   for (int jc = 0; jc < FM; jc += JC) {
-    int64_t obase[JC];
+    int64_t obase[JC], rbase[RES ? JC : 1];
     bool valid[JC];
 #pragma unroll
     for (int jj = 0; jj < JC; ++jj) {
@@ -113,6 +116,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
       const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
       const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
       obase[jj] = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+      if constexpr (RES) rbase[jj] = res_compact ? (int64_t)mm * a.Kout : obase[jj];
     }
     uint2 p_res[RES ? JC : 1][RES ? FN : 1], p_y1[LY1 ? JC : 1][LY1 ? FN : 1], p_y2[LY2 ? JC : 1][LY2 ? FN : 1];
     uint32_t p_m[LM ? JC : 1][LM ? FN : 1];
@@ -121,7 +125,8 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int64_t o = obase[jj] + n0 + wn * WN + i * 16 + 4 * fq;
-        if constexpr (RES) p_res[jj][i] = *(const uint2*)(a.res + o);
+        if constexpr (RES)
+          p_res[jj][i] = has_res ? *(const uint2*)(a.res + rbase[jj] + (o - obase[jj])) : uint2{0u, 0u};
         if constexpr (LY1) p_y1[jj][i] = *(const uint2*)(a.bn_y1 + o);
         if constexpr (LY2) p_y2[jj][i] = *(const uint2*)(a.bn_y2 + o);
         if constexpr (LM) p_m[jj][i] = (uint32_t)a.bn_mask[o >> 3] >> ((int)o & 4);
@@ -257,6 +262,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
     a.w = args.w + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
+    if (args.res_phase >= 0 && ph != args.res_phase) a.res = nullptr;
     if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
   }
   using E = E16<DT>;
@@ -487,6 +493,7 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
     a.w = args.w + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
+    if (args.res_phase >= 0 && ph != args.res_phase) a.res = nullptr;
     if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
   }
   using E = E16<DT>;

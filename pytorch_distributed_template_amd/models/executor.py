@@ -121,6 +121,8 @@ class ResNetExecutor:
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
         # stem backward: weight gradient with in-kernel dY (PDT_STEM_FUSED=0: separate apply pass + wgrad)
         self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
+        # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad (PDT_COMPACT_DS=0: off)
+        self.compact_ds = os.environ.get("PDT_COMPACT_DS", "1") == "1"
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -323,11 +325,16 @@ class ResNetExecutor:
         self.C.bn_eval_coef(self._p(bn.gslot), self._p(bn.bslot), bn.mod.running_mean, bn.mod.running_var,
                             bn.eps, bn.coef)
 
-    def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None, bnb=None):
+    def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None, bnb=None,
+                 res_phase: int = -1, compact: bool = False):
         """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``.
 
         ``bnb`` = (mode, y1, coef1, y2, coef2, out_mask, slots): fuse the consuming BatchNorm's backward
-        reduce into the data-gradient epilogue (``dx`` then holds dz = dx * relu'; see conv_fwd.h)."""
+        reduce into the data-gradient epilogue (``dx`` then holds dz = dx * relu'; see conv_fwd.h).
+        ``res_phase >= 0``: ``res`` is compact and belongs to that sub-pixel phase only (conv_fwd.h).
+        ``compact``: a 1x1 strided conv's data gradient written only on its nonzero phase (0, 0), as a dense
+        [N, P, Q, Cin] tensor -- a stride-1 GEMM over the P x Q pixels (the zeros of the other phases are
+        neither written nor re-read by the consumer)."""
         # --- wgrad
         if wgrad_geom is None:
             xg, Hx, Wx, Cx, R, S, st, pad = x, H, W, c.cin, c.R, c.S, c.st, c.pad
@@ -341,16 +348,22 @@ class ResNetExecutor:
         if dx is None:
             return
         bk = 64 if c.cout % 64 == 0 else 32
-        phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
-                  if H - ph > 0 and W - pw > 0]
+        dst = c.st
+        if compact:
+            ph0 = c.phases[0]
+            assert c.R == 1 and c.S == 1 and c.pad == 0 and tuple(ph0[:6]) == (0, 0, 1, 1, 0, 0), "compact: 1x1 only"
+            phases, H, W, dst = [[0, 0, 1, 1, 0, 0, ph0[6]]], P, Q, 1
+        else:
+            phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
+                      if H - ph > 0 and W - pw > 0]
 
         def launch(bm, bn):
-            if bnb is None:
-                self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn, bk)
+            if bnb is None and res_phase < 0:
+                self.C.conv_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, dst, phases, bm, bn, bk)
             else:
-                self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, bm, bn,
-                                     bk, *bnb)
-        key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, c.st, res is not None, bnb[0] if bnb else 0)
+                self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, dst, phases, bm, bn,
+                                     bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
+        key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
         bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
         launch(bm, bn)
 
@@ -587,11 +600,21 @@ class ResNetExecutor:
                                 convs[-1].cout)
             # gradient w.r.t. the block input accumulates in g_next
             gnext = self._buf("g_b" if gsel == 0 else "g_a", N * Hin * Win * Cin)
+            res_phase = -1
             if ds:
                 dc = b["ds_conv"]
                 P, Q = dc.out_hw(Hin, Win)
-                self.conv_bwd(dc, x, N, Hin, Win, dyd, P, Q, gnext)  # writes every element of gnext
-                res = gnext
+                c0 = convs[0]
+                if (self.compact_ds and dc.R == 1 and dc.st == 2 and dc.pad == 0 and c0.st == 2 and c0.R == 3
+                        and c0.S == 3 and c0.pad == 1):
+                    # the 1x1/2 downsample's data gradient is nonzero only on sub-pixel phase (0, 0), which is
+                    # exactly phase 0 of the 3x3/2 conv's dgrad: write it compact and let that phase add it
+                    res = self._buf("ds_compact", N * P * Q * Cin)
+                    self.conv_bwd(dc, x, N, Hin, Win, dyd, P, Q, res, compact=True)
+                    res_phase = 0
+                else:
+                    self.conv_bwd(dc, x, N, Hin, Win, dyd, P, Q, gnext)  # writes every element of gnext
+                    res = gnext
             else:
                 res = dz
             # chain through the block's convs in reverse
@@ -622,10 +645,10 @@ class ResNetExecutor:
                     slots = self._buf(("bnslots", c.cin, K), self.n_slots * c.cin * K, torch.float64)
                     bnb = (3 if pds else 2, prec["ys"][-1], pb["bns"][-1].coef, prec["yd"] if pds else None,
                            pb["ds_bn"].coef if pds else None, prec["omask"], slots)
-                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, bnb=bnb)
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, bnb=bnb, res_phase=res_phase)
                     g_fused = slots
                 else:
-                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res)
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, res_phase=res_phase)
                     g_fused = None
             g = gnext
             gsel ^= 1

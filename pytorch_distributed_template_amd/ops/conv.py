@@ -101,12 +101,14 @@ def pack_relu_mask(out: torch.Tensor) -> torch.Tensor:
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 1, pad: int = 0,
                residual: Optional[torch.Tensor] = None, bnb: Optional[tuple] = None,
-               tile: Optional[Tuple[int, int, int]] = None) -> torch.Tensor:
+               tile: Optional[Tuple[int, int, int]] = None, res_phase: int = -1) -> torch.Tensor:
     """dX (NHWC, [N, H, W, Cin]) of ``y = conv(x, w)`` given dY ([N, P, Q, Cout]).
 
     ``bnb = (mode, y1, coef1, y2, coef2, out_mask, slots)`` fuses the consuming BatchNorm's backward
     reduce into the epilogue (the result is then dz = dX * relu'; sums land in ``slots``); ``out_mask`` is
-    the block output's ReLU bitmask (:func:`pack_relu_mask`, modes 2/3)."""
+    the block output's ReLU bitmask (:func:`pack_relu_mask`, modes 2/3).  ``res_phase >= 0``: ``residual`` is
+    compact ([N, ceil(H/stride), ceil(W/stride), Cin]) and added on that sub-pixel phase only (index into the
+    phases kept for this launch), e.g. a 1x1/2 downsample's data gradient added to a 3x3/2 one."""
     N, P, Q, K = dy.shape
     K2, R, S, C = w.shape
     assert K == K2
@@ -126,10 +128,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
         phases.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, off])
         off += idx.numel()
     wt = torch.cat(pieces).contiguous() if pieces else torch.zeros(1, dtype=w.dtype, device=w.device)
-    if bnb is None:
+    if bnb is None and res_phase < 0:
         native.C.conv_dgrad(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk)
     else:
-        native.C.conv_dgrad_bn(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk, *bnb)
+        native.C.conv_dgrad_bn(dy, wt, dx, residual, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk,
+                               *(bnb or (0, None, None, None, None, None, None)), res_phase)
     return dx
 
 

@@ -577,3 +577,27 @@ def test_conv_wgrad_pp_256(case, target):
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
                                       stride=st, padding=pad).permute(0, 2, 3, 1)
     assert _rel(dw, ref) < 2e-3
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 128), (3, 28, 28, 128, 256), (2, 7, 7, 256, 512)])
+@pytest.mark.parametrize("tile", [None, (256, 256, 64), (128, 128, 64), (256, 64, 64)])
+def test_conv_dgrad_compact_phase_residual(case, tile):
+    """3x3/2 dgrad + a 1x1/2 downsample's dgrad given COMPACT (phase (0,0) only, res_phase=0) vs torch fp32."""
+    from pytorch_distributed_template_amd.ops import conv
+    N, H, W, C, K = case
+    if tile is not None and C % tile[1]:
+        pytest.skip("tile N does not divide Cin")
+    torch.manual_seed(12)
+    P, Q = conv.out_hw(H, W, 3, 3, 2, 1)
+    dy = _rand16(N, P, Q, K)
+    dyd = _rand16(N, P, Q, K)
+    w = _rand16(K, 3, 3, C, scale=(1.0 / (K * 9)) ** 0.5)
+    wd = _rand16(K, 1, 1, C, scale=(1.0 / K) ** 0.5)
+    # the downsample's data gradient on the compact P x Q grid: a stride-1 1x1 dgrad
+    rc = conv.conv_dgrad(dyd, wd, P, Q, 1, 0)
+    dx = conv.conv_dgrad(dy, w, H, W, 2, 1, residual=rc, res_phase=0, tile=tile)
+    ref = (torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                      stride=2, padding=1)
+           + torch.nn.grad.conv2d_input((N, C, H, W), wd.float().permute(0, 3, 1, 2),
+                                        dyd.float().permute(0, 3, 1, 2), stride=2, padding=0)).permute(0, 2, 3, 1)
+    assert _rel(dx, ref) < 1e-2
