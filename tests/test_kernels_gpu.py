@@ -23,6 +23,8 @@ CONV_CASES = [
     (2, 15, 13, 64, 128, 3, 2, 1),
     (3, 14, 14, 128, 256, 1, 2, 0),
     (2, 7, 7, 256, 64, 1, 1, 0),
+    (2, 12, 12, 64, 256, 1, 1, 0),  # one K-step forward (single-buffer variant)
+    (3, 14, 14, 64, 128, 1, 2, 0),  # one K-step strided 1x1
     (1, 9, 9, 128, 128, 3, 1, 1),
     (2, 8, 8, 512, 512, 3, 1, 1),
     (2, 9, 56, 64, 64, 3, 1, 1),   # ResNet layer1 geometry -> halo-reuse kernel (conv_l1.hip), partial row tile
@@ -367,7 +369,7 @@ def test_stem_kernel_persistent_tiles():
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 1, 1), (2, 15, 13, 128, 128, 3, 2, 1), (3, 14, 14, 256, 128, 1, 2, 0),
-                                  (3, 10, 56, 64, 64, 3, 1, 1)])
+                                  (3, 10, 56, 64, 64, 3, 1, 1), (2, 10, 10, 256, 64, 1, 1, 0)])
 def test_conv_dgrad_fused_bn_backward(case, mode):
     """dgrad epilogue with the consumer BN's backward reduce (ReLU mask + sum dz, sum dz*xhat) vs torch."""
     from pytorch_distributed_template_amd.ops import conv, native
