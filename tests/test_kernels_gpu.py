@@ -152,7 +152,9 @@ def test_bn_relu_maxpool_and_backward():
     torch.manual_seed(6)
     N, H, W, C = 2, 12, 11, 64
     y = _rand16(N, H, W, C)
-    coef = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1,
+    # mixed-sign BN scales: the kernel pools the raw input (sign-flipped where the scale is negative)
+    sign = torch.where(torch.rand(C, device=DEV) < 0.5, -1.0, 1.0)
+    coef = torch.cat([(torch.rand(C, device=DEV) + 0.5) * sign, torch.randn(C, device=DEV) * 0.1,
                       torch.zeros(2 * C, device=DEV)])
     OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     out = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=DEV)
@@ -603,3 +605,15 @@ def test_conv_dgrad_compact_phase_residual(case, tile):
            + torch.nn.grad.conv2d_input((N, C, H, W), wd.float().permute(0, 3, 1, 2),
                                         dyd.float().permute(0, 3, 1, 2), stride=2, padding=0)).permute(0, 2, 3, 1)
     assert _rel(dx, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,ld,ncols", [(1200, 1024, 1000), (37, 1024, 1000), (5, 130, 130), (64, 136, 128)])
+def test_colsum_matches_torch(B, ld, ncols):
+    """fc bias gradient: column sums of the 16-bit logit gradient (vectorised kernel and scalar fallback)."""
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(13)
+    d = _rand16(B, ld)
+    out = torch.full((ncols,), float("nan"), device=DEV)
+    native.C.colsum(d, B, ld, ncols, out, 0.5)
+    ref = d[:, :ncols].float().sum(0) * 0.5
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-3)
