@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--sync-bn", action="store_true")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--last-bucket-mb", type=float, default=1.0,
+                    help="last-produced gradient bucket (the only all-reduce not overlapped with backward); <= 0: "
+                         "DDP's first-bucket policy")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--graph", action="store_true", help="replay the training step as a captured HIP graph")
     ap.add_argument("--autotune", action="store_true", help="time every conv tile candidate once per shape")
@@ -64,7 +67,8 @@ def main():
     model = registry.create(args.arch)
     tr = NativeTrainer(model, dev, dtype=dtype, lr=0.1, momentum=0.9, weight_decay=1e-4,
                        use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb,
-                       graph=args.graph, autotune=args.autotune)
+                       graph=args.graph, autotune=args.autotune,
+                       last_bucket_mb=args.last_bucket_mb if args.last_bucket_mb > 0 else None)
     B = args.batch_per_gpu
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)

@@ -112,7 +112,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--iters-per-epoch", type=int, default=0, help="cap on train iterations per epoch (0 = full)")
     g.add_argument("--val-iters", type=int, default=0, help="cap on val iterations per epoch (0 = full)")
     g.add_argument("--bucket-cap-mb", type=float, default=25.0, help="DDP gradient bucket size (MiB)")
-    g.add_argument("--first-bucket-mb", type=float, default=1.0)
+    g.add_argument("--first-bucket-mb", type=float, default=1.0, help="first-produced bucket (DDP policy, torch engine)")
+    g.add_argument("--last-bucket-mb", type=float, default=1.0,
+                   help="last-produced (stem-side) bucket of the native engine; <= 0: DDP's first-bucket policy")
     g.add_argument("--strict-sync", default=False, type=str2bool, nargs="?", const=True,
                    help="keep the reference's per-iteration barrier and host read of the metrics")
     g.add_argument("--exist-policy", default=os.environ.get("PDT_EXIST_POLICY", "prompt"),

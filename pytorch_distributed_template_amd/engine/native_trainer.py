@@ -29,7 +29,7 @@ class NativeTrainer:
                  weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
-                 force_comm: bool = False, graph: bool = False):
+                 force_comm: bool = False, graph: bool = False, last_bucket_mb: Optional[float] = 1.0):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -39,7 +39,8 @@ class NativeTrainer:
         self.flat = FlatParams(model, self.device, dtype)
         self.buffers = FlatBuffers(model, self.device)
         broadcast_parameters(self.flat, self.buffers, process_group)
-        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
+        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed,
+                              last_bucket_mb=last_bucket_mb)
         # collectives: torch.distributed (RCCL via c10d) or our own RCCL communicator + C++ bucketer
         # (--comm native; force_comm exercises it on a single rank)
         self.ncomm = None

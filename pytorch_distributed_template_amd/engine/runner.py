@@ -187,8 +187,10 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
               first_bucket_mb=args.first_bucket_mb)
     if engine == "native":
         from .native_trainer import NativeTrainer
+        lb = float(getattr(args, "last_bucket_mb", 1.0))
         return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)),
-                             comm=getattr(args, "comm", "torch"), graph=bool(getattr(args, "graph", False)), **kw)
+                             comm=getattr(args, "comm", "torch"), graph=bool(getattr(args, "graph", False)),
+                             last_bucket_mb=lb if lb > 0 else None, **kw)
     from .torch_trainer import TorchTrainer
     return TorchTrainer(model, device, dtype=dtype, **kw)
 

@@ -174,3 +174,26 @@ def test_launcher_kills_group_on_failure(tmp_path):
                         "--grace_s=2", str(script)], cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert r.returncode == 3
     assert "terminating the group" in r.stderr
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_bucket_policies_cover_params_in_production_order(arch):
+    """DDP's policy (small first-produced bucket) and the native default (small LAST-produced bucket: the only
+    all-reduce that cannot overlap backward) both partition the flat gradient into contiguous buckets listed in
+    gradient-production order (reverse registration)."""
+    from pytorch_distributed_template_amd.models import registry
+    from pytorch_distributed_template_amd.optim.flat import FlatParams
+    from pytorch_distributed_template_amd.parallel.ddp import GradBucketer
+    flat = FlatParams(registry.create(arch), torch.device("cpu"), torch.bfloat16)
+    n = len(flat.slots)
+    for lb in (None, 1.0):
+        b = GradBucketer(flat, None, 25.0, 1.0, enabled=True, last_bucket_mb=lb)
+        order = [i for bk in b.buckets for i in bk["params"]]
+        assert order == list(range(n - 1, -1, -1))
+        for bk in b.buckets:  # contiguous slices of the flat buffer
+            assert bk["hi"] - bk["lo"] == sum(flat.slots[i].numel for i in bk["params"])
+        sizes = b.bucket_sizes_mb()
+        if lb is None:
+            assert sizes[0] >= 1.0 and sizes[0] < 25.0
+        else:
+            assert 1.0 <= sizes[-1] < 4.0 and sum(sizes[:-1]) > 20 * sizes[-1]
