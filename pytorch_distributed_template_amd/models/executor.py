@@ -123,6 +123,8 @@ class ResNetExecutor:
         self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
         # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad (PDT_COMPACT_DS=0: off)
         self.compact_ds = os.environ.get("PDT_COMPACT_DS", "1") == "1"
+        # backward-only derived weight layouts gathered on the side stream under the forward (PDT_SPLIT_DERIVED=0: off)
+        self.split_derived = os.environ.get("PDT_SPLIT_DERIVED", "1") == "1"
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -201,8 +203,33 @@ class ResNetExecutor:
 
     # ---------------------------------------------------------------------------------- helpers
     def update_derived(self) -> None:
-        """Rebuild every derived 16-bit weight layout from the shadow (after each optimizer step)."""
-        self.C.gather16(self.flat.shadow, self.derived_idx, self.derived)
+        """Rebuild every derived 16-bit weight layout from the shadow (after each optimizer step).
+
+        With the side stream, only the layouts the forward pass reads (stem, fc) are gathered on the compute
+        stream; the backward-data layouts (every conv's phase weights, the transposed fc) are gathered on the
+        side stream, overlapped with the forward pass, and backward waits for them (``_derived_ev``)."""
+        if self.side is None or not self.split_derived or torch.cuda.is_current_stream_capturing():
+            # (a captured step must end joined: no side-stream work may trail the graph)
+            self.C.gather16(self.flat.shadow, self.derived_idx, self.derived)
+            return
+        lo, hi = self.stem_w_off, self.fc_wt_off
+        with torch.cuda.device(self.device):
+            self.C.gather16(self.flat.shadow, self.derived_idx[lo:hi], self.derived[lo:hi])
+            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                if lo > 0:
+                    self.C.gather16(self.flat.shadow, self.derived_idx[:lo], self.derived[:lo])
+                if hi < self.derived.numel():
+                    self.C.gather16(self.flat.shadow, self.derived_idx[hi:], self.derived[hi:])
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+        self._derived_ev = ev
+
+    def _wait_derived(self) -> None:
+        ev = getattr(self, "_derived_ev", None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            self._derived_ev = None
 
     def _buf(self, key, numel: int, dtype=None) -> torch.Tensor:
         dtype = dtype or self.dtype
@@ -551,6 +578,7 @@ class ResNetExecutor:
     def _backward(self, saved, dlog):
         Cn = self.C
         N = saved["N"]
+        self._wait_derived()  # backward-data weight layouts (gathered on the side stream after the last step)
         # fc: bias grad (column sums), weight grad (1x1 wgrad over the batch), data grad
         Cn.colsum(dlog, N, self.ncls_pad, self.ncls, self._g(self.fcb_slot), 1.0)
         self.grad_ready(self.fcb_slot.index)
