@@ -191,6 +191,11 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
       TORCH_CHECK(f.size() == 7, "conv_dgrad: phase = (ph, pw, T, U, ioff_h, ioff_w, woff)");
       const int64_t Pm = (H - f[0] + stride - 1) / stride, Qm = (W - f[1] + stride - 1) / stride;
       TORCH_CHECK(res->numel() == N * Pm * Qm * C, "conv_dgrad: compact residual size mismatch");
+      // every phase reads the compact residual unconditionally (its add is selected per phase): its rows must
+      // cover every phase's GEMM rows
+      for (const auto& g : phases)
+        TORCH_CHECK(g.size() == 7 && ((H - g[0] + stride - 1) / stride) * ((W - g[1] + stride - 1) / stride) <= Pm * Qm,
+                    "conv_dgrad: the compact residual's phase must be the largest");
     } else {
       TORCH_CHECK(res->numel() == dx.numel(), "conv_dgrad: residual size mismatch");
     }

@@ -41,7 +41,10 @@ PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 
 // Shared epilogue of the implicit-GEMM conv kernels: the wave's accumulators acc[i][j] hold output
 // channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m = m0 + wm*WM + j*16 + fr.
-template <int DT, int EPI, bool RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_>
+// RES: 0 no residual | 1 residual in the output's layout | 2 compact residual of sub-pixel phase a.res_phase
+// (ConvFwdArgs::res_phase), indexed by GEMM row; its loads stay unconditional (in range on every phase) and
+// only the add is selected, so the hoisted-load structure of the RES == 1 path is kept.
+template <int DT, int EPI, int RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_>
 PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int64_t m0, int n0, int tile_m, int wn,
                               int wm, int tid, int lane, char* smem) {
   using E = E16<DT>;
@@ -92,19 +95,19 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
   constexpr bool LY1 = EPI >= 2, LY2 = EPI == 4, LM = EPI == 3 || EPI == 4;
   // registers per pixel fragment of hoisted operands; chunk size keeps them within the budget left
   // beside the accumulators (FN*FM*4) so no variant spills or loses occupancy
-  constexpr int PER_J = FN * (2 * RES + 2 * LY1 + 2 * LY2 + LM);
+  constexpr int PER_J = FN * (2 * (RES != 0) + 2 * LY1 + 2 * LY2 + LM);
   constexpr int BUDGET = FN * FM * 4 >= 128 ? 64 : 96;
   constexpr int JC = PER_J == 0 ? FM
                      : (8 * PER_J <= BUDGET && FM % 8 == 0) ? 8
                      : (4 * PER_J <= BUDGET && FM % 4 == 0) ? 4
                      : (2 * PER_J <= BUDGET && FM % 2 == 0) ? 2 : 1;
   static_assert(FM % JC == 0, "epilogue chunking");
-  // compact per-phase residual (see ConvFwdArgs::res_phase): absent on the other phases (block-uniform)
-  const bool has_res = RES && a.res != nullptr;
-  const bool res_compact = RES && a.res_phase >= 0;
+  constexpr bool RC = RES == 2;
+  const bool res_on = !RC || (int)blockIdx.y == a.res_phase;  // compact: this block's phase owns the residual
 #pragma unroll
   for (int jc = 0; jc < FM; jc += JC) {
-    int64_t obase[JC], rbase[RES ? JC : 1];
+    int64_t obase[JC];
+    uint32_t rbase[RC ? JC : 1];
     bool valid[JC];
 #pragma unroll
     for (int jj = 0; jj < JC; ++jj) {
@@ -116,7 +119,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
       const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
       const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
       obase[jj] = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
-      if constexpr (RES) rbase[jj] = res_compact ? (int64_t)mm * a.Kout : obase[jj];
+      if constexpr (RC) rbase[jj] = (uint32_t)mm * (uint32_t)a.Kout;
     }
     uint2 p_res[RES ? JC : 1][RES ? FN : 1], p_y1[LY1 ? JC : 1][LY1 ? FN : 1], p_y2[LY2 ? JC : 1][LY2 ? FN : 1];
     uint32_t p_m[LM ? JC : 1][LM ? FN : 1];
@@ -125,8 +128,8 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int64_t o = obase[jj] + n0 + wn * WN + i * 16 + 4 * fq;
-        if constexpr (RES)
-          p_res[jj][i] = has_res ? *(const uint2*)(a.res + rbase[jj] + (o - obase[jj])) : uint2{0u, 0u};
+        if constexpr (RES == 1) p_res[jj][i] = *(const uint2*)(a.res + o);
+        if constexpr (RC) p_res[jj][i] = *(const uint2*)(a.res + rbase[jj] + (uint32_t)(n0 + wn * WN + i * 16 + 4 * fq));
         if constexpr (LY1) p_y1[jj][i] = *(const uint2*)(a.bn_y1 + o);
         if constexpr (LY2) p_y2[jj][i] = *(const uint2*)(a.bn_y2 + o);
         if constexpr (LM) p_m[jj][i] = (uint32_t)a.bn_mask[o >> 3] >> ((int)o & 4);
@@ -141,7 +144,11 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
         const int64_t o = obase[jj] + n;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if constexpr (RES) {
-          const uint2 rr = p_res[jj][i];
+          uint2 rr = p_res[jj][i];
+          if constexpr (RC) {
+            rr.x = res_on ? rr.x : 0u;
+            rr.y = res_on ? rr.y : 0u;
+          }
           v[0] += E::to_f((uint16_t)(rr.x & 0xffff));
           v[1] += E::to_f((uint16_t)(rr.x >> 16));
           v[2] += E::to_f((uint16_t)(rr.y & 0xffff));
@@ -248,7 +255,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
   }
 }
 
-template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, bool RES, int STAGES, int NW>
+template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, int RES, int STAGES, int NW>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
@@ -262,7 +269,6 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
     a.w = args.w + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
-    if (args.res_phase >= 0 && ph != args.res_phase) a.res = nullptr;
     if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
   }
   using E = E16<DT>;
@@ -479,7 +485,7 @@ PDT_DEVICE void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <int DT, int BM, int BN, int EPI, bool RES>
+template <int DT, int BM, int BN, int EPI, int RES>
 __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch (strided backward-data): this block's phase geometry
@@ -493,7 +499,6 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
     a.w = args.w + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
-    if (args.res_phase >= 0 && ph != args.res_phase) a.res = nullptr;
     if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
   }
   using E = E16<DT>;
@@ -692,19 +697,19 @@ static void launch_pp(const ConvFwdArgs& a, hipStream_t s) {
     for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
   }
   dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(512);
-  const bool rs = a.res != nullptr;
+  const int rs = a.res == nullptr ? 0 : (a.res_phase >= 0 && a.nphase > 0 ? 2 : 1);
   const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
 #define PDT_K(E_, R_) hipLaunchKernelGGL((conv_pp_kernel<DT, BM, BN, E_, R_>), grid, block, 0, s, a)
   if (epi == 0) {
-    if (rs) PDT_K(0, true); else PDT_K(0, false);
-  } else if (epi == 1) {
-    if (rs) PDT_K(1, true); else PDT_K(1, false);
+    if (rs == 1) PDT_K(0, 1); else if (rs == 2) PDT_K(0, 2); else PDT_K(0, 0);
+  } else if (epi == 1 && rs != 2) {
+    if (rs) PDT_K(1, 1); else PDT_K(1, 0);
   } else if (epi == 2 && !rs) {
-    PDT_K(2, false);
+    PDT_K(2, 0);
   } else if (epi == 3 && rs) {
-    PDT_K(3, true);
+    if (rs == 2) PDT_K(3, 2); else PDT_K(3, 1);
   } else if (epi == 4 && rs) {
-    PDT_K(4, true);
+    if (rs == 2) PDT_K(4, 2); else PDT_K(4, 1);
   } else {
     pdt_hip_fail("conv_pp: unsupported epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
   }
@@ -720,19 +725,19 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
   }
   dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(NW * 64);
-  const bool rs = a.res != nullptr;
+  const int rs = a.res == nullptr ? 0 : (a.res_phase >= 0 && a.nphase > 0 ? 2 : 1);
   const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
 #define PDT_K(E_, R_) hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, E_, R_, STAGES, NW>), grid, block, 0, s, a)
   if (epi == 0) {
-    if (rs) PDT_K(0, true); else PDT_K(0, false);
-  } else if (epi == 1) {
-    if (rs) PDT_K(1, true); else PDT_K(1, false);
+    if (rs == 1) PDT_K(0, 1); else if (rs == 2) PDT_K(0, 2); else PDT_K(0, 0);
+  } else if (epi == 1 && rs != 2) {
+    if (rs) PDT_K(1, 1); else PDT_K(1, 0);
   } else if constexpr ((BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 4096 * NW) ||
                        (BM == 256 && BN == 256)) {
     // fused BN-backward epilogues: only on the backward-data tiles (128x128x64, 256x64x64)
-    if (epi == 2 && !rs) PDT_K(2, false);
-    else if (epi == 3 && rs) PDT_K(3, true);
-    else if (epi == 4 && rs) PDT_K(4, true);
+    if (epi == 2 && !rs) PDT_K(2, 0);
+    else if (epi == 3 && rs) { if (rs == 2) PDT_K(3, 2); else PDT_K(3, 1); }
+    else if (epi == 4 && rs) { if (rs == 2) PDT_K(4, 2); else PDT_K(4, 1); }
     else pdt_hip_fail("conv_fwd: unsupported BN-backward epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
   } else {
     pdt_hip_fail("conv_fwd: BN-backward epilogue needs a 128x128x64 or 256x64x64 tile", hipErrorInvalidValue,
