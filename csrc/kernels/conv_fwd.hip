@@ -44,7 +44,10 @@ PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 // RES: 0 no residual | 1 residual in the output's layout | 2 compact residual of sub-pixel phase a.res_phase
 // (ConvFwdArgs::res_phase), indexed by GEMM row; its loads stay unconditional (in range on every phase) and
 // only the add is selected, so the hoisted-load structure of the RES == 1 path is kept.
-template <int DT, int EPI, int RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_>
+// SMEM > 0 (the kernel's LDS bytes): with a.stage_out the output tile is staged in LDS and written back as
+// whole 16-byte-per-lane rows; a lane's accumulators otherwise hold 4 channels of one pixel, so every store
+// instruction writes 16 rows x 32 B.
+template <int DT, int EPI, int RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_, int SMEM = 0>
 PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int64_t m0, int n0, int tile_m, int wn,
                               int wm, int tid, int lane, char* smem) {
   using E = E16<DT>;
@@ -102,6 +105,13 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
                      : (4 * PER_J <= BUDGET && FM % 4 == 0) ? 4
                      : (2 * PER_J <= BUDGET && FM % 2 == 0) ? 2 : 1;
   static_assert(FM % JC == 0, "epilogue chunking");
+  constexpr int BM_T = WAVES_M * WM;
+  constexpr int SPITCH = BN * 2 + 16;  // staged row pitch (+16 B: consecutive rows rotate by 4 banks)
+  constexpr int STG_OFF = 16384;       // behind the statistics scratch and the BN coefficients
+  constexpr bool CAN_STAGE = SMEM >= STG_OFF + BM_T * SPITCH;
+  static_assert(!CAN_STAGE || RED_BYTES + 6 * BN * 4 <= STG_OFF, "epilogue LDS regions overlap");
+  const bool stage = CAN_STAGE && a.stage_out;
+  char* stg = smem + STG_OFF;
   constexpr bool RC = RES == 2;
   const bool res_on = !RC || (int)blockIdx.y == a.res_phase;  // compact: this block's phase owns the residual
 #pragma unroll
@@ -184,7 +194,10 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
         uint2 packed;
         packed.x = (uint32_t)ov[0] | ((uint32_t)ov[1] << 16);
         packed.y = (uint32_t)ov[2] | ((uint32_t)ov[3] << 16);
-        *(uint2*)(a.y + o) = packed;
+        if (CAN_STAGE && stage)
+          *(uint2*)(stg + (wm * WM + j * 16 + fr) * SPITCH + (wn * WN + i * 16 + 4 * fq) * 2) = packed;
+        else
+          *(uint2*)(a.y + o) = packed;
         if constexpr (EPI == 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -207,6 +220,26 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
 #pragma unroll
             for (int r = 0; r < 4; ++r) sacc[i][r][2] += E::to_f(ov[r]) * (y2[r] - m2[r]) * i2[r];
           }
+        }
+      }
+    }
+  }
+
+  if constexpr (CAN_STAGE) {
+    if (stage) {  // write the staged tile back: 16 B per lane, whole BN-channel rows per pixel
+      __syncthreads();
+      constexpr int CPR = BN / 8;
+      for (int q = tid; q < BM_T * CPR; q += NW_ * 64) {
+        const int row = q / CPR, ch = q - row * CPR;
+        const int64_t m = m0 + row;
+        if (m < a.M) {
+          const int mm = (int)m;
+          const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
+          const int rem = mm - nimg * PQ;
+          const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
+          const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
+          const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout + n0 + ch * 8;
+          *(uint4*)(a.y + ob) = *(const uint4*)(stg + row * SPITCH + ch * 16);
         }
       }
     }
@@ -453,7 +486,8 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
     }
   }
 
-  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW, STAGES * STAGE>(a, acc, m0, n0, tile_m, wn, wm, tid,
+                                                                             lane, smem);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -748,6 +782,12 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
 
 template <int DT>
 static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
+  // LDS-staged output write-back (PDT_STAGE_OUT=0: direct 8-byte stores from the accumulators)
+  static const bool stage_env = [] {
+    const char* e = getenv("PDT_STAGE_OUT");
+    return !(e && e[0] == '0');
+  }();
+  a.stage_out = stage_env && a.Kout % 8 == 0 ? 1 : 0;
   a.m_tiles = (int)((a.M + bm - 1) / bm);
   a.n_tiles = a.Kout / bn;
   {
