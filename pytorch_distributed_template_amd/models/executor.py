@@ -123,6 +123,7 @@ class ResNetExecutor:
         self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
         # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad (PDT_COMPACT_DS=0: off)
         self.compact_ds = os.environ.get("PDT_COMPACT_DS", "1") == "1"
+        self.bwd_buf_per_block = os.environ.get("PDT_BWD_BUF_PER_BLOCK", "1") == "1"
         # backward-only derived weight layouts gathered on the side stream under the forward (PDT_SPLIT_DERIVED=0: off)
         self.split_derived = os.environ.get("PDT_SPLIT_DERIVED", "1") == "1"
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
@@ -613,9 +614,13 @@ class ResNetExecutor:
             else:
                 self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["omask"], cnt, dsbn, rec["yd"] if ds else None)
                 mask_src = rec["omask"]
-            dy_last = self._buf("dy_a", rec["ys"][-1].numel())
+            # per-block dY buffers (PDT_BWD_BUF_PER_BLOCK=0: two shared ones): a shared buffer's next write has
+            # to wait for the side-stream weight gradient still reading it, and each such cross-stream
+            # wait left the GPU idle ~20-35 us (rocprof trace); per block costs a few GB of HBM, not time
+            bk_ = (lambda nm: (nm, bi)) if self.bwd_buf_per_block else (lambda nm: nm)
+            dy_last = self._buf(bk_("dy_a"), rec["ys"][-1].numel())
             if ds:
-                dyd = self._buf("dy_b", rec["yd"].numel())
+                dyd = self._buf(bk_("dy_b"), rec["yd"].numel())
                 Cn.bn_bwd_apply(g, mask_src, rec["ys"][-1], bns[-1].bcoef, dy_last, rec["yd"], dsbn.bcoef,
                                 dyd, None, convs[-1].cout)
             elif g_fused is not None:
@@ -661,7 +666,7 @@ class ResNetExecutor:
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, da, bnb=(1, yp, bnp.coef, None, None, None, slots))
                     self._bn_bwd_finish(slots, N * h * w, bnp)
                     dname = "dy_c" if dname == "dy_a" else "dy_a"
-                    dyp = self._buf(dname, yp.numel())
+                    dyp = self._buf(bk_(dname), yp.numel())
                     Cn.bn_bwd_apply(da, None, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
                     dy = dyp
                 elif bi > 0:
