@@ -107,7 +107,8 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
                    help="use synthetic ImageNet-shaped data instead of --data")
     g.add_argument("--synthetic-train-size", type=int, default=1281167)
     g.add_argument("--synthetic-val-size", type=int, default=50000)
-    g.add_argument("--image-size", type=int, default=224)
+    g.add_argument("--image-size", type=int, default=None,
+                   help="crop size (default 224; 299 for inception_v3, whose aux head needs it)")
     g.add_argument("--num-classes", type=int, default=1000)
     g.add_argument("--iters-per-epoch", type=int, default=0, help="cap on train iterations per epoch (0 = full)")
     g.add_argument("--val-iters", type=int, default=0, help="cap on val iterations per epoch (0 = full)")
@@ -148,5 +149,7 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
 def parse_args(mode: str, argv: Optional[List[str]] = None) -> argparse.Namespace:
     args = build_parser(mode).parse_args(argv)
     args.step = parse_steps(args.step)
+    if args.image_size is None:
+        args.image_size = 299 if args.arch == "inception_v3" else 224
     args.mode = mode
     return args

@@ -131,7 +131,8 @@ def build_loaders(args, world: int, rank: int, device, distributed: bool, batch_
         val_ds = SyntheticImageNet(args.synthetic_val_size, args.image_size, args.num_classes, seed=1, uint8=u8)
     else:
         train_ds = ImageFolder(os.path.join(args.data, "train"), train_transform(args.image_size, gpu_normalize=u8))
-        val_ds = ImageFolder(os.path.join(args.data, "val"), val_transform(args.image_size, gpu_normalize=u8))
+        resize = round(args.image_size * 256 / 224)  # 256 for the 224 crop, 342 for Inception-v3's 299
+        val_ds = ImageFolder(os.path.join(args.data, "val"), val_transform(args.image_size, resize, gpu_normalize=u8))
     if distributed:
         train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
         val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank)

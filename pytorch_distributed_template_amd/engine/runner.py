@@ -27,6 +27,7 @@ import torch.distributed as dist
 from .. import cli
 from ..data.loader import build_loaders
 from ..models import registry
+from ..models.inception import AUX_LOSS_WEIGHT
 from ..optim.lr import build_scheduler
 from ..utils.io import load_checkpoint, make_checkpoint_state, output_process, save_checkpoint, write_settings
 from ..utils.logging import close_logger, ddp_print, get_logger
@@ -176,13 +177,14 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
     use_amp = bool(getattr(args, "use_amp", False)) and dtype == torch.float16
     sync_bn = bool(getattr(args, "sync_batchnorm", False))
     common = dict(lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    torch_kw = dict(aux_loss_weight=AUX_LOSS_WEIGHT.get(args.arch, 0.3))
     if mode == "dp":
         if engine == "native":
             from ..parallel.dp import NativeDataParallelTrainer
             ids = list(range(torch.cuda.device_count()))
             return NativeDataParallelTrainer(model, ids, dtype=dtype, use_amp=use_amp, **common)
         from .torch_trainer import TorchTrainer
-        return TorchTrainer(model, device, dtype=dtype, use_amp=use_amp, **common)
+        return TorchTrainer(model, device, dtype=dtype, use_amp=use_amp, **common, **torch_kw)
     kw = dict(common, use_amp=use_amp, sync_bn=sync_bn, bucket_cap_mb=args.bucket_cap_mb,
               first_bucket_mb=args.first_bucket_mb)
     if engine == "native":
@@ -192,7 +194,7 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
                              comm=getattr(args, "comm", "torch"), graph=bool(getattr(args, "graph", False)),
                              last_bucket_mb=lb if lb > 0 else None, **kw)
     from .torch_trainer import TorchTrainer
-    return TorchTrainer(model, device, dtype=dtype, **kw)
+    return TorchTrainer(model, device, dtype=dtype, **kw, **torch_kw)
 
 
 def main(mode: str, argv: Optional[list] = None) -> int:

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..amp.scaler import DeviceGradScaler
+from ..models.inception import split_outputs
 from ..optim.flat import FlatBuffers, FlatParams
 from ..optim.sgd import FusedSGD
 from ..parallel.ddp import GradBucketer, broadcast_parameters, sync_buffers
@@ -28,7 +29,8 @@ class TorchTrainer:
     def __init__(self, model: nn.Module, device, dtype: torch.dtype = torch.float32, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
-                 process_group=None, reduce_metrics: bool = True, channels_last: bool = True):
+                 process_group=None, reduce_metrics: bool = True, channels_last: bool = True,
+                 aux_loss_weight: float = 0.3):
         self.device = torch.device(device)
         self.pg = process_group
         self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
@@ -49,6 +51,8 @@ class TorchTrainer:
         self.scaler = DeviceGradScaler(self.device, enabled=use_amp and dtype == torch.float16)
         self.broadcast_buffers = broadcast_buffers and self.distributed
         self.reduce_metrics = reduce_metrics and self.distributed
+        # GoogLeNet / Inception-v3 return auxiliary logits in training; their CE losses are added with this weight
+        self.aux_loss_weight = aux_loss_weight
         self._steps = 0
 
     def _autocast(self):
@@ -73,8 +77,10 @@ class TorchTrainer:
             sync_buffers(self.buffers, self.pg)
         self.optimizer.zero_grad()
         with self._autocast():
-            out = self.model(self._inputs(images))
+            out, aux = split_outputs(self.model(self._inputs(images)))
             loss = F.cross_entropy(out.float(), target)
+            for a in aux:
+                loss = loss + self.aux_loss_weight * F.cross_entropy(a.float(), target)
         acc = accuracy(out.detach().float(), target, 1)
         met = self._reduce(torch.stack([loss.detach().float(), acc.float()]))
         scale = self.scaler.scale_tensor

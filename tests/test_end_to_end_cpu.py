@@ -111,3 +111,15 @@ def test_two_simulated_nodes_cpu(tmp_path):
     assert "nprocs: 4" in settings
     # node 1 hosts global ranks 2, 3: no rank-0 duties there
     assert "Train epoch" not in outs[1]
+
+
+def test_distributed_googlenet_aux_heads_cpu(tmp_path):
+    """GoogLeNet trains through the DDP entry point: the aux heads' losses join the main loss (the
+    reference would hand the output namedtuple to CrossEntropyLoss and fail)."""
+    out = str(tmp_path / "output")
+    args = [a if a != "32" else "64" for a in COMMON]
+    _run(["-m", "torch.distributed.run", "--nproc_per_node", "2", "--master-addr", "127.0.0.1", "--master-port",
+          "29561", "distributed.py", "--outpath", out, "-b", "8", "-a", "googlenet", "--dist-backend", "gloo"] + args)
+    log = open(os.path.join(out + "_googlenet", "experiment.log")).read()
+    assert "=> creating model: googlenet" in log
+    assert re.search(r"\|\|==> total_time_cost=\d+\.\d{4}s", log)

@@ -70,3 +70,57 @@ def test_pretrained_local(tmp_path):
         assert torch.equal(a, b), k
     with pytest.raises(FileNotFoundError):
         registry.create("resnet18", pretrained=True, pretrained_path=str(tmp_path / "missing.pth"))
+
+
+@pytest.mark.parametrize("arch,nparams", [
+    ("googlenet", 13004888), ("inception_v3", 27161264), ("mnasnet0_5", 2218512), ("mnasnet0_75", 3170208),
+    ("mnasnet1_0", 4383312), ("mnasnet1_3", 6282256), ("mobilenet_v3_large", 5483032),
+    ("mobilenet_v3_small", 2542856)])
+def test_inception_mnas_v3_param_counts(arch, nparams):
+    """torchvision parameter counts (GoogLeNet / Inception-v3 with their auxiliary heads, as built untrained)."""
+    assert sum(p.numel() for p in registry.create(arch).parameters()) == nparams
+
+
+def test_googlenet_without_aux_matches_released_size():
+    assert sum(p.numel() for p in registry.create("googlenet", aux_logits=False).parameters()) == 6624904
+
+
+@pytest.mark.parametrize("arch,size", [("googlenet", 64), ("inception_v3", 299), ("mnasnet0_5", 64),
+                                       ("mobilenet_v3_small", 64), ("mobilenet_v3_large", 64)])
+def test_inception_mnas_v3_train_and_eval(arch, size):
+    """Train mode returns (logits, aux...) for the Inception family and plain logits otherwise; backward
+    reaches every parameter through the trainer's aux-loss split; eval mode returns plain logits."""
+    from pytorch_distributed_template_amd.models.inception import split_outputs
+    torch.manual_seed(0)
+    m = registry.create(arch, num_classes=5)
+    m.train()
+    out, aux = split_outputs(m(torch.randn(2, 3, size, size)))
+    assert out.shape == (2, 5) and len(aux) == {"googlenet": 2, "inception_v3": 1}.get(arch, 0)
+    loss = sum(torch.nn.functional.cross_entropy(o, torch.tensor([0, 3])) for o in [out] + aux)
+    loss.backward()
+    assert all(p.grad is not None for p in m.parameters())
+    m.eval()
+    with torch.no_grad():
+        assert m(torch.randn(1, 3, size, size)).shape == (1, 5)
+
+
+def test_state_dict_keys_inception_family():
+    g = registry.create("googlenet").state_dict()
+    assert {"conv1.conv.weight", "conv1.bn.running_var", "inception3a.branch2.1.conv.weight",
+            "inception4e.branch4.1.bn.bias", "aux1.fc1.weight", "aux2.fc2.bias", "fc.weight"} <= set(g)
+    i = registry.create("inception_v3").state_dict()
+    assert {"Conv2d_1a_3x3.conv.weight", "Mixed_6e.branch7x7dbl_5.bn.weight", "Mixed_7c.branch3x3_2b.conv.weight",
+            "AuxLogits.conv1.conv.weight", "AuxLogits.fc.bias", "fc.weight"} <= set(i)
+    assert i["Mixed_6b.branch7x7_2.conv.weight"].shape == (128, 128, 1, 7)
+    v3 = registry.create("mobilenet_v3_large").state_dict()
+    assert {"features.0.0.weight", "features.4.block.2.fc1.weight", "features.16.1.running_mean",
+            "classifier.3.weight"} <= set(v3)
+    mn = registry.create("mnasnet1_0").state_dict()
+    assert {"layers.0.weight", "layers.8.0.layers.3.weight", "layers.14.weight", "classifier.1.weight"} <= set(mn)
+
+
+def test_inception_v3_default_image_size():
+    from pytorch_distributed_template_amd import cli
+    assert cli.parse_args("ddp", ["-a", "inception_v3"]).image_size == 299
+    assert cli.parse_args("ddp", ["-a", "resnet18"]).image_size == 224
+    assert cli.parse_args("ddp", ["-a", "inception_v3", "--image-size", "320"]).image_size == 320
