@@ -1,9 +1,11 @@
-"""MNASNet and MobileNetV3 with torchvision-identical module names, shapes and init.
+"""MNASNet, MobileNetV3 and EfficientNet-B0..B7 with torchvision-identical module names, shapes and init.
 
 Registry members (reference C05, `dataparallel.py:36-37`); executed by the stock-PyTorch engine.
 """
 from __future__ import annotations
 
+import copy
+import math
 from functools import partial
 from typing import Callable, List, Optional
 
@@ -120,13 +122,15 @@ class ConvBNActivation(nn.Sequential):
 
 
 class SqueezeExcitation(nn.Module):
-    def __init__(self, input_channels: int, squeeze_channels: int):
+    def __init__(self, input_channels: int, squeeze_channels: int,
+                 activation: Callable[..., nn.Module] = nn.ReLU,
+                 scale_activation: Callable[..., nn.Module] = nn.Hardsigmoid):
         super().__init__()
         self.avgpool = nn.AdaptiveAvgPool2d(1)
         self.fc1 = nn.Conv2d(input_channels, squeeze_channels, 1)
         self.fc2 = nn.Conv2d(squeeze_channels, input_channels, 1)
-        self.activation = nn.ReLU()
-        self.scale_activation = nn.Hardsigmoid()
+        self.activation = activation()
+        self.scale_activation = scale_activation()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.scale_activation(self.fc2(self.activation(self.fc1(self.avgpool(x))))) * x
@@ -225,3 +229,120 @@ def mobilenet_v3_large(**kwargs) -> MobileNetV3:
 def mobilenet_v3_small(**kwargs) -> MobileNetV3:
     setting, last = _v3_setting("mobilenet_v3_small")
     return MobileNetV3(setting, last, **kwargs)
+
+
+# ------------------------------------------------------------------------------------- EfficientNet
+class StochasticDepth(nn.Module):
+    """Drop the whole residual branch per sample with probability ``p`` in training ("row" mode)."""
+
+    def __init__(self, p: float):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self.training or self.p == 0.0:
+            return x
+        survival = 1.0 - self.p
+        noise = torch.empty((x.shape[0],) + (1,) * (x.ndim - 1), dtype=x.dtype, device=x.device)
+        return x * noise.bernoulli_(survival).div_(survival)
+
+
+class _MBConvConfig:
+    def __init__(self, expand_ratio: float, kernel: int, stride: int, in_ch: int, out_ch: int, num_layers: int,
+                 width_mult: float, depth_mult: float):
+        self.expand_ratio = expand_ratio
+        self.kernel = kernel
+        self.stride = stride
+        self.input_channels = _make_divisible(in_ch * width_mult)
+        self.out_channels = _make_divisible(out_ch * width_mult)
+        self.num_layers = int(math.ceil(num_layers * depth_mult))
+
+
+class MBConv(nn.Module):
+    def __init__(self, cnf: _MBConvConfig, stochastic_depth_prob: float, norm_layer: Callable[..., nn.Module]):
+        super().__init__()
+        self.use_res_connect = cnf.stride == 1 and cnf.input_channels == cnf.out_channels
+        expanded = _make_divisible(cnf.input_channels * cnf.expand_ratio)
+        layers: List[nn.Module] = []
+        if expanded != cnf.input_channels:
+            layers.append(ConvBNActivation(cnf.input_channels, expanded, 1, norm_layer=norm_layer,
+                                           activation_layer=nn.SiLU))
+        layers.append(ConvBNActivation(expanded, expanded, cnf.kernel, cnf.stride, groups=expanded,
+                                       norm_layer=norm_layer, activation_layer=nn.SiLU))
+        layers.append(SqueezeExcitation(expanded, max(1, cnf.input_channels // 4),
+                                        activation=partial(nn.SiLU, inplace=True), scale_activation=nn.Sigmoid))
+        layers.append(ConvBNActivation(expanded, cnf.out_channels, 1, norm_layer=norm_layer, activation_layer=None))
+        self.block = nn.Sequential(*layers)
+        self.stochastic_depth = StochasticDepth(stochastic_depth_prob)
+        self.out_channels = cnf.out_channels
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = self.block(x)
+        return self.stochastic_depth(y) + x if self.use_res_connect else y
+
+
+class EfficientNet(nn.Module):
+    def __init__(self, setting: List[_MBConvConfig], dropout: float, stochastic_depth_prob: float = 0.2,
+                 num_classes: int = 1000, norm_layer: Optional[Callable[..., nn.Module]] = None):
+        super().__init__()
+        norm_layer = norm_layer or nn.BatchNorm2d
+        layers: List[nn.Module] = [ConvBNActivation(3, setting[0].input_channels, 3, 2, norm_layer=norm_layer,
+                                                    activation_layer=nn.SiLU)]
+        total = sum(c.num_layers for c in setting)
+        block_id = 0
+        for cnf in setting:
+            stage: List[nn.Module] = []
+            for _ in range(cnf.num_layers):
+                bc = copy.copy(cnf)
+                if stage:  # every block after a stage's first keeps the width and stride 1
+                    bc.input_channels = bc.out_channels
+                    bc.stride = 1
+                stage.append(MBConv(bc, stochastic_depth_prob * float(block_id) / total, norm_layer))
+                block_id += 1
+            layers.append(nn.Sequential(*stage))
+        last_in = setting[-1].out_channels
+        layers.append(ConvBNActivation(last_in, 4 * last_in, 1, norm_layer=norm_layer, activation_layer=nn.SiLU))
+        self.features = nn.Sequential(*layers)
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.classifier = nn.Sequential(nn.Dropout(p=dropout, inplace=True), nn.Linear(4 * last_in, num_classes))
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out")
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.Linear):
+                r = 1.0 / math.sqrt(m.out_features)
+                nn.init.uniform_(m.weight, -r, r)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.classifier(torch.flatten(self.avgpool(self.features(x)), 1))
+
+
+# (width multiplier, depth multiplier, dropout) per variant
+_EFFNET = {"b0": (1.0, 1.0, 0.2), "b1": (1.0, 1.1, 0.2), "b2": (1.1, 1.2, 0.3), "b3": (1.2, 1.4, 0.3),
+           "b4": (1.4, 1.8, 0.4), "b5": (1.6, 2.2, 0.4), "b6": (1.8, 2.6, 0.5), "b7": (2.0, 3.1, 0.5)}
+# (expand ratio, kernel, stride, in, out, layers) per stage
+_EFFNET_STAGES = [(1, 3, 1, 32, 16, 1), (6, 3, 2, 16, 24, 2), (6, 5, 2, 24, 40, 2), (6, 3, 2, 40, 80, 3),
+                  (6, 5, 1, 80, 112, 3), (6, 5, 2, 112, 192, 4), (6, 3, 1, 192, 320, 1)]
+
+
+def _efficientnet(variant: str, **kwargs) -> EfficientNet:
+    w, d, dropout = _EFFNET[variant]
+    setting = [_MBConvConfig(*st, width_mult=w, depth_mult=d) for st in _EFFNET_STAGES]
+    if variant in ("b5", "b6", "b7"):
+        kwargs.setdefault("norm_layer", partial(nn.BatchNorm2d, eps=0.001, momentum=0.01))
+    return EfficientNet(setting, kwargs.pop("dropout", dropout), **kwargs)
+
+
+def _effnet_ctor(variant: str):
+    def ctor(**kwargs) -> EfficientNet:
+        return _efficientnet(variant, **kwargs)
+    ctor.__name__ = f"efficientnet_{variant}"
+    return ctor
+
+
+EFFICIENTNETS = {f"efficientnet_{v}": _effnet_ctor(v) for v in _EFFNET}

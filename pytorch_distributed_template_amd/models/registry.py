@@ -3,8 +3,8 @@ lowercase callable in ``torchvision.models``; `:112-117` instantiates ``models._
 
 torchvision is not available offline here, so the registry is ours, with torchvision-identical
 parameter names, shapes and initialisation: ResNet / ResNeXt / Wide-ResNet (native executor on GPU),
-AlexNet, VGG (with and without BN), SqueezeNet, DenseNet, MobileNetV2/V3, ShuffleNetV2, MNASNet, GoogLeNet
-and Inception-v3 (stock-PyTorch engine).  ``pretrained=True`` loads weights
+AlexNet, VGG (with and without BN), SqueezeNet, DenseNet, MobileNetV2/V3, ShuffleNetV2, MNASNet, EfficientNet-B0..B7,
+GoogLeNet and Inception-v3 (stock-PyTorch engine).  ``pretrained=True`` loads weights
 from a LOCAL torchvision-format checkpoint (``--pretrained-path`` or ``$PDT_PRETRAINED_DIR/<arch>.pth``)
 with the safe ``weights_only`` loader -- the GPU box has no network.
 """
@@ -40,6 +40,7 @@ _REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
     "mnasnet0_5": efficient.mnasnet0_5, "mnasnet0_75": efficient.mnasnet0_75, "mnasnet1_0": efficient.mnasnet1_0,
     "mnasnet1_3": efficient.mnasnet1_3,
     "mobilenet_v3_large": efficient.mobilenet_v3_large, "mobilenet_v3_small": efficient.mobilenet_v3_small,
+    **efficient.EFFICIENTNETS,
 }
 
 

@@ -124,3 +124,25 @@ def test_inception_v3_default_image_size():
     assert cli.parse_args("ddp", ["-a", "inception_v3"]).image_size == 299
     assert cli.parse_args("ddp", ["-a", "resnet18"]).image_size == 224
     assert cli.parse_args("ddp", ["-a", "inception_v3", "--image-size", "320"]).image_size == 320
+
+
+@pytest.mark.parametrize("variant,nparams", [(0, 5288548), (1, 7794184), (2, 9109994), (3, 12233232),
+                                             (4, 19341616), (5, 30389784), (6, 43040704), (7, 66347960)])
+def test_efficientnet_param_counts(variant, nparams):
+    assert sum(p.numel() for p in registry.create(f"efficientnet_b{variant}").parameters()) == nparams
+
+
+def test_efficientnet_train_eval_and_stochastic_depth():
+    torch.manual_seed(0)
+    m = registry.create("efficientnet_b0", num_classes=5)
+    assert {"features.0.0.weight", "features.2.1.block.2.fc2.bias", "features.8.1.running_var",
+            "classifier.1.weight"} <= set(m.state_dict())
+    sd = [b.stochastic_depth.p for st in m.features[1:-1] for b in st]
+    assert sd[0] == 0.0 and abs(sd[-1] - 0.2 * 15 / 16) < 1e-12 and sorted(sd) == sd
+    x = torch.randn(4, 3, 64, 64)
+    m.train()
+    torch.nn.functional.cross_entropy(m(x), torch.tensor([0, 1, 2, 3])).backward()
+    assert all(p.grad is not None for p in m.parameters())
+    m.eval()
+    with torch.no_grad():
+        assert torch.equal(m(x), m(x))  # no stochastic depth / dropout in eval

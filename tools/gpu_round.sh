@@ -8,7 +8,7 @@ ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 for stage in "$@"; do
   case "$stage" in
     test)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
       tail -30 gpurun_out/pytest_gpu.log
       ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
     testk)
