@@ -4,7 +4,7 @@ lowercase callable in ``torchvision.models``; `:112-117` instantiates ``models._
 torchvision is not available offline here, so the registry is ours, with torchvision-identical
 parameter names, shapes and initialisation: ResNet / ResNeXt / Wide-ResNet (native executor on GPU),
 AlexNet, VGG (with and without BN), SqueezeNet, DenseNet, MobileNetV2/V3, ShuffleNetV2, MNASNet, EfficientNet-B0..B7,
-GoogLeNet and Inception-v3 (stock-PyTorch engine).  ``pretrained=True`` loads weights
+GoogLeNet, Inception-v3, RegNet-X/Y, ConvNeXt and ViT (stock-PyTorch engine).  ``pretrained=True`` loads weights
 from a LOCAL torchvision-format checkpoint (``--pretrained-path`` or ``$PDT_PRETRAINED_DIR/<arch>.pth``)
 with the safe ``weights_only`` loader -- the GPU box has no network.
 """
@@ -15,7 +15,7 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
-from . import classic, efficient, inception, mobile, resnet
+from . import classic, efficient, inception, mobile, modern, resnet
 
 _REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
     "resnet18": resnet.resnet18,
@@ -25,6 +25,7 @@ _REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
     "resnet152": resnet.resnet152,
     "resnext50_32x4d": resnet.resnext50_32x4d,
     "resnext101_32x8d": resnet.resnext101_32x8d,
+    "resnext101_64x4d": resnet.resnext101_64x4d,
     "wide_resnet50_2": resnet.wide_resnet50_2,
     "wide_resnet101_2": resnet.wide_resnet101_2,
     "alexnet": classic.alexnet,
@@ -41,6 +42,7 @@ _REGISTRY: Dict[str, Callable[..., torch.nn.Module]] = {
     "mnasnet1_3": efficient.mnasnet1_3,
     "mobilenet_v3_large": efficient.mobilenet_v3_large, "mobilenet_v3_small": efficient.mobilenet_v3_small,
     **efficient.EFFICIENTNETS,
+    **modern.MODERN,
 }
 
 

@@ -191,6 +191,11 @@ def resnext101_32x8d(pretrained: bool = False, **kwargs) -> ResNet:
     return _resnet(Bottleneck, [3, 4, 23, 3], pretrained, **kwargs)
 
 
+def resnext101_64x4d(pretrained: bool = False, **kwargs) -> ResNet:
+    kwargs.update(groups=64, width_per_group=4)
+    return _resnet(Bottleneck, [3, 4, 23, 3], pretrained, **kwargs)
+
+
 def wide_resnet50_2(pretrained: bool = False, **kwargs) -> ResNet:
     kwargs.update(width_per_group=64 * 2)
     return _resnet(Bottleneck, [3, 4, 6, 3], pretrained, **kwargs)

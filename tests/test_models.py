@@ -146,3 +146,45 @@ def test_efficientnet_train_eval_and_stochastic_depth():
     m.eval()
     with torch.no_grad():
         assert torch.equal(m(x), m(x))  # no stochastic depth / dropout in eval
+
+
+@pytest.mark.parametrize("arch,nparams", [
+    ("resnext101_64x4d", 83455272), ("regnet_y_400mf", 4344144), ("regnet_y_800mf", 6432512),
+    ("regnet_y_1_6gf", 11202430), ("regnet_y_3_2gf", 19436338), ("regnet_y_8gf", 39381472),
+    ("regnet_x_400mf", 5495976), ("regnet_x_800mf", 7259656), ("regnet_x_1_6gf", 9190136),
+    ("regnet_x_3_2gf", 15296552), ("regnet_x_8gf", 39572648), ("regnet_x_16gf", 54278536),
+    ("convnext_tiny", 28589128), ("convnext_small", 50223688), ("convnext_base", 88591464),
+    ("vit_b_16", 86567656), ("vit_b_32", 88224232)])
+def test_regnet_convnext_vit_param_counts(arch, nparams):
+    """torchvision parameter counts for RegNet-X/Y, ConvNeXt, ViT and ResNeXt-101 64x4d."""
+    assert sum(p.numel() for p in registry.create(arch).parameters()) == nparams
+
+
+@pytest.mark.parametrize("arch,kwargs,size", [
+    ("regnet_y_400mf", {}, 64), ("regnet_x_400mf", {}, 64), ("convnext_tiny", {}, 64),
+    ("vit_b_32", {"image_size": 64}, 64)])
+def test_modern_families_train_eval(arch, kwargs, size):
+    """One forward+backward in train mode reaches every parameter; eval returns [N, classes] logits."""
+    torch.manual_seed(0)
+    m = registry.create(arch, num_classes=7, **kwargs)
+    x = torch.randn(2, 3, size, size)
+    loss = torch.nn.functional.cross_entropy(m(x), torch.tensor([1, 3]))
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert all(p.grad is not None for p in m.parameters())
+    m.eval()
+    with torch.no_grad():
+        assert m(x).shape == (2, 7)
+
+
+def test_modern_state_dict_names():
+    """torchvision state-dict key spelling for the new families (loadable with torchvision checkpoints)."""
+    keys = set(registry.create("regnet_y_400mf").state_dict())
+    assert "trunk_output.block1.block1-0.f.se.fc1.weight" in keys and "stem.1.running_mean" in keys
+    assert "trunk_output.block1.block1-0.proj.0.weight" in keys and "fc.bias" in keys
+    keys = set(registry.create("convnext_tiny").state_dict())
+    assert "features.1.0.layer_scale" in keys and "features.1.0.block.3.weight" in keys
+    assert "features.2.0.weight" in keys and "classifier.0.weight" in keys
+    keys = set(registry.create("vit_b_32").state_dict())
+    assert {"class_token", "encoder.pos_embedding", "encoder.layers.encoder_layer_0.self_attention.in_proj_weight",
+            "encoder.layers.encoder_layer_11.mlp.3.bias", "encoder.ln.weight", "heads.head.weight"} <= keys
