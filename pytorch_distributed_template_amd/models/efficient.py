@@ -1,4 +1,4 @@
-"""MNASNet, MobileNetV3 and EfficientNet-B0..B7 with torchvision-identical module names, shapes and init.
+"""MNASNet, MobileNetV3, EfficientNet-B0..B7 and EfficientNetV2-S/M/L with torchvision-identical module names, shapes and init.
 
 Registry members (reference C05, `dataparallel.py:36-37`); executed by the stock-PyTorch engine.
 """
@@ -281,9 +281,40 @@ class MBConv(nn.Module):
         return self.stochastic_depth(y) + x if self.use_res_connect else y
 
 
+class _FusedMBConvConfig(_MBConvConfig):
+    """EfficientNetV2 early-stage block config (no width/depth scaling)."""
+
+    def __init__(self, expand_ratio: float, kernel: int, stride: int, in_ch: int, out_ch: int, num_layers: int):
+        super().__init__(expand_ratio, kernel, stride, in_ch, out_ch, num_layers, 1.0, 1.0)
+
+
+class FusedMBConv(nn.Module):
+    """Fused expand (kxk conv + BN + SiLU) -> 1x1 project; a single kxk conv when the expand ratio is 1."""
+
+    def __init__(self, cnf: _MBConvConfig, stochastic_depth_prob: float, norm_layer: Callable[..., nn.Module]):
+        super().__init__()
+        self.use_res_connect = cnf.stride == 1 and cnf.input_channels == cnf.out_channels
+        expanded = _make_divisible(cnf.input_channels * cnf.expand_ratio)
+        if expanded != cnf.input_channels:
+            layers = [ConvBNActivation(cnf.input_channels, expanded, cnf.kernel, cnf.stride, norm_layer=norm_layer,
+                                       activation_layer=nn.SiLU),
+                      ConvBNActivation(expanded, cnf.out_channels, 1, norm_layer=norm_layer, activation_layer=None)]
+        else:
+            layers = [ConvBNActivation(cnf.input_channels, cnf.out_channels, cnf.kernel, cnf.stride,
+                                       norm_layer=norm_layer, activation_layer=nn.SiLU)]
+        self.block = nn.Sequential(*layers)
+        self.stochastic_depth = StochasticDepth(stochastic_depth_prob)
+        self.out_channels = cnf.out_channels
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = self.block(x)
+        return self.stochastic_depth(y) + x if self.use_res_connect else y
+
+
 class EfficientNet(nn.Module):
     def __init__(self, setting: List[_MBConvConfig], dropout: float, stochastic_depth_prob: float = 0.2,
-                 num_classes: int = 1000, norm_layer: Optional[Callable[..., nn.Module]] = None):
+                 num_classes: int = 1000, norm_layer: Optional[Callable[..., nn.Module]] = None,
+                 last_channel: Optional[int] = None):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
         layers: List[nn.Module] = [ConvBNActivation(3, setting[0].input_channels, 3, 2, norm_layer=norm_layer,
@@ -297,14 +328,16 @@ class EfficientNet(nn.Module):
                 if stage:  # every block after a stage's first keeps the width and stride 1
                     bc.input_channels = bc.out_channels
                     bc.stride = 1
-                stage.append(MBConv(bc, stochastic_depth_prob * float(block_id) / total, norm_layer))
+                block = FusedMBConv if isinstance(cnf, _FusedMBConvConfig) else MBConv
+                stage.append(block(bc, stochastic_depth_prob * float(block_id) / total, norm_layer))
                 block_id += 1
             layers.append(nn.Sequential(*stage))
         last_in = setting[-1].out_channels
-        layers.append(ConvBNActivation(last_in, 4 * last_in, 1, norm_layer=norm_layer, activation_layer=nn.SiLU))
+        last_channel = last_channel or 4 * last_in
+        layers.append(ConvBNActivation(last_in, last_channel, 1, norm_layer=norm_layer, activation_layer=nn.SiLU))
         self.features = nn.Sequential(*layers)
         self.avgpool = nn.AdaptiveAvgPool2d(1)
-        self.classifier = nn.Sequential(nn.Dropout(p=dropout, inplace=True), nn.Linear(4 * last_in, num_classes))
+        self.classifier = nn.Sequential(nn.Dropout(p=dropout, inplace=True), nn.Linear(last_channel, num_classes))
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out")
@@ -346,3 +379,32 @@ def _effnet_ctor(variant: str):
 
 
 EFFICIENTNETS = {f"efficientnet_{v}": _effnet_ctor(v) for v in _EFFNET}
+
+
+# EfficientNetV2: (fused?, expand ratio, kernel, stride, in, out, layers) per stage, dropout
+_EFFNET_V2 = {
+    "s": ([(1, 1, 3, 1, 24, 24, 2), (1, 4, 3, 2, 24, 48, 4), (1, 4, 3, 2, 48, 64, 4), (0, 4, 3, 2, 64, 128, 6),
+           (0, 6, 3, 1, 128, 160, 9), (0, 6, 3, 2, 160, 256, 15)], 0.2),
+    "m": ([(1, 1, 3, 1, 24, 24, 3), (1, 4, 3, 2, 24, 48, 5), (1, 4, 3, 2, 48, 80, 5), (0, 4, 3, 2, 80, 160, 7),
+           (0, 6, 3, 1, 160, 176, 14), (0, 6, 3, 2, 176, 304, 18), (0, 6, 3, 1, 304, 512, 5)], 0.3),
+    "l": ([(1, 1, 3, 1, 32, 32, 4), (1, 4, 3, 2, 32, 64, 7), (1, 4, 3, 2, 64, 96, 7), (0, 4, 3, 2, 96, 192, 10),
+           (0, 6, 3, 1, 192, 224, 19), (0, 6, 3, 2, 224, 384, 25), (0, 6, 3, 1, 384, 640, 7)], 0.4),
+}
+
+
+def _efficientnet_v2(variant: str, **kwargs) -> EfficientNet:
+    stages, dropout = _EFFNET_V2[variant]
+    setting = [_FusedMBConvConfig(*st[1:]) if st[0] else _MBConvConfig(*st[1:], width_mult=1.0, depth_mult=1.0)
+               for st in stages]
+    kwargs.setdefault("norm_layer", partial(nn.BatchNorm2d, eps=1e-3))
+    return EfficientNet(setting, kwargs.pop("dropout", dropout), last_channel=1280, **kwargs)
+
+
+def _effnet_v2_ctor(variant: str):
+    def ctor(**kwargs) -> EfficientNet:
+        return _efficientnet_v2(variant, **kwargs)
+    ctor.__name__ = f"efficientnet_v2_{variant}"
+    return ctor
+
+
+EFFICIENTNETS.update({f"efficientnet_v2_{v}": _effnet_v2_ctor(v) for v in _EFFNET_V2})

@@ -1,4 +1,4 @@
-"""RegNet-X/Y, ConvNeXt and Vision Transformer with torchvision-identical module names, shapes, parameter
+"""RegNet-X/Y, ConvNeXt, Vision Transformer and Swin Transformer with torchvision-identical module names, shapes, parameter
 counts and init.
 
 Registry members (reference C05, `dataparallel.py:36-37` exposes every lowercase torchvision constructor as an
@@ -314,9 +314,145 @@ def vit_h_14(**kwargs) -> VisionTransformer:
     return _vit(14, 32, 16, 1280, 5120, **kwargs)
 
 
+# ------------------------------------------------------------------------------------------ Swin
+class ShiftedWindowAttention(nn.Module):
+    """Windowed MHSA with a learned relative-position bias and cyclic shift; the (bias + shift mask) is one
+    additive mask so the attention itself runs as PyTorch's fused scaled-dot-product kernel."""
+
+    def __init__(self, dim: int, window: int, shift: int, heads: int, attn_dropout: float, dropout: float):
+        super().__init__()
+        self.window_size, self.shift_size, self.num_heads = [window, window], [shift, shift], heads
+        self.attention_dropout, self.dropout = attn_dropout, dropout
+        self.qkv = nn.Linear(dim, dim * 3)
+        self.proj = nn.Linear(dim, dim)
+        self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * window - 1) ** 2, heads))
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
+        c = torch.stack(torch.meshgrid(torch.arange(window), torch.arange(window), indexing="ij")).flatten(1)
+        rel = (c[:, :, None] - c[:, None, :]).permute(1, 2, 0) + (window - 1)
+        self.register_buffer("relative_position_index", (rel[..., 0] * (2 * window - 1) + rel[..., 1]).flatten())
+
+    def _bias(self) -> torch.Tensor:
+        n = self.window_size[0] * self.window_size[1]
+        b = self.relative_position_bias_table[self.relative_position_index].view(n, n, -1)
+        return b.permute(2, 0, 1).unsqueeze(0)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, H, W, C = x.shape
+        ws = self.window_size[0]
+        pad_r, pad_b = (ws - W % ws) % ws, (ws - H % ws) % ws
+        x = nn.functional.pad(x, (0, 0, 0, pad_r, 0, pad_b))
+        pH, pW = x.shape[1], x.shape[2]
+        sh = self.shift_size[0] if ws < pH else 0
+        sw = self.shift_size[1] if ws < pW else 0
+        if sh or sw:
+            x = torch.roll(x, shifts=(-sh, -sw), dims=(1, 2))
+        nwin = (pH // ws) * (pW // ws)
+        x = x.view(B, pH // ws, ws, pW // ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B * nwin, ws * ws, C)
+        hd = C // self.num_heads
+        q, k, v = self.qkv(x).reshape(x.size(0), x.size(1), 3, self.num_heads, hd).permute(2, 0, 3, 1, 4)
+        mask = self._bias().to(q.dtype)                                     # [1, heads, N, N]
+        if sh or sw:
+            region = x.new_zeros((pH, pW))
+            cnt = 0
+            for hs in ((0, -ws), (-ws, -sh), (-sh, None)):
+                for wsl in ((0, -ws), (-ws, -sw), (-sw, None)):
+                    region[hs[0]:hs[1], wsl[0]:wsl[1]] = cnt
+                    cnt += 1
+            region = region.view(pH // ws, ws, pW // ws, ws).permute(0, 2, 1, 3).reshape(nwin, ws * ws)
+            shift = (region.unsqueeze(1) - region.unsqueeze(2)).ne(0).to(q.dtype) * -100.0
+            mask = (mask + shift.unsqueeze(1)).repeat(B, 1, 1, 1)           # [B*nwin, heads, N, N]
+        y = nn.functional.scaled_dot_product_attention(
+            q, k, v, attn_mask=mask, dropout_p=self.attention_dropout if self.training else 0.0)
+        y = self.proj(y.transpose(1, 2).reshape(x.size(0), x.size(1), C))
+        y = nn.functional.dropout(y, self.dropout, self.training)
+        y = y.view(B, pH // ws, pW // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, pH, pW, C)
+        if sh or sw:
+            y = torch.roll(y, shifts=(sh, sw), dims=(1, 2))
+        return y[:, :H, :W, :].contiguous()
+
+
+class SwinTransformerBlock(nn.Module):
+    def __init__(self, dim: int, heads: int, window: int, shift: int, sd_prob: float, dropout: float = 0.0,
+                 attn_dropout: float = 0.0):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-5)
+        self.attn = ShiftedWindowAttention(dim, window, shift, heads, attn_dropout, dropout)
+        self.stochastic_depth = StochasticDepth(sd_prob)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-5)
+        self.mlp = _MLPBlock(dim, 4 * dim, dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x + self.stochastic_depth(self.attn(self.norm1(x)))
+        return x + self.stochastic_depth(self.mlp(self.norm2(x)))
+
+
+class PatchMerging(nn.Module):
+    """2x2 space-to-depth (channels-last), LayerNorm, linear 4C -> 2C."""
+
+    def __init__(self, dim: int):
+        super().__init__()
+        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+        self.norm = nn.LayerNorm(4 * dim, eps=1e-5)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        H, W = x.shape[-3], x.shape[-2]
+        x = nn.functional.pad(x, (0, 0, 0, W % 2, 0, H % 2))
+        x = torch.cat([x[..., 0::2, 0::2, :], x[..., 1::2, 0::2, :], x[..., 0::2, 1::2, :],
+                       x[..., 1::2, 1::2, :]], -1)
+        return self.reduction(self.norm(x))
+
+
+class SwinTransformer(nn.Module):
+    def __init__(self, embed_dim: int, depths: List[int], heads: List[int], sd_prob: float, window: int = 7,
+                 patch: int = 4, num_classes: int = 1000):
+        super().__init__()
+        layers: List[nn.Module] = [nn.Sequential(nn.Conv2d(3, embed_dim, patch, patch), _Permute([0, 2, 3, 1]),
+                                                 nn.LayerNorm(embed_dim, eps=1e-5))]
+        total, bid = sum(depths), 0
+        for i, (depth, h) in enumerate(zip(depths, heads)):
+            dim = embed_dim * 2 ** i
+            stage = []
+            for j in range(depth):
+                stage.append(SwinTransformerBlock(dim, h, window, 0 if j % 2 == 0 else window // 2,
+                                                  sd_prob * bid / (total - 1.0)))
+                bid += 1
+            layers.append(nn.Sequential(*stage))
+            if i + 1 < len(depths):
+                layers.append(PatchMerging(dim))
+        self.features = nn.Sequential(*layers)
+        nf = embed_dim * 2 ** (len(depths) - 1)
+        self.norm = nn.LayerNorm(nf, eps=1e-5)
+        self.permute = _Permute([0, 3, 1, 2])
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.flatten = nn.Flatten(1)
+        self.head = nn.Linear(nf, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.permute(self.norm(self.features(x)))
+        return self.head(self.flatten(self.avgpool(x)))
+
+
+def swin_t(**kwargs) -> SwinTransformer:
+    return SwinTransformer(96, [2, 2, 6, 2], [3, 6, 12, 24], kwargs.pop("stochastic_depth_prob", 0.2), **kwargs)
+
+
+def swin_s(**kwargs) -> SwinTransformer:
+    return SwinTransformer(96, [2, 2, 18, 2], [3, 6, 12, 24], kwargs.pop("stochastic_depth_prob", 0.3), **kwargs)
+
+
+def swin_b(**kwargs) -> SwinTransformer:
+    return SwinTransformer(128, [2, 2, 18, 2], [4, 8, 16, 32], kwargs.pop("stochastic_depth_prob", 0.5), **kwargs)
+
+
 MODERN = {
     **REGNETS,
     "convnext_tiny": convnext_tiny, "convnext_small": convnext_small, "convnext_base": convnext_base,
     "convnext_large": convnext_large,
     "vit_b_16": vit_b_16, "vit_b_32": vit_b_32, "vit_l_16": vit_l_16, "vit_l_32": vit_l_32, "vit_h_14": vit_h_14,
+    "swin_t": swin_t, "swin_s": swin_s, "swin_b": swin_b,
 }

@@ -188,3 +188,60 @@ def test_modern_state_dict_names():
     keys = set(registry.create("vit_b_32").state_dict())
     assert {"class_token", "encoder.pos_embedding", "encoder.layers.encoder_layer_0.self_attention.in_proj_weight",
             "encoder.layers.encoder_layer_11.mlp.3.bias", "encoder.ln.weight", "heads.head.weight"} <= keys
+
+
+@pytest.mark.parametrize("arch,nparams", [
+    ("efficientnet_v2_s", 21458488), ("efficientnet_v2_m", 54139356), ("swin_t", 28288354),
+    ("swin_s", 49606258), ("swin_b", 87768224)])
+def test_effnet_v2_swin_param_counts(arch, nparams):
+    assert sum(p.numel() for p in registry.create(arch).parameters()) == nparams
+
+
+@pytest.mark.parametrize("arch", ["efficientnet_v2_s", "swin_t"])
+def test_effnet_v2_swin_train_eval(arch):
+    torch.manual_seed(0)
+    m = registry.create(arch, num_classes=7)
+    x = torch.randn(2, 3, 64, 64)
+    loss = torch.nn.functional.cross_entropy(m(x), torch.tensor([1, 3]))
+    loss.backward()
+    assert torch.isfinite(loss) and all(p.grad is not None for p in m.parameters())
+    m.eval()
+    with torch.no_grad():
+        assert m(x).shape == (2, 7)
+
+
+@pytest.mark.parametrize("shift,size", [(0, 14), (3, 14), (3, 10)])
+def test_shifted_window_attention_matches_explicit(shift, size):
+    """Fused-SDPA shifted-window attention == explicit softmax(QK^T*s + rel-bias + shift-mask)V (fp32)."""
+    from pytorch_distributed_template_amd.models.modern import ShiftedWindowAttention
+    torch.manual_seed(0)
+    ws, C, heads, B = 7, 24, 3, 2
+    att = ShiftedWindowAttention(C, ws, shift, heads, 0.0, 0.0).eval()
+    x = torch.randn(B, size, size, C)
+    got = att(x)
+    # explicit reference on the padded, rolled, windowed grid
+    pad = (ws - size % ws) % ws
+    xp = torch.nn.functional.pad(x, (0, 0, 0, pad, 0, pad))
+    P = xp.shape[1]
+    s = shift if ws < P else 0
+    xr = torch.roll(xp, (-s, -s), (1, 2))
+    region = torch.zeros(P, P)
+    if s:
+        cnt = 0
+        for h in ((0, -ws), (-ws, -s), (-s, None)):
+            for w in ((0, -ws), (-ws, -s), (-s, None)):
+                region[h[0]:h[1], w[0]:w[1]] = cnt
+                cnt += 1
+    out = torch.zeros_like(xr)
+    bias = att._bias()[0]
+    for i in range(0, P, ws):
+        for j in range(0, P, ws):
+            win = xr[:, i:i + ws, j:j + ws].reshape(B, ws * ws, C)
+            reg = region[i:i + ws, j:j + ws].reshape(-1)
+            q, k, v = att.qkv(win).reshape(B, ws * ws, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+            a = q @ k.transpose(-1, -2) * (C // heads) ** -0.5 + bias
+            a = a + (reg[None, :] != reg[:, None]).float() * -100.0
+            o = (a.softmax(-1) @ v).transpose(1, 2).reshape(B, ws * ws, C)
+            out[:, i:i + ws, j:j + ws] = att.proj(o).reshape(B, ws, ws, C)
+    ref = torch.roll(out, (s, s), (1, 2))[:, :size, :size]
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-4)

@@ -118,3 +118,22 @@ dist.destroy_process_group()
     r = _run(["-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=2", f"--master_port={_free_port()}",
               "--no_local_rank", str(script)], timeout=600)
     assert "SUMS" in r.stdout
+
+
+@pytest.mark.parametrize("arch", ["regnet_y_400mf", "convnext_tiny", "swin_t", "efficientnet_v2_s", "vit_b_32"])
+def test_modern_families_torch_engine_gpu(arch):
+    """RegNet / ConvNeXt / Swin / EfficientNetV2 / ViT train (bf16 autocast, SGD) and evaluate on cuda:0."""
+    from pytorch_distributed_template_amd.engine.torch_trainer import TorchTrainer
+    from pytorch_distributed_template_amd.models import registry
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    kw = {"image_size": 64} if arch.startswith("vit") else {}
+    tr = TorchTrainer(registry.create(arch, num_classes=10, **kw), dev, dtype=torch.bfloat16, lr=0.01)
+    x = torch.randn(8, 3, 64, 64, device=dev)
+    t = torch.randint(0, 10, (8,), device=dev)
+    for _ in range(2):
+        _, met = tr.train_step(x, t)
+    assert torch.isfinite(torch.as_tensor(met[0])).all()
+    out = tr.eval_step(x, t)
+    torch.cuda.synchronize()
+    assert out is not None
