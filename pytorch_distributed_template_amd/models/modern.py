@@ -319,22 +319,32 @@ class ShiftedWindowAttention(nn.Module):
     """Windowed MHSA with a learned relative-position bias and cyclic shift; the (bias + shift mask) is one
     additive mask so the attention itself runs as PyTorch's fused scaled-dot-product kernel."""
 
-    def __init__(self, dim: int, window: int, shift: int, heads: int, attn_dropout: float, dropout: float):
+    def __init__(self, dim: int, window: int, shift: int, heads: int, attn_dropout: float, dropout: float,
+                 v2: bool = False):
         super().__init__()
         self.window_size, self.shift_size, self.num_heads = [window, window], [shift, shift], heads
-        self.attention_dropout, self.dropout = attn_dropout, dropout
+        self.attention_dropout, self.dropout, self.v2 = attn_dropout, dropout, v2
         self.qkv = nn.Linear(dim, dim * 3)
         self.proj = nn.Linear(dim, dim)
-        self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * window - 1) ** 2, heads))
-        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
+        if v2:  # Swin V2: cosine attention with a learned per-head temperature, log-spaced continuous bias MLP
+            self.logit_scale = nn.Parameter(torch.log(10 * torch.ones((heads, 1, 1))))
+            self.cpb_mlp = nn.Sequential(nn.Linear(2, 512), nn.ReLU(inplace=True), nn.Linear(512, heads, bias=False))
+            r = torch.arange(-(window - 1), window, dtype=torch.float32) / (window - 1) * 8
+            t = torch.stack(torch.meshgrid(r, r, indexing="ij")).permute(1, 2, 0).unsqueeze(0)
+            self.register_buffer("relative_coords_table", torch.sign(t) * torch.log2(t.abs() + 1.0) / 3.0)
+        else:
+            self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * window - 1) ** 2, heads))
+            nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
         c = torch.stack(torch.meshgrid(torch.arange(window), torch.arange(window), indexing="ij")).flatten(1)
         rel = (c[:, :, None] - c[:, None, :]).permute(1, 2, 0) + (window - 1)
         self.register_buffer("relative_position_index", (rel[..., 0] * (2 * window - 1) + rel[..., 1]).flatten())
 
     def _bias(self) -> torch.Tensor:
         n = self.window_size[0] * self.window_size[1]
-        b = self.relative_position_bias_table[self.relative_position_index].view(n, n, -1)
-        return b.permute(2, 0, 1).unsqueeze(0)
+        table = (self.cpb_mlp(self.relative_coords_table).view(-1, self.num_heads) if self.v2
+                 else self.relative_position_bias_table)
+        b = table[self.relative_position_index].view(n, n, -1).permute(2, 0, 1).unsqueeze(0)
+        return 16 * torch.sigmoid(b) if self.v2 else b
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, H, W, C = x.shape
@@ -349,7 +359,16 @@ class ShiftedWindowAttention(nn.Module):
         nwin = (pH // ws) * (pW // ws)
         x = x.view(B, pH // ws, ws, pW // ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B * nwin, ws * ws, C)
         hd = C // self.num_heads
-        q, k, v = self.qkv(x).reshape(x.size(0), x.size(1), 3, self.num_heads, hd).permute(2, 0, 3, 1, 4)
+        qkv_bias = self.qkv.bias
+        if self.v2:  # the key bias is held at zero
+            qkv_bias = torch.cat([qkv_bias[:C], torch.zeros_like(qkv_bias[C:2 * C]), qkv_bias[2 * C:]])
+        qkv = nn.functional.linear(x, self.qkv.weight, qkv_bias)
+        q, k, v = qkv.reshape(x.size(0), x.size(1), 3, self.num_heads, hd).permute(2, 0, 3, 1, 4)
+        scale = None
+        if self.v2:
+            q = nn.functional.normalize(q, dim=-1) * torch.clamp(self.logit_scale, max=math.log(100.0)).exp()
+            k = nn.functional.normalize(k, dim=-1)
+            scale = 1.0
         mask = self._bias().to(q.dtype)                                     # [1, heads, N, N]
         if sh or sw:
             region = x.new_zeros((pH, pW))
@@ -362,7 +381,7 @@ class ShiftedWindowAttention(nn.Module):
             shift = (region.unsqueeze(1) - region.unsqueeze(2)).ne(0).to(q.dtype) * -100.0
             mask = (mask + shift.unsqueeze(1)).repeat(B, 1, 1, 1)           # [B*nwin, heads, N, N]
         y = nn.functional.scaled_dot_product_attention(
-            q, k, v, attn_mask=mask, dropout_p=self.attention_dropout if self.training else 0.0)
+            q, k, v, attn_mask=mask, dropout_p=self.attention_dropout if self.training else 0.0, scale=scale)
         y = self.proj(y.transpose(1, 2).reshape(x.size(0), x.size(1), C))
         y = nn.functional.dropout(y, self.dropout, self.training)
         y = y.view(B, pH // ws, pW // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, pH, pW, C)
@@ -373,15 +392,19 @@ class ShiftedWindowAttention(nn.Module):
 
 class SwinTransformerBlock(nn.Module):
     def __init__(self, dim: int, heads: int, window: int, shift: int, sd_prob: float, dropout: float = 0.0,
-                 attn_dropout: float = 0.0):
+                 attn_dropout: float = 0.0, v2: bool = False):
         super().__init__()
+        self.v2 = v2
         self.norm1 = nn.LayerNorm(dim, eps=1e-5)
-        self.attn = ShiftedWindowAttention(dim, window, shift, heads, attn_dropout, dropout)
+        self.attn = ShiftedWindowAttention(dim, window, shift, heads, attn_dropout, dropout, v2)
         self.stochastic_depth = StochasticDepth(sd_prob)
         self.norm2 = nn.LayerNorm(dim, eps=1e-5)
         self.mlp = _MLPBlock(dim, 4 * dim, dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.v2:  # residual post-norm
+            x = x + self.stochastic_depth(self.norm1(self.attn(x)))
+            return x + self.stochastic_depth(self.norm2(self.mlp(x)))
         x = x + self.stochastic_depth(self.attn(self.norm1(x)))
         return x + self.stochastic_depth(self.mlp(self.norm2(x)))
 
@@ -389,22 +412,23 @@ class SwinTransformerBlock(nn.Module):
 class PatchMerging(nn.Module):
     """2x2 space-to-depth (channels-last), LayerNorm, linear 4C -> 2C."""
 
-    def __init__(self, dim: int):
+    def __init__(self, dim: int, v2: bool = False):
         super().__init__()
+        self.v2 = v2
         self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
-        self.norm = nn.LayerNorm(4 * dim, eps=1e-5)
+        self.norm = nn.LayerNorm(2 * dim if v2 else 4 * dim, eps=1e-5)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         H, W = x.shape[-3], x.shape[-2]
         x = nn.functional.pad(x, (0, 0, 0, W % 2, 0, H % 2))
         x = torch.cat([x[..., 0::2, 0::2, :], x[..., 1::2, 0::2, :], x[..., 0::2, 1::2, :],
                        x[..., 1::2, 1::2, :]], -1)
-        return self.reduction(self.norm(x))
+        return self.norm(self.reduction(x)) if self.v2 else self.reduction(self.norm(x))
 
 
 class SwinTransformer(nn.Module):
     def __init__(self, embed_dim: int, depths: List[int], heads: List[int], sd_prob: float, window: int = 7,
-                 patch: int = 4, num_classes: int = 1000):
+                 patch: int = 4, num_classes: int = 1000, v2: bool = False):
         super().__init__()
         layers: List[nn.Module] = [nn.Sequential(nn.Conv2d(3, embed_dim, patch, patch), _Permute([0, 2, 3, 1]),
                                                  nn.LayerNorm(embed_dim, eps=1e-5))]
@@ -414,11 +438,11 @@ class SwinTransformer(nn.Module):
             stage = []
             for j in range(depth):
                 stage.append(SwinTransformerBlock(dim, h, window, 0 if j % 2 == 0 else window // 2,
-                                                  sd_prob * bid / (total - 1.0)))
+                                                  sd_prob * bid / (total - 1.0), v2=v2))
                 bid += 1
             layers.append(nn.Sequential(*stage))
             if i + 1 < len(depths):
-                layers.append(PatchMerging(dim))
+                layers.append(PatchMerging(dim, v2))
         self.features = nn.Sequential(*layers)
         nf = embed_dim * 2 ** (len(depths) - 1)
         self.norm = nn.LayerNorm(nf, eps=1e-5)
@@ -449,10 +473,26 @@ def swin_b(**kwargs) -> SwinTransformer:
     return SwinTransformer(128, [2, 2, 18, 2], [4, 8, 16, 32], kwargs.pop("stochastic_depth_prob", 0.5), **kwargs)
 
 
+def swin_v2_t(**kwargs) -> SwinTransformer:
+    return SwinTransformer(96, [2, 2, 6, 2], [3, 6, 12, 24], kwargs.pop("stochastic_depth_prob", 0.2), window=8,
+                           v2=True, **kwargs)
+
+
+def swin_v2_s(**kwargs) -> SwinTransformer:
+    return SwinTransformer(96, [2, 2, 18, 2], [3, 6, 12, 24], kwargs.pop("stochastic_depth_prob", 0.3), window=8,
+                           v2=True, **kwargs)
+
+
+def swin_v2_b(**kwargs) -> SwinTransformer:
+    return SwinTransformer(128, [2, 2, 18, 2], [4, 8, 16, 32], kwargs.pop("stochastic_depth_prob", 0.5), window=8,
+                           v2=True, **kwargs)
+
+
 MODERN = {
     **REGNETS,
     "convnext_tiny": convnext_tiny, "convnext_small": convnext_small, "convnext_base": convnext_base,
     "convnext_large": convnext_large,
     "vit_b_16": vit_b_16, "vit_b_32": vit_b_32, "vit_l_16": vit_l_16, "vit_l_32": vit_l_32, "vit_h_14": vit_h_14,
     "swin_t": swin_t, "swin_s": swin_s, "swin_b": swin_b,
+    "swin_v2_t": swin_v2_t, "swin_v2_s": swin_v2_s, "swin_v2_b": swin_v2_b,
 }

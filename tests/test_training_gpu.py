@@ -120,7 +120,8 @@ dist.destroy_process_group()
     assert "SUMS" in r.stdout
 
 
-@pytest.mark.parametrize("arch", ["regnet_y_400mf", "convnext_tiny", "swin_t", "efficientnet_v2_s", "vit_b_32"])
+@pytest.mark.parametrize("arch", ["regnet_y_400mf", "convnext_tiny", "swin_t", "swin_v2_t", "efficientnet_v2_s",
+                                  "vit_b_32"])
 def test_modern_families_torch_engine_gpu(arch):
     """RegNet / ConvNeXt / Swin / EfficientNetV2 / ViT train (bf16 autocast, SGD) and evaluate on cuda:0."""
     from pytorch_distributed_template_amd.engine.torch_trainer import TorchTrainer
