@@ -1,4 +1,4 @@
-"""RegNet-X/Y, ConvNeXt, Vision Transformer and Swin Transformer with torchvision-identical module names, shapes, parameter
+"""RegNet-X/Y, ConvNeXt, Vision Transformer, Swin Transformer (V1/V2) and MaxViT with torchvision-identical module names, shapes, parameter
 counts and init.
 
 Registry members (reference C05, `dataparallel.py:36-37` exposes every lowercase torchvision constructor as an
@@ -488,6 +488,159 @@ def swin_v2_b(**kwargs) -> SwinTransformer:
                            v2=True, **kwargs)
 
 
+# ------------------------------------------------------------------------------------------ MaxViT
+class _MaxVitMBConv(nn.Module):
+    """Pre-norm inverted bottleneck (1x1 -> 3x3 depthwise -> SE -> 1x1) with an avg-pool + 1x1 projection."""
+
+    def __init__(self, cin: int, cout: int, expansion: float, squeeze: float, stride: int,
+                 norm: Callable[..., nn.Module], sd_prob: float):
+        super().__init__()
+        mid, sqz = int(cout * expansion), int(cout * squeeze)
+        self.stochastic_depth = StochasticDepth(sd_prob) if sd_prob else nn.Identity()
+        if stride != 1 or cin != cout:
+            proj: List[nn.Module] = [nn.AvgPool2d(3, stride, 1)] if stride == 2 else []
+            self.proj = nn.Sequential(*proj, nn.Conv2d(cin, cout, 1, bias=True))
+        else:
+            self.proj = nn.Identity()
+        f = OrderedDict()
+        f["pre_norm"] = norm(cin)
+        f["conv_a"] = nn.Sequential(nn.Conv2d(cin, mid, 1, bias=False), norm(mid), nn.GELU())
+        f["conv_b"] = nn.Sequential(nn.Conv2d(mid, mid, 3, stride, 1, groups=mid, bias=False), norm(mid), nn.GELU())
+        f["squeeze_excitation"] = _SE(mid, sqz)
+        f["conv_c"] = nn.Conv2d(mid, cout, 1, bias=True)
+        self.layers = nn.Sequential(f)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.proj(x) + self.stochastic_depth(self.layers(x))
+
+
+class _SE(_RegNetSE):
+    """Squeeze-excitation with a SiLU squeeze."""
+
+    def __init__(self, channels: int, squeeze: int):
+        super().__init__(channels, squeeze)
+        self.activation = nn.SiLU()
+
+
+class RelativePositionalMultiHeadAttention(nn.Module):
+    """MHSA over a P-token partition with a learned 2-D relative-position bias (fused SDPA; the query scale is
+    feat_dim^-0.5, as in torchvision's MaxViT)."""
+
+    def __init__(self, feat_dim: int, head_dim: int, max_seq_len: int):
+        super().__init__()
+        self.n_heads, self.head_dim = feat_dim // head_dim, head_dim
+        self.size, self.max_seq_len = int(math.sqrt(max_seq_len)), max_seq_len
+        self.to_qkv = nn.Linear(feat_dim, self.n_heads * head_dim * 3)
+        self.scale_factor = feat_dim ** -0.5
+        self.merge = nn.Linear(self.n_heads * head_dim, feat_dim)
+        n = self.size
+        self.relative_position_bias_table = nn.Parameter(torch.empty((2 * n - 1) ** 2, self.n_heads))
+        c = torch.stack(torch.meshgrid(torch.arange(n), torch.arange(n), indexing="ij")).flatten(1)
+        rel = (c[:, :, None] - c[:, None, :]).permute(1, 2, 0) + (n - 1)
+        self.register_buffer("relative_position_index", rel[..., 0] * (2 * n - 1) + rel[..., 1])
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
+
+    def get_relative_positional_bias(self) -> torch.Tensor:
+        b = self.relative_position_bias_table[self.relative_position_index.view(-1)]
+        return b.view(self.max_seq_len, self.max_seq_len, -1).permute(2, 0, 1).unsqueeze(0)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, G, P, D = x.shape
+        q, k, v = (t.reshape(B, G, P, self.n_heads, self.head_dim).permute(0, 1, 3, 2, 4)
+                   for t in self.to_qkv(x).chunk(3, dim=-1))
+        bias = self.get_relative_positional_bias().to(q.dtype)
+        out = nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=self.scale_factor)
+        return self.merge(out.permute(0, 1, 3, 2, 4).reshape(B, G, P, D))
+
+
+class PartitionAttentionLayer(nn.Module):
+    """Block (window) or grid (dilated) partition -> attention + MLP (pre-LN, stochastic depth) -> departition."""
+
+    def __init__(self, channels: int, head_dim: int, partition: int, kind: str, grid: int, mlp_ratio: int,
+                 attn_dropout: float, mlp_dropout: float, sd_prob: float):
+        super().__init__()
+        self.n_partitions = grid // partition
+        self.p = partition if kind == "window" else self.n_partitions
+        self.grid = kind == "grid"
+        self.attn_layer = nn.Sequential(nn.LayerNorm(channels),
+                                        RelativePositionalMultiHeadAttention(channels, head_dim, partition ** 2),
+                                        nn.Dropout(attn_dropout))
+        self.mlp_layer = nn.Sequential(nn.LayerNorm(channels), nn.Linear(channels, channels * mlp_ratio), nn.GELU(),
+                                       nn.Linear(channels * mlp_ratio, channels), nn.Dropout(mlp_dropout))
+        self.stochastic_dropout = StochasticDepth(sd_prob)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, C, H, W = x.shape
+        p, gh, gw = self.p, H // self.p, W // self.p
+        x = x.reshape(B, C, gh, p, gw, p).permute(0, 2, 4, 3, 5, 1).reshape(B, gh * gw, p * p, C)
+        if self.grid:
+            x = x.transpose(-2, -3)
+        x = x + self.stochastic_dropout(self.attn_layer(x))
+        x = x + self.stochastic_dropout(self.mlp_layer(x))
+        if self.grid:
+            x = x.transpose(-2, -3)
+        return x.reshape(B, gh, gw, p, p, C).permute(0, 5, 1, 3, 2, 4).reshape(B, C, gh * p, gw * p)
+
+
+class MaxVit(nn.Module):
+    def __init__(self, input_size=(224, 224), stem_channels: int = 64, partition_size: int = 7,
+                 block_channels=(64, 128, 256, 512), block_layers=(2, 2, 5, 2), head_dim: int = 32,
+                 stochastic_depth_prob: float = 0.2, squeeze_ratio: float = 0.25, expansion_ratio: float = 4,
+                 mlp_ratio: int = 4, mlp_dropout: float = 0.0, attention_dropout: float = 0.0,
+                 num_classes: int = 1000):
+        super().__init__()
+        norm = partial(nn.BatchNorm2d, eps=1e-3, momentum=0.01)
+        self.stem = nn.Sequential(
+            nn.Sequential(nn.Conv2d(3, stem_channels, 3, 2, 1, bias=False), norm(stem_channels), nn.GELU()),
+            nn.Sequential(nn.Conv2d(stem_channels, stem_channels, 3, 1, 1, bias=True)))
+        grid = (input_size[0] - 1) // 2 + 1
+        sd = torch.linspace(0, stochastic_depth_prob, sum(block_layers)).tolist()
+        self.partition_size = partition_size
+        self.blocks = nn.ModuleList()
+        cin, li = stem_channels, 0
+        for cout, n in zip(block_channels, block_layers):
+            grid = (grid - 1) // 2 + 1
+            if grid % partition_size:
+                raise ValueError(f"feature grid {grid} not divisible by partition size {partition_size}")
+            blk = nn.Module()
+            blk.layers = nn.ModuleList()
+            for j in range(n):
+                f = OrderedDict()
+                f["MBconv"] = _MaxVitMBConv(cin if j == 0 else cout, cout, expansion_ratio, squeeze_ratio,
+                                            2 if j == 0 else 1, norm, sd[li])
+                for kind in ("window", "grid"):
+                    f[f"{kind}_attention"] = PartitionAttentionLayer(cout, head_dim, partition_size, kind, grid,
+                                                                     mlp_ratio, attention_dropout, mlp_dropout, sd[li])
+                layer = nn.Module()
+                layer.layers = nn.Sequential(f)
+                blk.layers.append(layer)
+                li += 1
+            self.blocks.append(blk)
+            cin = cout
+        c = block_channels[-1]
+        self.classifier = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.LayerNorm(c), nn.Linear(c, c),
+                                        nn.Tanh(), nn.Linear(c, num_classes, bias=False))
+        for m in self.modules():
+            if isinstance(m, (nn.Conv2d, nn.Linear)):
+                nn.init.normal_(m.weight, std=0.02)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.stem(x)
+        for blk in self.blocks:
+            for layer in blk.layers:
+                x = layer.layers(x)
+        return self.classifier(x)
+
+
+def maxvit_t(**kwargs) -> MaxVit:
+    return MaxVit(**kwargs)
+
+
 MODERN = {
     **REGNETS,
     "convnext_tiny": convnext_tiny, "convnext_small": convnext_small, "convnext_base": convnext_base,
@@ -495,4 +648,5 @@ MODERN = {
     "vit_b_16": vit_b_16, "vit_b_32": vit_b_32, "vit_l_16": vit_l_16, "vit_l_32": vit_l_32, "vit_h_14": vit_h_14,
     "swin_t": swin_t, "swin_s": swin_s, "swin_b": swin_b,
     "swin_v2_t": swin_v2_t, "swin_v2_s": swin_v2_s, "swin_v2_b": swin_v2_b,
+    "maxvit_t": maxvit_t,
 }

@@ -4,7 +4,7 @@ lowercase callable in ``torchvision.models``; `:112-117` instantiates ``models._
 torchvision is not available offline here, so the registry is ours, with torchvision-identical
 parameter names, shapes and initialisation: ResNet / ResNeXt / Wide-ResNet (native executor on GPU),
 AlexNet, VGG (with and without BN), SqueezeNet, DenseNet, MobileNetV2/V3, ShuffleNetV2, MNASNet, EfficientNet-B0..B7,
-GoogLeNet, Inception-v3, EfficientNetV2, RegNet-X/Y, ConvNeXt, ViT and Swin (stock-PyTorch engine).  ``pretrained=True`` loads weights
+GoogLeNet, Inception-v3, EfficientNetV2, RegNet-X/Y, ConvNeXt, ViT, Swin V1/V2 and MaxViT (stock-PyTorch engine).  ``pretrained=True`` loads weights
 from a LOCAL torchvision-format checkpoint (``--pretrained-path`` or ``$PDT_PRETRAINED_DIR/<arch>.pth``)
 with the safe ``weights_only`` loader -- the GPU box has no network.
 """

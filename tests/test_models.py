@@ -275,3 +275,28 @@ def test_swin_v2_train_eval_and_keys():
     loss = torch.nn.functional.cross_entropy(m(torch.randn(2, 3, 64, 64)), torch.tensor([1, 3]))
     loss.backward()
     assert torch.isfinite(loss) and all(p.grad is not None for p in m.parameters())
+
+
+def test_maxvit_param_count_and_train_eval():
+    assert sum(p.numel() for p in registry.create("maxvit_t").parameters()) == 30919624
+    torch.manual_seed(0)
+    m = registry.create("maxvit_t", input_size=(64, 64), partition_size=2, num_classes=7)
+    assert "blocks.3.layers.1.layers.grid_attention.attn_layer.1.relative_position_bias_table" in m.state_dict()
+    loss = torch.nn.functional.cross_entropy(m(torch.randn(2, 3, 64, 64)), torch.tensor([1, 3]))
+    loss.backward()
+    assert torch.isfinite(loss) and all(p.grad is not None for p in m.parameters())
+    with pytest.raises(ValueError):
+        registry.create("maxvit_t", input_size=(64, 64))  # grid 2 not divisible by the 7x7 partition
+
+
+def test_maxvit_relative_attention_matches_explicit():
+    """Fused-SDPA relative-position attention == explicit softmax(Q K^T * feat_dim^-0.5 + bias) V (fp32)."""
+    from pytorch_distributed_template_amd.models.modern import RelativePositionalMultiHeadAttention
+    torch.manual_seed(0)
+    D, hd, P = 64, 16, 9
+    att = RelativePositionalMultiHeadAttention(D, hd, P).eval()
+    x = torch.randn(2, 5, P, D)
+    q, k, v = (t.reshape(2, 5, P, D // hd, hd).permute(0, 1, 3, 2, 4) for t in att.to_qkv(x).chunk(3, -1))
+    a = torch.einsum("bghid,bghjd->bghij", q, k * D ** -0.5) + att.get_relative_positional_bias()
+    ref = att.merge(torch.einsum("bghij,bghjd->bghid", a.softmax(-1), v).permute(0, 1, 3, 2, 4).reshape(2, 5, P, D))
+    torch.testing.assert_close(att(x), ref, atol=1e-5, rtol=1e-4)

@@ -121,14 +121,14 @@ dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("arch", ["regnet_y_400mf", "convnext_tiny", "swin_t", "swin_v2_t", "efficientnet_v2_s",
-                                  "vit_b_32"])
+                                  "vit_b_32", "maxvit_t"])
 def test_modern_families_torch_engine_gpu(arch):
     """RegNet / ConvNeXt / Swin / EfficientNetV2 / ViT train (bf16 autocast, SGD) and evaluate on cuda:0."""
     from pytorch_distributed_template_amd.engine.torch_trainer import TorchTrainer
     from pytorch_distributed_template_amd.models import registry
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    kw = {"image_size": 64} if arch.startswith("vit") else {}
+    kw = {"vit_b_32": {"image_size": 64}, "maxvit_t": {"input_size": (64, 64), "partition_size": 2}}.get(arch, {})
     tr = TorchTrainer(registry.create(arch, num_classes=10, **kw), dev, dtype=torch.bfloat16, lr=0.01)
     x = torch.randn(8, 3, 64, 64, device=dev)
     t = torch.randint(0, 10, (8,), device=dev)
