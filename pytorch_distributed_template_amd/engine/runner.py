@@ -243,7 +243,8 @@ def main(mode: str, argv: Optional[list] = None) -> int:
     else:
         ddp_print("=> creating model: {}".format(args.arch), logger, rank)
     model = registry.create(args.arch, pretrained=args.pretrained, pretrained_path=args.pretrained_path,
-                            num_classes=args.num_classes)
+                            num_classes=args.num_classes,
+                            **registry.resolution_kwargs(args.arch, getattr(args, "image_size", None) or 224))
     if mode == "ddp_amp":
         if distributed and args.sync_batchnorm:
             ddp_print("=> using sync BN", logger, rank)

@@ -341,9 +341,10 @@ class ShiftedWindowAttention(nn.Module):
 
     def _bias(self) -> torch.Tensor:
         n = self.window_size[0] * self.window_size[1]
-        table = (self.cpb_mlp(self.relative_coords_table).view(-1, self.num_heads) if self.v2
+        # buffers are cloned: the trainer's buffer sync may rewrite them in place before backward
+        table = (self.cpb_mlp(self.relative_coords_table.clone()).view(-1, self.num_heads) if self.v2
                  else self.relative_position_bias_table)
-        b = table[self.relative_position_index].view(n, n, -1).permute(2, 0, 1).unsqueeze(0)
+        b = table[self.relative_position_index.clone()].view(n, n, -1).permute(2, 0, 1).unsqueeze(0)
         return 16 * torch.sigmoid(b) if self.v2 else b
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -541,7 +542,7 @@ class RelativePositionalMultiHeadAttention(nn.Module):
         nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
 
     def get_relative_positional_bias(self) -> torch.Tensor:
-        b = self.relative_position_bias_table[self.relative_position_index.view(-1)]
+        b = self.relative_position_bias_table[self.relative_position_index.view(-1).clone()]  # see _bias above
         return b.view(self.max_seq_len, self.max_seq_len, -1).permute(2, 0, 1).unsqueeze(0)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

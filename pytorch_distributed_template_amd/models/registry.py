@@ -56,6 +56,19 @@ def model_names() -> List[str]:
     return sorted(_REGISTRY)
 
 
+def resolution_kwargs(arch: str, size: int) -> dict:
+    """Constructor kwargs for the fixed-resolution archs (ViT position table, MaxViT partition grid) at a
+    ``size`` x ``size`` crop; empty for the resolution-agnostic CNNs."""
+    if arch.startswith("vit_"):
+        return {"image_size": size}
+    if arch == "maxvit_t":
+        g = size
+        for _ in range(5):
+            g = (g - 1) // 2 + 1
+        return {"input_size": (size, size), "partition_size": max(d for d in range(1, 8) if g % d == 0)}
+    return {}
+
+
 def create(arch: str, pretrained: bool = False, pretrained_path: Optional[str] = None, **kwargs) -> torch.nn.Module:
     if arch not in _REGISTRY:
         raise KeyError(f"unknown arch {arch!r}; choices: {model_names()}")
