@@ -123,3 +123,16 @@ def test_distributed_googlenet_aux_heads_cpu(tmp_path):
     log = open(os.path.join(out + "_googlenet", "experiment.log")).read()
     assert "=> creating model: googlenet" in log
     assert re.search(r"\|\|==> total_time_cost=\d+\.\d{4}s", log)
+
+
+def test_fixed_resolution_archs_follow_cli_crop(tmp_path):
+    """ViT / MaxViT are built for ``--image-size`` (position table / partition grid), so the CLI runs them at
+    a non-224 crop."""
+    from pytorch_distributed_template_amd.models import registry
+    assert registry.resolution_kwargs("vit_b_16", 64) == {"image_size": 64}
+    assert registry.resolution_kwargs("maxvit_t", 224) == {"input_size": (224, 224), "partition_size": 7}
+    assert registry.resolution_kwargs("resnet18", 64) == {}
+    out = str(tmp_path / "out")
+    args = [a if a != "32" else "64" for a in COMMON]
+    _run(["dataparallel.py", "--outpath", out, "-b", "4", "--arch", "vit_b_32"] + args)
+    assert "total_time_cost" in open(os.path.join(out + "_vit_b_32", "experiment.log")).read()
