@@ -10,6 +10,9 @@
 
 #include <cstdio>
 #include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <optional>
 #include <vector>
 #include <stdexcept>
@@ -39,6 +42,28 @@ void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line) {
   snprintf(buf, sizeof(buf), "%s failed: %s (%s:%d)", expr, hipGetErrorString(e), file, line);
   throw std::runtime_error(buf);
 }
+
+// ------------------------------------------------------------------------------- dispatch counters
+namespace pdt {
+namespace {
+struct CounterRegistry {
+  std::mutex mu;
+  std::vector<std::pair<std::string, std::unique_ptr<long long>>> entries;
+};
+CounterRegistry& counters() {
+  static CounterRegistry r;
+  return r;
+}
+}  // namespace
+long long* dispatch_counter(const char* name) {
+  auto& r = counters();
+  std::lock_guard<std::mutex> lk(r.mu);
+  for (auto& e : r.entries)
+    if (e.first == name) return e.second.get();
+  r.entries.emplace_back(name, std::make_unique<long long>(0));
+  return r.entries.back().second.get();
+}
+}  // namespace pdt
 
 namespace {
 
@@ -634,6 +659,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pdt_store::register_store(m);
   pdt_dp::register_dp(m);
   m.doc() = "gfx950 (MI355X) HIP kernels of pytorch_distributed_template_amd";
+  m.def("dispatch_counts", []() {
+    std::map<std::string, long long> out;
+    auto& r = pdt::counters();
+    std::lock_guard<std::mutex> lk(r.mu);
+    for (auto& e : r.entries) out[e.first] = __atomic_load_n(e.second.get(), __ATOMIC_RELAXED);
+    return out;
+  });
+  m.def("reset_dispatch_counts", []() {
+    auto& r = pdt::counters();
+    std::lock_guard<std::mutex> lk(r.mu);
+    for (auto& e : r.entries) __atomic_store_n(e.second.get(), 0LL, __ATOMIC_RELAXED);
+  });
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_m_tiles", &conv_m_tiles);
   m.def("conv_dgrad", &conv_dgrad);

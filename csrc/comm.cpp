@@ -11,17 +11,30 @@
 //     launches that bucket's all-reduce (in place, SUM; 1/world is folded into the SGD kernel) as soon as
 //     its count reaches zero, so the reductions overlap the rest of backward; finish() launches leftover
 //     buckets (unused parameters) and joins the comm stream into the compute stream.
-//   * Failure handling: async_error() polls ncclCommGetAsyncError; abort() tears the communicator down
-//     (ncclCommAbort) so a hung peer cannot wedge this process forever.
+//   * Failure handling (the reference has none; c10d's ProcessGroupNCCL watchdog is the model): every
+//     collective records a completion event on the comm stream; a watchdog thread polls those events and
+//     ncclCommGetAsyncError.  A collective still pending after ``timeout_s`` (the trainer's
+//     --dist-timeout) or an asynchronous RCCL error aborts the communicator (ncclCommAbort, which also
+//     unblocks a host thread stuck in RCCL) and ends the process with a non-zero status, so the launcher
+//     tears the group down instead of every rank hanging in a ring that will never complete.
+//     async_error()/abort() stay available for explicit polling.
 // RCCL is the copy PyTorch already loaded (same soname), so there is one RCCL instance per process.
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <torch/extension.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace pdt_comm {
@@ -69,7 +82,8 @@ py::bytes unique_id() {
 
 class Communicator {
  public:
-  Communicator(const std::string& id, int world, int rank, int device) : world_(world), rank_(rank), device_(device) {
+  Communicator(const std::string& id, int world, int rank, int device, double timeout_s = 0.0, int exit_code = 75)
+      : world_(world), rank_(rank), device_(device), timeout_s_(timeout_s), exit_code_(exit_code) {
     TORCH_CHECK(id.size() == sizeof(ncclUniqueId::internal), "rccl: unique id must be ", sizeof(ncclUniqueId::internal),
                 " bytes");
     TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rccl: bad rank / world");
@@ -80,9 +94,14 @@ class Communicator {
     PDT_HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     PDT_HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     PDT_NCCL_CHECK(ncclCommInitRank(&comm_, world, uid, rank));
+    if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });
   }
   ~Communicator() {
+    stop_watchdog();
     if (comm_) ncclCommDestroy(comm_);
+    for (auto& p : pending_)
+      if (p.ev) (void)hipEventDestroy(p.ev);
+    for (hipEvent_t e : free_evs_) (void)hipEventDestroy(e);
     if (ev_in_) (void)hipEventDestroy(ev_in_);
     if (ev_out_) (void)hipEventDestroy(ev_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -94,8 +113,40 @@ class Communicator {
   int world() const { return world_; }
   hipStream_t stream() const { return stream_; }
   ncclComm_t comm() const {
-    TORCH_CHECK(comm_ != nullptr, "rccl: communicator was aborted");
+    TORCH_CHECK(comm_ != nullptr && !aborted_.load(), "rccl: communicator was aborted");
     return comm_;
+  }
+  int count() const {
+    int n = 0;
+    PDT_NCCL_CHECK(ncclCommCount(comm(), &n));
+    return n;
+  }
+  double timeout_s() const { return timeout_s_; }
+
+  // Watchdog bookkeeping: a completion event on the comm stream behind the collective just enqueued.
+  void track(const char* what) {
+    if (timeout_s_ <= 0) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    hipEvent_t ev;
+    if (!free_evs_.empty()) {
+      ev = free_evs_.back();
+      free_evs_.pop_back();
+    } else {
+      PDT_HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    PDT_HIP_OK(hipEventRecord(ev, stream_));
+    pending_.push_back({ev, std::chrono::steady_clock::now(), what});
+  }
+  // Test hook: a pending "collective" that never completes, enqueued ``age_s`` seconds ago.
+  void inject_stall(double age_s) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto t = std::chrono::steady_clock::now() -
+             std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(age_s));
+    pending_.push_back({nullptr, t, "injected stall"});
+  }
+  int64_t pending() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (int64_t)pending_.size();
   }
 
   // comm stream <- everything already enqueued on the caller's compute stream
@@ -115,12 +166,14 @@ class Communicator {
     check(t);
     join_compute();
     PDT_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), nccl_op(op), comm(), stream_));
+    track("all_reduce");
     if (!async_op) wait();
   }
   void broadcast(Tensor& t, int root, bool async_op) {
     check(t);
     join_compute();
     PDT_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), root, comm(), stream_));
+    track("broadcast");
     if (!async_op) wait();
   }
   void all_gather(const Tensor& in, Tensor& out, bool async_op) {
@@ -130,6 +183,7 @@ class Communicator {
                 "rccl all_gather: out must hold world x in");
     join_compute();
     PDT_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_type(in), comm(), stream_));
+    track("all_gather");
     if (!async_op) wait();
   }
   void barrier() {
@@ -143,22 +197,91 @@ class Communicator {
     PDT_NCCL_CHECK(ncclCommGetAsyncError(comm_, &e));
     return e == ncclSuccess ? std::string() : std::string(ncclGetErrorString(e));
   }
-  void abort() {
-    if (comm_) {
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
+  // Collective teardown: every rank calls it at the same point (after a barrier).
+  void destroy() {
+    stop_watchdog();
+    if (comm_ && !aborted_.load()) {
+      PDT_HIP_OK(hipStreamSynchronize(stream_));
+      PDT_NCCL_CHECK(ncclCommDestroy(comm_));
     }
+    comm_ = nullptr;
+  }
+  void abort() {
+    stop_watchdog();
+    if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+    comm_ = nullptr;
   }
 
  private:
+  struct Pending {
+    hipEvent_t ev;  // nullptr: injected stall (never completes)
+    std::chrono::steady_clock::time_point t;
+    const char* what;
+  };
+
+  void stop_watchdog() {
+    if (!watchdog_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();
+  }
+
+  [[noreturn]] void fail(const std::string& why) {
+    std::fprintf(stderr, "[pdt comm watchdog] rank %d/%d: %s; aborting the RCCL communicator and exiting (%d)\n",
+                 rank_, world_, why.c_str(), exit_code_);
+    std::fflush(stderr);
+    if (!aborted_.exchange(true)) ncclCommAbort(comm_);
+    std::_Exit(exit_code_);
+  }
+
+  // Poll the oldest pending collective and RCCL's async error every 50 ms.
+  void watch() {
+    (void)hipSetDevice(device_);
+    const auto limit = std::chrono::duration<double>(timeout_s_);
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stop_) {
+      cv_.wait_for(lk, std::chrono::milliseconds(50));
+      if (stop_) break;
+      while (!pending_.empty()) {
+        Pending& p = pending_.front();
+        hipError_t q = p.ev ? hipEventQuery(p.ev) : hipErrorNotReady;
+        if (q == hipSuccess) {
+          free_evs_.push_back(p.ev);
+          pending_.pop_front();
+          continue;
+        }
+        if (q != hipErrorNotReady) fail(std::string("comm stream error: ") + hipGetErrorString(q));
+        if (std::chrono::steady_clock::now() - p.t > limit)
+          fail(std::string(p.what) + " did not complete within " + std::to_string(timeout_s_) + " s");
+        break;
+      }
+      ncclResult_t e = ncclSuccess;
+      if (comm_ && !aborted_ && ncclCommGetAsyncError(comm_, &e) == ncclSuccess && e != ncclSuccess &&
+          e != ncclInProgress)
+        fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(e));
+    }
+  }
+
   void check(const Tensor& t) const {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl: expected a contiguous GPU tensor");
     TORCH_CHECK(t.get_device() == device_, "rccl: tensor on device ", t.get_device(), ", communicator on ", device_);
   }
   int world_, rank_, device_;
+  double timeout_s_;
+  int exit_code_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  std::atomic<bool> aborted_{false};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  std::deque<Pending> pending_;
+  std::vector<hipEvent_t> free_evs_;
+  std::thread watchdog_;
 };
 
 class Bucketer {
@@ -202,6 +325,7 @@ class Bucketer {
     comm_->join_compute();
     float* p = grad_.data_ptr<float>() + lo_[b];
     PDT_NCCL_CHECK(ncclAllReduce(p, p, hi_[b] - lo_[b], ncclFloat32, ncclSum, comm_->comm(), comm_->stream()));
+    comm_->track("gradient bucket all_reduce");
     launched_[b] = true;
   }
   void reset() {
@@ -222,16 +346,22 @@ void register_comm(py::module& m) {
     return v;
   });
   py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")
-      .def(py::init<const std::string&, int, int, int>())
+      .def(py::init<const std::string&, int, int, int, double, int>(), py::arg("uid"), py::arg("world"),
+           py::arg("rank"), py::arg("device"), py::arg("timeout_s") = 0.0, py::arg("exit_code") = 75)
       .def_property_readonly("rank", &Communicator::rank)
       .def_property_readonly("world", &Communicator::world)
+      .def_property_readonly("timeout_s", &Communicator::timeout_s)
+      .def("count", &Communicator::count)
+      .def("pending", &Communicator::pending)
+      .def("inject_stall", &Communicator::inject_stall)
       .def("all_reduce", &Communicator::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
       .def("broadcast", &Communicator::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
       .def("all_gather", &Communicator::all_gather, py::arg("inp"), py::arg("out"), py::arg("async_op") = false)
       .def("barrier", &Communicator::barrier)
       .def("wait", &Communicator::wait)
       .def("async_error", &Communicator::async_error)
-      .def("abort", &Communicator::abort);
+      .def("abort", &Communicator::abort)
+      .def("destroy", &Communicator::destroy);
   py::class_<Bucketer>(m, "Bucketer")
       .def(py::init<std::shared_ptr<Communicator>, Tensor, std::vector<int64_t>, std::vector<int64_t>,
                     std::vector<int64_t>>())

@@ -143,3 +143,14 @@ PDT_DEVICE int xcd_remap(int bid, int nwg) {
   } while (0)
 
 void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line);
+
+// Host-side kernel-dispatch counters (defined in bindings.cpp, read by C.dispatch_counts()): tests assert
+// which specialised kernel variant a shape actually ran.  One relaxed atomic increment per launch.
+namespace pdt {
+long long* dispatch_counter(const char* name);
+}
+#define PDT_COUNT(name)                                                             \
+  do {                                                                             \
+    static long long* _pdt_ctr = pdt::dispatch_counter(name);                      \
+    __atomic_fetch_add(_pdt_ctr, 1LL, __ATOMIC_RELAXED);                           \
+  } while (0)

@@ -915,6 +915,7 @@ int wgrad3x3_c64_blocks() {
 }
 
 void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s) {
+  PDT_COUNT("wgrad3x3_c64");
   if (dtype == kBF16)
     hipLaunchKernelGGL((wgrad3x3_c64_kernel<kBF16>), dim3(blocks), dim3(256), 0, s, a);
   else
@@ -1020,17 +1021,20 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
   a.div_pq_mul = dpq.mul; a.div_pq_shift = dpq.shift; a.div_q_mul = dq.mul; a.div_q_shift = dq.shift;
   if (a.tile == 256) {
+    PDT_COUNT("conv_wgrad_pp");
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kBF16>), dim3(nwg), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
   } else if (a.tile == 128) {
+    PDT_COUNT("conv_wgrad_128");
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16>), dim3(nwg), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad128_kernel<kF16>), dim3(nwg), dim3(256), 0, s, a);
   } else if (a.win && a.T == 4 && a.U == 1 && a.C == 64 && a.Kout == 64 && a.ldw >= 256) {
     // ResNet stem (4 kernel-row pairs): one block per split covers all pairs
+    PDT_COUNT(a.f_y != nullptr ? "wgrad_stem_fused" : "wgrad_stem");
     if (a.f_y != nullptr) {
       if (dtype == kBF16)
         hipLaunchKernelGGL((wgrad_stem_kernel<kBF16, true>), dim3(a.splits), dim3(256), 0, s, a);
@@ -1042,11 +1046,13 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((wgrad_stem_kernel<kF16, false>), dim3(a.splits), dim3(256), 0, s, a);
     }
   } else if (a.win) {
+    PDT_COUNT("conv_wgrad_window");
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, true>), dim3(nwg), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad_kernel<kF16, true>), dim3(nwg), dim3(256), 0, s, a);
   } else {
+    PDT_COUNT("conv_wgrad_generic");
     if (dtype == kBF16)
       hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, false>), dim3(nwg), dim3(256), 0, s, a);
     else

@@ -203,6 +203,7 @@ bool stem_fwd_supported(int Hp, int Wp, int P, int Q) {
 }
 
 void stem_fwd_launch(StemFwdArgs a, int dtype, hipStream_t s) {
+  PDT_COUNT("stem_fwd");
   a.TP = (a.P + kOutRows - 1) / kOutRows;
   a.tiles = a.N * a.TP;
   const FastDiv f = make_fastdiv((uint32_t)a.TP);

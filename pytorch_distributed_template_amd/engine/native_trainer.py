@@ -29,7 +29,8 @@ class NativeTrainer:
                  weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
-                 force_comm: bool = False, graph: bool = False, last_bucket_mb: Optional[float] = 1.0):
+                 force_comm: bool = False, graph: bool = False, last_bucket_mb: Optional[float] = 1.0,
+                 comm_timeout_s: float = 0.0, time_comm: bool = False):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -38,18 +39,25 @@ class NativeTrainer:
         self.world = dist.get_world_size(process_group) if self.distributed else 1
         self.flat = FlatParams(model, self.device, dtype)
         self.buffers = FlatBuffers(model, self.device)
-        broadcast_parameters(self.flat, self.buffers, process_group)
-        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed,
-                              last_bucket_mb=last_bucket_mb)
         # collectives: torch.distributed (RCCL via c10d) or our own RCCL communicator + C++ bucketer
-        # (--comm native; force_comm exercises it on a single rank)
+        # (--comm native; force_comm exercises it on a single rank).  With the native communicator EVERY
+        # GPU collective of the step (constructor broadcast, buffer broadcast, gradient buckets, SyncBN
+        # statistics, metrics) goes through it; torch.distributed only provides the rendezvous store.
         self.ncomm = None
         if comm == "native" and (self.distributed or force_comm):
-            from ..parallel.comm import NativeBucketer, NativeComm
-            self.ncomm = NativeComm(self.device, process_group)
+            from ..parallel.comm import NativeComm
+            self.ncomm = NativeComm(self.device, process_group, timeout_s=comm_timeout_s)
+        self._broadcast_initial()
+        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed,
+                              last_bucket_mb=last_bucket_mb)
+        if self.ncomm is not None:
+            from ..parallel.comm import NativeBucketer
             self.bucketer = NativeBucketer(layout, self.ncomm)
         else:
             self.bucketer = layout
+        # HIP events around bucketer.finish(): the time the compute stream waits for gradient all-reduces
+        # that backward did not hide (exposed communication)
+        self._comm_events = [] if time_comm else None
         self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
                                        syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed)
                                        else None, autotune=autotune,
@@ -65,6 +73,37 @@ class NativeTrainer:
         self.use_graph = graph and not self.distributed and self.ncomm is None
         self._graphs = {}
         self._graph_warm = 0
+
+    def _broadcast_initial(self) -> None:
+        """DDP constructor semantics (X2): every rank starts from rank 0's parameters and buffers."""
+        if self.ncomm is None:
+            broadcast_parameters(self.flat, self.buffers, self.pg)
+            return
+        if self.ncomm.world > 1:
+            self.ncomm.broadcast(self.flat.data, 0)
+            self._sync_buffers()
+            self.flat.refresh_shadow()
+
+    def on_state_loaded(self) -> None:
+        """After ``model.load_state_dict`` (resume): re-derive the 16-bit shadow and the kernel weight layouts."""
+        self.flat.refresh_shadow()
+        self.executor.update_derived()
+
+    def exposed_comm_ms(self) -> Optional[float]:
+        """Mean per-step exposed gradient-communication time since the last call (needs ``time_comm``)."""
+        if not self._comm_events:
+            return None
+        torch.cuda.synchronize(self.device)
+        ms = sum(a.elapsed_time(b) for a, b in self._comm_events) / len(self._comm_events)
+        self._comm_events.clear()
+        return ms
+
+    def param_checksum(self) -> torch.Tensor:
+        """[sum, sum of squares, position-weighted sum] of the fp32 master parameters (fp64): equal on every
+        rank iff the data-parallel replicas stayed in lock-step."""
+        d = self.flat.data.double()
+        w = torch.linspace(0.5, 1.5, d.numel(), dtype=torch.float64, device=d.device)
+        return torch.stack([d.sum(), (d * d).sum(), (d * w).sum()])
 
     def _reduce(self, met: torch.Tensor) -> torch.Tensor:
         if self.reduce_metrics:
@@ -124,7 +163,14 @@ class NativeTrainer:
         if self.buffers.n_int:
             self.buffers.idata.add_(1)  # BatchNorm num_batches_tracked
         met = self._reduce(met)
-        self.bucketer.finish()
+        if self._comm_events is not None and not torch.cuda.is_current_stream_capturing():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.bucketer.finish()
+            e1.record()
+            self._comm_events.append((e0, e1))
+        else:
+            self.bucketer.finish()
         self.scaler.unscale_check(self.flat.grad)
         self.optimizer.step(grad_scale=self.bucketer.grad_scale(), loss_scale=self.scaler.scale_tensor,
                             found_inf=self.scaler.found_inf)

@@ -184,7 +184,11 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
             ids = list(range(torch.cuda.device_count()))
             return NativeDataParallelTrainer(model, ids, dtype=dtype, use_amp=use_amp, **common)
         from .torch_trainer import TorchTrainer
-        return TorchTrainer(model, device, dtype=dtype, use_amp=use_amp, **common, **torch_kw)
+        # nn.DataParallel semantics on the torch engine too: the node-total batch is scattered over every
+        # visible GPU (`dataparallel.py:119`), not run on cuda:0 alone
+        ids = list(range(torch.cuda.device_count())) if device.type == "cuda" else []
+        return TorchTrainer(model, device, dtype=dtype, use_amp=use_amp, dp_device_ids=ids if len(ids) > 1 else None,
+                            **common, **torch_kw)
     kw = dict(common, use_amp=use_amp, sync_bn=sync_bn, bucket_cap_mb=args.bucket_cap_mb,
               first_bucket_mb=args.first_bucket_mb)
     if engine == "native":
@@ -192,7 +196,8 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
         lb = float(getattr(args, "last_bucket_mb", 1.0))
         return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)),
                              comm=getattr(args, "comm", "torch"), graph=bool(getattr(args, "graph", False)),
-                             last_bucket_mb=lb if lb > 0 else None, **kw)
+                             last_bucket_mb=lb if lb > 0 else None,
+                             comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)), **kw)
     from .torch_trainer import TorchTrainer
     return TorchTrainer(model, device, dtype=dtype, **kw, **torch_kw)
 
@@ -274,9 +279,7 @@ def main(mode: str, argv: Optional[list] = None) -> int:
     if args.resume:
         ck = load_checkpoint(args.resume)
         trainer.model.load_state_dict(ck["state_dict"])
-        trainer.flat.refresh_shadow()
-        if hasattr(trainer, "executor"):
-            trainer.executor.update_derived()
+        trainer.on_state_loaded()  # 16-bit shadows + derived kernel weight layouts of every replica
         if "optimizer" in ck:
             optimizer.load_state_dict(ck["optimizer"])
         if "scaler" in ck:

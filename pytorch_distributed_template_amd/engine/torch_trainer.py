@@ -30,7 +30,7 @@ class TorchTrainer:
                  momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, channels_last: bool = True,
-                 aux_loss_weight: float = 0.3):
+                 aux_loss_weight: float = 0.3, dp_device_ids=None):
         self.device = torch.device(device)
         self.pg = process_group
         self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
@@ -43,6 +43,9 @@ class TorchTrainer:
         self.model = model
         self.dtype = dtype
         self.flat = FlatParams(model, self.device, None)
+        # single-process multi-GPU (dataparallel.py on the torch engine): nn.DataParallel scatters the batch,
+        # replicates the module per forward and reduce-adds the gradients into the flat views on device 0
+        self.net = nn.DataParallel(model, device_ids=list(dp_device_ids)) if dp_device_ids else model
         self.buffers = FlatBuffers(model, self.device)
         broadcast_parameters(self.flat, self.buffers, process_group)
         self.bucketer = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
@@ -54,6 +57,9 @@ class TorchTrainer:
         # GoogLeNet / Inception-v3 return auxiliary logits in training; their CE losses are added with this weight
         self.aux_loss_weight = aux_loss_weight
         self._steps = 0
+
+    def on_state_loaded(self) -> None:
+        """Parameters are views of the flat buffer, so ``load_state_dict`` already updated them."""
 
     def _autocast(self):
         if self.dtype == torch.float32:
@@ -77,7 +83,7 @@ class TorchTrainer:
             sync_buffers(self.buffers, self.pg)
         self.optimizer.zero_grad()
         with self._autocast():
-            out, aux = split_outputs(self.model(self._inputs(images)))
+            out, aux = split_outputs(self.net(self._inputs(images)))
             loss = F.cross_entropy(out.float(), target)
             for a in aux:
                 loss = loss + self.aux_loss_weight * F.cross_entropy(a.float(), target)
@@ -97,7 +103,7 @@ class TorchTrainer:
         self.model.eval()
         if self.broadcast_buffers and self._steps > 0:
             sync_buffers(self.buffers, self.pg)
-        out = self.model(self._inputs(images)).float()  # validation runs without autocast (`:316-317`)
+        out = self.net(self._inputs(images)).float()  # validation runs without autocast (`:316-317`)
         loss = F.cross_entropy(out, target)
         acc = accuracy(out, target, 1)
         return out, self._reduce(torch.stack([loss.float(), acc.float()]))

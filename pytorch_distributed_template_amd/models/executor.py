@@ -446,14 +446,18 @@ class ResNetExecutor:
         self.C.bn_slot_sum(slots, C, K, sums)
         self._sync_sum(sums)
         count = count * self.syncbn_world
-        # sums layout: k*C + c for k in [sum dz1, sum dz1*x1, (sum dz2, sum dz2*x2)]
+        # sums layout: k*C + c for k in [sum dz1, sum dz1*x1, (sum dz2, sum dz2*x2)].  The data gradient needs
+        # the GLOBAL sums, but dgamma/dbeta must be this rank's share: upstream SyncBN returns the local sums
+        # and DDP then averages them, i.e. global / world after averaging.  Writing global / world here gives
+        # exactly that after the bucket all-reduce + 1/world (global sums would make them world x too large).
+        gs = 1.0 / self.syncbn_world
         self.C.bn_bwd_finalize(sums[:2 * C], float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot),
-                               self._g(bn1.bslot), 1.0, bn1.bcoef)
+                               self._g(bn1.bslot), gs, bn1.bcoef)
         self.grad_ready(bn1.gslot.index)
         self.grad_ready(bn1.bslot.index)
         if bn2 is not None:
             self.C.bn_bwd_finalize(sums[2 * C:4 * C], float(count), bn2.coef, self._p(bn2.gslot), self._g(bn2.gslot),
-                                   self._g(bn2.bslot), 1.0, bn2.bcoef)
+                                   self._g(bn2.bslot), gs, bn2.bcoef)
             self.grad_ready(bn2.gslot.index)
             self.grad_ready(bn2.bslot.index)
 

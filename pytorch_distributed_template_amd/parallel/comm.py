@@ -26,9 +26,13 @@ _COUNTER = itertools.count()
 class NativeComm:
     """A process-group-like wrapper over :class:`_C.Communicator`."""
 
-    def __init__(self, device: torch.device, process_group=None, store=None):
+    def __init__(self, device: torch.device, process_group=None, store=None, timeout_s: float = 0.0):
         """The RCCL unique id travels through ``store``: c10d's store when torch.distributed is up,
-        otherwise (or when given) our native TCP store (:class:`~.store.NativeStore`, env://)."""
+        otherwise (or when given) our native TCP store (:class:`~.store.NativeStore`, env://).
+
+        ``timeout_s > 0`` starts the C++ watchdog (csrc/comm.cpp): a collective pending longer than that, or
+        an asynchronous RCCL error, aborts the communicator and exits the process non-zero (the launcher
+        then tears the group down) -- the counterpart of ProcessGroupNCCL's watchdog + ``timeout``."""
         self.device = torch.device(device)
         key = f"pdt_rccl_uid_{next(_COUNTER)}"
         if store is None and dist.is_initialized():
@@ -50,7 +54,12 @@ class NativeComm:
             self.rank, self.world = 0, 1
             uid = native.C.rccl_unique_id()
         self.store = store
-        self.comm = native.C.Communicator(bytes(uid), self.world, self.rank, self.device.index or 0)
+        self.comm = native.C.Communicator(bytes(uid), self.world, self.rank, self.device.index or 0,
+                                          float(timeout_s))
+
+    def count(self) -> int:
+        """Ranks in the RCCL communicator (``ncclCommCount``)."""
+        return self.comm.count()
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> None:
         self.comm.all_reduce(t, op, async_op)
@@ -76,6 +85,10 @@ class NativeComm:
 
     def abort(self) -> None:
         self.comm.abort()
+
+    def destroy(self) -> None:
+        """Collective teardown (every rank, same point): stop the watchdog, ncclCommDestroy."""
+        self.comm.destroy()
 
 
 class NativeBucketer:

@@ -56,6 +56,13 @@ class NativeDataParallelTrainer:
             from ..ops import native
             self.group = native.C.DeviceGroup(self.device_ids)
 
+    def on_state_loaded(self) -> None:
+        """After ``model.load_state_dict`` (resume): GPU 0's shadow and derived layouts; the other replicas
+        receive them with the next forward's replication."""
+        with torch.cuda.device(self.devices[0]):
+            self.flat.refresh_shadow()
+            self.executors[0].update_derived()
+
     def _replicate(self) -> None:
         if len(self.devices) == 1:
             return
@@ -90,6 +97,8 @@ class NativeDataParallelTrainer:
                 logits, met = ex.train_step(x, t, loss_scale=ls, grad_div=float(B))
             outs.append(logits)
             mets.append(met.to(self.devices[0]) * (x.shape[0] / B))
+        if self.buffers[0].n_int:
+            self.buffers[0].idata.add_(1)  # num_batches_tracked of GPU 0's BatchNorms, as nn.DataParallel
         if self.group is not None:
             self.group.reduce([f.grad for f in self.flats], 0)  # in place into GPU 0's flat gradient
         self.scaler.unscale_check(self.flat.grad)

@@ -1,0 +1,155 @@
+"""Native-executor DDP and SyncBN numerics at world = 2, at the real 224x224 geometry (so the specialised
+layer1 / stem / ping-pong kernels run), rehearsed on ONE GPU: two ranks share cuda:0 over gloo (RCCL refuses
+duplicate GPUs).  Each 2-rank result is compared with a single-process oracle on the same kernels:
+
+* DDP (2 x B/2, per-rank BN)  ==  one process computing each half's gradient and averaging them
+  (the upstream DDP contract, `distributed.py:144`);
+* SyncBN DDP (2 x B/2)        ==  one process running the full batch B with plain BN
+  (SyncBN's contract, `distributed_syncBN_amp.py:142-147`; upstream semantics SURVEY §3.5).
+
+Parameter UPDATES (after - before) are compared per parameter, so a wrong gradient scale on any tensor
+(e.g. BN gamma/beta gradients world x too large) fails the test rather than hiding in a sum.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from _ddp_common import make_batch, make_model  # noqa: E402
+
+B = 16  # per rank
+HW = 224
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_ranks(tmp_path, nproc=2, **env):
+    out = str(tmp_path / "rank0.pt")
+    e = dict(os.environ, PYTHONUNBUFFERED="1", PDT_TEST_OUT=out, PDT_TEST_B=str(B), PDT_TEST_HW=str(HW))
+    e.update({k: str(v) for k, v in env.items()})
+    r = subprocess.run([sys.executable, "-m", "pytorch_distributed_template_amd.launch", f"--nproc_per_node={nproc}",
+                        f"--master_port={_free_port()}", "--no_local_rank", os.path.join(HERE, "_native_ddp_worker.py")],
+                       cwd=ROOT, env=e, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return torch.load(out, weights_only=True)
+
+
+def _single(steps_fn):
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    model = make_model(seed=0)
+    tr = NativeTrainer(model, "cuda:0", dtype=torch.bfloat16)
+    before = tr.flat.data.clone()
+    steps_fn(tr)
+    torch.cuda.synchronize()
+    return tr, before
+
+
+def _compare_updates(tr, before, data, per_tensor_tol, total_tol):
+    before = before.cpu()
+    ours = data - before
+    want = tr.flat.data.cpu() - before
+    bad = []
+    for s in tr.flat.slots:
+        a = ours[s.offset:s.offset + s.numel]
+        b = want[s.offset:s.offset + s.numel]
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        if rel > per_tensor_tol:
+            bad.append((s.name, round(rel, 4)))
+    total = ((ours - want).norm() / want.norm()).item()
+    assert not bad, bad[:8]
+    assert total < total_tol, total
+
+
+def test_native_ddp_equals_averaged_half_batches(tmp_path):
+    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=1)
+    X, T = make_batch(2 * B, HW)
+    xa, ta = X[:B].cuda(), T[:B].cuda()
+    xb, tb = X[B:].cuda(), T[B:].cuda()
+    box = {}
+
+    def steps(tr):
+        _, ma = tr.executor.train_step(xa, ta, grad_div=float(B))
+        ga = tr.flat.grad.clone()
+        box["fbuf"] = tr.buffers.fdata.clone()  # rank 0's running stats come from its own half only
+        _, mb = tr.executor.train_step(xb, tb, grad_div=float(B))
+        tr.flat.grad.add_(ga)
+        tr.optimizer.step(grad_scale=0.5)
+        box["met"] = (ma + mb) / 2
+
+    tr, before = _single(steps)
+    _compare_updates(tr, before, res["data"], per_tensor_tol=2e-3, total_tol=5e-4)
+    assert torch.allclose(res["fbuf"], box["fbuf"].cpu(), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(res["met"][0], box["met"].cpu(), rtol=1e-4, atol=1e-5)
+
+
+def test_native_syncbn_equals_full_batch(tmp_path):
+    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=2)
+    X, T = make_batch(2 * B, HW)
+    x, t = X.cuda(), T.cuda()
+    mets = []
+
+    def steps(tr):
+        for _ in range(2):
+            _, m = tr.train_step(x, t)
+            mets.append(m.clone())
+
+    tr, before = _single(steps)
+    # global statistics == full-batch statistics up to fp64 summation order; weight-gradient split-K
+    # partitions differ between B and B/2, so updates agree to fp32/bf16 rounding, not bitwise
+    _compare_updates(tr, before, res["data"], per_tensor_tol=3e-2, total_tol=5e-3)
+    fb = tr.buffers.fdata.cpu()
+    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-4  # running mean / var (unbiased, global count)
+    assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
+    assert torch.allclose(res["met"], torch.stack(mets).cpu(), rtol=2e-3, atol=2e-3)
+
+
+def test_native_dp_state_reload_refreshes_derived_layouts():
+    """--resume into the native DataParallel trainer: the kernels' derived weight layouts follow the loaded
+    weights (evaluation logits equal the saving trainer's)."""
+    from pytorch_distributed_template_amd.models import registry
+    from pytorch_distributed_template_amd.parallel.dp import NativeDataParallelTrainer
+    torch.manual_seed(0)
+    a = NativeDataParallelTrainer(registry.create("resnet18"), [0], dtype=torch.bfloat16)
+    X, T = make_batch(16, 64)
+    x, t = X.cuda(), T.cuda()
+    a.train_step(x, t)
+    assert int(a.buffers[0].idata[0].item()) == 1  # num_batches_tracked advances like nn.DataParallel
+    la, _ = a.eval_step(x, t)
+    sd = {k: v.detach().cpu().clone() for k, v in a.model.state_dict().items()}
+    torch.manual_seed(1)
+    b = NativeDataParallelTrainer(registry.create("resnet18"), [0], dtype=torch.bfloat16)
+    b.model.load_state_dict(sd)
+    b.on_state_loaded()
+    lb, _ = b.eval_step(x, t)
+    torch.cuda.synchronize()
+    assert torch.equal(la, lb)
+
+
+def test_seeded_training_is_bitwise_repeatable():
+    """Two identically seeded trainers on identical data end bit-identical after three steps (224 px)."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    X, T = make_batch(B, HW)
+    x, t = X.cuda(), T.cuda()
+    outs = []
+    for _ in range(2):
+        tr = NativeTrainer(make_model(seed=0), "cuda:0", dtype=torch.bfloat16)
+        for _ in range(3):
+            tr.train_step(x, t)
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), tr.buffers.fdata.clone()))
+        del tr
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

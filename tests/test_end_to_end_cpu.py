@@ -136,3 +136,16 @@ def test_fixed_resolution_archs_follow_cli_crop(tmp_path):
     args = [a if a != "32" else "64" for a in COMMON]
     _run(["dataparallel.py", "--outpath", out, "-b", "4", "--arch", "vit_b_32"] + args)
     assert "total_time_cost" in open(os.path.join(out + "_vit_b_32", "experiment.log")).read()
+
+
+def test_bench_multi_gpu_request_fails_loudly_without_gpus():
+    """bench.py --gpus 2 never silently runs one rank: with too few GPUs it exits non-zero and says why."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "needs 2 visible GPUs" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
