@@ -146,6 +146,7 @@ void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line);
 
 // Host-side kernel-dispatch counters (defined in bindings.cpp, read by C.dispatch_counts()): tests assert
 // which specialised kernel variant a shape actually ran.  One relaxed atomic increment per launch.
+// The counter is bound to ``name`` at the site's first execution: one literal name per call site.
 namespace pdt {
 long long* dispatch_counter(const char* name);
 }

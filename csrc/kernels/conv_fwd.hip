@@ -824,6 +824,24 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
     return;                                                              \
   }
 #define PDT_CFG(BM_, BN_, BK_, WN_, ST_) PDT_CFGN(BM_, BN_, BK_, WN_, ST_, 4)
+  {
+    const bool dg = a.nphase > 0;  // backward-data (sub-pixel phases)
+    const bool pp = bk == 64 && a.C % 64 == 0 && ((bm == 256 && bn == 256) || (bm == 512 && bn == 128));
+    if (pp && dg)
+      PDT_COUNT("conv_pp_dgrad");
+    else if (pp)
+      PDT_COUNT("conv_pp_fwd");
+    else if (dg && a.nphase > 1)
+      PDT_COUNT("conv_generic_dgrad_phased");
+    else if (dg)
+      PDT_COUNT("conv_generic_dgrad");
+    else if (a.cs != a.C)
+      PDT_COUNT("conv_generic_fwd_window");
+    else
+      PDT_COUNT("conv_generic_fwd");
+    if (dg && a.res_phase >= 0) PDT_COUNT("conv_dgrad_compact_residual");
+    if (dg && a.bnb) PDT_COUNT("conv_dgrad_bn_reduce_epilogue");
+  }
   // BK = 64 tiles: 2-stage ring; BK = 32 tiles: 3-stage ring (counted vmcnt, more latency hiding)
   PDT_CFG(128, 128, 64, 2, 2)
   PDT_CFG(256, 64, 64, 1, 2)
@@ -832,22 +850,13 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   PDT_CFG(256, 64, 32, 1, 3)
   PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
-  const bool dg = a.tstep_h < 0;  // backward-data (transposed taps)
   if (bk == 64 && bm == 256 && bn == 256 && a.C % 64 == 0) {
-    PDT_COUNT(dg ? "conv_pp_dgrad" : "conv_pp_fwd");
     launch_pp<DT, 256, 256>(a, s);
     return;
   }
   if (bk == 64 && bm == 512 && bn == 128 && a.C % 64 == 0) {
-    PDT_COUNT(dg ? "conv_pp_dgrad" : "conv_pp_fwd");
     launch_pp<DT, 512, 128>(a, s);
     return;
-  }
-  if (dg) {
-    PDT_COUNT(a.nphase > 1 ? "conv_generic_dgrad_phased" : "conv_generic_dgrad");
-    if (a.res_phase >= 0) PDT_COUNT("conv_dgrad_compact_residual");
-  } else {
-    PDT_COUNT(a.cs != a.C ? "conv_generic_fwd_window" : "conv_generic_fwd");
   }
   PDT_CFGN(256, 128, 64, 2, 2, 8)  // 8 waves (4 x 2 of 64 x 64), 96 KB LDS: 25% less L2->LDS traffic per FLOP
   PDT_CFGN(256, 256, 32, 4, 4, 8)  // 8 waves (2 x 4 of 128 x 64), 4-stage BK=32 ring (128 KB), 2 steps in flight
@@ -865,7 +874,10 @@ void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hi
   }();
   int flip = 0;
   if (l1_on && conv_l1_eligible(a, &flip)) {
-    PDT_COUNT(a.nphase > 1 || a.tstep_h < 0 ? "conv_l1_dgrad" : "conv_l1_fwd");
+    if (a.nphase > 0)
+      PDT_COUNT("conv_l1_dgrad");
+    else
+      PDT_COUNT("conv_l1_fwd");
     conv_l1_launch(a, flip, dtype, s);
     return;
   }

@@ -1034,7 +1034,10 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad128_kernel<kF16>), dim3(nwg), dim3(256), 0, s, a);
   } else if (a.win && a.T == 4 && a.U == 1 && a.C == 64 && a.Kout == 64 && a.ldw >= 256) {
     // ResNet stem (4 kernel-row pairs): one block per split covers all pairs
-    PDT_COUNT(a.f_y != nullptr ? "wgrad_stem_fused" : "wgrad_stem");
+    if (a.f_y != nullptr)
+      PDT_COUNT("wgrad_stem_fused");
+    else
+      PDT_COUNT("wgrad_stem");
     if (a.f_y != nullptr) {
       if (dtype == kBF16)
         hipLaunchKernelGGL((wgrad_stem_kernel<kBF16, true>), dim3(a.splits), dim3(256), 0, s, a);

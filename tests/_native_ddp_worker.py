@@ -32,7 +32,8 @@ def main():
     sync_bn = os.environ.get("PDT_TEST_SYNCBN", "0") == "1"
     # ranks start from different weights: the constructor broadcast must equalise them
     model = make_model(seed=0 if rank == 0 else rank + 100)
-    tr = NativeTrainer(model, dev, dtype=torch.bfloat16, sync_bn=sync_bn, bucket_cap_mb=4, comm=comm,
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}[os.environ.get("PDT_TEST_DTYPE", "bf16")]
+    tr = NativeTrainer(model, dev, dtype=dtype, sync_bn=sync_bn, bucket_cap_mb=4, comm=comm,
                        comm_timeout_s=300.0)
     X, T = make_batch(B * world, hw)
     x = X[rank * B:(rank + 1) * B].to(dev)

@@ -67,7 +67,7 @@ def _compare_updates(tr, before, data, per_tensor_tol, total_tol):
         b = want[s.offset:s.offset + s.numel]
         rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
         if rel > per_tensor_tol:
-            bad.append((s.name, round(rel, 4)))
+            bad.append((s.name, round(rel, 4), round(b.norm().item(), 6), round(a.norm().item(), 6)))
     total = ((ours - want).norm() / want.norm()).item()
     assert not bad, bad[:8]
     assert total < total_tol, total
@@ -95,23 +95,47 @@ def test_native_ddp_equals_averaged_half_batches(tmp_path):
     assert torch.allclose(res["met"][0], box["met"].cpu(), rtol=1e-4, atol=1e-5)
 
 
-def test_native_syncbn_equals_full_batch(tmp_path):
-    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=2)
+def _update_errors(tr, before, a, b):
+    """Per-parameter relative error of update (a - before) against update (b - before)."""
+    out = {}
+    for s in tr.flat.slots:
+        da = (a - before)[s.offset:s.offset + s.numel]
+        db = (b - before)[s.offset:s.offset + s.numel]
+        out[s.name] = ((da - db).norm() / db.norm().clamp_min(1e-12)).item()
+    return out
+
+
+@pytest.mark.parametrize("steps", [1, 2])
+def test_native_syncbn_equals_full_batch(tmp_path, steps):
+    """A random-init ResNet's gradient is chaotic in 16-bit arithmetic: nudging the INPUT by one part in 1e6
+    already moves the parameter updates by 10-60 % (the "floor", measured here).  SyncBN(2 x B/2) must
+    agree with the full batch within that floor, and far better than plain DDP(2 x B/2), whose per-rank
+    BN statistics genuinely differ; a scale error on any tensor (e.g. gamma/beta gradients world x) is
+    >= 100 % and fails.  Running statistics, num_batches_tracked and the loss must match closely."""
+    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=steps)
+    nosync = _run_ranks(tmp_path, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=steps)["data"]
     X, T = make_batch(2 * B, HW)
     x, t = X.cuda(), T.cuda()
     mets = []
 
-    def steps(tr):
-        for _ in range(2):
-            _, m = tr.train_step(x, t)
-            mets.append(m.clone())
+    def run(tr, xx, keep):
+        for _ in range(steps):
+            _, m = tr.train_step(xx, t)
+            if keep:
+                mets.append(m.clone())
 
-    tr, before = _single(steps)
-    # global statistics == full-batch statistics up to fp64 summation order; weight-gradient split-K
-    # partitions differ between B and B/2, so updates agree to fp32/bf16 rounding, not bitwise
-    _compare_updates(tr, before, res["data"], per_tensor_tol=3e-2, total_tol=5e-3)
+    tr, before = _single(lambda tr: run(tr, x, True))
+    floor_tr, _ = _single(lambda tr: run(tr, x * (1 + 1e-6), False))
+    before, full = before.cpu(), tr.flat.data.cpu()
+    e_sync = _update_errors(tr, before, res["data"], full)
+    e_nosync = _update_errors(tr, before, nosync, full)
+    e_floor = _update_errors(tr, before, floor_tr.flat.data.cpu(), full)
+    bad = [(k, round(e_sync[k], 4), round(e_floor[k], 4), round(e_nosync[k], 4)) for k in e_sync
+           if e_sync[k] > max(1.5 * e_floor[k], 0.02) or (e_nosync[k] > 0.05 and e_sync[k] > 0.75 * e_nosync[k])]
+    assert not bad, bad[:8]
+    assert e_sync["fc.weight"] < 0.02 and e_sync["fc.bias"] < 1e-3
     fb = tr.buffers.fdata.cpu()
-    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-4  # running mean / var (unbiased, global count)
+    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-3  # running mean / var (unbiased, global count)
     assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
     assert torch.allclose(res["met"], torch.stack(mets).cpu(), rtol=2e-3, atol=2e-3)
 
