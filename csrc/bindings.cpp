@@ -6,6 +6,7 @@
 // the ops compose with PyTorch's stream semantics, hipGraph capture and RCCL's stream ordering.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 
 #include <cstdio>
@@ -63,6 +64,11 @@ long long* dispatch_counter(const char* name) {
   r.entries.emplace_back(name, std::make_unique<long long>(0));
   return r.entries.back().second.get();
 }
+
+void* scratch_alloc(size_t bytes, hipStream_t s) {
+  return c10::hip::HIPCachingAllocator::raw_alloc_with_stream(bytes, s);
+}
+void scratch_free(void* p) { c10::hip::HIPCachingAllocator::raw_delete(p); }
 }  // namespace pdt
 
 namespace {

@@ -144,6 +144,25 @@ PDT_DEVICE int xcd_remap(int bid, int nwg) {
 
 void pdt_hip_fail(const char* expr, hipError_t e, const char* file, int line);
 
+// Stream-ordered device scratch from PyTorch's caching allocator (defined in bindings.cpp): the memory may
+// be released right after the launches that use it were enqueued on ``s`` -- the allocator hands it out
+// again only to later work on the same stream (and hipGraph capture draws it from the graph's pool).
+namespace pdt {
+void* scratch_alloc(size_t bytes, hipStream_t s);
+void scratch_free(void* p);
+struct Scratch {
+  void* p;
+  Scratch(size_t bytes, hipStream_t s) : p(bytes ? scratch_alloc(bytes, s) : nullptr) {}
+  ~Scratch() {
+    if (p) scratch_free(p);
+  }
+  Scratch(const Scratch&) = delete;
+  Scratch& operator=(const Scratch&) = delete;
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+}  // namespace pdt
+
 // Host-side kernel-dispatch counters (defined in bindings.cpp, read by C.dispatch_counts()): tests assert
 // which specialised kernel variant a shape actually ran.  One relaxed atomic increment per launch.
 // The counter is bound to ``name`` at the site's first execution: one literal name per call site.

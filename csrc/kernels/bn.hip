@@ -15,7 +15,28 @@
 namespace pdt {
 
 // -------------------------------------------------------------------------------------------------
-// slots [kStatSlots][C][K] double (accumulated by the conv epilogue / bn_bwd_reduce with fp64 atomics)
+// rows [R][CK] fp32 per-block partials -> slots [kStatSlots][CK] fp64, slot s = sum of rows s, s + 64, ...
+// in ascending order (deterministic: no atomics anywhere in the statistics path, see conv_fwd.h)
+__global__ __launch_bounds__(256) void stat_rows_reduce_kernel(const float* __restrict__ rows, int R, int CK,
+                                                               double* __restrict__ slots) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= CK) return;
+  const int s = blockIdx.y;
+  double a0 = 0.0, a1 = 0.0;  // two chains (even / odd visits), combined in a fixed order
+  int r = s;
+  for (; r + kStatSlots < R; r += 2 * kStatSlots) {
+    a0 += (double)rows[(int64_t)r * CK + idx];
+    a1 += (double)rows[(int64_t)(r + kStatSlots) * CK + idx];
+  }
+  if (r < R) a0 += (double)rows[(int64_t)r * CK + idx];
+  slots[(int64_t)s * CK + idx] = a0 + a1;
+}
+
+void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s) {
+  hipLaunchKernelGGL(stat_rows_reduce_kernel, dim3((CK + 255) / 256, kStatSlots), dim3(256), 0, s, rows, R, CK, slots);
+}
+
+// slots [kStatSlots][C][K] double (the fixed-order row sums of stat_rows_reduce)
 //   -> sums[k*C + c] double  (channel-major per quantity: the SyncBN all-reduce message)
 __global__ void bn_slot_sum_kernel(const double* __restrict__ slots, int C, int K, double* __restrict__ sums) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ coef1,
                                                             const uint16_t* __restrict__ y2,
                                                             const float* __restrict__ coef2,
-                                                            double* __restrict__ slots, int64_t rows, int C) {
+                                                            float* __restrict__ srows, int64_t rows, int C) {
   using E = E16<DT>;
   const int vpr = C / 8;              // 16-byte vectors per row
   const int rpi = 256 / vpr;          // rows per block iteration (C <= 2048)
@@ -288,11 +309,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       for (int k = 0; k < NBR * 2; ++k) red[((int64_t)rl * C + c0 + e) * K + k] = s[k][e];
   }
   __syncthreads();
-  double* dst = slots + (int64_t)(blockIdx.x % kStatSlots) * C * K;
+  float* dst = srows + (int64_t)blockIdx.x * C * K;  // this block's own partial row
   for (int idx = threadIdx.x; idx < C * K; idx += 256) {
     float t = 0.f;
     for (int r = 0; r < rpi; ++r) t += red[(int64_t)r * C * K + idx];
-    atomicAdd(dst + idx, (double)t);
+    dst[idx] = t;
   }
 }
 
@@ -308,13 +329,15 @@ void bn_bwd_reduce_launch(int dtype, const uint16_t* g, const uint8_t* out, cons
                           hipStream_t s) {
   const int rpi = 256 / (C / 8);
   const int nbr = y2 ? 2 : 1;
-  PDT_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(double) * kStatSlots * C * nbr * 2, s));
+  Scratch part((size_t)blocks * C * nbr * 2 * sizeof(float), s);
+  float* srows = part.as<float>();
   const size_t smem = (size_t)rpi * C * nbr * 2 * sizeof(float);
   const bool mask = out != nullptr;
 #define PDT_BR(DT_, M_, NB_)                                                                              \
   if (mask == M_ && nbr == NB_) {                                                                         \
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<DT_, M_, NB_>), dim3(blocks), dim3(256), smem, s, g, out, y1, \
-                       coef1, y2, coef2, slots, rows, C);                                                  \
+                       coef1, y2, coef2, srows, rows, C);                                                  \
+    stat_rows_reduce_launch(srows, blocks, C * nbr * 2, slots, s);                                        \
     return;                                                                                               \
   }
   if (dtype == kBF16) {

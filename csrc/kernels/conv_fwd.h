@@ -6,6 +6,15 @@ namespace pdt {
 
 constexpr int kStatSlots = 64;  // slot copies of per-channel statistics accumulators
 
+// Deterministic per-channel statistics (BN forward sums, BN-backward sums): every producing block writes
+// its fp32 partials to its OWN row of rows[R][CK] with plain stores (no atomics, so no order-dependent
+// rounding: fp64 atomics of cancelling partials made BN-backward sums -- and, through the chaotic 16-bit
+// backward of a random-init ResNet, whole gradients -- depend on block scheduling), then
+// stat_rows_reduce sums the rows in a FIXED order (row r -> slot r % kStatSlots, rows ascending, fp64)
+// into slots[kStatSlots][CK], the layout the finalize kernels and the SyncBN all-reduce read.  Every slot
+// is written, so the slots need no zeroing.
+void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s);
+
 // Generalised implicit-GEMM convolution (see conv_fwd.hip for the geometry contract).
 struct ConvFwdArgs {
   const uint16_t* x;    // [N][H][W][C] input activations
@@ -14,6 +23,8 @@ struct ConvFwdArgs {
   const uint16_t* res;  // optional: residual in y's layout, added before rounding (nullptr = none)
   double* stats;        // optional: [kStatSlots][Kout][2] fp64 (sum, sumsq) BN statistics (nullptr = none);
                         // with bnb != 0: [kStatSlots][Kout][2 or 4] BN-backward sums (sum dz, sum dz*xhat ...)
+  float* srows;         // per-block partial rows [R][Kout][2 or 4] behind ``stats`` (set by the launcher)
+  int srows_pp;         // rows per phase (multi-phase launches: row = phase * srows_pp + M tile)
   // Fused BN-backward reduce (backward-data use): 0 none | 1 mask from bn_y1 * coef1 (inner BN + ReLU)
   // | 2 mask from bn_mask (ReLU bitmask of the block output, bit e of byte v = element 8v+e > 0)
   // | 3 as 2 with a second BN branch bn_y2 / bn_coef2.

@@ -247,8 +247,8 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
 
   if constexpr (KS > 0) {
     // reduce over the 16 lanes (pixels) that share fq (DPP row scan: lane fr == 15 holds the total),
-    // then over the WAVES_M waves through LDS, then fp64 atomics into one of kStatSlots slot copies
-    // (by M tile: low per-address contention).  Slot layout [kStatSlots][Kout][KO].
+    // then over the WAVES_M waves through LDS, then plain stores into this block's own partial row
+    // (phase, M tile) of [rows][Kout][KO] (deterministic statistics, conv_fwd.h).
     constexpr int KO = EPI == 4 ? 4 : 2;  // stored quantities (EPI 4: sum dz is stored twice)
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -277,14 +277,26 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
       for (int w = 0; w < WAVES_M; ++w)
 #pragma unroll
         for (int k = 0; k < KS; ++k) t[k] += red[(w * BN + tid) * KS + k];
-      double* dst = a.stats + ((int64_t)(tile_m % kStatSlots) * a.Kout + n0 + tid) * KO;
-      atomicAdd(dst, (double)t[0]);
-      atomicAdd(dst + 1, (double)t[1]);
-      if constexpr (EPI == 4) {
-        atomicAdd(dst + 2, (double)t[0]);
-        atomicAdd(dst + 3, (double)t[2]);
-      }
+      const int64_t row = (a.nphase > 0 ? (int64_t)blockIdx.y * a.srows_pp : 0) + tile_m;
+      float* dst = a.srows + (row * a.Kout + n0 + tid) * KO;
+      if constexpr (EPI == 4)
+        *(float4*)dst = make_float4(t[0], t[1], t[0], t[2]);
+      else
+        *(float2*)dst = make_float2(t[0], t[1]);
     }
+  }
+}
+
+// Multi-phase launches size the grid for the largest phase; a block beyond its phase's tiles writes zeros
+// into the statistics row slice it owns (row = phase * srows_pp + M tile), so the fixed-order row reduction
+// never reads unwritten memory.
+template <int EPI, int BN_>
+PDT_DEVICE void zero_stat_row(const ConvFwdArgs& a, int nthreads) {
+  if constexpr (EPI != 0) {
+    constexpr int KO = EPI == 4 ? 4 : 2;
+    const int tm = (int)blockIdx.x / a.n_tiles, tn = (int)blockIdx.x - tm * a.n_tiles;
+    float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * KO + (int64_t)tn * BN_ * KO;
+    for (int i = threadIdx.x; i < BN_ * KO; i += nthreads) dst[i] = 0.f;
   }
 }
 
@@ -302,7 +314,10 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
     a.w = args.w + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
-    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
+    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) {
+      zero_stat_row<EPI, BN>(a, NW * 64);
+      return;
+    }
   }
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -533,7 +548,10 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
     a.w = args.w + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
-    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) return;
+    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) {
+      zero_stat_row<EPI, BN>(a, 512);
+      return;
+    }
   }
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -781,6 +799,9 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
 }
 
 template <int DT>
+static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_t s);
+
+template <int DT>
 static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   // LDS-staged output write-back (PDT_STAGE_OUT=0: direct 8-byte stores from the accumulators)
   static const bool stage_env = [] {
@@ -794,20 +815,36 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
     const FastDiv f1 = make_fastdiv((uint32_t)(a.Pm * a.Qm)), f2 = make_fastdiv((uint32_t)a.Qm);
     a.pq_mul = f1.mul; a.pq_shift = f1.shift; a.q_mul = f2.mul; a.q_shift = f2.shift;
   }
+  int srows = 0;  // statistics rows: one per (phase, M tile)
   if (a.nphase > 0) {
-    int any = 0;
+    int any = 0, maxmt = 0;
     for (int p = 0; p < a.nphase; ++p) {
       a.pmt[p] = (int)(((int64_t)a.N * a.pPm[p] * a.pQm[p] + bm - 1) / bm);
       any |= a.pmt[p];
+      maxmt = maxmt > a.pmt[p] ? maxmt : a.pmt[p];
       if (a.pPm[p] > 0 && a.pQm[p] > 0) {
         const FastDiv f1 = make_fastdiv((uint32_t)(a.pPm[p] * a.pQm[p])), f2 = make_fastdiv((uint32_t)a.pQm[p]);
         a.ppq_mul[p] = f1.mul; a.ppq_shift[p] = f1.shift; a.pq1_mul[p] = f2.mul; a.pq1_shift[p] = f2.shift;
       }
     }
     if (!any || a.n_tiles == 0) return;
+    a.srows_pp = maxmt;
+    srows = a.nphase * maxmt;
   } else if (a.m_tiles * a.n_tiles == 0) {
     return;
+  } else {
+    a.srows_pp = a.m_tiles;
+    srows = a.m_tiles;
   }
+  const int KO = a.bnb == 3 ? 4 : 2;
+  Scratch part(a.stats ? (size_t)srows * a.Kout * KO * sizeof(float) : 0, s);
+  a.srows = part.as<float>();
+  launch_tile<DT>(a, bm, bn, bk, s);
+  if (a.stats) stat_rows_reduce_launch(a.srows, srows, a.Kout * KO, a.stats, s);
+}
+
+template <int DT>
+static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_t s) {
   // PDT_FWD_STAGES=2|3 forces the LDS ring depth (tuning sweeps); default: 2 for BK=64, 3 for BK=32
   static const int force_stages = [] {
     const char* e = getenv("PDT_FWD_STAGES");
@@ -881,8 +918,6 @@ void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hi
     conv_l1_launch(a, flip, dtype, s);
     return;
   }
-  if (a.stats)
-    PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * (a.bnb == 3 ? 4 : 2) * kStatSlots * a.Kout, s));
   if (dtype == kBF16)
     launch_dt<kBF16>(a, bm, bn, bk, s);
   else

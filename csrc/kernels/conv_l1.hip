@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
 
   if constexpr (EPI > 0) {
     // block totals: DPP row scan over the 16 pixel lanes, then the 4 waves through LDS (stage 0 is
-    // free once every wave passed the barrier below), fp64 atomics into slot blockIdx % kStatSlots
+    // free once every wave passed the barrier below), stored to this block's own partial row (conv_fwd.h)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -318,10 +318,7 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
         }
     }
     __syncthreads();
-    if (tid < 128) {
-      const float s = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
-      atomicAdd(a.stats + (int64_t)(blockIdx.x % kStatSlots) * 128 + tid, (double)s);
-    }
+    if (tid < 128) a.srows[(int64_t)blockIdx.x * 128 + tid] = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
   }
 }
 
@@ -358,7 +355,8 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
   if (G > cap) G = cap;
   const bool rs = a.res != nullptr;
   const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
-  if (a.stats) PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * 2 * kStatSlots * 64, s));
+  Scratch part(a.stats ? (size_t)G * 128 * sizeof(float) : 0, s);
+  a.srows = part.as<float>();
 #define PDT_L1(DT_, E_, R_) hipLaunchKernelGGL((conv_l1_kernel<DT_, E_, R_>), dim3(G), dim3(256), 0, s, a, flip)
 #define PDT_L1_DT(DT_)                                                                                 \
   if (epi == 0 && !rs) PDT_L1(DT_, 0, false);                                                          \
@@ -374,6 +372,7 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
   }
 #undef PDT_L1_DT
 #undef PDT_L1
+  if (a.stats) stat_rows_reduce_launch(a.srows, G, 128, a.stats, s);
 }
 
 }  // namespace pdt

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(const uint16_
                                                                    const uint8_t* __restrict__ idx,
                                                                    const uint16_t* __restrict__ y,
                                                                    const float* __restrict__ coef,
-                                                                   double* __restrict__ slots, int N, int H, int W,
+                                                                   float* __restrict__ srows, int N, int H, int W,
                                                                    int C, int OH, int OW) {
   using E = E16<DT>;
   const int vpr = C / 8;
@@ -212,28 +212,30 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(const uint16_
     }
   }
   __syncthreads();
-  double* dst = slots + (int64_t)(blockIdx.x % kStatSlots) * C * 2;
+  float* dst = srows + (int64_t)blockIdx.x * C * 2;  // this block's own partial row (conv_fwd.h)
   for (int i = threadIdx.x; i < C * 2; i += 256) {
     float t = 0.f;
     for (int q = 0; q < rpi; ++q) t += red[(int64_t)q * C * 2 + i];
-    atomicAdd(dst + i, (double)t);
+    dst[i] = t;
   }
 }
 
 void stem_pool_bwd_reduce_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y,
                                  const float* coef, double* slots, int N, int H, int W, int C, hipStream_t s) {
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  PDT_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(double) * kStatSlots * C * 2, s));
   const int rpi = 256 / (C / 8);
   int64_t blocks = ((int64_t)N * OH * OW + rpi * 8 - 1) / (rpi * 8);
   if (blocks > 4096) blocks = 4096;
   const size_t smem = (size_t)rpi * C * 2 * sizeof(float);
+  Scratch part((size_t)blocks * C * 2 * sizeof(float), s);
+  float* srows = part.as<float>();
   if (dtype == kBF16)
-    hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel<kBF16>, dim3((int)blocks), dim3(256), smem, s, dp, idx, y, coef, slots,
+    hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel<kBF16>, dim3((int)blocks), dim3(256), smem, s, dp, idx, y, coef, srows,
                        N, H, W, C, OH, OW);
   else
-    hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel<kF16>, dim3((int)blocks), dim3(256), smem, s, dp, idx, y, coef, slots,
+    hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel<kF16>, dim3((int)blocks), dim3(256), smem, s, dp, idx, y, coef, srows,
                        N, H, W, C, OH, OW);
+  stat_rows_reduce_launch(srows, (int)blocks, C * 2, slots, s);
 }
 
 // Stem backward, pass 1 without touching the 112x112 tensor: the pooled output IS relu(scale*y + shift)
@@ -245,7 +247,7 @@ template <int DT>
 __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_out_kernel(const uint16_t* __restrict__ dp,
                                                                        const uint16_t* __restrict__ out,
                                                                        const float* __restrict__ coef,
-                                                                       double* __restrict__ slots, int64_t rows,
+                                                                       float* __restrict__ srows, int64_t rows,
                                                                        int C) {
   using E = E16<DT>;
   const int vpr = C / 8;
@@ -288,29 +290,31 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_out_kernel(const uin
     }
   }
   __syncthreads();
-  double* dst = slots + (int64_t)(blockIdx.x % kStatSlots) * C * 2;
+  float* dst = srows + (int64_t)blockIdx.x * C * 2;  // this block's own partial row (conv_fwd.h)
   for (int i = threadIdx.x; i < C * 2; i += 256) {
     float t = 0.f;
     for (int q = 0; q < rpi; ++q) t += red[(int64_t)q * C * 2 + i];
-    atomicAdd(dst + i, (double)t);
+    dst[i] = t;
   }
 }
 
 void stem_pool_bwd_reduce_out_launch(int dtype, const uint16_t* dp, const uint16_t* out, const float* coef,
                                      double* slots, int N, int H, int W, int C, hipStream_t s) {
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  PDT_HIP_CHECK(hipMemsetAsync(slots, 0, sizeof(double) * kStatSlots * C * 2, s));
   const int rpi = 256 / (C / 8);
   const int64_t rows = (int64_t)N * OH * OW;
   int64_t blocks = (rows + rpi * 8 - 1) / (rpi * 8);
   if (blocks > 2048) blocks = 2048;
   const size_t smem = (size_t)rpi * C * 2 * sizeof(float);
+  Scratch part((size_t)blocks * C * 2 * sizeof(float), s);
+  float* srows = part.as<float>();
   if (dtype == kBF16)
     hipLaunchKernelGGL(stem_pool_bwd_reduce_out_kernel<kBF16>, dim3((int)blocks), dim3(256), smem, s, dp, out, coef,
-                       slots, rows, C);
+                       srows, rows, C);
   else
     hipLaunchKernelGGL(stem_pool_bwd_reduce_out_kernel<kF16>, dim3((int)blocks), dim3(256), smem, s, dp, out, coef,
-                       slots, rows, C);
+                       srows, rows, C);
+  stat_rows_reduce_launch(srows, (int)blocks, C * 2, slots, s);
 }
 
 // Stem backward, pass 2: dy = A*dz + B*y + Cc at every conv-output element, with dz gathered from the

@@ -11,6 +11,7 @@ struct StemFwdArgs {
   const uint16_t* w;  // [64][7][32] window-row weights
   uint16_t* y;        // [N][P][Q][64]
   double* stats;      // optional [kStatSlots][64][2] fp64 (sum, sumsq) of the rounded outputs
+  float* srows;       // per-block partial rows [grid][64][2] behind ``stats`` (set by the launcher)
   int N, Hp, Wp, P, Q;
   int blocks_per_cu;  // persistent grid size = CUs x blocks_per_cu (rounded to a multiple of 8)
   // filled by the launcher

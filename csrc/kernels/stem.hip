@@ -191,10 +191,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if constexpr (STATS) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid < kCout * 2) {
-      double* dst = a.stats + (int64_t)(blockIdx.x % kStatSlots) * kCout * 2;
-      atomicAdd(dst + tid, (double)(red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]));
-    }
+    if (tid < kCout * 2)  // this block's own partial row (deterministic statistics, conv_fwd.h)
+      a.srows[(int64_t)blockIdx.x * kCout * 2 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   }
 }
 
@@ -216,8 +214,9 @@ void stem_fwd_launch(StemFwdArgs a, int dtype, hipStream_t s) {
   const int cap = (a.tiles + 7) / 8 * 8;
   if (G > cap) G = cap;
   G = (G + 7) / 8 * 8;
-  if (a.stats) PDT_HIP_CHECK(hipMemsetAsync(a.stats, 0, sizeof(double) * 2 * kStatSlots * kCout, s));
   const bool st = a.stats != nullptr;
+  Scratch part(st ? (size_t)G * kCout * 2 * sizeof(float) : 0, s);
+  a.srows = part.as<float>();
 #define PDT_STEM(DT_, ST_) hipLaunchKernelGGL((stem_fwd_kernel<DT_, ST_>), dim3(G), dim3(256), 0, s, a)
   if (dtype == kBF16) {
     if (st) PDT_STEM(kBF16, true); else PDT_STEM(kBF16, false);
@@ -225,6 +224,7 @@ void stem_fwd_launch(StemFwdArgs a, int dtype, hipStream_t s) {
     if (st) PDT_STEM(kF16, true); else PDT_STEM(kF16, false);
   }
 #undef PDT_STEM
+  if (st) stat_rows_reduce_launch(a.srows, G, kCout * 2, a.stats, s);
 }
 
 }  // namespace pdt

@@ -208,8 +208,12 @@ def main(mode: str, argv: Optional[list] = None) -> int:
         os.environ["HIP_VISIBLE_DEVICES"] = args.gpus
     if args.seed is not None:
         seed_everything(args.seed)
-        warnings.warn("You have chosen to seed training. Kernel selection is deterministic in this framework "
-                      "(no autotuning), so seeded runs are reproducible.")
+        # Native engine: every kernel (BN statistics included: per-block partial rows reduced in a fixed order)
+        # is deterministic, so a seeded run repeats bit for bit (tests/test_ddp_numerics_gpu.py) -- unless
+        # --autotune picks conv tiles by timing.  The stock-PyTorch engine keeps cuDNN/MIOpen's caveat.
+        warnings.warn("You have chosen to seed training. The native engine is deterministic (bitwise repeatable "
+                      "unless --autotune picks tiles by timing); the torch engine may still pick "
+                      "nondeterministic MIOpen algorithms, which can slow down training.")
     args.outpath = args.outpath + "_" + args.arch
     world, rank = (1, 0) if mode == "dp" else _dist_env()
     local_rank = getattr(args, "local_rank", 0) if mode != "dp" else 0

@@ -35,6 +35,19 @@ def main():
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}[os.environ.get("PDT_TEST_DTYPE", "bf16")]
     tr = NativeTrainer(model, dev, dtype=dtype, sync_bn=sync_bn, bucket_cap_mb=4, comm=comm,
                        comm_timeout_s=300.0)
+    local = None
+    if os.environ.get("PDT_TEST_SAVE_LOCAL") == "1":  # diagnostics: each bucket's local gradient before its all-reduce
+        local = torch.zeros_like(tr.flat.grad)
+        bk = tr.bucketer
+        orig = bk.grad_ready
+
+        def grad_ready(pid):
+            b = bk.buckets[bk.bucket_of[pid]]
+            if bk._pending[b["id"]] == 1:
+                local[b["lo"]:b["hi"]].copy_(tr.flat.grad[b["lo"]:b["hi"]])
+            orig(pid)
+        bk.grad_ready = grad_ready
+        tr.executor._user_grad_ready = grad_ready
     X, T = make_batch(B * world, hw)
     x = X[rank * B:(rank + 1) * B].to(dev)
     t = T[rank * B:(rank + 1) * B].to(dev)
@@ -43,9 +56,13 @@ def main():
         _, met = tr.train_step(x, t)
         mets.append(met.clone())
     torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    if local is not None:
+        torch.save({"local": local.cpu(), "grad": tr.flat.grad.cpu()}, os.environ["PDT_TEST_OUT"] + f".r{rank}")
     if rank == 0:
         torch.save({"data": tr.flat.data.cpu(), "fbuf": tr.buffers.fdata.cpu(), "ibuf": tr.buffers.idata.cpu(),
-                    "met": torch.stack(mets).cpu(), "buckets": len(tr.bucketer.buckets)},
+                    "met": torch.stack(mets).cpu(), "buckets": len(tr.bucketer.buckets),
+                    "grad": tr.flat.grad.cpu()},
                    os.environ["PDT_TEST_OUT"])
     dist.barrier()
     if tr.ncomm is not None:

@@ -148,3 +148,80 @@ def test_train_step_matches_reference_224(arch, N):
             if ours > 1.5 * theirs + 0.01:
                 bad.append((n, ours, theirs))
     assert not bad, bad[:5]
+
+
+def _grads_after_step(side: bool, delay_side: int = 0, delay_main: int = 0, arch="resnet18", N=16, steps=1):
+    """Run ``steps`` train steps (+ SGD + derived-layout refresh) and return (grad, data, buffers) copies.
+    ``delay_side`` / ``delay_main`` spin-kernel cycles are injected ahead of every side-stream weight
+    gradient / after it on the compute stream, to shake out missing cross-stream dependencies."""
+    import os
+    from pytorch_distributed_template_amd.optim.sgd import FusedSGD
+    old = os.environ.get("PDT_WGRAD_STREAM")
+    os.environ["PDT_WGRAD_STREAM"] = "1" if side else "0"
+    try:
+        model, ref, flat, ex, x, t = _setup(arch, N=N, HW=224, dtype=torch.bfloat16)
+    finally:
+        if old is None:
+            os.environ.pop("PDT_WGRAD_STREAM")
+        else:
+            os.environ["PDT_WGRAD_STREAM"] = old
+    del ref
+    if delay_side or delay_main:
+        orig = ex._side_wgrad
+
+        def slow(reads, fn):
+            def fn2():
+                if delay_side:
+                    torch.cuda._sleep(delay_side)  # on the side stream: the wgrad starts late
+                fn()
+            orig(reads, fn2)
+            if delay_main:
+                torch.cuda._sleep(delay_main)  # compute stream falls behind the side stream
+        ex._side_wgrad = slow
+    opt = FusedSGD(flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for _ in range(steps):
+        ex.train_step(x, t)
+        ex._join_side()
+        opt.step()
+        ex.update_derived()
+    torch.cuda.synchronize()
+    bufs = torch.cat([b.float().reshape(-1) for n, b in model.named_buffers() if "running" in n])
+    return flat.grad.clone(), flat.data.clone(), bufs, flat.slots
+
+
+@pytest.mark.parametrize("delay_side,delay_main", [(0, 0), (2_000_000, 0), (0, 2_000_000)])
+def test_side_stream_bitwise_equals_single_stream(delay_side, delay_main):
+    """Race detector for the two-stream backward (weight gradients on a side stream): with or without
+    injected delays on either stream, gradients, the SGD update and running statistics must be BIT-identical
+    to the single-stream schedule (same kernels, same arithmetic order -- any difference is a missing
+    cross-stream dependency)."""
+    g0, d0, b0, slots = _grads_after_step(False, steps=2)
+    g1, d1, b1, _ = _grads_after_step(True, delay_side, delay_main, steps=2)
+    bad = [(s.name, int((g0[s.offset:s.offset + s.numel] != g1[s.offset:s.offset + s.numel]).sum()))
+           for s in slots if not torch.equal(g0[s.offset:s.offset + s.numel], g1[s.offset:s.offset + s.numel])]
+    assert not bad, bad[:10]
+    assert torch.equal(d0, d1)
+    assert torch.equal(b0, b1)
+
+
+def _poison_allocator(gib: float = 24.0):
+    """Fill the caching allocator's free memory with 0xFF bytes (NaN in every float format) so a kernel that
+    reads memory nobody wrote produces NaN / different bits instead of silently reading zeros."""
+    big = [torch.full((int(gib * 2 ** 30) // 4,), -1, dtype=torch.int32, device=DEV)]
+    small = [torch.full((128 * 1024,), -1, dtype=torch.int32, device=DEV) for _ in range(2048)]  # 512 KiB each
+    torch.cuda.synchronize()
+    del big, small
+
+
+def test_no_reads_of_unwritten_memory():
+    """Two identical 224-px training steps, the second with the allocator pre-filled with NaN bytes: results
+    must be bit-identical (no kernel may read a buffer region that was never written)."""
+    g0, d0, b0, slots = _grads_after_step(True, steps=2)
+    torch.cuda.empty_cache()
+    _poison_allocator()
+    g1, d1, b1, _ = _grads_after_step(True, steps=2)
+    bad = [(s.name, int((g0[s.offset:s.offset + s.numel] != g1[s.offset:s.offset + s.numel]).sum()))
+           for s in slots if not torch.equal(g0[s.offset:s.offset + s.numel], g1[s.offset:s.offset + s.numel])]
+    assert not bad, bad[:10]
+    assert torch.equal(d0, d1)
+    assert torch.equal(b0, b1)

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Usage (on the GPU box via gpurun): bash tools/gpu_check.sh <stage...>
+# Stages: tests (full GPU suite, no -x), diag (DDP bitwise diagnostic), bench (1-GPU headline bench).
+# Every GPU step has its own time limit; a crash / timeout ends the script.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+for stage in "$@"; do
+  case "$stage" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/pytest_all.log 2>&1; rc=$?
+      grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_all.log | tail -25
+      [ $rc -le 1 ] || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    diag)
+      timeout -k 10 500 python -u tools/diag_ddp.py 6 > gpurun_out/diag_ddp.log 2>&1; rc=$?
+      grep "allreduced\|local" gpurun_out/diag_ddp.log | cut -c1-200
+      [ $rc -eq 0 ] || { tail -20 gpurun_out/diag_ddp.log; echo "diag failed rc=$rc"; exit $rc; } ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1; rc=$?
+      grep metric gpurun_out/bench.log
+      [ $rc -eq 0 ] || { tail -20 gpurun_out/bench.log; echo "bench failed rc=$rc"; exit $rc; } ;;
+    bench50)
+      timeout -k 10 600 python bench.py --arch resnet50 --dtype fp16 --steps 10 --warmup 3 > gpurun_out/bench50.log 2>&1; rc=$?
+      grep metric gpurun_out/bench50.log
+      [ $rc -eq 0 ] || { tail -20 gpurun_out/bench50.log; echo "bench50 failed rc=$rc"; exit $rc; } ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      grep metric gpurun_out/prof.log
+      [ $rc -eq 0 ] || { tail -5 gpurun_out/prof.log; echo "prof failed rc=$rc"; exit $rc; } ;;
+  esac
+done
+echo "ALL DONE"
