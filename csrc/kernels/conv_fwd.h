@@ -10,7 +10,7 @@ constexpr int kStatSlots = 64;  // slot copies of per-channel statistics accumul
 // its fp32 partials to its OWN row of rows[R][CK] with plain stores (no atomics, so no order-dependent
 // rounding: fp64 atomics of cancelling partials made BN-backward sums -- and, through the chaotic 16-bit
 // backward of a random-init ResNet, whole gradients -- depend on block scheduling), then
-// stat_rows_reduce sums the rows in a FIXED order (row r -> slot r % kStatSlots, rows ascending, fp64)
+// stat_rows_reduce sums the rows in a FIXED order (slot s <- contiguous row range s*R/64.., fp64)
 // into slots[kStatSlots][CK], the layout the finalize kernels and the SyncBN all-reduce read.  Every slot
 // is written, so the slots need no zeroing.
 void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s);

@@ -167,6 +167,19 @@ def validate(loader, trainer, epoch: int, args, logger, writer, rank: int, devic
     return acc_avg
 
 
+def _peak_memory(device, devices=None):
+    """(peak allocated, peak reserved) GiB since the last reset, max over ``devices`` (the DP replicas) --
+    the memory column of the reference's results table (`README.md:9-14`)."""
+    if device.type != "cuda":
+        return None
+    ids = devices or [device.index if device.index is not None else torch.cuda.current_device()]
+    alloc = max(torch.cuda.max_memory_allocated(d) for d in ids) / 2 ** 30
+    res = max(torch.cuda.max_memory_reserved(d) for d in ids) / 2 ** 30
+    for d in ids:
+        torch.cuda.reset_peak_memory_stats(d)
+    return alloc, res
+
+
 def _dist_env():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -299,6 +312,8 @@ def main(mode: str, argv: Optional[list] = None) -> int:
         return 0
 
     total_start = time.time()
+    mem_devices = list(range(torch.cuda.device_count())) if mode == "dp" and device.type == "cuda" else None
+    _peak_memory(device, mem_devices)  # reset: report per-epoch peaks
     for epoch in range(start_epoch, args.epochs):
         if train_sampler is not None:
             train_sampler.set_epoch(epoch)
@@ -315,6 +330,12 @@ def main(mode: str, argv: Optional[list] = None) -> int:
         epoch_end = time.time()
         ddp_print("||==> Epoch=[{:d}/{:d}]\tbest_acc1={:.4f}\tbest_acc1_index={}\ttime_cost={:.4f}s"
                   .format(epoch, args.epochs, best_acc1, best_acc1_index, epoch_end - epoch_start), logger, rank)
+        mem = _peak_memory(device, mem_devices)
+        if mem is not None:
+            ddp_print("||==> Peak GPU memory: {:.2f} GiB allocated, {:.2f} GiB reserved (per GPU)".format(*mem),
+                      logger, rank)
+            if rank == 0 and writer is not None:
+                writer.add_scalar("Peak_memory_GiB", mem[0], epoch)
         if rank == 0:
             save_checkpoint(make_checkpoint_state(epoch + 1, args.arch, trainer.model, best_acc1, optimizer,
                                                   trainer.scaler, lr_scheduler,

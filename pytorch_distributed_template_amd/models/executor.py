@@ -126,6 +126,11 @@ class ResNetExecutor:
         self.bwd_buf_per_block = os.environ.get("PDT_BWD_BUF_PER_BLOCK", "1") == "1"
         # backward-only derived weight layouts gathered on the side stream under the forward (PDT_SPLIT_DERIVED=0: off)
         self.split_derived = os.environ.get("PDT_SPLIT_DERIVED", "1") == "1"
+        # block-output BN-backward reduce fused into the next block's first dgrad epilogue only where dX has at
+        # most this many pixels per image (PDT_FUSE_BLOCK_BN_MAXHW; larger: plain dgrad + reduce pass).  The
+        # fused 2-branch / masked epilogues are VALU-heavy (conv_l1 dgrad 290 -> 756 us at layer1, rocprof
+        # r2): at 56x56 and 28x28 the separate bandwidth-bound reduce is cheaper (22.64 -> 22.54 ms/step A/B)
+        self.fuse_block_bn_maxhw = int(os.environ.get("PDT_FUSE_BLOCK_BN_MAXHW", "200"))
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -673,7 +678,7 @@ class ResNetExecutor:
                     dyp = self._buf(bk_(dname), yp.numel())
                     Cn.bn_bwd_apply(da, None, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
                     dy = dyp
-                elif bi > 0:
+                elif bi > 0 and h * w <= self.fuse_block_bn_maxhw:
                     # gnext is the previous block's output gradient: fuse that block's output-BN reduce
                     # (ReLU mask from its output, one or two BN branches) into this dgrad's epilogue
                     pb, prec = self.blocks[bi - 1], saved["blocks"][bi - 1]

@@ -35,6 +35,8 @@ def test_entry_scripts_native_gpu(tmp_path, script, extra):
     assert len(losses) == 2 and all(l == l and l < 20 for l in losses)
     if script == "distributed_syncBN_amp.py":
         assert "compute dtype: float16" in log
+    peaks = [float(x) for x in re.findall(r"Peak GPU memory: ([\d.]+) GiB allocated", log)]
+    assert len(peaks) == 2 and all(0 < p < 300 for p in peaks)  # per-epoch peak memory (README memory column)
     ck = torch.load(os.path.join(out + "_resnet18", "checkpoint.pth.tar"), map_location="cpu", weights_only=True)
     assert ck["epoch"] == 2 and torch.isfinite(ck["state_dict"]["conv1.weight"]).all()
 

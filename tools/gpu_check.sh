@@ -31,6 +31,40 @@ for stage in "$@"; do
       cd "${GRAFT_REPO_ROOT:-/root/repo}"
       grep metric gpurun_out/prof.log
       [ $rc -eq 0 ] || { tail -5 gpurun_out/prof.log; echo "prof failed rc=$rc"; exit $rc; } ;;
+    profs)
+      cd /tmp && export TMPDIR=/tmp
+      PDT_WGRAD_STREAM=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/profs" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/profs.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      [ $rc -eq 0 ] || { tail -5 gpurun_out/profs.log; echo "profs failed rc=$rc"; exit $rc; } ;;
+    prof50)
+      cd /tmp && export TMPDIR=/tmp
+      PDT_WGRAD_STREAM=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof50s" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --arch resnet50 --dtype fp16 --steps 3 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof50s.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      [ $rc -eq 0 ] || { tail -5 gpurun_out/prof50s.log; echo "prof50 failed rc=$rc"; exit $rc; } ;;
+    pmcbytes)
+      bash tools/pmc_bytes.sh || exit 1 ;;
+    pmcbytes50)
+      BENCH_ARGS="--arch resnet50 --dtype fp16" bash tools/pmc_bytes.sh || exit 1
+      mv gpurun_out/pmc_bytes gpurun_out/pmc_bytes50 ;;
+    pmcsq)
+      bash tools/pmc_step.sh || exit 1 ;;
+    testk)
+      timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_executor_gpu.py tests/test_ddp_numerics_gpu.py -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/pytest_k.log 2>&1; rc=$?
+      grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_k.log | tail -15
+      [ $rc -le 1 ] || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    convbench)
+      timeout -k 10 600 python -u tools/conv_bench.py --skip-stem > gpurun_out/conv_bench.log 2>&1; rc=$?
+      grep shape gpurun_out/conv_bench.log | cut -c1-400
+      [ $rc -eq 0 ] || { tail -5 gpurun_out/conv_bench.log; echo "conv_bench failed rc=$rc"; exit $rc; } ;;
+    torch50)
+      timeout -k 10 600 python tools/torch_baseline.py --arch resnet50 --dtype fp16 > gpurun_out/torch50.log 2>&1 || { tail gpurun_out/torch50.log; exit 1; }
+      tail -2 gpurun_out/torch50.log ;;
+    torch18fp32)
+      timeout -k 10 600 python tools/torch_baseline.py --arch resnet18 --dtype fp32 > gpurun_out/torch18fp32.log 2>&1 || { tail gpurun_out/torch18fp32.log; exit 1; }
+      tail -2 gpurun_out/torch18fp32.log ;;
   esac
 done
 echo "ALL DONE"
