@@ -123,15 +123,19 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--resume", default="", metavar="PATH", help="resume from a checkpoint written by this framework")
     g.add_argument("--pretrained-path", default=None, help="local torchvision-format weights for --pretrained")
     g.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
+    g.add_argument("--jpeg-draft", default=False, type=str2bool, nargs="?", const=True,
+                   help="decode JPEGs at reduced size (libjpeg DCT scaling) ahead of the crop/resize "
+                        "(throughput option; pixels differ slightly from a full decode)")
     g.add_argument("--gpu-normalize", default="auto", choices=["auto", "on", "off"],
                    help="ship uint8 images to the GPU and normalise there (fused into the native stem kernel); "
                         "auto = on for the native engine, off otherwise")
     g.add_argument("--graph", default=False, type=str2bool, nargs="?", const=True,
                    help="capture the whole native training step in a HIP graph and replay it (single process; "
                         "pays off when small batches make the step launch-bound)")
-    g.add_argument("--comm", default="torch", choices=["torch", "native"],
-                   help="collectives: torch.distributed (RCCL via c10d) or this framework's own RCCL communicator "
-                        "and C++ gradient bucketer")
+    g.add_argument("--comm", default="native", choices=["torch", "native"],
+                   help="native engine collectives: this framework's own RCCL communicator and C++ gradient "
+                        "bucketer (default; torch.distributed then only provides the rendezvous store) or "
+                        "torch.distributed (RCCL via c10d)")
     g.add_argument("--dist-timeout", type=float, default=1800.0,
                    help="collective timeout in seconds (a hung rank fails the job instead of hanging it)")
     g.add_argument("--profile", default=False, type=str2bool, nargs="?", const=True,

@@ -23,6 +23,13 @@ def pil_loader(path: str) -> Image.Image:
         return img.convert("RGB")
 
 
+def lazy_pil_loader(path: str) -> Image.Image:
+    """Header-only open: pixels are decoded by the first transform that needs them, so a JPEG can still be
+    asked for a reduced-size decode (``Image.draft``, transforms ``draft=True``).  Non-RGB modes are
+    converted by ToTensor / ToUint8Tensor at the end of the pipeline."""
+    return Image.open(path)
+
+
 def find_classes(directory: str) -> Tuple[List[str], dict]:
     classes = sorted(e.name for e in os.scandir(directory) if e.is_dir())
     if not classes:

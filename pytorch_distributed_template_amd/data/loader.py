@@ -16,7 +16,7 @@ from typing import Optional
 import torch
 from torch.utils.data import DataLoader
 
-from .datasets import ImageFolder, SyntheticImageNet
+from .datasets import ImageFolder, SyntheticImageNet, lazy_pil_loader, pil_loader
 from .sampler import DistributedSampler
 from .transforms import normalize_on_device, train_transform, val_transform
 
@@ -130,9 +130,13 @@ def build_loaders(args, world: int, rank: int, device, distributed: bool, batch_
         train_ds = SyntheticImageNet(args.synthetic_train_size, args.image_size, args.num_classes, seed=0, uint8=u8)
         val_ds = SyntheticImageNet(args.synthetic_val_size, args.image_size, args.num_classes, seed=1, uint8=u8)
     else:
-        train_ds = ImageFolder(os.path.join(args.data, "train"), train_transform(args.image_size, gpu_normalize=u8))
+        draft = bool(getattr(args, "jpeg_draft", False))
+        ld = lazy_pil_loader if draft else pil_loader
+        train_ds = ImageFolder(os.path.join(args.data, "train"),
+                               train_transform(args.image_size, gpu_normalize=u8, draft=draft), loader=ld)
         resize = round(args.image_size * 256 / 224)  # 256 for the 224 crop, 342 for Inception-v3's 299
-        val_ds = ImageFolder(os.path.join(args.data, "val"), val_transform(args.image_size, resize, gpu_normalize=u8))
+        val_ds = ImageFolder(os.path.join(args.data, "val"),
+                             val_transform(args.image_size, resize, gpu_normalize=u8, draft=draft), loader=ld)
     if distributed:
         train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
         val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank)

@@ -7,6 +7,12 @@ Reference pipelines (`dataparallel.py:133-151`):
 Implemented on PIL images + numpy; random draws use ``torch``'s global RNG exactly like
 torchvision (``torch.empty(1).uniform_``, ``torch.randint``, ``torch.rand``), so a seeded run draws
 the same crop boxes.
+
+``draft=True`` (``--jpeg-draft``, off by default): JPEG decode at reduced size.  The crop box / resize target
+is known from the file header before any pixel is decoded, so libjpeg is asked (``Image.draft``) for the
+largest DCT-domain downscale (1/2, 1/4, 1/8) that still leaves at least the output resolution inside the
+crop; decode cost falls roughly with the pixel count.  Pixels differ slightly from a full decode
+(DCT-domain vs bilinear downscale), so it is an opt-in throughput option (tools/data_bench.py).
 """
 from __future__ import annotations
 
@@ -35,14 +41,27 @@ def _size(img: Image.Image) -> Tuple[int, int]:
     return img.size  # (w, h)
 
 
+def _draft(img: Image.Image, factor: float) -> Tuple[float, float]:
+    """Ask a not-yet-decoded JPEG for a DCT-domain downscale of up to ``factor`` (>= 2 to matter); returns
+    the (x, y) scale actually applied (1.0 when not a JPEG / already decoded / factor < 2)."""
+    if factor < 2 or getattr(img, "format", None) != "JPEG" or not getattr(img, "tile", None):  # tile: undecoded
+        return 1.0, 1.0
+    W, H = img.size
+    img.draft("RGB", (max(1, math.ceil(W / factor)), max(1, math.ceil(H / factor))))
+    return img.size[0] / W, img.size[1] / H
+
+
 class Resize:
     """Resize the shorter side to ``size`` (int) keeping the aspect ratio, bilinear."""
 
-    def __init__(self, size, interpolation=Image.BILINEAR):
+    def __init__(self, size, interpolation=Image.BILINEAR, draft: bool = False):
         self.size = size
         self.interpolation = interpolation
+        self.draft = draft
 
     def __call__(self, img: Image.Image) -> Image.Image:
+        if self.draft and not isinstance(self.size, (tuple, list)):
+            _draft(img, min(_size(img)) / self.size)
         if isinstance(self.size, (tuple, list)):
             h, w = self.size
             return img.resize((w, h), self.interpolation)
@@ -73,11 +92,13 @@ class CenterCrop:
 
 
 class RandomResizedCrop:
-    def __init__(self, size, scale=(0.08, 1.0), ratio=(3.0 / 4.0, 4.0 / 3.0), interpolation=Image.BILINEAR):
+    def __init__(self, size, scale=(0.08, 1.0), ratio=(3.0 / 4.0, 4.0 / 3.0), interpolation=Image.BILINEAR,
+                 draft: bool = False):
         self.size = (size, size) if isinstance(size, int) else tuple(size)
         self.scale = scale
         self.ratio = ratio
         self.interpolation = interpolation
+        self.draft = draft
 
     @staticmethod
     def get_params(img: Image.Image, scale, ratio):
@@ -105,8 +126,12 @@ class RandomResizedCrop:
         return (height - h) // 2, (width - w) // 2, h, w
 
     def __call__(self, img: Image.Image) -> Image.Image:
-        i, j, h, w = self.get_params(img, self.scale, self.ratio)
+        i, j, h, w = self.get_params(img, self.scale, self.ratio)  # on the header size: no decode yet
         th, tw = self.size
+        if self.draft:
+            fx, fy = _draft(img, min(w / tw, h / th))
+            if (fx, fy) != (1.0, 1.0):  # crop box in the reduced image (float box: no re-rounding)
+                return img.resize((tw, th), self.interpolation, box=(j * fx, i * fy, (j + w) * fx, (i + h) * fy))
         return img.crop((j, i, j + w, i + h)).resize((tw, th), self.interpolation)
 
 
@@ -145,16 +170,17 @@ class Normalize:
         return (t - self.mean) / self.std
 
 
-def train_transform(image_size: int = 224, gpu_normalize: bool = False) -> Compose:
+def train_transform(image_size: int = 224, gpu_normalize: bool = False, draft: bool = False) -> Compose:
     """Reference train transform (`dataparallel.py:133-141`); with ``gpu_normalize`` the samples stay
     uint8 (4x less host->device traffic) and ToTensor + Normalize happen on the GPU."""
     tail = [ToUint8Tensor()] if gpu_normalize else [ToTensor(), Normalize(IMAGENET_MEAN, IMAGENET_STD)]
-    return Compose([RandomResizedCrop(image_size), RandomHorizontalFlip()] + tail)
+    return Compose([RandomResizedCrop(image_size, draft=draft), RandomHorizontalFlip()] + tail)
 
 
-def val_transform(image_size: int = 224, resize: int = 256, gpu_normalize: bool = False) -> Compose:
+def val_transform(image_size: int = 224, resize: int = 256, gpu_normalize: bool = False,
+                  draft: bool = False) -> Compose:
     tail = [ToUint8Tensor()] if gpu_normalize else [ToTensor(), Normalize(IMAGENET_MEAN, IMAGENET_STD)]
-    return Compose([Resize(resize), CenterCrop(image_size)] + tail)
+    return Compose([Resize(resize, draft=draft), CenterCrop(image_size)] + tail)
 
 
 def normalize_on_device(x: torch.Tensor) -> torch.Tensor:

@@ -58,10 +58,14 @@ class NativeTrainer:
         # HIP events around bucketer.finish(): the time the compute stream waits for gradient all-reduces
         # that backward did not hide (exposed communication)
         self._comm_events = [] if time_comm else None
+        # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full
+        # SyncBN path with identity all-reduces), else over torch.distributed at world > 1
+        nsync = sync_bn and self.ncomm is not None
         self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
-                                       syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed)
-                                       else None, autotune=autotune,
-                                       syncbn_allreduce=self.ncomm.all_reduce if self.ncomm is not None else None)
+                                       syncbn_group=(process_group or dist.group.WORLD)
+                                       if (sync_bn and self.distributed and not nsync) else None, autotune=autotune,
+                                       syncbn_allreduce=self.ncomm.all_reduce if nsync else None,
+                                       syncbn_world=self.ncomm.world if nsync else 0)
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executor.update_derived)
         # fp16 needs dynamic loss scaling; bf16 has fp32's exponent range and does not

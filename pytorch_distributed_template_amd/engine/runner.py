@@ -101,8 +101,9 @@ def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, de
         if i >= n_iter:
             break
         data_times.update(time.time() - end)
-        images = images.to(device, non_blocking=True)
-        target = target.to(device, non_blocking=True)
+        if not getattr(trainer, "host_batches", False):  # native DP scatters host batches to every GPU itself
+            images = images.to(device, non_blocking=True)
+            target = target.to(device, non_blocking=True)
         with roctx_range("train_step", args.profile):
             _, met = trainer.train_step(images, target)
         meter.update(met, images.size(0))
@@ -143,8 +144,9 @@ def validate(loader, trainer, epoch: int, args, logger, writer, rank: int, devic
         for i, (images, target) in enumerate(loader):
             if i >= n_iter:
                 break
-            images = images.to(device, non_blocking=True)
-            target = target.to(device, non_blocking=True)
+            if not getattr(trainer, "host_batches", False):
+                images = images.to(device, non_blocking=True)
+                target = target.to(device, non_blocking=True)
             with roctx_range("eval_step", args.profile):
                 _, met = trainer.eval_step(images, target)
             meter.update(met, images.size(0))
@@ -208,7 +210,7 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
         from .native_trainer import NativeTrainer
         lb = float(getattr(args, "last_bucket_mb", 1.0))
         return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)),
-                             comm=getattr(args, "comm", "torch"), graph=bool(getattr(args, "graph", False)),
+                             comm=getattr(args, "comm", "native"), graph=bool(getattr(args, "graph", False)),
                              last_bucket_mb=lb if lb > 0 else None,
                              comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)), **kw)
     from .torch_trainer import TorchTrainer
@@ -247,8 +249,14 @@ def main(mode: str, argv: Optional[list] = None) -> int:
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
+    dtype = resolve_precision(args, device)
+    engine = resolve_engine(args, device, dtype)
     if distributed:
-        backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if on_gpu else "gloo")
+        # native engine + native communicator: every GPU collective goes through our RCCL communicator, so the
+        # process group is only the rendezvous store (+ CPU barriers): gloo, not a second RCCL communicator
+        native_comm = engine == "native" and getattr(args, "comm", "native") == "native"
+        backend = args.dist_backend if args.dist_backend != "auto" else (
+            "nccl" if on_gpu and not native_comm else "gloo")
         timeout = datetime.timedelta(seconds=args.dist_timeout)
         if backend == "nccl":
             dist.init_process_group(backend, device_id=device, timeout=timeout)
@@ -275,8 +283,6 @@ def main(mode: str, argv: Optional[list] = None) -> int:
     if mode != "dp":
         args.batch_size = int(args.batch_size / args.nprocs)
 
-    dtype = resolve_precision(args, device)
-    engine = resolve_engine(args, device, dtype)
     ddp_print("=> engine: {} | compute dtype: {} | device: {} | world: {}".format(engine, str(dtype).split(".")[-1],
                                                                                 device, world), logger, rank)
     trainer = build_trainer(mode, model, args, device, dtype, engine, world)

@@ -81,7 +81,7 @@ class ResNetExecutor:
     def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None,
                  syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512, autotune: bool = False,
-                 syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None):
+                 syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not isinstance(model, ResNet) or model.groups != 1:
@@ -106,12 +106,17 @@ class ResNetExecutor:
         self._on_side = False
         self._pending_reads: Dict[int, "torch.cuda.Event"] = {}
         self.syncbn_group = syncbn_group
-        # SyncBN statistic all-reduce (fp64 sums): torch.distributed on syncbn_group, or a native RCCL
-        # communicator's all_reduce when one is given
-        if syncbn_group is not None:
+        # SyncBN statistic all-reduce (fp64 sums): a native RCCL communicator's all_reduce when one is given
+        # (``syncbn_world`` = its size; a world of 1 runs the whole SyncBN path with identity all-reduces, which
+        # measures its overhead on one GPU), else torch.distributed on syncbn_group
+        self.syncbn = syncbn_allreduce is not None or syncbn_group is not None
+        if syncbn_allreduce is not None:
+            self.syncbn_world = int(syncbn_world) if syncbn_world else 1
+            self._sync_sum = syncbn_allreduce
+        elif syncbn_group is not None:
             import torch.distributed as dist
             self.syncbn_world = dist.get_world_size(syncbn_group)
-            self._sync_sum = syncbn_allreduce or (lambda t: dist.all_reduce(t, group=syncbn_group))
+            self._sync_sum = lambda t: dist.all_reduce(t, group=syncbn_group)
         self.wgrad_blocks = wgrad_blocks  # split-K targets (tools/conv_bench.py sweep: 3x3 best ~2048, 1x1 ~512)
         self.wgrad_blocks_1x1 = wgrad_blocks_1x1
         # generic-path stem tile (window mode, BK=32); PDT_STEM_TILE=BMxBN overrides (tuning)
@@ -344,7 +349,7 @@ class ResNetExecutor:
 
     def bn_train_finalize(self, bn: _BN, sp, tiles: int, count: int):
         C = bn.C
-        if self.syncbn_group is None:  # slot sum + finalize in one launch
+        if not self.syncbn:  # slot sum + finalize in one launch
             self.C.bn_finalize_slots(sp, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
                                      bn.mod.running_mean, bn.mod.running_var, bn.coef, bn.sums, True)
             return
@@ -436,7 +441,7 @@ class ResNetExecutor:
         """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients."""
         C = bn1.C
         K = 4 if bn2 is not None else 2
-        if self.syncbn_group is None:  # slot sum + finalize of both branches in one launch
+        if not self.syncbn:  # slot sum + finalize of both branches in one launch
             self.C.bn_bwd_finalize_slots(
                 slots, K, float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot), self._g(bn1.bslot),
                 bn1.bcoef, bn2.coef if bn2 is not None else None, self._p(bn2.gslot) if bn2 is not None else None,

@@ -15,11 +15,18 @@ device's current stream): the per-forward weight broadcast moves the 16-bit shad
 the fp32 parameters) and the BN buffers from GPU 0 over xGMI, and gradients are reduce-added in place
 into GPU 0's flat gradient buffer.  All devices run concurrently because every launch is asynchronous on
 its device's stream; no host synchronisation is needed anywhere in the step.
+
+One host thread drives every device, so eager launching would serialise: a replica's step is ~300 kernel
+launches (a few ms of host time) while its GPU work at the reference's per-GPU batch is only a few ms, and
+N replicas would wait on one launching thread.  With ``graph=True`` (the default on > 1 device) each
+replica's forward + backward (plus its derived weight layouts) is captured once per input shape as a HIP
+graph on its own device and replayed: per step the host issues the broadcast, N graph launches, the
+gradient reduce and the SGD -- the devices' work overlaps instead of queueing behind the host.
 """
 from __future__ import annotations
 
 import copy
-from typing import List
+from typing import List, Optional
 
 import torch
 
@@ -31,8 +38,13 @@ from ..optim.sgd import FusedSGD
 
 class NativeDataParallelTrainer:
     def __init__(self, model, device_ids: List[int], dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
-                 momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False):
+                 momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False,
+                 graph: Optional[bool] = None):
         self.device_ids = list(device_ids)
+        # per-replica HIP graphs (see module doc); two eager warm-up steps settle buffers and tile choices
+        self.use_graph = (len(self.device_ids) > 1) if graph is None else bool(graph)
+        self._graphs = {}
+        self._graph_warm = 0
         self.devices = [torch.device("cuda", i) for i in self.device_ids]
         self.dtype = dtype
         replicas = [model] + [copy.deepcopy(model) for _ in self.devices[1:]]
@@ -52,6 +64,9 @@ class NativeDataParallelTrainer:
         self.optimizer.post_step_hooks.append(self.executors[0].update_derived)
         self.scaler = DeviceGradScaler(self.devices[0], enabled=use_amp and dtype == torch.float16)
         self.group = None
+        # the runner hands host (pinned) batches straight to _scatter: each shard is copied host -> its own
+        # GPU, instead of the whole batch going to GPU 0 first (nn.DataParallel's scatter from GPU 0)
+        self.host_batches = len(self.devices) > 1
         if len(self.devices) > 1:
             from ..ops import native
             self.group = native.C.DeviceGroup(self.device_ids)
@@ -63,15 +78,56 @@ class NativeDataParallelTrainer:
             self.flat.refresh_shadow()
             self.executors[0].update_derived()
 
-    def _replicate(self) -> None:
+    def _replicate(self, derived: bool = True) -> None:
         if len(self.devices) == 1:
             return
         self.group.broadcast([f.shadow for f in self.flats], 0)
         if self.buffers[0].n_float:
             self.group.broadcast([b.fdata for b in self.buffers], 0)
-        for i in range(1, len(self.devices)):
+        if derived:
+            for i in range(1, len(self.devices)):
+                with torch.cuda.device(self.devices[i]):
+                    self.executors[i].update_derived()
+
+    def _replica_step(self, i: int, x, t, ls, B: int, derived: bool):
+        """Replica i's forward + backward on its device (gradients into its flat buffer)."""
+        if derived and i > 0:
+            self.executors[i].update_derived()
+        return self.executors[i].train_step(x, t, loss_scale=ls, grad_div=float(B))
+
+    def _run_replicas(self, xs, ts, B: int):
+        """Every replica's step: eager, or -- once warm -- one captured HIP graph replay per device."""
+        scale = self.scaler.scale_tensor
+        res = []
+        warm = self.use_graph and self._graph_warm >= 2
+        for i, (x, t) in enumerate(zip(xs, ts)):
+            if x.shape[0] == 0:
+                res.append(None)
+                continue
             with torch.cuda.device(self.devices[i]):
-                self.executors[i].update_derived()
+                ls = scale if i == 0 or scale is None else scale.to(self.devices[i])
+                if not warm:
+                    res.append(self._replica_step(i, x, t, ls, B, derived=False))
+                    continue
+                key = (i, tuple(x.shape), x.dtype, B)
+                ent = self._graphs.get(key)
+                if ent is None:
+                    sx, st = x.clone(), t.clone()
+                    sls = ls.clone() if ls is not None else None
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        out = self._replica_step(i, sx, st, sls, B, derived=True)
+                    ent = self._graphs[key] = (g, sx, st, sls, out)
+                g, sx, st, sls, out = ent
+                sx.copy_(x, non_blocking=True)
+                st.copy_(t, non_blocking=True)
+                if sls is not None:
+                    sls.copy_(ls, non_blocking=True)
+                g.replay()
+                res.append(tuple(o.clone() for o in out))
+        if self.use_graph and not warm:
+            self._graph_warm += 1
+        return res, warm
 
     def _scatter(self, images, target):
         n = len(self.devices)
@@ -85,16 +141,16 @@ class NativeDataParallelTrainer:
 
     def train_step(self, images, target):
         B = images.shape[0]
-        self._replicate()
+        warm = self.use_graph and self._graph_warm >= 2
+        self._replicate(derived=not warm)  # graphed replicas gather their derived layouts inside the graph
         xs, ts = self._scatter(images, target)
-        outs, mets = [], []
         scale = self.scaler.scale_tensor
-        for i, (ex, x, t) in enumerate(zip(self.executors, xs, ts)):
-            if x.shape[0] == 0:
+        outs, mets = [], []
+        res, _ = self._run_replicas(xs, ts, B)
+        for x, r in zip(xs, res):
+            if r is None:
                 continue
-            with torch.cuda.device(self.devices[i]):
-                ls = scale if i == 0 or scale is None else scale.to(self.devices[i])
-                logits, met = ex.train_step(x, t, loss_scale=ls, grad_div=float(B))
+            logits, met = r
             outs.append(logits)
             mets.append(met.to(self.devices[0]) * (x.shape[0] / B))
         if self.buffers[0].n_int:

@@ -86,3 +86,30 @@ def test_synthetic_deterministic():
     a, ya = ds[4]
     b, yb = ds[4]
     assert torch.equal(a, b) and ya == yb and a.shape == (3, 16, 16) and 0 <= ya < 5
+
+
+def test_jpeg_draft_decode_matches_full_decode(tmp_path):
+    """--jpeg-draft: a reduced-size DCT decode ahead of RandomResizedCrop / Resize gives the same output size and
+    nearly the same pixels as the full decode (crop boxes drawn from the same RNG state)."""
+    import numpy as np
+    import torch
+    from PIL import Image
+    from pytorch_distributed_template_amd.data.datasets import lazy_pil_loader, pil_loader
+    from pytorch_distributed_template_amd.data.transforms import (RandomResizedCrop, Resize, ToUint8Tensor,
+                                                                  _draft)
+    rng = np.random.default_rng(0)
+    low = rng.integers(0, 256, size=(40, 60, 3)).astype(np.uint8)
+    p = str(tmp_path / "big.jpg")
+    Image.fromarray(low).resize((1800, 1200), Image.BICUBIC).save(p, quality=92)
+    full = ToUint8Tensor()
+    for seed in range(4):
+        torch.manual_seed(seed)
+        a = full(RandomResizedCrop(224)(pil_loader(p))).float()
+        torch.manual_seed(seed)
+        b = full(RandomResizedCrop(224, draft=True)(lazy_pil_loader(p))).float()
+        assert a.shape == b.shape == (3, 224, 224)
+        assert (a - b).abs().mean().item() < 6.0  # DCT-domain vs bilinear downscale of a smooth image
+    img = lazy_pil_loader(p)
+    assert _draft(img, 4.0) == (0.25, 0.25) and img.size == (450, 300)  # header-only until decoded
+    r = Resize(256, draft=True)(lazy_pil_loader(p))
+    assert min(r.size) == 256

@@ -59,6 +59,18 @@ for stage in "$@"; do
       timeout -k 10 600 python -u tools/conv_bench.py --skip-stem > gpurun_out/conv_bench.log 2>&1; rc=$?
       grep shape gpurun_out/conv_bench.log | cut -c1-400
       [ $rc -eq 0 ] || { tail -5 gpurun_out/conv_bench.log; echo "conv_bench failed rc=$rc"; exit $rc; } ;;
+    testt)
+      timeout -k 10 900 python -u -m pytest tests/test_training_gpu.py tests/test_comm_gpu.py tests/test_ddp_numerics_gpu.py -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/pytest_t.log 2>&1; rc=$?
+      grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_t.log | tail -15
+      [ $rc -le 1 ] || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    syncbn1)
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/sb_plain.log 2>&1 && \
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 --force-comm > gpurun_out/sb_comm.log 2>&1 && \
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 --force-comm --sync-bn > gpurun_out/sb_sync.log 2>&1 && \
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 --force-comm --sync-bn --dtype fp16 > gpurun_out/sb_sync16.log 2>&1; rc=$?
+      for f in sb_plain sb_comm sb_sync sb_sync16; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log)"; done
+      [ $rc -eq 0 ] || { tail -20 gpurun_out/sb_sync.log; exit $rc; } ;;
     torch50)
       timeout -k 10 600 python tools/torch_baseline.py --arch resnet50 --dtype fp16 > gpurun_out/torch50.log 2>&1 || { tail gpurun_out/torch50.log; exit 1; }
       tail -2 gpurun_out/torch50.log ;;
