@@ -43,7 +43,8 @@ def _parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--arch", default="resnet18")
     ap.add_argument("--batch-per-gpu", type=int, default=1200)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="compute dtype (fp32: the reference's distributed.py precision, native fp32 MFMA kernels)")
     ap.add_argument("--sync-bn", action="store_true")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--last-bucket-mb", type=float, default=1.0,
@@ -122,7 +123,7 @@ def main() -> int:
         else:
             dist.init_process_group("nccl", device_id=dev)
     torch.manual_seed(0)
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
     model = registry.create(args.arch)
     tr = NativeTrainer(model, dev, dtype=dtype, lr=0.1, momentum=0.9, weight_decay=1e-4,
                        use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb,

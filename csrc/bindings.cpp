@@ -23,6 +23,7 @@
 #include "kernels/bn.h"
 #include "kernels/conv_fwd.h"
 #include "kernels/conv_wgrad.h"
+#include "kernels/fp32.h"
 #include "kernels/loss.h"
 #include "kernels/optim.h"
 #include "kernels/pool.h"
@@ -658,6 +659,172 @@ void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
   pdt::gather32_launch(pf(src, "src"), idx.data_ptr<int>(), pf(dst, "dst"), dst.numel(), cur_stream());
 }
 
+// ------------------------------------------------------------------------------------------ fp32 path
+const float* pfc(const OptT& t, const char* name) { return t.has_value() ? pf(*t, name) : nullptr; }
+
+// forward conv over fp32 NHWC / KRSC (same geometry arguments as conv_fwd; stats -> fp64 slots)
+void conv32_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N, int64_t H,
+                int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride,
+                int64_t pad, int64_t bm, int64_t bn) {
+  TORCH_CHECK(x.numel() == N * H * W * C && w.numel() == Kout * T * U * C && y.numel() == N * Pm * Qm * Kout,
+              "conv32_fwd: size mismatch");
+  TORCH_CHECK(C % 32 == 0 && Kout % bn == 0, "conv32_fwd: C % 32 / Kout % bn must be 0");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && w.numel() < (int64_t(1) << 30) && N * Pm * Qm < (int64_t(1) << 31),
+              "conv32_fwd: operands exceed 4 GiB (32-bit buffer offsets)");
+  pdt::Conv32Args a{};
+  a.x = pf(x, "x"); a.w = pf(w, "w"); a.y = pf(y, "y");
+  if (res.has_value()) {
+    TORCH_CHECK(res->numel() == y.numel(), "conv32_fwd: residual size");
+    a.res = pf(*res, "res");
+  }
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * Kout * 2, "conv32_fwd: stats buffer too small");
+    a.stats = pd(*stats, "stats");
+  }
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
+  a.ist_h = stride; a.ist_w = stride; a.ioff_h = -pad; a.ioff_w = -pad; a.tstep_h = 1; a.tstep_w = 1;
+  a.OH = Pm; a.OW = Qm; a.ost_h = 1; a.ost_w = 1; a.ooff_h = 0; a.ooff_w = 0;
+  a.M = N * Pm * Qm;
+  pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
+}
+
+// backward-data over fp32 in ONE launch for every sub-pixel phase (phases as in conv_dgrad)
+void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
+                  int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride,
+                  const std::vector<std::vector<int64_t>>& phases, int64_t bm, int64_t bn) {
+  TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv32_dgrad: size mismatch");
+  TORCH_CHECK(K % 32 == 0 && C % bn == 0, "conv32_dgrad: K % 32 / C % bn must be 0");
+  TORCH_CHECK(dy.numel() < (int64_t(1) << 30) && wt.numel() < (int64_t(1) << 30), "conv32_dgrad: operands too large");
+  TORCH_CHECK(!phases.empty() && phases.size() <= 4, "conv32_dgrad: 1..4 phases");
+  pdt::Conv32Args a{};
+  a.x = pf(dy, "dy"); a.w = pf(wt, "wt"); a.y = pf(dx, "dx");
+  if (res.has_value()) {
+    TORCH_CHECK(res->numel() == dx.numel(), "conv32_dgrad: residual size");
+    a.res = pf(*res, "res");
+  }
+  a.N = N; a.H = P; a.W = Q; a.C = K; a.Kout = C;
+  a.ist_h = 1; a.ist_w = 1; a.tstep_h = -1; a.tstep_w = -1;
+  a.OH = H; a.OW = W; a.ost_h = stride; a.ost_w = stride;
+  a.nphase = (int)phases.size();
+  int64_t maxM = 0;
+  for (size_t i = 0; i < phases.size(); ++i) {
+    const auto& f = phases[i];
+    TORCH_CHECK(f.size() == 7, "conv32_dgrad: phase = (ph, pw, T, U, ioff_h, ioff_w, woff)");
+    const int64_t Pm = (H - f[0] + stride - 1) / stride, Qm = (W - f[1] + stride - 1) / stride;
+    TORCH_CHECK(Pm > 0 && Qm > 0 && f[6] + C * f[2] * f[3] * K <= wt.numel(), "conv32_dgrad: bad phase");
+    a.pooff_h[i] = (int)f[0]; a.pooff_w[i] = (int)f[1]; a.pT[i] = (int)f[2]; a.pU[i] = (int)f[3];
+    a.pioff_h[i] = (int)f[4]; a.pioff_w[i] = (int)f[5]; a.pwoff[i] = f[6];
+    a.pPm[i] = (int)Pm; a.pQm[i] = (int)Qm;
+    maxM = std::max(maxM, N * Pm * Qm);
+  }
+  TORCH_CHECK(maxM < (int64_t(1) << 31), "conv32_dgrad: too many pixels");
+  a.M = maxM;
+  a.Pm = a.pPm[0]; a.Qm = a.pQm[0];
+  pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
+}
+
+void wgrad32(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
+             int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw, int64_t splits,
+             int64_t pix_per_split) {
+  TORCH_CHECK(C % 64 == 0 && Kout % 64 == 0, "wgrad32: C and Kout must be multiples of 64");
+  TORCH_CHECK(x.numel() == N * H * W * C && dy.numel() == N * Pm * Qm * Kout, "wgrad32: size mismatch");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30), "wgrad32: operands too large");
+  TORCH_CHECK(ldw >= T * U * C && ws.numel() >= splits * Kout * ldw, "wgrad32: workspace too small");
+  TORCH_CHECK(pix_per_split % 64 == 0 && splits * pix_per_split >= N * Pm * Qm, "wgrad32: bad split plan");
+  pdt::Wgrad32Args a{};
+  a.x = pf(x, "x"); a.dy = pf(dy, "dy"); a.ws = pf(ws, "ws");
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
+  a.stride = stride; a.pad = pad; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
+  a.P = N * Pm * Qm;
+  pdt::wgrad32_launch(a, cur_stream());
+}
+
+void bn_apply32(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& rcoef, Tensor& out, int64_t C,
+                int64_t resmode, bool relu) {
+  TORCH_CHECK(C % 4 == 0 && y.numel() % C == 0 && out.numel() == y.numel(), "bn_apply32: bad sizes");
+  if (resmode != 0) TORCH_CHECK(res.has_value() && res->numel() == y.numel(), "bn_apply32: residual");
+  if (resmode == 2) TORCH_CHECK(rcoef.has_value(), "bn_apply32: residual coefficients");
+  pdt::bn_apply32_launch(pf(y, "y"), pf(coef, "coef"), pfc(res, "res"), pfc(rcoef, "rcoef"), pf(out, "out"), y.numel(),
+                         C, (int)resmode, relu, cur_stream());
+}
+
+int64_t bn_bwd_reduce32_blocks(int64_t rows, int64_t C) { return pdt::bn_bwd_reduce32_blocks(rows, (int)C); }
+
+void bn_bwd_reduce32(const Tensor& g, const OptT& mref, const Tensor& y1, const Tensor& coef1, const OptT& y2,
+                     const OptT& coef2, Tensor& slots, int64_t blocks, int64_t rows, int64_t C) {
+  TORCH_CHECK(C % 4 == 0 && C <= 2048 && g.numel() == rows * C && y1.numel() == rows * C, "bn_bwd_reduce32: sizes");
+  if (mref.has_value()) TORCH_CHECK(mref->numel() == g.numel(), "bn_bwd_reduce32: mask reference size");
+  const int K = y2.has_value() ? 4 : 2;
+  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K, "bn_bwd_reduce32: slots too small");
+  pdt::bn_bwd_reduce32_launch(pf(g, "g"), pfc(mref, "mref"), pf(y1, "y1"), pf(coef1, "coef1"), pfc(y2, "y2"),
+                              pfc(coef2, "coef2"), pd(slots, "slots"), (int)blocks, rows, (int)C, cur_stream());
+}
+
+void bn_bwd_apply32(const Tensor& g, const OptT& mref, const Tensor& y1, const Tensor& b1, Tensor& dy1, const OptT& y2,
+                    const OptT& b2, const OptT& dy2, const OptT& dz, int64_t C) {
+  TORCH_CHECK(C % 4 == 0 && g.numel() % C == 0 && dy1.numel() == g.numel(), "bn_bwd_apply32: bad sizes");
+  pdt::bn_bwd_apply32_launch(pf(g, "g"), pfc(mref, "mref"), pf(y1, "y1"), pf(b1, "b1"), pf(dy1, "dy1"), pfc(y2, "y2"),
+                             pfc(b2, "b2"), dy2.has_value() ? pf(*dy2, "dy2") : nullptr,
+                             dz.has_value() ? pf(*dz, "dz") : nullptr, g.numel(), C, cur_stream());
+}
+
+void bn_relu_maxpool32(const Tensor& y, const Tensor& coef, Tensor& out, Tensor& idx, int64_t N, int64_t H, int64_t W,
+                       int64_t C) {
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(y.numel() == N * H * W * C && out.numel() == N * OH * OW * C && idx.numel() == out.numel() && C % 4 == 0,
+              "bn_relu_maxpool32: bad sizes");
+  check_dev(idx, "idx");
+  pdt::bn_relu_maxpool32_launch(pf(y, "y"), pf(coef, "coef"), pf(out, "out"), idx.data_ptr<uint8_t>(), N, H, W, C,
+                                cur_stream());
+}
+
+void maxpool_bwd_relu32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& dz, int64_t N,
+                        int64_t H, int64_t W, int64_t C) {
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dp.numel() == N * OH * OW * C && y.numel() == N * H * W * C && dz.numel() == y.numel() &&
+                  idx.numel() == dp.numel() && C % 4 == 0,
+              "maxpool_bwd_relu32: bad sizes");
+  check_dev(idx, "idx");
+  pdt::maxpool_bwd_relu32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"), pf(dz, "dz"), N, H,
+                                 W, C, cur_stream());
+}
+
+void avgpool32_fwd(const Tensor& x, Tensor& feat, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
+  TORCH_CHECK(x.numel() == N * HW * C && feat.numel() >= N * ldf, "avgpool32_fwd: bad sizes");
+  pdt::avgpool32_fwd_launch(pf(x, "x"), pf(feat, "feat"), N, HW, C, ldf, cur_stream());
+}
+
+void avgpool32_bwd(const Tensor& dfeat, Tensor& g, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
+  TORCH_CHECK(g.numel() == N * HW * C && dfeat.numel() >= N * ldf, "avgpool32_bwd: bad sizes");
+  pdt::avgpool32_bwd_launch(pf(dfeat, "dfeat"), pf(g, "g"), N, HW, C, ldf, cur_stream());
+}
+
+void xent32(const Tensor& logits, int64_t ldl, const OptT& bias, const Tensor& target, int64_t B, int64_t ncls,
+            const OptT& out_logits, const OptT& dlogits, const OptT& loss_scale, double grad_div, Tensor& row_loss,
+            Tensor& row_correct) {
+  check_dev(target, "target");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == B, "xent32: target must be int64 [B]");
+  TORCH_CHECK(logits.numel() >= B * ldl && ncls <= ldl, "xent32: logits too small");
+  if (out_logits.has_value()) TORCH_CHECK(out_logits->numel() == B * ncls, "xent32: out_logits size");
+  if (dlogits.has_value()) TORCH_CHECK(dlogits->numel() >= B * ldl, "xent32: dlogits size");
+  pdt::xent32_launch(pf(logits, "logits"), ldl, pfc(bias, "bias"), target.data_ptr<int64_t>(), B, ncls,
+                     out_logits.has_value() ? pf(*out_logits, "out_logits") : nullptr,
+                     dlogits.has_value() ? pf(*dlogits, "dlogits") : nullptr, pfc(loss_scale, "loss_scale"),
+                     (float)grad_div, pf(row_loss, "row_loss"), pf(row_correct, "row_correct"), cur_stream());
+}
+
+void colsum32(const Tensor& d, int64_t B, int64_t ld, int64_t ncols, Tensor& out, double scale) {
+  TORCH_CHECK(d.numel() >= B * ld && out.numel() >= ncols, "colsum32: bad sizes");
+  pdt::colsum32_launch(pf(d, "d"), B, ld, ncols, pf(out, "out"), (float)scale, cur_stream());
+}
+
+void im2col32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
+              int64_t stride, int64_t pad, int64_t ldk) {
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(x.numel() >= N * C * H * W && out.numel() == N * OH * OW * ldk && ldk >= R * S * C, "im2col32: sizes");
+  pdt::im2col32_launch(pf(x, "x"), pf(out, "out"), N, C, H, W, R, S, stride, pad, ldk, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -722,4 +889,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_pack", &stem_pack);
   m.def("stem_pack_u8", &stem_pack_u8);
   m.def("gather32", &gather32);
+  m.def("conv32_fwd", &conv32_fwd);
+  m.def("conv32_dgrad", &conv32_dgrad);
+  m.def("wgrad32", &wgrad32);
+  m.def("bn_apply32", &bn_apply32);
+  m.def("bn_bwd_reduce32_blocks", &bn_bwd_reduce32_blocks);
+  m.def("bn_bwd_reduce32", &bn_bwd_reduce32);
+  m.def("bn_bwd_apply32", &bn_bwd_apply32);
+  m.def("bn_relu_maxpool32", &bn_relu_maxpool32);
+  m.def("maxpool_bwd_relu32", &maxpool_bwd_relu32);
+  m.def("avgpool32_fwd", &avgpool32_fwd);
+  m.def("avgpool32_bwd", &avgpool32_bwd);
+  m.def("xent32", &xent32);
+  m.def("colsum32", &colsum32);
+  m.def("im2col32", &im2col32);
 }

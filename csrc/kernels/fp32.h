@@ -1,0 +1,62 @@
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pdt {
+
+// fp32 implicit-GEMM convolution (same geometry contract as ConvFwdArgs, conv_fwd.hip): forward, multi-phase
+// backward-data, 1x1 / linear layers.  Optional residual add and BN statistics rows.
+struct Conv32Args {
+  const float* x;
+  const float* w;
+  float* y;
+  const float* res;
+  double* stats;  // optional [kStatSlots][Kout][2] (sum, sumsq); filled through per-block rows (srows)
+  float* srows;
+  int srows_pp;
+  int N, H, W, C, Kout, T, U;
+  int Pm, Qm;
+  int ist_h, ist_w, ioff_h, ioff_w, tstep_h, tstep_w;
+  int OH, OW, ost_h, ost_w, ooff_h, ooff_w;
+  int64_t M;
+  int m_tiles, n_tiles;
+  uint32_t pq_mul, pq_shift, q_mul, q_shift;
+  int nphase;
+  int pT[4], pU[4], pioff_h[4], pioff_w[4], pPm[4], pQm[4], pooff_h[4], pooff_w[4], pmt[4];
+  int64_t pwoff[4];
+  uint32_t ppq_mul[4], ppq_shift[4], pq1_mul[4], pq1_shift[4];
+};
+void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s);
+
+// fp32 weight gradient: ws[split][Kout][ldw], column tap*C + c, split-K over pixels (sum with wgrad_reduce).
+struct Wgrad32Args {
+  const float* x;   // [N][H][W][C]
+  const float* dy;  // [N][Pm][Qm][Kout]
+  float* ws;
+  int N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, ldw, splits, pix_per_split;
+  int64_t P;
+};
+void wgrad32_launch(const Wgrad32Args& a, hipStream_t s);
+
+// elementwise / reduction kernels over NHWC fp32 activations (C % 4 == 0)
+void bn_apply32_launch(const float* y, const float* coef, const float* res, const float* rcoef, float* out, int64_t n,
+                       int C, int resmode, bool relu, hipStream_t s);
+int bn_bwd_reduce32_blocks(int64_t rows, int C);
+void bn_bwd_reduce32_launch(const float* g, const float* mref, const float* y1, const float* coef1, const float* y2,
+                            const float* coef2, double* slots, int blocks, int64_t rows, int C, hipStream_t s);
+void bn_bwd_apply32_launch(const float* g, const float* mref, const float* y1, const float* b1, float* dy1,
+                           const float* y2, const float* b2, float* dy2, float* dz, int64_t n, int C, hipStream_t s);
+void bn_relu_maxpool32_launch(const float* y, const float* coef, float* out, uint8_t* idx, int N, int H, int W, int C,
+                              hipStream_t s);
+void maxpool_bwd_relu32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, float* dz, int N,
+                               int H, int W, int C, hipStream_t s);
+void avgpool32_fwd_launch(const float* x, float* feat, int N, int HW, int C, int ldf, hipStream_t s);
+void avgpool32_bwd_launch(const float* dfeat, float* g, int N, int HW, int C, int ldf, hipStream_t s);
+void xent32_launch(const float* logits, int ldl, const float* bias, const int64_t* target, int B, int ncls,
+                   float* out_logits, float* dlogits, const float* loss_scale, float grad_div, float* row_loss,
+                   float* row_correct, hipStream_t s);
+void colsum32_launch(const float* d, int B, int ld, int ncols, float* out, float scale, hipStream_t s);
+void im2col32_launch(const float* x, float* out, int N, int C, int H, int W, int R, int S, int stride, int pad, int ldk,
+                     hipStream_t s);
+
+}  // namespace pdt

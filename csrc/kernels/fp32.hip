@@ -1,0 +1,795 @@
+// fp32 compute path: the precision of the reference's `distributed.py` / `dataparallel.py` (plain fp32, no
+// autocast; SURVEY K1 "fp32 path via v_mfma_f32_16x16x4_f32").  Storage, products and accumulation are all
+// fp32; the matrix work runs on the CDNA4 fp32 MFMA (v_mfma_f32_16x16x4f32, 32 cycles per 16x16x4 on one
+// SIMD: 1/16 of the bf16 rate, so an fp32 step is MFMA-bound by construction).
+//
+//   * conv32: implicit GEMM, NHWC x KRSC, the geometry contract of conv_fwd.hip (forward, multi-phase strided
+//     backward-data with one launch for every sub-pixel phase, 1x1 / linear).  Tiles of 32 fp32 K-elements
+//     (128-byte LDS rows, 8 16-byte chunks, source-side XOR swizzle: conflict-free ds_read_b128) are staged by
+//     LDS-DMA into a 2-deep ring.  A lane's b128 fragment holds 4 consecutive K-elements of one row; MFMA e
+//     (e = 0..3) consumes element e of every lane, i.e. the 16 K-elements of a fragment pair are split across
+//     4 MFMAs by residue -- any permutation of K is valid as long as A and B use the same one -- so every
+//     fragment is ONE ds_read_b128 instead of four ds_read_b32.  Epilogues: residual add and BN statistics
+//     (per-block partial rows, fixed-order reduction: deterministic, conv_fwd.h).
+//   * wgrad32: split-K weight gradient over 64-pixel chunks; the [pixel][channel] tiles are DMA'd with the
+//     16-byte chunk index XOR-ed by (row & 3) << 2 so that the four pixel rows one MFMA reads (lane / 16) hit
+//     four different bank groups (ds_read_b32, conflict free).
+//   * BN apply / backward reduce / backward apply, stem BN+ReLU+max-pool and its backward, average pool,
+//     softmax cross-entropy + accuracy, bias column sums, stem im2col: float4-vectorised NHWC kernels.
+#include "../common.h"
+#include "conv_fwd.h"
+#include "fp32.h"
+
+namespace pdt {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+PDT_DEVICE f32x4_t mfma4(float a, float b, f32x4_t c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+static int ew_blocks(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 16384) b = 16384;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// ------------------------------------------------------------------------------------------------ conv32
+template <int EPI, int BN_>
+PDT_DEVICE void zero_stat_row32(const Conv32Args& a) {
+  if constexpr (EPI != 0) {
+    const int tm = (int)blockIdx.x / a.n_tiles, tn = (int)blockIdx.x - tm * a.n_tiles;
+    float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * 2 + (int64_t)tn * BN_ * 2;
+    for (int i = threadIdx.x; i < BN_ * 2; i += 256) dst[i] = 0.f;
+  }
+}
+
+template <int BM, int BN, int EPI, bool RES>
+__global__ __launch_bounds__(256) void conv32_kernel(Conv32Args args) {
+  Conv32Args a = args;
+  if (args.nphase > 0) {  // multi-phase launch (strided backward-data): this block's phase geometry
+    const int ph = blockIdx.y;
+    a.T = args.pT[ph]; a.U = args.pU[ph];
+    a.ioff_h = args.pioff_h[ph]; a.ioff_w = args.pioff_w[ph];
+    a.Pm = args.pPm[ph]; a.Qm = args.pQm[ph];
+    a.ooff_h = args.pooff_h[ph]; a.ooff_w = args.pooff_w[ph];
+    a.m_tiles = args.pmt[ph];
+    a.M = (int64_t)a.N * a.Pm * a.Qm;
+    a.w = args.w + args.pwoff[ph];
+    a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
+    a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
+    if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) {
+      zero_stat_row32<EPI, BN>(a);
+      return;
+    }
+  }
+  constexpr int NW = 4, WAVES_N = 2, WAVES_M = 2;
+  constexpr int WN = BN / WAVES_N, WM = BM / WAVES_M;
+  constexpr int FN = WN / 16, FM = WM / 16;
+  constexpr int ROWB = 128;               // 32 fp32 K-elements per LDS row
+  constexpr int RPI = 1024 / ROWB;        // rows per LDS-DMA wave-instruction
+  constexpr int A_INSTR = BN / RPI / NW;  // weight rows
+  constexpr int B_INSTR = BM / RPI / NW;  // activation rows
+  constexpr int A_BYTES = BN * ROWB;
+  constexpr int STAGE = (BN + BM) * ROWB;
+  static_assert(A_INSTR * RPI * NW == BN && B_INSTR * RPI * NW == BM, "conv32 tile/instr mismatch");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WAVES_N, wm = wave / WAVES_N;
+  const int nwg = a.m_tiles * a.n_tiles;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile_m = bid / a.n_tiles, tile_n = bid % a.n_tiles;
+  const int64_t m0 = (int64_t)tile_m * BM;
+  const int n0 = tile_n * BN;
+  const int PQ = a.Pm * a.Qm;
+  const FastDiv fd_pq{a.pq_mul, a.pq_shift}, fd_q{a.q_mul, a.q_shift};
+  const int TU = a.T * a.U;
+  const int ksteps = TU * (a.C / 32);
+
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * a.C * 4u));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)((uint64_t)a.Kout * TU * a.C * 4u));
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  int brow_h[B_INSTR], brow_w[B_INSTR];
+  uint32_t brow_off[B_INSTR];
+#pragma unroll
+  for (int j = 0; j < B_INSTR; ++j) {
+    const int row = (wave * B_INSTR + j) * RPI + lrow;
+    const int64_t m = m0 + row;
+    const int bch = pchunk ^ ((row >> 1) & 7);
+    if (m < a.M) {
+      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
+      const int rem = (int)m - nimg * PQ;
+      const int i = (int)fdiv((uint32_t)rem, fd_q), jj = rem - i * a.Qm;
+      brow_h[j] = i * a.ist_h + a.ioff_h;
+      brow_w[j] = jj * a.ist_w + a.ioff_w;
+      brow_off[j] = (uint32_t)((((int64_t)(nimg * a.H + brow_h[j]) * a.W + brow_w[j]) * a.C + bch * 4) * 4);
+    } else {
+      brow_h[j] = -(1 << 29);
+      brow_w[j] = 0;
+      brow_off[j] = 0;
+    }
+  }
+  uint32_t arow_off[A_INSTR];
+#pragma unroll
+  for (int j = 0; j < A_INSTR; ++j) {
+    const int row = (wave * A_INSTR + j) * RPI + lrow;
+    arow_off[j] = (uint32_t)((((int64_t)(n0 + row) * TU * a.C) + (pchunk ^ ((row >> 1) & 7)) * 4) * 4);
+  }
+  int cur_t = 0, cur_u = 0, cur_c = 0;
+  auto stage_load = [&](int buf) {
+    const int t = cur_t, u = cur_u, c0 = cur_c;
+    cur_c += 32;
+    if (cur_c == a.C) {
+      cur_c = 0;
+      if (++cur_u == a.U) { cur_u = 0; ++cur_t; }
+    }
+    char* sbase = smem + buf * STAGE;
+    const uint32_t a_delta = (uint32_t)((t * a.U + u) * a.C + c0) * 4u;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j) buf_lds16(rw, sbase + (wave * A_INSTR + j) * 1024, arow_off[j] + a_delta);
+    const int dh = t * a.tstep_h, dw = u * a.tstep_w;
+    const int b_delta = ((dh * a.W + dw) * a.C + c0) * 4;
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j) {
+      const int h = brow_h[j] + dh, w = brow_w[j] + dw;
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      buf_lds16(rx, sbase + A_BYTES + (wave * B_INSTR + j) * 1024, ok ? brow_off[j] + (uint32_t)b_delta : kOOB);
+    }
+  };
+
+  f32x4_t acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_off[FN], b_off[FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) a_off[i] = (wn * WN + i * 16 + fr) * ROWB;
+#pragma unroll
+  for (int j = 0; j < FM; ++j) b_off[j] = A_BYTES + (wm * WM + j * 16 + fr) * ROWB;
+  const int sw = (fr >> 1) & 7;  // row swizzle: every fragment base is a multiple of 16 rows
+
+  auto compute_stage = [&](const char* sb) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f32x4v af[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = *(const f32x4v*)(sb + a_off[i] + (((kk * 4 + fq) ^ sw) << 4));
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfr[j] = *(const f32x4v*)(sb + b_off[j] + (((kk * 4 + fq) ^ sw) << 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = mfma4(af[i][e], bfr[j][e], acc[i][j]);
+    }
+  };
+
+  if (ksteps > 0) {
+    stage_load(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < ksteps) stage_load(cur ^ 1);
+      compute_stage(smem + cur * STAGE);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: lane holds output channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
+  float sacc[FN][4][2];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { sacc[i][r][0] = 0.f; sacc[i][r][1] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int64_t m = m0 + wm * WM + j * 16 + fr;
+    if (m >= a.M) continue;
+    const int mm = (int)m;
+    const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
+    const int rem = mm - nimg * PQ;
+    const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
+    const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
+    const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * WN + i * 16 + 4 * fq;
+      f32x4v v = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if constexpr (RES) v += *(const f32x4v*)(a.res + ob + n);
+      *(f32x4v*)(a.y + ob + n) = v;
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sacc[i][r][0] += v[r];
+          sacc[i][r][1] += v[r] * v[r];
+        }
+      }
+    }
+  }
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sacc[i][r][0] = row16_sum(sacc[i][r][0]);
+        sacc[i][r][1] = row16_sum(sacc[i][r][1]);
+      }
+    float* red = (float*)smem;  // [WAVES_M][BN][2] (the LDS ring is free: every wave passed the last barrier)
+    if (fr == 15) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * WN + i * 16 + 4 * fq + r;
+          red[(wm * BN + nl) * 2 + 0] = sacc[i][r][0];
+          red[(wm * BN + nl) * 2 + 1] = sacc[i][r][1];
+        }
+    }
+    __syncthreads();
+    if (tid < BN * 2) {
+      const int nl = tid >> 1, k = tid & 1;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w) t += red[(w * BN + nl) * 2 + k];
+      const int64_t row = (a.nphase > 0 ? (int64_t)blockIdx.y * a.srows_pp : 0) + tile_m;
+      a.srows[(row * a.Kout + n0 + nl) * 2 + k] = t;
+    }
+  }
+}
+
+void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
+  a.m_tiles = (int)((a.M + bm - 1) / bm);
+  a.n_tiles = a.Kout / bn;
+  {
+    const FastDiv f1 = make_fastdiv((uint32_t)(a.Pm * a.Qm)), f2 = make_fastdiv((uint32_t)a.Qm);
+    a.pq_mul = f1.mul; a.pq_shift = f1.shift; a.q_mul = f2.mul; a.q_shift = f2.shift;
+  }
+  int srows = 0, gx = a.m_tiles * a.n_tiles;
+  if (a.nphase > 0) {
+    int maxmt = 0;
+    for (int p = 0; p < a.nphase; ++p) {
+      a.pmt[p] = (int)(((int64_t)a.N * a.pPm[p] * a.pQm[p] + bm - 1) / bm);
+      maxmt = maxmt > a.pmt[p] ? maxmt : a.pmt[p];
+      if (a.pPm[p] > 0 && a.pQm[p] > 0) {
+        const FastDiv f1 = make_fastdiv((uint32_t)(a.pPm[p] * a.pQm[p])), f2 = make_fastdiv((uint32_t)a.pQm[p]);
+        a.ppq_mul[p] = f1.mul; a.ppq_shift[p] = f1.shift; a.pq1_mul[p] = f2.mul; a.pq1_shift[p] = f2.shift;
+      }
+    }
+    a.srows_pp = maxmt;
+    srows = a.nphase * maxmt;
+    gx = maxmt * a.n_tiles;
+  } else {
+    a.srows_pp = a.m_tiles;
+    srows = a.m_tiles;
+  }
+  if (gx == 0 || a.n_tiles == 0) return;
+  PDT_COUNT(a.nphase > 0 ? "conv32_dgrad" : "conv32_fwd");
+  Scratch part(a.stats ? (size_t)srows * a.Kout * 2 * sizeof(float) : 0, s);
+  a.srows = part.as<float>();
+  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(256);
+  const bool st = a.stats != nullptr, rs = a.res != nullptr;
+#define PDT_C32(BM_, BN_)                                                                                  \
+  if (bm == BM_ && bn == BN_) {                                                                          \
+    if (st && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 1, true>), grid, block, 0, s, a);           \
+    else if (st) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 1, false>), grid, block, 0, s, a);           \
+    else if (rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 0, true>), grid, block, 0, s, a);            \
+    else hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 0, false>), grid, block, 0, s, a);                   \
+    if (st) stat_rows_reduce_launch(a.srows, srows, a.Kout * 2, a.stats, s);                               \
+    return;                                                                                              \
+  }
+  PDT_C32(128, 128)
+  PDT_C32(128, 64)
+#undef PDT_C32
+  pdt_hip_fail("conv32: unsupported tile (128x128 or 128x64)", hipErrorInvalidValue, __FILE__, __LINE__);
+}
+
+// ----------------------------------------------------------------------------------------------- wgrad32
+// Block: 64 output channels x 64 input channels of ONE tap over a pixel range; 4 waves in 2 x 2 (32 x 32 each).
+__global__ __launch_bounds__(256) void wgrad32_kernel(Wgrad32Args a) {
+  constexpr int PIX = 64;              // pixels per staged chunk
+  constexpr int TILE = PIX * 64 * 4;   // 16 KiB per operand tile ([pixel][64 channels] fp32, 256 B rows)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave >> 1, wc = wave & 1;
+  const int split = blockIdx.x, k0 = blockIdx.y * 64;
+  const int cblocks = a.C / 64;
+  const int tap = blockIdx.z / cblocks, c0 = (blockIdx.z - tap * cblocks) * 64;
+  const int t = tap / a.U, u = tap - t * a.U;
+  const int64_t p_begin = (int64_t)split * a.pix_per_split;
+  const int64_t p_end = p_begin + a.pix_per_split < a.P ? p_begin + a.pix_per_split : a.P;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * a.C * 4u));
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (uint32_t)((uint64_t)a.P * a.Kout * 4u));
+  // DMA lane geometry: one wave-instruction = 4 rows x 16 chunks of 16 B; source chunk = LDS chunk ^ (row & 3) << 2
+  const int lrow = lane >> 4, pc = lane & 15;
+  const int sc = pc ^ (lrow << 2);
+  const int PQ = a.Pm * a.Qm;
+  auto stage = [&](int64_t p0, int buf) {
+    char* dyb = smem + buf * 2 * TILE;
+    char* xb = dyb + TILE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // 16 instructions per tile, 4 per wave
+      const int ins = wave * 4 + q;
+      const int row = ins * 4 + lrow;
+      const int64_t p = p0 + row;
+      uint32_t od = kOOB, ox = kOOB;
+      if (p < p_end) {
+        od = (uint32_t)((p * a.Kout + k0 + sc * 4) * 4);
+        const int n = (int)(p / PQ);
+        const int rem = (int)(p - (int64_t)n * PQ);
+        const int i = rem / a.Qm, j = rem - (rem / a.Qm) * a.Qm;
+        const int ih = i * a.stride - a.pad + t, iw = j * a.stride - a.pad + u;
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+          ox = (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0 + sc * 4) * 4);
+      }
+      buf_lds16(rd, dyb + ins * 1024, od);
+      buf_lds16(rx, xb + ins * 1024, ox);
+    }
+  };
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  // element (row, col) of a tile lives at row*256 + (((col >> 2) ^ ((row & 3) << 2)) << 4) + (col & 3)*4;
+  // the rows read together are 4s + fq, so (row & 3) == fq
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int col = wk * 32 + i * 16 + fr;
+    aoff[i] = fq * 256 + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wc * 32 + j * 16 + fr;
+    boff[j] = TILE + fq * 256 + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+  const int nchunks = p_end > p_begin ? (int)((p_end - p_begin + PIX - 1) / PIX) : 0;
+  if (nchunks > 0) {
+    stage(p_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const int cur = ch & 1;
+      if (ch + 1 < nchunks) stage(p_begin + (int64_t)(ch + 1) * PIX, cur ^ 1);
+      const char* base = smem + cur * 2 * TILE;
+#pragma unroll 4
+      for (int s4 = 0; s4 < PIX / 4; ++s4) {
+        const char* sb = base + s4 * 4 * 256;
+        float av[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) av[i] = *(const float*)(sb + aoff[i]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = *(const float*)(sb + boff[j]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // lane holds dW[k = k0 + wk*32 + i*16 + 4*fq + r][c = c0 + wc*32 + j*16 + fr]
+  float* out = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + wk * 32 + i * 16 + 4 * fq + r;
+        const int c = c0 + wc * 32 + j * 16 + fr;
+        out[(int64_t)k * a.ldw + tap * a.C + c] = acc[i][j][r];
+      }
+}
+
+void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
+  PDT_COUNT("wgrad32");
+  dim3 grid(a.splits, a.Kout / 64, a.T * a.U * (a.C / 64)), block(256);
+  hipLaunchKernelGGL(wgrad32_kernel, grid, block, 0, s, a);
+}
+
+// ----------------------------------------------------------------------------------------- elementwise
+// out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift
+template <int RESMODE, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply32_kernel(const float* __restrict__ y, const float* __restrict__ coef,
+                                                         const float* __restrict__ res, const float* __restrict__ rcoef,
+                                                         float* __restrict__ out, int64_t n4, int C) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
+    const int c = (int)((v * 4) % C);
+    f32x4v val = ((const f32x4v*)y)[v] * *(const f32x4v*)(coef + c) + *(const f32x4v*)(coef + C + c);
+    if constexpr (RESMODE == 1) val += ((const f32x4v*)res)[v];
+    if constexpr (RESMODE == 2)
+      val += ((const f32x4v*)res)[v] * *(const f32x4v*)(rcoef + c) + *(const f32x4v*)(rcoef + C + c);
+    if constexpr (RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) val[e] = fmaxf(val[e], 0.f);
+    }
+    ((f32x4v*)out)[v] = val;
+  }
+}
+
+void bn_apply32_launch(const float* y, const float* coef, const float* res, const float* rcoef, float* out, int64_t n,
+                       int C, int resmode, bool relu, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  dim3 g(ew_blocks(n4)), b(256);
+#define PDT_A32(RM, RL)                                                                                          \
+  if (resmode == RM && relu == RL) {                                                                             \
+    hipLaunchKernelGGL((bn_apply32_kernel<RM, RL>), g, b, 0, s, y, coef, res, rcoef, out, n4, C);                 \
+    return;                                                                                                      \
+  }
+  PDT_A32(0, true) PDT_A32(1, true) PDT_A32(2, true) PDT_A32(0, false) PDT_A32(1, false) PDT_A32(2, false)
+#undef PDT_A32
+}
+
+// Backward reduce: dz = g * (mref > 0) (mref: the post-ReLU activation, optional); per branch b:
+//   sum dz, sum dz * (y_b - mean_b) * invstd_b   -> this block's partial row [C][K] (K = 2 or 4)
+// A thread owns NV float4 channel groups of a row (C <= 2048), rows strided over the grid.
+template <bool MASK, int NBR, int NV>
+__global__ __launch_bounds__(256) void bn_bwd_reduce32_kernel(const float* __restrict__ g, const float* __restrict__ mref,
+                                                              const float* __restrict__ y1, const float* __restrict__ coef1,
+                                                              const float* __restrict__ y2, const float* __restrict__ coef2,
+                                                              float* __restrict__ srows, int64_t rows, int C) {
+  const int vpr = C / 4;
+  const int lanes_c = vpr / NV;              // threads per row
+  const int rpi = 256 / lanes_c;             // rows per block iteration
+  const int cl = threadIdx.x % lanes_c, rl = threadIdx.x / lanes_c;
+  constexpr int K = NBR * 2;
+  float s[NV][K][4];
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[q][k][e] = 0.f;
+  if (rl < rpi) {
+    for (int64_t r = (int64_t)blockIdx.x * rpi + rl; r < rows; r += (int64_t)gridDim.x * rpi) {
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const int c0 = (cl + q * lanes_c) * 4;
+        const int64_t off = r * C + c0;
+        f32x4v dz = *(const f32x4v*)(g + off);
+        if constexpr (MASK) {
+          const f32x4v m = *(const f32x4v*)(mref + off);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dz[e] = m[e] > 0.f ? dz[e] : 0.f;
+        }
+        const f32x4v x1 = (*(const f32x4v*)(y1 + off) - *(const f32x4v*)(coef1 + 2 * C + c0)) *
+                          *(const f32x4v*)(coef1 + 3 * C + c0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[q][0][e] += dz[e];
+          s[q][1][e] += dz[e] * x1[e];
+        }
+        if constexpr (NBR == 2) {
+          const f32x4v x2 = (*(const f32x4v*)(y2 + off) - *(const f32x4v*)(coef2 + 2 * C + c0)) *
+                            *(const f32x4v*)(coef2 + 3 * C + c0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s[q][2][e] += dz[e];
+            s[q][3][e] += dz[e] * x2[e];
+          }
+        }
+      }
+    }
+  }
+  extern __shared__ float red[];  // [rpi][C][K]
+  if (rl < rpi) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[((int64_t)rl * C + (cl + q * lanes_c) * 4 + e) * K + k] = s[q][k][e];
+  }
+  __syncthreads();
+  float* dst = srows + (int64_t)blockIdx.x * C * K;
+  for (int idx = threadIdx.x; idx < C * K; idx += 256) {
+    float tt = 0.f;
+    for (int q = 0; q < rpi; ++q) tt += red[(int64_t)q * C * K + idx];
+    dst[idx] = tt;
+  }
+}
+
+int bn_bwd_reduce32_blocks(int64_t rows, int C) {
+  const int vpr = C / 4;
+  const int rpi = vpr >= 256 ? 1 : 256 / vpr;
+  int64_t b = (rows + rpi * 16 - 1) / (rpi * 16);
+  if (b > 1024) b = 1024;
+  return (int)(b < 1 ? 1 : b);
+}
+
+void bn_bwd_reduce32_launch(const float* g, const float* mref, const float* y1, const float* coef1, const float* y2,
+                            const float* coef2, double* slots, int blocks, int64_t rows, int C, hipStream_t s) {
+  const int vpr = C / 4;
+  const int nv = vpr > 256 ? vpr / 256 : 1;
+  if (nv > 2 || (vpr > 256 && vpr % 256 != 0))
+    pdt_hip_fail("bn_bwd_reduce32: C must be <= 2048 (and a multiple of 1024 above 1024)", hipErrorInvalidValue,
+                 __FILE__, __LINE__);
+  const int rpi = 256 / (vpr / nv);
+  const int nbr = y2 ? 2 : 1;
+  Scratch part((size_t)blocks * C * nbr * 2 * sizeof(float), s);
+  float* srows = part.as<float>();
+  const size_t smem = (size_t)rpi * C * nbr * 2 * sizeof(float);
+  const bool mask = mref != nullptr;
+#define PDT_R32(M_, NB_, NV_)                                                                                \
+  if (mask == M_ && nbr == NB_ && nv == NV_) {                                                               \
+    hipLaunchKernelGGL((bn_bwd_reduce32_kernel<M_, NB_, NV_>), dim3(blocks), dim3(256), smem, s, g, mref, y1, \
+                       coef1, y2, coef2, srows, rows, C);                                                     \
+    stat_rows_reduce_launch(srows, blocks, C * nbr * 2, slots, s);                                           \
+    return;                                                                                                  \
+  }
+  PDT_R32(true, 1, 1) PDT_R32(true, 2, 1) PDT_R32(false, 1, 1) PDT_R32(false, 2, 1)
+  PDT_R32(true, 1, 2) PDT_R32(true, 2, 2) PDT_R32(false, 1, 2) PDT_R32(false, 2, 2)
+#undef PDT_R32
+}
+
+// dy_b = A_b*dz + B_b*y_b + C_b, dz = g * (mref > 0); optionally writes dz (identity-branch gradient)
+template <bool MASK, int NBR, bool WDZ>
+__global__ __launch_bounds__(256) void bn_bwd_apply32_kernel(const float* __restrict__ g, const float* __restrict__ mref,
+                                                             const float* __restrict__ y1, const float* __restrict__ b1,
+                                                             float* __restrict__ dy1, const float* __restrict__ y2,
+                                                             const float* __restrict__ b2, float* __restrict__ dy2,
+                                                             float* __restrict__ dz_out, int64_t n4, int C) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
+    const int c = (int)((v * 4) % C);
+    f32x4v dz = ((const f32x4v*)g)[v];
+    if constexpr (MASK) {
+      const f32x4v m = ((const f32x4v*)mref)[v];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dz[e] = m[e] > 0.f ? dz[e] : 0.f;
+    }
+    ((f32x4v*)dy1)[v] = *(const f32x4v*)(b1 + c) * dz + *(const f32x4v*)(b1 + C + c) * ((const f32x4v*)y1)[v] +
+                        *(const f32x4v*)(b1 + 2 * C + c);
+    if constexpr (NBR == 2)
+      ((f32x4v*)dy2)[v] = *(const f32x4v*)(b2 + c) * dz + *(const f32x4v*)(b2 + C + c) * ((const f32x4v*)y2)[v] +
+                          *(const f32x4v*)(b2 + 2 * C + c);
+    if constexpr (WDZ) ((f32x4v*)dz_out)[v] = dz;
+  }
+}
+
+void bn_bwd_apply32_launch(const float* g, const float* mref, const float* y1, const float* b1, float* dy1,
+                           const float* y2, const float* b2, float* dy2, float* dz, int64_t n, int C, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  dim3 gr(ew_blocks(n4)), bl(256);
+  const bool mask = mref != nullptr, wdz = dz != nullptr;
+  const int nbr = y2 ? 2 : 1;
+#define PDT_B32(M_, NB_, WZ_)                                                                                     \
+  if (mask == M_ && nbr == NB_ && wdz == WZ_) {                                                                   \
+    hipLaunchKernelGGL((bn_bwd_apply32_kernel<M_, NB_, WZ_>), gr, bl, 0, s, g, mref, y1, b1, dy1, y2, b2, dy2, dz, \
+                       n4, C);                                                                                    \
+    return;                                                                                                       \
+  }
+  PDT_B32(true, 1, false) PDT_B32(true, 1, true) PDT_B32(true, 2, false) PDT_B32(true, 2, true)
+  PDT_B32(false, 1, false) PDT_B32(false, 1, true) PDT_B32(false, 2, false) PDT_B32(false, 2, true)
+#undef PDT_B32
+}
+
+// stem BN + ReLU + MaxPool(3, 2, 1), argmax (0..8) as uint8 (the backward's routing)
+__global__ __launch_bounds__(256) void bn_relu_maxpool32_kernel(const float* __restrict__ y, const float* __restrict__ coef,
+                                                                float* __restrict__ out, uint8_t* __restrict__ idx, int N,
+                                                                int H, int W, int C, int OH, int OW) {
+  const int cv = C / 4;
+  const int64_t total = (int64_t)N * OH * OW * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int64_t pix = v / cv;
+    const int c0 = (int)(v - pix * cv) * 4;
+    const int ow = (int)(pix % OW);
+    const int64_t tq = pix / OW;
+    const int oh = (int)(tq % OH), n = (int)(tq / OH);
+    const f32x4v sc = *(const f32x4v*)(coef + c0), sh = *(const f32x4v*)(coef + C + c0);
+    f32x4v best = {-1.f, -1.f, -1.f, -1.f};
+    uint8_t bi[4] = {0, 0, 0, 0};
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = oh * 2 - 1 + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = ow * 2 - 1 + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const f32x4v q = *(const f32x4v*)(y + (((int64_t)n * H + h) * W + w) * C + c0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float val = fmaxf(q[e] * sc[e] + sh[e], 0.f);
+          if (val > best[e]) { best[e] = val; bi[e] = (uint8_t)(kh * 3 + kw); }
+        }
+      }
+    }
+    *(f32x4v*)(out + pix * C + c0) = best;
+    *(uint32_t*)(idx + pix * C + c0) = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) |
+                                       ((uint32_t)bi[3] << 24);
+  }
+}
+
+void bn_relu_maxpool32_launch(const float* y, const float* coef, float* out, uint8_t* idx, int N, int H, int W, int C,
+                              hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(bn_relu_maxpool32_kernel, dim3(ew_blocks((int64_t)N * OH * OW * (C / 4))), dim3(256), 0, s, y,
+                     coef, out, idx, N, H, W, C, OH, OW);
+}
+
+// gather-form max-pool backward fused with the ReLU mask recomputed from the BN input y
+__global__ __launch_bounds__(256) void maxpool_bwd_relu32_kernel(const float* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                                                 const float* __restrict__ y, const float* __restrict__ coef,
+                                                                 float* __restrict__ dz, int N, int H, int W, int C, int OH,
+                                                                 int OW) {
+  const int cv = C / 4;
+  const int64_t total = (int64_t)N * H * W * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)(v % cv) * 4;
+    int64_t pix = v / cv;
+    const int w = (int)(pix % W);
+    pix /= W;
+    const int h = (int)(pix % H), n = (int)(pix / H);
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+    for (int oh = h / 2; oh <= (h + 1) / 2; ++oh) {
+      const int kh = h - (oh * 2 - 1);
+      if (oh >= OH || kh < 0 || kh > 2) continue;
+      for (int ow = w / 2; ow <= (w + 1) / 2; ++ow) {
+        const int kw = w - (ow * 2 - 1);
+        if (ow >= OW || kw < 0 || kw > 2) continue;
+        const uint8_t pos = (uint8_t)(kh * 3 + kw);
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+        const uint32_t ib = *(const uint32_t*)(idx + o);
+        const f32x4v gv = *(const f32x4v*)(dp + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((uint8_t)(ib >> (8 * e)) == pos) acc[e] += gv[e];
+      }
+    }
+    const int64_t i = (((int64_t)n * H + h) * W + w) * C + c0;
+    const f32x4v yy = *(const f32x4v*)(y + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (!(yy[e] * coef[c0 + e] + coef[C + c0 + e] > 0.f)) acc[e] = 0.f;
+    *(f32x4v*)(dz + i) = acc;
+  }
+}
+
+void maxpool_bwd_relu32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, float* dz, int N,
+                               int H, int W, int C, hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_bwd_relu32_kernel, dim3(ew_blocks((int64_t)N * H * W * (C / 4))), dim3(256), 0, s, dp, idx,
+                     y, coef, dz, N, H, W, C, OH, OW);
+}
+
+// global average pool [N][HW][C] -> feat [N][ldf] (columns >= C are left alone) and its backward
+__global__ __launch_bounds__(256) void avgpool32_fwd_kernel(const float* __restrict__ x, float* __restrict__ feat, int N,
+                                                            int HW, int C, int ldf) {
+  const int64_t total = (int64_t)N * C;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int n = (int)(v / C), c = (int)(v - (int64_t)n * C);
+    const float* p = x + (int64_t)n * HW * C + c;
+    float s = 0.f;
+    for (int i = 0; i < HW; ++i) s += p[(int64_t)i * C];
+    feat[(int64_t)n * ldf + c] = s / (float)HW;
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool32_bwd_kernel(const float* __restrict__ dfeat, float* __restrict__ g, int N,
+                                                            int HW, int C, int ldf) {
+  const int64_t total = (int64_t)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int c = (int)(v % C);
+    const int n = (int)(v / ((int64_t)HW * C));
+    g[v] = dfeat[(int64_t)n * ldf + c] * inv;
+  }
+}
+
+void avgpool32_fwd_launch(const float* x, float* feat, int N, int HW, int C, int ldf, hipStream_t s) {
+  hipLaunchKernelGGL(avgpool32_fwd_kernel, dim3(ew_blocks((int64_t)N * C)), dim3(256), 0, s, x, feat, N, HW, C, ldf);
+}
+
+void avgpool32_bwd_launch(const float* dfeat, float* g, int N, int HW, int C, int ldf, hipStream_t s) {
+  hipLaunchKernelGGL(avgpool32_bwd_kernel, dim3(ew_blocks((int64_t)N * HW * C)), dim3(256), 0, s, dfeat, g, N, HW, C,
+                     ldf);
+}
+
+// softmax cross-entropy forward + backward + top-1 (first maximum) over fp32 logits, one wave per row
+__global__ __launch_bounds__(256) void xent32_kernel(const float* __restrict__ logits, int ldl, const float* __restrict__ bias,
+                                                     const int64_t* __restrict__ target, int B, int ncls,
+                                                     float* __restrict__ out_logits, float* __restrict__ dlogits,
+                                                     const float* __restrict__ loss_scale, float grad_div,
+                                                     float* __restrict__ row_loss, float* __restrict__ row_correct) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* lr = logits + (int64_t)row * ldl;
+  const int tgt = (int)target[row];
+  float mx = -INFINITY;
+  int amax = 0x7fffffff;
+  for (int c = lane; c < ncls; c += 64) {
+    const float v = lr[c] + (bias ? bias[c] : 0.f);
+    if (out_logits) out_logits[(int64_t)row * ncls + c] = v;
+    if (v > mx) { mx = v; amax = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(amax, o, 64);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
+  float se = 0.f;
+  for (int c = lane; c < ncls; c += 64) se += __expf(lr[c] + (bias ? bias[c] : 0.f) - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const float xt = lr[tgt] + (bias ? bias[tgt] : 0.f);
+  if (dlogits) {
+    const float gsc = (loss_scale ? *loss_scale : 1.f) / grad_div;
+    float* dr = dlogits + (int64_t)row * ldl;
+    const float inv = 1.f / se;
+    for (int c = lane; c < ldl; c += 64) {
+      float d = 0.f;
+      if (c < ncls) d = (__expf(lr[c] + (bias ? bias[c] : 0.f) - mx) * inv - (c == tgt ? 1.f : 0.f)) * gsc;
+      dr[c] = d;
+    }
+  }
+  if (lane == 0) {
+    row_loss[row] = lse - xt;
+    row_correct[row] = (amax == tgt) ? 1.f : 0.f;
+  }
+}
+
+void xent32_launch(const float* logits, int ldl, const float* bias, const int64_t* target, int B, int ncls,
+                   float* out_logits, float* dlogits, const float* loss_scale, float grad_div, float* row_loss,
+                   float* row_correct, hipStream_t s) {
+  hipLaunchKernelGGL(xent32_kernel, dim3((B + 3) / 4), dim3(256), 0, s, logits, ldl, bias, target, B, ncls, out_logits,
+                     dlogits, loss_scale, grad_div, row_loss, row_correct);
+}
+
+// out[c] = scale * sum_b d[b][c]: 64 columns x 4 row lanes per block, fixed-order LDS reduction
+__global__ __launch_bounds__(256) void colsum32_kernel(const float* __restrict__ d, int B, int ld, int ncols,
+                                                       float* __restrict__ out, float scale) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < ncols)
+    for (int b = rl; b < B; b += 4) s += d[(int64_t)b * ld + c];
+  __shared__ float red[4][64];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && c < ncols)
+    out[c] = scale * (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x]);
+}
+
+void colsum32_launch(const float* d, int B, int ld, int ncols, float* out, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(colsum32_kernel, dim3((ncols + 63) / 64), dim3(256), 0, s, d, B, ld, ncols, out, scale);
+}
+
+// fp32 NCHW images -> im2col rows [N*OH*OW][ldk], column k = (r*S + s)*C + c (zero beyond R*S*C / outside)
+__global__ __launch_bounds__(256) void im2col32_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int C,
+                                                       int H, int W, int R, int S, int stride, int pad, int OH, int OW,
+                                                       int ldk) {
+  const int KK = R * S * C;
+  const int64_t total = (int64_t)N * OH * OW * ldk;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int k = (int)(v % ldk);
+    const int64_t pix = v / ldk;
+    float val = 0.f;
+    if (k < KK) {
+      const int c = k % C, rs = k / C;
+      const int r = rs / S, s_ = rs - r * S;
+      const int ow = (int)(pix % OW);
+      const int64_t tq = pix / OW;
+      const int oh = (int)(tq % OH), n = (int)(tq / OH);
+      const int h = oh * stride - pad + r, w = ow * stride - pad + s_;
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) val = x[(((int64_t)n * C + c) * H + h) * W + w];
+    }
+    out[v] = val;
+  }
+}
+
+void im2col32_launch(const float* x, float* out, int N, int C, int H, int W, int R, int S, int stride, int pad, int ldk,
+                     hipStream_t s) {
+  const int OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  hipLaunchKernelGGL(im2col32_kernel, dim3(ew_blocks((int64_t)N * OH * OW * ldk)), dim3(256), 0, s, x, out, N, C, H, W,
+                     R, S, stride, pad, OH, OW, ldk);
+}
+
+}  // namespace pdt

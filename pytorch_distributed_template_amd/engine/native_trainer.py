@@ -30,14 +30,15 @@ class NativeTrainer:
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
                  force_comm: bool = False, graph: bool = False, last_bucket_mb: Optional[float] = 1.0,
-                 comm_timeout_s: float = 0.0, time_comm: bool = False):
+                 comm_timeout_s: float = 0.0, time_comm: bool = False, eval_fp32: bool = False):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
         self.pg = process_group
         self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
         self.world = dist.get_world_size(process_group) if self.distributed else 1
-        self.flat = FlatParams(model, self.device, dtype)
+        # fp32 (the reference's distributed.py precision): kernels read the fp32 master directly, no shadow
+        self.flat = FlatParams(model, self.device, dtype if dtype != torch.float32 else None)
         self.buffers = FlatBuffers(model, self.device)
         # collectives: torch.distributed (RCCL via c10d) or our own RCCL communicator + C++ bucketer
         # (--comm native; force_comm exercises it on a single rank).  With the native communicator EVERY
@@ -61,11 +62,22 @@ class NativeTrainer:
         # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full
         # SyncBN path with identity all-reduces), else over torch.distributed at world > 1
         nsync = sync_bn and self.ncomm is not None
-        self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
-                                       syncbn_group=(process_group or dist.group.WORLD)
-                                       if (sync_bn and self.distributed and not nsync) else None, autotune=autotune,
-                                       syncbn_allreduce=self.ncomm.all_reduce if nsync else None,
-                                       syncbn_world=self.ncomm.world if nsync else 0)
+        sync_kw = dict(syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed and not nsync)
+                       else None, syncbn_allreduce=self.ncomm.all_reduce if nsync else None,
+                       syncbn_world=self.ncomm.world if nsync else 0)
+        if dtype == torch.float32:
+            from ..models.executor32 import ResNetExecutor32
+            self.executor = ResNetExecutor32(model, self.flat, self.device, grad_ready=self.bucketer.grad_ready,
+                                             **sync_kw)
+        else:
+            self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
+                                           autotune=autotune, **sync_kw)
+        # --eval-precision fp32: validation on the fp32 executor over the fp32 master weights (the reference
+        # validates without autocast, `distributed_syncBN_amp.py:311-317`), whatever the training dtype
+        self._eval32 = None
+        if eval_fp32 and dtype != torch.float32:
+            from ..models.executor32 import ResNetExecutor32
+            self._eval32 = ResNetExecutor32(model, self.flat, self.device)
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executor.update_derived)
         # fp16 needs dynamic loss scaling; bf16 has fp32's exponent range and does not
@@ -186,5 +198,9 @@ class NativeTrainer:
     def eval_step(self, images: torch.Tensor, target: torch.Tensor):
         if self.broadcast_buffers and self._steps > 0:
             self._sync_buffers()
-        logits, met = self.executor.eval_step(images, target)
+        if self._eval32 is not None:
+            self._eval32.update_derived()  # fp32 layouts of the current master weights
+            logits, met = self._eval32.eval_step(images, target)
+        else:
+            logits, met = self.executor.eval_step(images, target)
         return logits, self._reduce(met)

@@ -60,12 +60,13 @@ def resolve_precision(args, device: torch.device) -> torch.dtype:
 
 def resolve_engine(args, device: torch.device, dtype: torch.dtype) -> str:
     e = args.engine
-    native_ok = device.type == "cuda" and args.arch in NATIVE_ARCHS and dtype in (torch.bfloat16, torch.float16)
+    native_ok = device.type == "cuda" and args.arch in NATIVE_ARCHS and dtype in (torch.bfloat16, torch.float16,
+                                                                                  torch.float32)
     if e == "auto":
         return "native" if native_ok else "torch"
     if e == "native" and not native_ok:
-        raise ValueError(f"--engine native needs a GPU, a supported arch ({', '.join(NATIVE_ARCHS)}) and "
-                         f"bf16/fp16 precision (got device={device.type}, arch={args.arch}, dtype={dtype})")
+        raise ValueError(f"--engine native needs a GPU and a supported arch ({', '.join(NATIVE_ARCHS)}) "
+                         f"(got device={device.type}, arch={args.arch}, dtype={dtype})")
     return e
 
 
@@ -212,7 +213,8 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
         return NativeTrainer(model, device, dtype=dtype, autotune=bool(getattr(args, "autotune", False)),
                              comm=getattr(args, "comm", "native"), graph=bool(getattr(args, "graph", False)),
                              last_bucket_mb=lb if lb > 0 else None,
-                             comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)), **kw)
+                             comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)),
+                             eval_fp32=getattr(args, "eval_precision", "compute") == "fp32", **kw)
     from .torch_trainer import TorchTrainer
     return TorchTrainer(model, device, dtype=dtype, **kw, **torch_kw)
 

@@ -1,0 +1,393 @@
+"""Native fp32 ResNet executor: the reference's own precision on our HIP kernels.
+
+`distributed.py` and `dataparallel.py` train in plain fp32 (no autocast, `distributed.py:245-263`,
+`dataparallel.py:211-222`) and every script validates in fp32 (`distributed_syncBN_amp.py:311-317`).  This
+executor runs that precision end to end on the fp32 kernels of ``csrc/kernels/fp32.hip`` -- conv forward /
+multi-phase backward-data / weight gradient on ``v_mfma_f32_16x16x4f32``, BatchNorm statistics through the
+deterministic per-block rows, BN apply / backward, stem BN+ReLU+max-pool, average pool, cross-entropy -- with
+fp32 activations and weights read straight from the fp32 master buffer (no 16-bit shadow).
+
+Structure mirrors :class:`~.executor.ResNetExecutor` (torchvision-layout Basic / Bottleneck ResNets, flat
+gradient buffer, per-parameter ``grad_ready`` for the DDP bucketer, SyncBN through the same fp64 statistic
+all-reduce) without its 16-bit-specific fusions: BN-backward reductions are separate passes and the stem runs
+as an im2col GEMM (K = 7*7*3 padded to 192), processed in image chunks so every operand stays within the
+32-bit buffer offsets of the LDS-DMA loads.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import torch
+
+from ..ops import native
+from .executor import ResNetExecutor, _BN, _Conv
+from .resnet import BasicBlock, ResNet
+
+STEM_K = 192  # im2col width of the 7x7x3 stem (147 columns, zero padded to a multiple of 64)
+
+
+class ResNetExecutor32(ResNetExecutor):
+    """fp32 counterpart of :class:`ResNetExecutor` (same public interface)."""
+
+    def __init__(self, model: ResNet, flat, device: torch.device,
+                 grad_ready: Optional[Callable[[int], None]] = None, syncbn_group=None,
+                 syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0,
+                 wgrad_blocks: int = 2048):
+        if not isinstance(model, ResNet) or model.groups != 1:
+            raise NotImplementedError("native fp32 executor supports torchvision-style ResNets with groups=1")
+        self.C = native.C
+        self.n_slots = self.C.stat_slots()
+        self.model = model
+        self.flat = flat
+        self.device = torch.device(device)
+        self.dtype = torch.float32
+        self._user_grad_ready = grad_ready or (lambda pid: None)
+        self.side = None  # one stream: every kernel here is MFMA- or bandwidth-bound on its own
+        self._on_side = False
+        self._pending_reads = {}
+        self.syncbn_group = syncbn_group
+        self.syncbn = syncbn_allreduce is not None or syncbn_group is not None
+        if syncbn_allreduce is not None:
+            self.syncbn_world = int(syncbn_world) if syncbn_world else 1
+            self._sync_sum = syncbn_allreduce
+        elif syncbn_group is not None:
+            import torch.distributed as dist
+            self.syncbn_world = dist.get_world_size(syncbn_group)
+            self._sync_sum = lambda t: dist.all_reduce(t, group=syncbn_group)
+        self.wgrad_blocks = wgrad_blocks
+        from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
+        self.mean = torch.tensor(IMAGENET_MEAN, device=self.device).view(1, 3, 1, 1)
+        self.std = torch.tensor(IMAGENET_STD, device=self.device).view(1, 3, 1, 1)
+        derived_maps: List[torch.Tensor] = []
+        off = [0]
+
+        def conv(c):
+            return _Conv(c, flat, derived_maps, off)
+
+        st = model.conv1
+        assert st.in_channels * st.kernel_size[0] * st.kernel_size[1] <= STEM_K, "stem too wide for the im2col GEMM"
+        self.stem = conv(st)
+        self.stem_bn = _BN(model.bn1, flat, self.device)
+        self.blocks = []
+        for layer in (model.layer1, model.layer2, model.layer3, model.layer4):
+            for blk in layer:
+                kind = "basic" if isinstance(blk, BasicBlock) else "bottleneck"
+                convs = [blk.conv1, blk.conv2] + ([blk.conv3] if kind == "bottleneck" else [])
+                bns = [blk.bn1, blk.bn2] + ([blk.bn3] if kind == "bottleneck" else [])
+                d = {"kind": kind, "convs": [conv(c) for c in convs], "bns": [_BN(b, flat, self.device) for b in bns],
+                     "ds_conv": conv(blk.downsample[0]) if blk.downsample is not None else None,
+                     "ds_bn": _BN(blk.downsample[1], flat, self.device) if blk.downsample is not None else None}
+                self.blocks.append(d)
+        # stem weight as a [64][STEM_K] GEMM operand (KRSC flattening == im2col column order), zero padded
+        s = self.stem
+        kk = s.R * s.S * s.cin
+        o = torch.arange(s.cout).view(-1, 1)
+        k = torch.arange(STEM_K).view(1, -1)
+        m = torch.where(k < kk, s.slot.offset + o * kk + k, torch.full_like(o * k, -1))
+        self.stem_w_off = off[0]
+        derived_maps.append(m.reshape(-1).to(torch.int32))
+        off[0] += m.numel()
+        # stem weight gradient: [64][STEM_K] GEMM result -> KRSC slot
+        self.stem_gidx = (torch.arange(s.cout).view(-1, 1) * STEM_K + torch.arange(kk).view(1, -1)).reshape(-1).to(
+            torch.int32).to(self.device)
+        fc = model.fc
+        self.ncls, self.feat = fc.out_features, fc.in_features
+        self.ncls_pad = (self.ncls + 127) // 128 * 128
+        self.fc_slot = flat.slot(fc.weight)
+        self.fcb_slot = flat.slot(fc.bias)
+        o = torch.arange(self.ncls_pad).view(-1, 1)
+        f = torch.arange(self.feat).view(1, -1)
+        m = torch.where(o < self.ncls, self.fc_slot.offset + o * self.feat + f, torch.full_like(o * f, -1))
+        self.fc_w_off = off[0]
+        derived_maps.append(m.reshape(-1).to(torch.int32))
+        off[0] += m.numel()
+        self.fc_wt_off = off[0]
+        mt = m.t().contiguous()
+        derived_maps.append(mt.reshape(-1))
+        off[0] += mt.numel()
+        self.derived_idx = torch.cat([x.to(torch.int32) for x in derived_maps]).to(self.device)
+        self.derived = torch.zeros(off[0], dtype=torch.float32, device=self.device)
+        self._bufs = {}
+        self._plans = {}
+        self._tiles = {}
+        self.update_derived()
+
+    # ------------------------------------------------------------------------------------------ helpers
+    def update_derived(self) -> None:
+        """Derived fp32 weight layouts (dgrad phase weights, padded stem / fc matrices) from the master."""
+        self.C.gather32(self.flat.data, self.derived_idx, self.derived)
+
+    def _wait_derived(self) -> None:
+        pass
+
+    def _w32(self, c: _Conv) -> torch.Tensor:
+        s = c.slot
+        return self.flat.data[s.offset:s.offset + s.numel]
+
+    @staticmethod
+    def _bn_tile(n: int) -> int:
+        return 128 if n % 128 == 0 else 64
+
+    def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool):
+        P, Q = c.out_hw(H, W)
+        sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
+        self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, 128,
+                          self._bn_tile(c.cout))
+        return P, Q, sp
+
+    def _dgrad(self, c: _Conv, dy, N, H, W, P, Q, dx, res=None):
+        # every sub-pixel phase of the stride in one launch; a phase without taps (odd phases of a 1x1/2 conv)
+        # runs zero K-steps and writes zeros (+ the residual)
+        phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
+                  if H - ph > 0 and W - pw > 0]
+        self.C.conv32_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, 128,
+                            self._bn_tile(c.cin))
+
+    def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
+               accumulate=False):
+        ldw = R * S * C
+        npix = N * P * Q
+        key = (cout, R, S, C, npix)
+        plan = self._plans.get(key)
+        if plan is None:
+            per_split = (cout // 64) * R * S * (C // 64)
+            splits = max(1, min(self.wgrad_blocks // max(per_split, 1), (npix + 63) // 64))
+            pps = ((npix + splits - 1) // splits + 63) // 64 * 64
+            splits = (npix + pps - 1) // pps
+            plan = self._plans[key] = (splits, pps)
+        splits, pps = plan
+        ws = self._buf("ws", splits * cout * ldw, torch.float32)
+        self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps)
+        self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, accumulate)
+
+    def _stem_chunk(self, N: int) -> int:
+        # im2col rows of one chunk stay < 2^30 fp32 elements (32-bit LDS-DMA offsets)
+        P0, Q0 = self.stem.out_hw(self._HW[0], self._HW[1])
+        return max(1, min(N, ((1 << 30) - 1) // (P0 * Q0 * STEM_K)))
+
+    def bn_train_finalize(self, bn: _BN, sp, tiles: int, count: int, y: Optional[torch.Tensor] = None):
+        """Batch statistics with an accurate variance: the conv epilogue's fp32 partial sums give the mean; a
+        second pass over y accumulates sum y*(y - mean) (= sum (y - mean)^2 + mean * sum (y - mean)), so the
+        variance never comes from E[y^2] - E[y]^2 of fp32 partials (cancellation when |mean| >> std made fp32
+        training's activations ~50x less accurate than PyTorch's, enough to flip near-zero ReLU masks)."""
+        if y is None:
+            return super().bn_train_finalize(bn, sp, tiles, count)
+        C = bn.C
+        s1 = bn.sums
+        self.C.bn_slot_sum(sp, C, 2, s1)
+        n = float(count)
+        if self.syncbn:
+            self._sync_sum(s1)
+            n *= self.syncbn_world
+        mean = s1[:C] / n
+        cm = self._buf(("cmean", C), 4 * C, torch.float32)
+        cm[2 * C:3 * C].copy_(mean)
+        cm[3 * C:].fill_(1.0)
+        rows = y.numel() // C
+        slots = self._buf(("bnslots", C, 2), self.n_slots * C * 2, torch.float64)
+        self.C.bn_bwd_reduce32(y, None, y, cm, None, None, slots, self.C.bn_bwd_reduce32_blocks(rows, C), rows, C)
+        s2 = bn.bsums[:2 * C]
+        self.C.bn_slot_sum(slots, C, 2, s2)
+        if self.syncbn:
+            self._sync_sum(s2)
+        m2 = s2[C:] - mean * (s2[:C] - n * mean)  # sum (y - mean)^2 over every rank's batch
+        s1[C:] = m2 + n * mean * mean            # bn_finalize recovers var = s1[C:] / n - mean^2 in fp64
+        self.C.bn_finalize(s1, n, self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum, bn.mod.running_mean,
+                           bn.mod.running_var, bn.coef, True)
+
+    def bn_reduce(self, bn1: _BN, g, mref, y1, count, bn2: Optional[_BN] = None, y2=None):
+        C = bn1.C
+        rows = g.numel() // C
+        K = 4 if bn2 is not None else 2
+        slots = self._buf(("bnslots", C, K), self.n_slots * C * K, torch.float64)
+        blocks = self.C.bn_bwd_reduce32_blocks(rows, C)
+        self.C.bn_bwd_reduce32(g, mref, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows,
+                               C)
+        self._bn_bwd_finish(slots, count, bn1, bn2)
+
+    # ------------------------------------------------------------------------------------------ forward
+    def _forward(self, images: torch.Tensor, train: bool):
+        Cn = self.C
+        N, _, H, W = images.shape
+        if images.dtype == torch.uint8:  # raw pixels: ImageNet normalisation on the device
+            x32 = ((images.float() / 255.0 - self.mean) / self.std).contiguous()
+        else:
+            x32 = images.float().contiguous()
+        self._HW = (H, W)
+        st = self.stem
+        P0, Q0 = st.out_hw(H, W)
+        y0 = self._buf("y0", N * P0 * Q0 * st.cout, torch.float32)
+        wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * STEM_K]
+        ch = self._stem_chunk(N)
+        sp = None
+        if train:
+            sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64)
+            sp.zero_()
+        for n0 in range(0, N, ch):
+            n1 = min(N, n0 + ch)
+            cols = self._buf("stem_cols", (n1 - n0) * P0 * Q0 * STEM_K, torch.float32)
+            Cn.im2col32(x32[n0:n1], cols, n1 - n0, 3, H, W, st.R, st.S, st.st, st.pad, STEM_K)
+            spc = self._buf("stats_chunk", self.n_slots * st.cout * 2, torch.float64) if train else None
+            Cn.conv32_fwd(cols, wst, y0[n0 * P0 * Q0 * st.cout:n1 * P0 * Q0 * st.cout], None, spc,
+                          (n1 - n0) * P0 * Q0, 1, 1, STEM_K, st.cout, 1, 1, 1, 1, 1, 0, 128, 64)
+            if train:
+                sp.add_(spc)  # chunks in a fixed order: deterministic
+        if train:
+            self.bn_train_finalize(self.stem_bn, sp, 0, N * P0 * Q0, y0)
+        else:
+            self.bn_eval(self.stem_bn)
+        H1, W1 = (P0 - 1) // 2 + 1, (Q0 - 1) // 2 + 1
+        x = self._buf("act_in", N * H1 * W1 * st.cout, torch.float32)
+        idx = self._buf("mp_idx", N * H1 * W1 * st.cout, torch.uint8)
+        Cn.bn_relu_maxpool32(y0, self.stem_bn.coef, x, idx, N, P0, Q0, st.cout)
+        saved = {"N": N, "H": H, "W": W, "x32": x32, "y0": y0, "P0": P0, "Q0": Q0, "idx": idx, "x0": x, "H1": H1,
+                 "W1": W1}
+        Hc, Wc, Cc = H1, W1, st.cout
+        recs = []
+        for bi, b in enumerate(self.blocks):
+            rec = {"x": x, "H": Hc, "W": Wc, "C": Cc, "ys": [], "as": [], "hw": []}
+            cur, h, w = x, Hc, Wc
+            for ci, (c, bn) in enumerate(zip(b["convs"], b["bns"])):
+                P, Q = c.out_hw(h, w)
+                y = self._buf(("y", bi, ci), N * P * Q * c.cout, torch.float32)
+                _, _, sp = self._conv_fwd(c, cur, N, h, w, y, train)
+                if train:
+                    self.bn_train_finalize(bn, sp, 0, N * P * Q, y)
+                else:
+                    self.bn_eval(bn)
+                rec["ys"].append(y)
+                rec["hw"].append((h, w, P, Q))
+                if ci < len(b["convs"]) - 1:
+                    a = self._buf(("a", bi, ci), y.numel(), torch.float32)
+                    Cn.bn_apply32(y, bn.coef, None, None, a, c.cout, 0, True)
+                    rec["as"].append(a)
+                    cur = a
+                h, w = P, Q
+            cl, bnl = b["convs"][-1], b["bns"][-1]
+            out = self._buf(("out", bi), N * h * w * cl.cout, torch.float32)
+            if b["ds_conv"] is not None:
+                dc, dbn = b["ds_conv"], b["ds_bn"]
+                yd = self._buf(("yd", bi), N * h * w * dc.cout, torch.float32)
+                _, _, sp = self._conv_fwd(dc, x, N, Hc, Wc, yd, train)
+                if train:
+                    self.bn_train_finalize(dbn, sp, 0, N * h * w, yd)
+                else:
+                    self.bn_eval(dbn)
+                Cn.bn_apply32(rec["ys"][-1], bnl.coef, yd, dbn.coef, out, cl.cout, 2, True)
+                rec["yd"] = yd
+            else:
+                Cn.bn_apply32(rec["ys"][-1], bnl.coef, x, None, out, cl.cout, 1, True)
+            rec["out"] = out
+            recs.append(rec)
+            x, Hc, Wc, Cc = out, h, w, cl.cout
+        feat = self._buf("feat", N * self.feat, torch.float32)
+        Cn.avgpool32_fwd(x, feat, N, Hc * Wc, Cc, self.feat)
+        logits = self._buf("logits32", N * self.ncls_pad, torch.float32)
+        wfc = self.derived[self.fc_w_off:self.fc_w_off + self.ncls_pad * self.feat]
+        Cn.conv32_fwd(feat, wfc, logits, None, None, N, 1, 1, self.feat, self.ncls_pad, 1, 1, 1, 1, 1, 0, 128, 128)
+        saved.update(blocks=recs, feat=feat, logits=logits, Hc=Hc, Wc=Wc, Cc=Cc)
+        return saved
+
+    def _loss(self, saved, target, dlogits, loss_scale, grad_div):
+        N = saved["N"]
+        out = torch.empty(N, self.ncls, dtype=torch.float32, device=self.device)
+        rl = self._buf("row_loss", N, torch.float32)
+        rc = self._buf("row_correct", N, torch.float32)
+        self.C.xent32(saved["logits"], self.ncls_pad, self._p(self.fcb_slot), target, N, self.ncls, out, dlogits,
+                      loss_scale, float(grad_div), rl, rc)
+        met = torch.empty(2, dtype=torch.float32, device=self.device)
+        self.C.metrics(rl, rc, N, met)
+        return out, met
+
+    @torch.no_grad()
+    def train_step(self, images, target, loss_scale: Optional[torch.Tensor] = None, grad_div: Optional[float] = None):
+        saved = self._forward(images, train=True)
+        N = saved["N"]
+        dlog = self._buf("dlogits32", N * self.ncls_pad, torch.float32)
+        logits, met = self._loss(saved, target, dlog, loss_scale, grad_div or N)
+        self._backward(saved, dlog)
+        return logits, met
+
+    # ------------------------------------------------------------------------------------------ backward
+    def _backward(self, saved, dlog):
+        Cn = self.C
+        N = saved["N"]
+        Cn.colsum32(dlog, N, self.ncls_pad, self.ncls, self._g(self.fcb_slot), 1.0)
+        self.grad_ready(self.fcb_slot.index)
+        self._wgrad(self.ncls_pad, saved["feat"], dlog, N, 1, 1, self.feat, 1, 1, 1, 1, 1, 0, self._g(self.fc_slot),
+                    self.feat, rows=self.ncls, cols=self.feat)
+        self.grad_ready(self.fc_slot.index)
+        dfeat = self._buf("dfeat", N * self.feat, torch.float32)
+        wt = self.derived[self.fc_wt_off:self.fc_wt_off + self.ncls_pad * self.feat]
+        Cn.conv32_fwd(dlog, wt, dfeat, None, None, N, 1, 1, self.ncls_pad, self.feat, 1, 1, 1, 1, 1, 0, 128,
+                      self._bn_tile(self.feat))
+        Hc, Wc, Cc = saved["Hc"], saved["Wc"], saved["Cc"]
+        g = self._buf("g_a", N * Hc * Wc * Cc, torch.float32)
+        Cn.avgpool32_bwd(dfeat, g, N, Hc * Wc, Cc, self.feat)
+        gsel = 0
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b, rec = self.blocks[bi], saved["blocks"][bi]
+            convs, bns = b["convs"], b["bns"]
+            h_last, w_last = rec["hw"][-1][2], rec["hw"][-1][3]
+            x, Hin, Win, Cin = rec["x"], rec["H"], rec["W"], rec["C"]
+            ds = b["ds_conv"] is not None
+            dsbn = b["ds_bn"] if ds else None
+            # block output: dz = g * relu'(out); BN backward of the last BN (+ the downsample BN sharing dz)
+            self.bn_reduce(bns[-1], g, rec["out"], rec["ys"][-1], N * h_last * w_last, dsbn,
+                           rec["yd"] if ds else None)
+            dy = self._buf(("dy", 0), rec["ys"][-1].numel(), torch.float32)
+            gnext = self._buf("g_b" if gsel == 0 else "g_a", N * Hin * Win * Cin, torch.float32)
+            if ds:
+                dyd = self._buf("dyd", rec["yd"].numel(), torch.float32)
+                Cn.bn_bwd_apply32(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy, rec["yd"], dsbn.bcoef, dyd, None,
+                                  convs[-1].cout)
+                dc = b["ds_conv"]
+                P, Q = dc.out_hw(Hin, Win)
+                self._wgrad(dc.cout, x, dyd, N, Hin, Win, Cin, dc.R, dc.S, P, Q, dc.st, dc.pad, self._g(dc.slot),
+                            dc.R * dc.S * Cin)
+                self.grad_ready(dc.pid)
+                self._dgrad(dc, dyd, N, Hin, Win, P, Q, gnext)
+                res = gnext
+            else:
+                dz = self._buf("dz_id", g.numel(), torch.float32)
+                Cn.bn_bwd_apply32(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy, None, None, None, dz,
+                                  convs[-1].cout)
+                res = dz
+            for ci in range(len(convs) - 1, -1, -1):
+                c = convs[ci]
+                h, w, P, Q = rec["hw"][ci]
+                xin = rec["as"][ci - 1] if ci > 0 else x
+                self._wgrad(c.cout, xin, dy, N, h, w, c.cin, c.R, c.S, P, Q, c.st, c.pad, self._g(c.slot),
+                            c.R * c.S * c.cin)
+                self.grad_ready(c.pid)
+                if ci > 0:
+                    da = self._buf("da", N * h * w * c.cin, torch.float32)
+                    self._dgrad(c, dy, N, h, w, P, Q, da)
+                    bnp, yp, ap = bns[ci - 1], rec["ys"][ci - 1], rec["as"][ci - 1]
+                    self.bn_reduce(bnp, da, ap, yp, N * h * w)
+                    dyp = self._buf(("dy", (len(convs) - ci) % 2 + 1), yp.numel(), torch.float32)
+                    Cn.bn_bwd_apply32(da, ap, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
+                    dy = dyp
+                else:
+                    self._dgrad(c, dy, N, h, w, P, Q, gnext, res=res)
+            g = gnext
+            gsel ^= 1
+        # stem: max-pool backward + ReLU mask (from the BN input) -> BN backward -> im2col weight gradient
+        st, sbn = self.stem, self.stem_bn
+        P0, Q0, H, W = saved["P0"], saved["Q0"], saved["H"], saved["W"]
+        dz0 = self._buf("dz0", saved["y0"].numel(), torch.float32)
+        Cn.maxpool_bwd_relu32(g, saved["idx"], saved["y0"], sbn.coef, dz0, N, P0, Q0, st.cout)
+        self.bn_reduce(sbn, dz0, None, saved["y0"], N * P0 * Q0)
+        dy0 = dz0  # in place: each element read then written by the same thread
+        Cn.bn_bwd_apply32(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
+        tmp = self._buf("stem_dw", st.cout * STEM_K, torch.float32)
+        ch = self._stem_chunk(N)
+        for i, n0 in enumerate(range(0, N, ch)):
+            n1 = min(N, n0 + ch)
+            cols = self._buf("stem_cols", (n1 - n0) * P0 * Q0 * STEM_K, torch.float32)
+            Cn.im2col32(saved["x32"][n0:n1], cols, n1 - n0, 3, H, W, st.R, st.S, st.st, st.pad, STEM_K)
+            npix = (n1 - n0) * P0 * Q0
+            self._wgrad(st.cout, cols, dy0[n0 * P0 * Q0 * st.cout:n1 * P0 * Q0 * st.cout], npix, 1, 1, STEM_K, 1, 1,
+                        1, 1, 1, 0, tmp, STEM_K, accumulate=i > 0)
+        Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
+        self.grad_ready(st.pid)

@@ -53,11 +53,15 @@ class NativeDataParallelTrainer:
         self.executors = []
         for m, d in zip(replicas, self.devices):
             with torch.cuda.device(d):
-                f = FlatParams(m, d, dtype)
+                f = FlatParams(m, d, dtype if dtype != torch.float32 else None)
                 b = FlatBuffers(m, d)
                 self.flats.append(f)
                 self.buffers.append(b)
-                self.executors.append(ResNetExecutor(m, f, d, dtype))
+                if dtype == torch.float32:  # the reference's dataparallel.py precision
+                    from ..models.executor32 import ResNetExecutor32
+                    self.executors.append(ResNetExecutor32(m, f, d))
+                else:
+                    self.executors.append(ResNetExecutor(m, f, d, dtype))
         self.model = model
         self.flat = self.flats[0]
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
@@ -81,7 +85,8 @@ class NativeDataParallelTrainer:
     def _replicate(self, derived: bool = True) -> None:
         if len(self.devices) == 1:
             return
-        self.group.broadcast([f.shadow for f in self.flats], 0)
+        # the compute copy: the 16-bit shadow, or the fp32 master itself on the fp32 path
+        self.group.broadcast([f.shadow if f.shadow is not None else f.data for f in self.flats], 0)
         if self.buffers[0].n_float:
             self.group.broadcast([b.fdata for b in self.buffers], 0)
         if derived:

@@ -71,6 +71,15 @@ for stage in "$@"; do
       timeout -k 10 600 python bench.py --steps 20 --warmup 5 --force-comm --sync-bn --dtype fp16 > gpurun_out/sb_sync16.log 2>&1; rc=$?
       for f in sb_plain sb_comm sb_sync sb_sync16; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log)"; done
       [ $rc -eq 0 ] || { tail -20 gpurun_out/sb_sync.log; exit $rc; } ;;
+    test32)
+      timeout -k 10 600 python -u -m pytest tests/test_fp32_gpu.py -v -x --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/pytest_32.log 2>&1; rc=$?
+      grep -E "PASSED|FAILED|ERROR|passed|failed|Error|assert" gpurun_out/pytest_32.log | tail -30
+      [ $rc -le 1 ] || { echo "pytest crashed rc=$rc"; tail -30 gpurun_out/pytest_32.log; exit $rc; } ;;
+    bench32)
+      timeout -k 10 900 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32.log 2>&1; rc=$?
+      grep metric gpurun_out/bench32.log
+      [ $rc -eq 0 ] || { tail -20 gpurun_out/bench32.log; echo "bench32 failed rc=$rc"; exit $rc; } ;;
     torch50)
       timeout -k 10 600 python tools/torch_baseline.py --arch resnet50 --dtype fp16 > gpurun_out/torch50.log 2>&1 || { tail gpurun_out/torch50.log; exit 1; }
       tail -2 gpurun_out/torch50.log ;;
