@@ -129,9 +129,12 @@ def test_executor32_train_step_matches_torch_fp32(arch, N, HW, chunk):
     loss.backward()
     out64 = ref64(x.double())
     F.cross_entropy(out64, t).backward()
-    # sensitivity floor: the fp64 gradients themselves under a 2e-5 relative input nudge (ReLU-mask flips of
-    # near-zero pre-activations move whole blocks' gradients by up to ~1 % at these batch sizes)
-    F.cross_entropy(ref64b(x.double() * (1 + 2e-5)), t).backward()
+    # sensitivity floor: the fp64 gradients themselves under a 1e-4 relative input nudge -- the size of fp32's
+    # own forward rounding at ResNet-50 depth (torch fp32 and ours both reach ~7e-5 vs fp64 at the last block,
+    # tools/diag_fp32.py); ReLU-mask flips of near-zero pre-activations move whole blocks' gradients by ~1 %
+    # (an additive random nudge: BatchNorm normalises a uniform input scaling away)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    F.cross_entropy(ref64b(x.double() + 1e-4 * torch.randn(x.shape, device=DEV, generator=g).double()), t).backward()
     assert _rel(logits, out64.detach()) <= 3 * _rel(out.detach(), out64.detach()) + 1e-5
     assert abs(met[0].item() - loss.item()) < 1e-3 * max(1.0, loss.item())
     bad = []

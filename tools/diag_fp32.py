@@ -28,7 +28,8 @@ for arch, N, HW in [(a.split(":")[0], int(a.split(":")[1]), int(a.split(":")[2])
 
 
 def intermediates(arch="resnet50", N=4, HW=64):
-    """Compare the fp32 executor's saved forward tensors of the last block with an fp64 torch forward."""
+    """Forward error progression (stem output and every block output) of the fp32 executor and of torch fp32,
+    both vs an fp64 torch forward of the same weights."""
     model, ref, flat, ex, x, t = _setup(arch, N, HW)
     ref64 = copy.deepcopy(ref).double()
     box = {}
@@ -36,26 +37,40 @@ def intermediates(arch="resnet50", N=4, HW=64):
 
     def keep(saved, dlog):
         box["saved"] = saved
-        box["dlog"] = dlog.clone()
         return orig(saved, dlog)
     ex._backward = keep
-    acts = {}
-    blk = ref64.layer4[-1]
-    hooks = [blk.register_forward_hook(lambda m, i, o: acts.__setitem__("out", o)),
-             blk.register_forward_hook(lambda m, i, o: acts.__setitem__("in", i[0])),
-             blk.bn3.register_forward_hook(lambda m, i, o: acts.__setitem__("y3", i[0])),
-             blk.bn2.register_forward_hook(lambda m, i, o: acts.__setitem__("y2", i[0]))]
+    a64, a32 = {}, {}
+
+    def hook(store, name):
+        return lambda m, i, o: store.__setitem__(name, o.detach())
+    hs = []
+    for store, net in ((a64, ref64), (a32, ref)):
+        hs.append(net.maxpool.register_forward_hook(hook(store, "x0")))
+        hs.append(net.conv1.register_forward_hook(hook(store, "y0")))
+        for li, layer in enumerate((net.layer1, net.layer2, net.layer3, net.layer4)):
+            for bi, blk in enumerate(layer):
+                hs.append(blk.register_forward_hook(hook(store, f"l{li + 1}.{bi}")))
     ex.train_step(x, t)
     torch.cuda.synchronize()
-    ref64(x.double())
-    rec = box["saved"]["blocks"][-1]
+    with torch.no_grad():
+        ref64(x.double())
+        ref(x)
+    sv = box["saved"]
     nhwc = lambda a: a.permute(0, 2, 3, 1).reshape(-1)
-    print("block in ", _rel(rec["x"], nhwc(acts["in"])))
-    print("y2       ", _rel(rec["ys"][1], nhwc(acts["y2"])))
-    print("y3       ", _rel(rec["ys"][2], nhwc(acts["y3"])))
-    print("out      ", _rel(rec["out"], nhwc(acts["out"])))
-    print("feat     ", _rel(box["saved"]["feat"], acts["out"].mean((2, 3)).reshape(-1)))
-    for h in hooks:
+    print(f"y0    ours {_rel(sv['y0'], nhwc(a64['y0'])):.2e}  torch32 {_rel(a32['y0'], a64['y0']):.2e}")
+    print(f"x0    ours {_rel(sv['x0'], nhwc(a64['x0'])):.2e}  torch32 {_rel(a32['x0'], a64['x0']):.2e}")
+    k = 0
+    for li, layer in enumerate((ref64.layer1, ref64.layer2, ref64.layer3, ref64.layer4)):
+        for bi in range(len(layer)):
+            nm = f"l{li + 1}.{bi}"
+            print(f"{nm:5s} ours {_rel(sv['blocks'][k]['out'], nhwc(a64[nm])):.2e}  torch32 {_rel(a32[nm], a64[nm]):.2e}")
+            k += 1
+    last = sv["blocks"][-1]["out"]
+    ref_out = nhwc(a64[f"l4.{len(ref64.layer4) - 1}"])
+    flips = ((last > 0) != (ref_out > 0)).nonzero().flatten()
+    print(f"last block ReLU-mask disagreements vs fp64: {flips.numel()} "
+          f"(values ours / fp64: {[(float(last[i]), float(ref_out[i])) for i in flips[:4]]})")
+    for h in hs:
         h.remove()
 
 

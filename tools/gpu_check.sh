@@ -81,10 +81,10 @@ for stage in "$@"; do
       grep metric gpurun_out/bench32.log
       [ $rc -eq 0 ] || { tail -20 gpurun_out/bench32.log; echo "bench32 failed rc=$rc"; exit $rc; } ;;
     torch50)
-      timeout -k 10 600 python tools/torch_baseline.py --arch resnet50 --dtype fp16 > gpurun_out/torch50.log 2>&1 || { tail gpurun_out/torch50.log; exit 1; }
+      timeout -k 10 900 python -u tools/torch_baseline.py --arch resnet50 --dtype fp16 > gpurun_out/torch50.log 2>&1 || { tail gpurun_out/torch50.log; exit 1; }
       tail -2 gpurun_out/torch50.log ;;
     torch18fp32)
-      timeout -k 10 600 python tools/torch_baseline.py --arch resnet18 --dtype fp32 > gpurun_out/torch18fp32.log 2>&1 || { tail gpurun_out/torch18fp32.log; exit 1; }
+      timeout -k 10 900 python -u tools/torch_baseline.py --arch resnet18 --dtype fp32 --steps 5 > gpurun_out/torch18fp32.log 2>&1 || { tail gpurun_out/torch18fp32.log; exit 1; }
       tail -2 gpurun_out/torch18fp32.log ;;
   esac
 done

@@ -13,9 +13,20 @@ p.add_argument("--arch", default="resnet18")
 p.add_argument("--bs", type=int, default=1200)
 p.add_argument("--steps", type=int, default=10)
 p.add_argument("--dtype", default="bf16")
+p.add_argument("--benchmark", type=int, default=1, help="cudnn.benchmark (MIOpen search) as the reference sets it")
 p.add_argument("--cl", type=int, default=1)
 a = p.parse_args()
-torch.backends.cudnn.benchmark = True
+torch.backends.cudnn.benchmark = bool(a.benchmark)
+import threading
+
+
+def _heartbeat():  # MIOpen's search can stay silent for minutes: keep the run visibly alive
+    while True:
+        time.sleep(30)
+        print("...", flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
 dev = torch.device("cuda:0")
 m = getattr(resnet, a.arch)().to(dev)
 if a.cl:
@@ -34,13 +45,17 @@ def step():
     opt.zero_grad(set_to_none=True)
     loss.backward()
     opt.step()
-for _ in range(3):
+for i in range(3):  # warm-up (MIOpen's benchmark-mode search happens here: print progress, it can be long)
+    t0 = time.time()
     step()
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    print(f"warm-up step {i}: {time.time() - t0:.1f} s", flush=True)
 t = time.time()
 for _ in range(a.steps):
     step()
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    print(".", end="", flush=True)
+print()
 el = (time.time() - t) / a.steps
 print(json.dumps({"arch": a.arch, "bs": a.bs, "dtype": a.dtype, "channels_last": a.cl, "ms_per_step": el * 1e3,
                   "img_per_s": a.bs / el, "max_mem_GB": torch.cuda.max_memory_allocated() / 1e9}))
