@@ -62,16 +62,27 @@ def resolution_kwargs(arch: str, size: int) -> dict:
     if arch.startswith("vit_"):
         return {"image_size": size}
     if arch == "maxvit_t":
-        g = size
-        for _ in range(5):
+        # stem (stride 2) then four stride-2 stages: the block / grid partition must tile EVERY stage's map
+        maps, g = [], size
+        for i in range(5):
             g = (g - 1) // 2 + 1
-        return {"input_size": (size, size), "partition_size": max(d for d in range(1, 8) if g % d == 0)}
+            if i >= 1:
+                maps.append(g)
+        fits = [d for d in range(2, 8) if all(m % d == 0 for m in maps)]
+        if not fits:
+            raise ValueError(f"maxvit_t: a {size}px crop gives stage maps {maps}; no partition size in 2..7 divides "
+                             f"them all (use a multiple of 32, e.g. 224)")
+        return {"input_size": (size, size), "partition_size": max(fits)}
     return {}
 
 
 def create(arch: str, pretrained: bool = False, pretrained_path: Optional[str] = None, **kwargs) -> torch.nn.Module:
     if arch not in _REGISTRY:
         raise KeyError(f"unknown arch {arch!r}; choices: {model_names()}")
+    if pretrained and (arch.startswith("vit_") or arch == "maxvit_t"):
+        # position tables / relative-position biases are sized for the 224 crop the torchvision weights use
+        if kwargs.get("image_size", 224) != 224 or tuple(kwargs.get("input_size", (224, 224))) != (224, 224):
+            raise ValueError(f"--pretrained {arch} weights are for 224x224 crops; got {kwargs}")
     model = _REGISTRY[arch](**kwargs)
     if pretrained:
         path = pretrained_path or os.path.join(os.environ.get("PDT_PRETRAINED_DIR", "pretrained"), f"{arch}.pth")

@@ -300,3 +300,13 @@ def test_maxvit_relative_attention_matches_explicit():
     a = torch.einsum("bghid,bghjd->bghij", q, k * D ** -0.5) + att.get_relative_positional_bias()
     ref = att.merge(torch.einsum("bghij,bghjd->bghid", a.softmax(-1), v).permute(0, 1, 3, 2, 4).reshape(2, 5, P, D))
     torch.testing.assert_close(att(x), ref, atol=1e-5, rtol=1e-4)
+
+
+def test_maxvit_resolution_checks():
+    from pytorch_distributed_template_amd.models import registry
+    assert registry.resolution_kwargs("maxvit_t", 224)["partition_size"] == 7
+    assert registry.resolution_kwargs("maxvit_t", 64)["partition_size"] == 2  # maps 16, 8, 4, 2
+    with pytest.raises(ValueError):
+        registry.resolution_kwargs("maxvit_t", 100)  # maps 25, 13, 7, 4: no common partition
+    with pytest.raises(ValueError):
+        registry.create("vit_b_32", pretrained=True, image_size=64)
