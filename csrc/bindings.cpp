@@ -337,7 +337,7 @@ void conv_wgrad_stem_fused(const Tensor& x, const Tensor& dp, const Tensor& idx,
                   idx.numel() == dp.numel() && coef.numel() >= 2 * 64 && bcoef.numel() >= 3 * 64,
               "conv_wgrad_stem_fused: size mismatch");
   TORCH_CHECK(Qm % 2 == 0, "conv_wgrad_stem_fused: the conv output width must be even (pixel pairs)");
-  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && y0.numel() < (int64_t(1) << 31),
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && N * Pm * Qm * 64 < (int64_t(1) << 31),
               "conv_wgrad_stem_fused: operands exceed 32-bit offsets");
   TORCH_CHECK(pairs == 4 && ldw >= 256 && ws.numel() >= splits * 64 * ldw, "conv_wgrad_stem_fused: needs 4 row pairs");
   TORCH_CHECK((Pm - 1) * stride + (pairs - 1) * dil + 1 < Hp && ((Qm - 1) * stride + 8) <= Wp,
@@ -653,6 +653,11 @@ void stem_pack_u8(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H,
                            pf(scale, "scale"), pf(shift, "shift"), cur_stream());
 }
 
+void bw_probe(int64_t mode, const Tensor& x, const Tensor& y, Tensor& out, int64_t blocks) {
+  TORCH_CHECK(x.numel() == y.numel() && out.numel() == x.numel() && x.numel() % 8 == 0, "bw_probe: sizes");
+  pdt::bw_probe_launch((int)mode, p16(x, "x"), p16(y, "y"), p16(out, "out"), x.numel(), (int)blocks, cur_stream());
+}
+
 void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
   check_dev(idx, "idx");
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == dst.numel(), "gather32: idx must be int32 like dst");
@@ -889,6 +894,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_pack", &stem_pack);
   m.def("stem_pack_u8", &stem_pack_u8);
   m.def("gather32", &gather32);
+  m.def("bw_probe", &bw_probe);
   m.def("conv32_fwd", &conv32_fwd);
   m.def("conv32_dgrad", &conv32_dgrad);
   m.def("wgrad32", &wgrad32);

@@ -40,6 +40,29 @@ template <> struct E16<kF16> {
 };
 
 
+// 16-byte streaming (nontemporal) global load / store for the elementwise passes: the activations they
+// touch are hundreds of MB and are not re-read from L2 before eviction (tools/bw_probe.py:
+// 5.0 TB/s for grid-stride cached loops vs 6.2-6.5 TB/s for one-vector-per-thread streaming grids).
+typedef uint32_t pdt_u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+PDT_DEVICE uint4 ld16(const void* p) {
+  if constexpr (NT) {
+    const pdt_u32x4 t = __builtin_nontemporal_load((const pdt_u32x4*)p);
+    return make_uint4(t[0], t[1], t[2], t[3]);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+PDT_DEVICE void st16(void* p, uint4 v) {
+  if constexpr (NT) {
+    const pdt_u32x4 t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, (pdt_u32x4*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+
 // Inclusive scan over each 16-lane DPP row (row_shr 1, 2, 4, 8 with zero fill): lane 15 of every row
 // ends with the sum of the row's 16 values.  Pure VALU (no LDS permute traffic).
 PDT_DEVICE float row16_sum(float v) {

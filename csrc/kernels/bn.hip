@@ -8,6 +8,7 @@
 //                    branches that share dz, e.g. the main and downsample branch of a residual block)
 //                    -> bn_slot_sum -> bn_bwd_finalize (dgamma/dbeta into the grad buffer,
 //                    per-channel coefficients) -> bn_bwd_apply (dy = a*dz + b*y + c per branch).
+#include <cstdlib>
 #include "../common.h"
 #include "bn.h"
 #include "conv_fwd.h"
@@ -190,17 +191,18 @@ void bn_eval_coef_launch(const float* gamma, const float* beta, const float* rm,
 // out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift.
 // WM: also write the ReLU bitmask (bit e of mask[v] = out[8v+e] > 0) that the backward reads instead of
 // re-reading the 16-bit block output (1 bit instead of 16 per element).
-template <int DT, int RESMODE, bool RELU, bool WM>
+template <int DT, int RESMODE, bool RELU, bool WM, bool NT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                        const uint16_t* __restrict__ res,
                                                        const float* __restrict__ rcoef, uint16_t* __restrict__ out,
                                                        uint8_t* __restrict__ mask, int64_t n8, int C) {
   using E = E16<DT>;
+  const bool cpow2 = (C & (C - 1)) == 0;
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)((v * 8) % C);
-    const uint4 yy = ((const uint4*)y)[v];
+    const int c0 = cpow2 ? (int)(v * 8) & (C - 1) : (int)((v * 8) % C);
+    const uint4 yy = ld16<NT>(y + v * 8);
     uint4 rr;
-    if constexpr (RESMODE != 0) rr = ((const uint4*)res)[v];
+    if constexpr (RESMODE != 0) rr = ld16<NT>(res + v * 8);
     const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
     uint32_t rw[4];
     if constexpr (RESMODE != 0) { rw[0] = rr.x; rw[1] = rr.y; rw[2] = rr.z; rw[3] = rr.w; }
@@ -222,15 +224,28 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       if constexpr (WM) bits |= ((ow[e] & 0x7fffu) != 0 && !(ow[e] & 0x8000u) ? 1u : 0u) << (2 * e) |
                                 ((ow[e] & 0x7fff0000u) != 0 && !(ow[e] & 0x80000000u) ? 1u : 0u) << (2 * e + 1);
     }
-    ((uint4*)out)[v] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    st16<NT>(out + v * 8, make_uint4(ow[0], ow[1], ow[2], ow[3]));
     if constexpr (WM) mask[v] = (uint8_t)bits;
   }
 }
 
+// Elementwise grids: one 16-byte vector per thread (a grid-stride loop only past 2^20 blocks) -- the
+// in-order block dispatch then keeps the concurrently streamed window contiguous; capping the grid at a
+// few thousand looping blocks cost ~20% of bandwidth (tools/bw_probe.py).  Streams larger than the L2s
+// and MALL use nontemporal loads/stores.  PDT_EW_CAP / PDT_EW_NT override both (A/B experiments).
+static int64_t env_i64(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoll(e) : dflt;
+}
 static int ew_blocks(int64_t n) {
+  static const int64_t cap = env_i64("PDT_EW_CAP", 1 << 20);
   int64_t b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
+  if (b > cap) b = cap;
   return (int)(b < 1 ? 1 : b);
+}
+static bool ew_nt(int64_t bytes) {
+  static const int64_t thr = env_i64("PDT_EW_NT", 64ll << 20);
+  return thr >= 0 && bytes >= thr;
 }
 
 template <int DT>
@@ -238,11 +253,14 @@ static void bn_apply_dt(const uint16_t* y, const float* coef, const uint16_t* re
                         uint8_t* mask, int64_t n, int C, int resmode, bool relu, hipStream_t s) {
   const int64_t n8 = n / 8;
   dim3 g(ew_blocks(n8)), b(256);
-  const bool wm = mask != nullptr;
-#define PDT_AP(RM, RL, WM)                                                                                  \
-  if (resmode == RM && relu == RL && wm == WM) {                                                            \
-    hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL, WM>), g, b, 0, s, y, coef, res, rcoef, out, mask, n8, C); \
-    return;                                                                                                 \
+  const bool wm = mask != nullptr, nt = ew_nt(n * 2);
+#define PDT_AP(RM, RL, WM)                                                                                       \
+  if (resmode == RM && relu == RL && wm == WM) {                                                                 \
+    if (nt)                                                                                                      \
+      hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL, WM, true>), g, b, 0, s, y, coef, res, rcoef, out, mask, n8, C); \
+    else                                                                                                         \
+      hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL, WM, false>), g, b, 0, s, y, coef, res, rcoef, out, mask, n8, C); \
+    return;                                                                                                      \
   }
   PDT_AP(0, true, false) PDT_AP(1, true, false) PDT_AP(2, true, false) PDT_AP(0, false, false)
   PDT_AP(1, false, false) PDT_AP(2, false, false) PDT_AP(1, true, true) PDT_AP(2, true, true)
@@ -433,7 +451,7 @@ void bn_bwd_finalize_slots_launch(const double* slots, int K, double count, cons
 }
 
 // dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad)
-template <int DT, bool MASK, int NBR, bool WDZ>
+template <int DT, bool MASK, int NBR, bool WDZ, bool NT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ g,
                                                            const uint8_t* __restrict__ mask,
                                                            const uint16_t* __restrict__ y1,
@@ -442,16 +460,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            const float* __restrict__ b2, uint16_t* __restrict__ dy2,
                                                            uint16_t* __restrict__ dz_out, int64_t n8, int C) {
   using E = E16<DT>;
+  const bool cpow2 = (C & (C - 1)) == 0;
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)((v * 8) % C);
-    const uint4 gv = ((const uint4*)g)[v];
+    const int c0 = cpow2 ? (int)(v * 8) & (C - 1) : (int)((v * 8) % C);
+    const uint4 gv = ld16<NT>(g + v * 8);
     const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
     uint32_t mb = 0xffu;
     if constexpr (MASK) mb = mask[v];
-    const uint4 y1v = ((const uint4*)y1)[v];
+    const uint4 y1v = ld16<NT>(y1 + v * 8);
     const uint32_t y1w[4] = {y1v.x, y1v.y, y1v.z, y1v.w};
     uint32_t y2w[4] = {0, 0, 0, 0};
-    if constexpr (NBR == 2) { const uint4 y2v = ((const uint4*)y2)[v]; y2w[0] = y2v.x; y2w[1] = y2v.y; y2w[2] = y2v.z; y2w[3] = y2v.w; }
+    if constexpr (NBR == 2) { const uint4 y2v = ld16<NT>(y2 + v * 8); y2w[0] = y2v.x; y2w[1] = y2v.y; y2w[2] = y2v.z; y2w[3] = y2v.w; }
     uint32_t o1[4], o2[4], oz[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -470,9 +489,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
       if constexpr (NBR == 2) o2[e] = (uint32_t)r2[0] | ((uint32_t)r2[1] << 16);
       oz[e] = (uint32_t)rz[0] | ((uint32_t)rz[1] << 16);
     }
-    ((uint4*)dy1)[v] = make_uint4(o1[0], o1[1], o1[2], o1[3]);
-    if constexpr (NBR == 2) ((uint4*)dy2)[v] = make_uint4(o2[0], o2[1], o2[2], o2[3]);
-    if constexpr (WDZ) ((uint4*)dz_out)[v] = make_uint4(oz[0], oz[1], oz[2], oz[3]);
+    st16<NT>(dy1 + v * 8, make_uint4(o1[0], o1[1], o1[2], o1[3]));
+    if constexpr (NBR == 2) st16<NT>(dy2 + v * 8, make_uint4(o2[0], o2[1], o2[2], o2[3]));
+    if constexpr (WDZ) st16<NT>(dz_out + v * 8, make_uint4(oz[0], oz[1], oz[2], oz[3]));
   }
 }
 
@@ -481,13 +500,17 @@ void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint8_t* out, const
                          int C, hipStream_t s) {
   const int64_t n8 = n / 8;
   dim3 gr(ew_blocks(n8)), bl(256);
-  const bool mask = out != nullptr, wdz = dz_out != nullptr;
+  const bool mask = out != nullptr, wdz = dz_out != nullptr, nt = ew_nt(n * 2);
   const int nbr = y2 ? 2 : 1;
-#define PDT_BA(DT_, M_, NB_, WZ_)                                                                     \
-  if (mask == M_ && nbr == NB_ && wdz == WZ_) {                                                       \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<DT_, M_, NB_, WZ_>), gr, bl, 0, s, g, out, y1, b1, dy1, y2, b2, \
-                       dy2, dz_out, n8, C);                                                           \
-    return;                                                                                           \
+#define PDT_BA(DT_, M_, NB_, WZ_)                                                                           \
+  if (mask == M_ && nbr == NB_ && wdz == WZ_) {                                                             \
+    if (nt)                                                                                                 \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<DT_, M_, NB_, WZ_, true>), gr, bl, 0, s, g, out, y1, b1, dy1, \
+                         y2, b2, dy2, dz_out, n8, C);                                                       \
+    else                                                                                                    \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<DT_, M_, NB_, WZ_, false>), gr, bl, 0, s, g, out, y1, b1, dy1, \
+                         y2, b2, dy2, dz_out, n8, C);                                                       \
+    return;                                                                                                 \
   }
   if (dtype == kBF16) {
     PDT_BA(kBF16, true, 1, false) PDT_BA(kBF16, true, 1, true) PDT_BA(kBF16, true, 2, false)

@@ -240,3 +240,71 @@ void gather32_launch(const float* src, const int* idx, float* dst, int64_t n, hi
 }
 
 }  // namespace pdt
+
+namespace pdt {
+// ---------------------------------------------------------------------------------------------------------
+// Streaming-bandwidth probe (tools/bw_probe.py): out = 0.5 * x + y over n 16-bit elements (6 B per element,
+// the shape of the BN apply / backward-apply passes), in variants of bytes in flight per thread, grid size
+// and cache policy, to pick the structure of the elementwise kernels.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int U, bool NT_LD, bool NT_ST>
+__global__ __launch_bounds__(256) void bw_probe_kernel(const uint4* __restrict__ x, const uint4* __restrict__ y,
+                                                       uint4* __restrict__ out, int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x; v0 < n8; v0 += stride * U) {
+    uint4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * stride;
+      if (v < n8) {
+        if constexpr (NT_LD) {
+          const u32x4 ta = __builtin_nontemporal_load((const u32x4*)(x + v));
+          const u32x4 tb = __builtin_nontemporal_load((const u32x4*)(y + v));
+          a[u] = make_uint4(ta[0], ta[1], ta[2], ta[3]);
+          b[u] = make_uint4(tb[0], tb[1], tb[2], tb[3]);
+        } else {
+          a[u] = x[v];
+          b[u] = y[v];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * stride;
+      if (v >= n8) continue;
+      const uint32_t aw[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, bw[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float l = 0.5f * __uint_as_float(aw[e] << 16) + __uint_as_float(bw[e] << 16);
+        const float h = 0.5f * __uint_as_float(aw[e] & 0xffff0000u) + __uint_as_float(bw[e] & 0xffff0000u);
+        o[e] = (uint32_t)E16<kBF16>::from_f(l) | ((uint32_t)E16<kBF16>::from_f(h) << 16);
+      }
+      if constexpr (NT_ST) {
+        const u32x4 r = {o[0], o[1], o[2], o[3]};
+        __builtin_nontemporal_store(r, (u32x4*)(out + v));
+      } else {
+        out[v] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+}
+
+void bw_probe_launch(int mode, const uint16_t* x, const uint16_t* y, uint16_t* out, int64_t n, int blocks,
+                     hipStream_t s) {
+  const int64_t n8 = n / 8;
+  const uint4 *a = (const uint4*)x, *b = (const uint4*)y;
+  uint4* o = (uint4*)out;
+  dim3 g(blocks), bl(256);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((bw_probe_kernel<1, false, false>), g, bl, 0, s, a, b, o, n8); break;
+    case 1: hipLaunchKernelGGL((bw_probe_kernel<2, false, false>), g, bl, 0, s, a, b, o, n8); break;
+    case 2: hipLaunchKernelGGL((bw_probe_kernel<4, false, false>), g, bl, 0, s, a, b, o, n8); break;
+    case 3: hipLaunchKernelGGL((bw_probe_kernel<2, true, true>), g, bl, 0, s, a, b, o, n8); break;
+    case 4: hipLaunchKernelGGL((bw_probe_kernel<2, false, true>), g, bl, 0, s, a, b, o, n8); break;
+    case 5: hipLaunchKernelGGL((bw_probe_kernel<1, false, true>), g, bl, 0, s, a, b, o, n8); break;
+    case 6: hipLaunchKernelGGL((bw_probe_kernel<4, false, true>), g, bl, 0, s, a, b, o, n8); break;
+    default: hipLaunchKernelGGL((bw_probe_kernel<1, true, true>), g, bl, 0, s, a, b, o, n8); break;
+  }
+}
+}  // namespace pdt

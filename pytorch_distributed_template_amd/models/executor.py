@@ -265,9 +265,12 @@ class ResNetExecutor:
         with torch.cuda.stream(self.side):
             self._user_grad_ready(pid)
 
-    def _side_wgrad(self, reads: torch.Tensor, fn) -> None:
+    def _stem_fused_ok(self, Q0: int) -> bool:
+        return self.stem_fused and self.stem_pairs == 4 and Q0 % 2 == 0
+
+    def _side_wgrad(self, reads, fn) -> None:
         """Run ``fn`` (a weight gradient + its grad_ready) on the side stream behind the main stream's work
-        so far; later main-stream writes to ``reads`` wait for it."""
+        so far; later main-stream writes to ``reads`` (a tensor or a tuple of them) wait for it."""
         if self.side is None:
             fn()
             return
@@ -280,8 +283,9 @@ class ResNetExecutor:
                 self._on_side = False
             ev = torch.cuda.Event()
             ev.record(self.side)
-        reads.record_stream(self.side)  # the allocator must not recycle it before the side stream read it
-        self._pending_reads[reads.data_ptr()] = ev
+        for r in reads if isinstance(reads, tuple) else (reads,):
+            r.record_stream(self.side)  # the allocator must not recycle it before the side stream read it
+            self._pending_reads[r.data_ptr()] = ev
 
     def _join_side(self) -> None:
         if self.side is not None:
@@ -708,7 +712,7 @@ class ResNetExecutor:
         Cn.stem_pool_bwd_reduce_out(g, saved["x0"], sbn.coef, slots, N, P0, Q0, st.cout)
         self._bn_bwd_finish(slots, N * P0 * Q0, sbn)
         ldw = self.stem_pairs * 64
-        if self.stem_fused and self.stem_pairs == 4 and Q0 % 2 == 0:
+        if self._stem_fused_ok(Q0):
             # the stem weight gradient computes its dY tiles itself (max-pool backward + ReLU + BN-backward
             # apply from g / argmax / y0): the 112x112 dY is never written or re-read
             def stem_wg():

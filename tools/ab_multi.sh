@@ -7,7 +7,7 @@ for r in 1 2; do
   i=0
   for B in "$@"; do
     i=$((i+1))
-    timeout -k 10 300 env $B python bench.py --steps $K --warmup 5 ${AB_ARGS:-} > gpurun_out/ab_$r_$i.log 2>&1 || { echo "arm [$B] failed"; tail -5 gpurun_out/ab_$r_$i.log; exit 1; }
-    echo "round $r [$B] $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$r_$i.log)"
+    timeout -k 10 300 env $B python bench.py --steps $K --warmup 5 ${AB_ARGS:-} > gpurun_out/ab_${r}_${i}.log 2>&1 || { echo "arm [$B] failed"; tail -5 gpurun_out/ab_${r}_${i}.log; exit 1; }
+    echo "round $r [$B] $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${r}_${i}.log)"
   done
 done
