@@ -96,10 +96,15 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
   // one per (pixel fragment, channel fragment) -- the stores could alias the operands as far as the
   // compiler knows, so it would not hoist them itself.  Out-of-range pixels (M tail) load from pixel 0.
   constexpr bool LY1 = EPI >= 2, LY2 = EPI == 4, LM = EPI == 3 || EPI == 4;
+  // ReLU bitmask: one 8-byte load per pixel and 64 channels (the wave's WN channels are whole 64-bit words);
+  // a byte load per fragment, shifted right away, made the compiler wait for each one as it was issued
+  static_assert(!LM || WN % 64 == 0, "bitmask epilogue needs 64-channel wave columns");
+  constexpr int MW = LM ? WN / 64 : 1;
   // registers per pixel fragment of hoisted operands; chunk size keeps them within the budget left
-  // beside the accumulators (FN*FM*4) so no variant spills or loses occupancy
-  constexpr int PER_J = FN * (2 * (RES != 0) + 2 * LY1 + 2 * LY2 + LM);
-  constexpr int BUDGET = FN * FM * 4 >= 128 ? 64 : 96;
+  // beside the accumulators (FN*FM*4) and the statistics accumulators (beyond two per channel: EPI 4
+  // keeps three) so no variant spills or loses occupancy
+  constexpr int PER_J = FN * (2 * (RES != 0) + 2 * LY1 + 2 * LY2) + (LM ? 2 * MW : 0);
+  constexpr int BUDGET = (FN * FM * 4 >= 128 ? 64 : 96) - (KS > 2 ? FN * 4 * (KS - 2) * 2 : 0);
   constexpr int JC = PER_J == 0 ? FM
                      : (8 * PER_J <= BUDGET && FM % 8 == 0) ? 8
                      : (4 * PER_J <= BUDGET && FM % 4 == 0) ? 4
@@ -132,9 +137,9 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
       if constexpr (RC) rbase[jj] = (uint32_t)mm * (uint32_t)a.Kout;
     }
     uint2 p_res[RES ? JC : 1][RES ? FN : 1], p_y1[LY1 ? JC : 1][LY1 ? FN : 1], p_y2[LY2 ? JC : 1][LY2 ? FN : 1];
-    uint32_t p_m[LM ? JC : 1][LM ? FN : 1];
+    uint64_t p_m[LM ? JC : 1][MW];
 #pragma unroll
-    for (int jj = 0; jj < JC; ++jj)
+    for (int jj = 0; jj < JC; ++jj) {
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int64_t o = obase[jj] + n0 + wn * WN + i * 16 + 4 * fq;
@@ -142,8 +147,13 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
         if constexpr (RC) p_res[jj][i] = *(const uint2*)(a.res + rbase[jj] + (uint32_t)(n0 + wn * WN + i * 16 + 4 * fq));
         if constexpr (LY1) p_y1[jj][i] = *(const uint2*)(a.bn_y1 + o);
         if constexpr (LY2) p_y2[jj][i] = *(const uint2*)(a.bn_y2 + o);
-        if constexpr (LM) p_m[jj][i] = (uint32_t)a.bn_mask[o >> 3] >> ((int)o & 4);
       }
+      if constexpr (LM) {
+#pragma unroll
+        for (int g = 0; g < MW; ++g)
+          p_m[jj][g] = *(const uint64_t*)(a.bn_mask + ((obase[jj] + n0 + wn * WN + g * 64) >> 3));
+      }
+    }
 #pragma unroll
     for (int jj = 0; jj < JC; ++jj) {
       if (!valid[jj]) continue;
@@ -176,7 +186,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint32_t mb = p_m[jj][i];
+            const uint32_t mb = (uint32_t)(p_m[jj][i >> 2] >> ((i & 3) * 16 + 4 * fq));
             if (!(mb & 1u)) v[0] = 0.f;
             if (!(mb & 2u)) v[1] = 0.f;
             if (!(mb & 4u)) v[2] = 0.f;
@@ -301,7 +311,10 @@ PDT_DEVICE void zero_stat_row(const ConvFwdArgs& a, int nthreads) {
 }
 
 template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, int RES, int STAGES, int NW>
-__global__ __launch_bounds__(NW * 64) void conv_fwd_kernel(ConvFwdArgs args) {
+// min 2 waves per SIMD where LDS allows two workgroups per CU: the BN-backward epilogue variants otherwise
+// took > 256 registers and ran one workgroup per CU (half the 2-stage kernel's latency hiding)
+__global__ __launch_bounds__(NW * 64, (STAGES * (BN + BM) * BK * 2 <= 81920 || NW == 8) ? 2 : 1)
+void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
     const int ph = blockIdx.y;

@@ -31,7 +31,7 @@ constexpr int kXP = kW + 2;                // halo row pitch (pixels)
 constexpr int kXRows = 6 * kXP;            // 348 halo pixels per tile
 constexpr int kStageB = kXRows * 128;      // 44544 B
 constexpr int kWB = 64 * 9 * 64 * 2;       // 73728 B of resident weights
-constexpr int kLds = kWB + 2 * kStageB;    // 162816 B (< 160 KiB)
+constexpr int kLds = kWB + 2 * kStageB;    // 162816 B, plus 1 KiB of BN coefficients = the whole 160 KiB
 constexpr int kGroups = 4 * kW / 16;       // 14 groups of 16 pixels per tile
 
 // Halo row swizzle: 16-B chunk p of LDS row R holds logical chunk p ^ (R & 7).  ds_read_b128 serves a
@@ -50,7 +50,7 @@ template <int DT, int EPI, bool RES>
 __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
-  __shared__ __attribute__((aligned(1024))) char smem[kLds];
+  __shared__ __attribute__((aligned(1024))) char smem[kLds + 1024];
   char* const wl = smem;
   char* const stage0 = smem + kWB;
 
@@ -119,29 +119,20 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
 
-  // per-lane BN coefficients of the fused BN-backward epilogues (this lane's 16 channels never change;
-  // loading them once also keeps them from being re-fetched after every store)
-  float4 k_sc[EPI == 2 ? 4 : 1], k_sh[EPI == 2 ? 4 : 1], k_mu[EPI >= 2 ? 4 : 1], k_is[EPI >= 2 ? 4 : 1];
-  if constexpr (EPI >= 2) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c0 = i * 16 + 4 * fq;
-      if constexpr (EPI == 2) {
-        k_sc[i] = *(const float4*)(a.bn_coef1 + c0);
-        k_sh[i] = *(const float4*)(a.bn_coef1 + 64 + c0);
-      }
-      k_mu[i] = *(const float4*)(a.bn_coef1 + 128 + c0);
-      k_is[i] = *(const float4*)(a.bn_coef1 + 192 + c0);
-    }
-  }
+  // BN coefficients of the fused BN-backward epilogues ([scale, shift, mean, invstd] x 64 channels) in the
+  // last KiB of LDS, read per channel fragment in the epilogue: held in registers across the MFMA loop they
+  // cost 32-64 VGPRs per lane, which this kernel (one wave per SIMD, 18 unrolled K-steps) does not have.
+  float* const cfl = (float*)(smem + kLds);
+  if constexpr (EPI >= 2) cfl[tid] = a.bn_coef1[tid];  // published by the first tile's barrier
+  auto coef = [&](int q, int i) { return *(const float4*)(cfl + q * 64 + i * 16 + 4 * fq); };
 
   int t = t_begin + lb;
   int buf = 0;
   // Stores this wave issued in the previous tile's epilogue: they are the only vector-memory operations
   // younger than the halo DMA of the tile about to be computed, and vmcnt retires in issue order, so
   // vmcnt(n_st) proves the DMA landed without also waiting out the store latency (vmcnt(0) here used to
-  // expose ~1-2 us of store drain per tile: one wave per SIMD, nothing else to cover it).  Full tiles
-  // only (exactly 4 stores per pixel group with any valid lane); otherwise n_st = 0 (wait for all).
+  // expose ~1-2 us of store drain per tile: one wave per SIMD, nothing else to cover it).  Every live
+  // pixel group issues exactly 4 stores (H % 4 == 0: no partial row tiles), so n_st = 4 * ng.
   int n_st = 0;
   if (t < t_end) stage_tile(t, 0);
   for (; t < t_end; t += per_x) {
@@ -162,22 +153,21 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
     // hides under the MFMA loop (one block per CU: nothing else would cover an exposed epilogue)
     const int n = t / TH, h0 = (t - n * TH) * 4;
     int64_t obase[4];
-    bool pvalid[4];
     uint2 pre_res[RES ? 4 : 1][RES ? 4 : 1], pre_y1[EPI >= 2 ? 4 : 1][EPI >= 2 ? 4 : 1];
-    uint32_t pre_m[EPI == 3 ? 4 : 1][EPI == 3 ? 4 : 1];
+    uint64_t pre_m[EPI == 3 ? 4 : 1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int px = (g0 + j) * 16 + pix_of_lane(fr);
+      // a 3-group wave's 4th group re-reads group 0 (unused): every wave issues the same loads, unconditionally
+      const int px = (g0 + (j < ng ? j : 0)) * 16 + pix_of_lane(fr);
       const int r = px / kW, w = px - (px / kW) * kW;
-      pvalid[j] = (j < ng) && (h0 + r < a.H);
       obase[j] = ((int64_t)(n * a.H + h0 + r) * kW + w) * 64;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c0 = i * 16 + 4 * fq;
-        if constexpr (RES) pre_res[j][i] = pvalid[j] ? *(const uint2*)(a.res + obase[j] + c0) : make_uint2(0, 0);
-        if constexpr (EPI >= 2) pre_y1[j][i] = pvalid[j] ? *(const uint2*)(a.bn_y1 + obase[j] + c0) : make_uint2(0, 0);
-        if constexpr (EPI == 3) pre_m[j][i] = pvalid[j] ? (uint32_t)a.bn_mask[(obase[j] + c0) >> 3] >> (c0 & 4) : 0u;
+        if constexpr (RES) pre_res[j][i] = *(const uint2*)(a.res + obase[j] + c0);
+        if constexpr (EPI >= 2) pre_y1[j][i] = *(const uint2*)(a.bn_y1 + obase[j] + c0);
       }
+      if constexpr (EPI == 3) pre_m[j] = *(const uint64_t*)(a.bn_mask + (obase[j] >> 3));
     }
 
     f32x4_t acc[4][4];
@@ -229,13 +219,13 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
       run(std::integral_constant<int, 3>{});
 
     // ---- epilogue: lane holds couts n = i*16 + 4*fq + r of pixel (g0+j)*16 + fr ----
-    n_st = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) n_st += __builtin_amdgcn_ballot_w64(pvalid[j]) != 0 ? 4 : 0;
-    if (n_st != 4 * ng) n_st = 0;  // partial tile: no counted wait next time
+    // H % 4 == 0 (conv_l1_eligible): every pixel of a live group is in range, so the epilogue is straight-line
+    // code -- a branch around the stores would leave the waitcnt pass unsure how many were issued, and it
+    // then waited vmcnt(0) (the previous group's store latency) in front of every group.
+    n_st = 4 * ng;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (!pvalid[j]) continue;
+      if (j >= ng) break;  // wave-uniform
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c0 = i * 16 + 4 * fq;
@@ -253,13 +243,13 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
           y1[0] = E::to_f((uint16_t)(q1.x & 0xffff)); y1[1] = E::to_f((uint16_t)(q1.x >> 16));
           y1[2] = E::to_f((uint16_t)(q1.y & 0xffff)); y1[3] = E::to_f((uint16_t)(q1.y >> 16));
           if constexpr (EPI == 2) {
-            const float4 sc = k_sc[i], sh = k_sh[i];
+            const float4 sc = coef(0, i), sh = coef(1, i);
             if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
             if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint32_t mb = pre_m[j][i];
+            const uint32_t mb = (uint32_t)(pre_m[j] >> c0);
             if (!(mb & 1u)) v[0] = 0.f;
             if (!(mb & 2u)) v[1] = 0.f;
             if (!(mb & 4u)) v[2] = 0.f;
@@ -281,7 +271,7 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
             sacc[i][r2][1] += q * q;
           }
         } else if constexpr (EPI >= 2) {
-          const float4 mu = k_mu[i], is = k_is[i];
+          const float4 mu = coef(2, i), is = coef(3, i);
           const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
 #pragma unroll
           for (int r2 = 0; r2 < 4; ++r2) {
@@ -323,7 +313,8 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
 }
 
 bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
-  if (a.C != 64 || a.Kout != 64 || a.cs != 64 || a.W != kW || a.OW != kW || a.bnb == 3) return false;
+  // H % 4 == 0: whole 4-row tiles only (the epilogue has no per-pixel range checks; see conv_l1_kernel)
+  if (a.C != 64 || a.Kout != 64 || a.cs != 64 || a.W != kW || a.OW != kW || a.bnb == 3 || a.H % 4 != 0) return false;
   if (a.nphase == 0) {
     if (a.T == 3 && a.U == 3 && a.ist_h == 1 && a.ist_w == 1 && a.ioff_h == -1 && a.ioff_w == -1 &&
         a.tstep_h == 1 && a.tstep_w == 1 && a.ost_h == 1 && a.ost_w == 1 && a.ooff_h == 0 && a.ooff_w == 0 &&

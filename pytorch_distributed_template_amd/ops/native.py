@@ -7,6 +7,7 @@ a GPU code path that needs a kernel raises if the extension cannot be loaded.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -27,6 +28,12 @@ def load(build: bool = True):
             return _mod
         import torch  # noqa: F401  (loads libtorch / the HIP runtime the extension links against)
 
+        alt = os.environ.get("PDT_NATIVE_SO")  # A/B runs: load another build of the extension
+        if alt:
+            spec = importlib.util.spec_from_file_location("pytorch_distributed_template_amd._C", alt)
+            _mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+            return _mod
         if build and (not os.path.exists(_so_path()) or os.environ.get("PDT_AUTOBUILD", "0") == "1"):
             from . import _build
             _build.build()

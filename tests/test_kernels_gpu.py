@@ -27,7 +27,8 @@ CONV_CASES = [
     (3, 14, 14, 64, 128, 1, 2, 0),  # one K-step strided 1x1
     (1, 9, 9, 128, 128, 3, 1, 1),
     (2, 8, 8, 512, 512, 3, 1, 1),
-    (2, 9, 56, 64, 64, 3, 1, 1),   # ResNet layer1 geometry -> halo-reuse kernel (conv_l1.hip), partial row tile
+    (2, 8, 56, 64, 64, 3, 1, 1),   # ResNet layer1 geometry -> halo-reuse kernel (conv_l1.hip)
+    (2, 9, 56, 64, 64, 3, 1, 1),   # layer1 geometry with H % 4 != 0 -> generic kernel (conv_l1 takes whole row tiles)
 ]
 
 
@@ -371,7 +372,8 @@ def test_stem_kernel_persistent_tiles():
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 1, 1), (2, 15, 13, 128, 128, 3, 2, 1), (3, 14, 14, 256, 128, 1, 2, 0),
-                                  (3, 10, 56, 64, 64, 3, 1, 1), (2, 10, 10, 256, 64, 1, 1, 0)])
+                                  (3, 10, 56, 64, 64, 3, 1, 1), (3, 12, 56, 64, 64, 3, 1, 1),
+                                  (2, 10, 10, 256, 64, 1, 1, 0)])
 def test_conv_dgrad_fused_bn_backward(case, mode):
     """dgrad epilogue with the consumer BN's backward reduce (ReLU mask + sum dz, sum dz*xhat) vs torch."""
     from pytorch_distributed_template_amd.ops import conv, native
