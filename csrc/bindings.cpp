@@ -22,6 +22,7 @@
 #include "dtypes.h"
 #include "kernels/bn.h"
 #include "kernels/conv_fwd.h"
+#include "kernels/conv_l1.h"
 #include "kernels/conv_wgrad.h"
 #include "kernels/fp32.h"
 #include "kernels/loss.h"
@@ -167,6 +168,41 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   TORCH_CHECK(M < (int64_t(1) << 31), "conv_fwd: N*Pm*Qm must be < 2^31 (32-bit pixel indexing)");
   a.M = M;
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+}
+
+// ResNet layer1 3x3/s1/p1 64 -> 64 forward over the RAW output z of the block's first conv, with that conv's
+// BatchNorm + ReLU (pre_coef = [scale(64) | shift(64) | ...]) applied inside the kernel to each staged input tile:
+// y = conv(relu(bn(z))) with BN statistics of y, and relu(bn(z)) never written.
+bool conv_fwd_pre_supported(int64_t N, int64_t H, int64_t W) {
+  pdt::ConvFwdArgs a{};
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = 64; a.Kout = 64; a.T = 3; a.U = 3; a.cs = 64;
+  a.Pm = (int)H; a.Qm = (int)W; a.ist_h = 1; a.ist_w = 1; a.ioff_h = -1; a.ioff_w = -1; a.tstep_h = 1;
+  a.tstep_w = 1; a.OH = (int)H; a.OW = (int)W; a.ost_h = 1; a.ost_w = 1;
+  int flip = 0;
+  return pdt::conv_l1_eligible(a, &flip);
+}
+
+void conv_fwd_pre(const Tensor& z, const Tensor& w, Tensor& y, const Tensor& stats, const Tensor& pre_coef, int64_t N,
+                  int64_t H, int64_t W) {
+  const int dt = dt16(z, "z");
+  TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv_fwd_pre: mixed dtypes");
+  TORCH_CHECK(conv_fwd_pre_supported(N, H, W), "conv_fwd_pre: needs the layer1 geometry (64 -> 64, W == 56, H % 4 == 0)");
+  TORCH_CHECK(z.numel() == N * H * W * 64 && y.numel() == z.numel() && w.numel() == 64 * 9 * 64,
+              "conv_fwd_pre: size mismatch");
+  TORCH_CHECK(z.numel() < (int64_t(1) << 30), "conv_fwd_pre: operands exceed 2 GiB (32-bit buffer offsets)");
+  TORCH_CHECK(stats.numel() >= pdt::kStatSlots * 64 * 2, "conv_fwd_pre: stats buffer too small");
+  TORCH_CHECK(pre_coef.numel() >= 128, "conv_fwd_pre: pre_coef needs scale[64] | shift[64]");
+  pdt::ConvFwdArgs a{};
+  a.x = p16(z, "z");
+  a.w = p16(w, "w");
+  a.y = p16(y, "y");
+  a.stats = pd(stats, "stats");
+  a.pre_coef = pf(pre_coef, "pre_coef");
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = 64; a.Kout = 64; a.T = 3; a.U = 3; a.cs = 64;
+  a.Pm = (int)H; a.Qm = (int)W; a.ist_h = 1; a.ist_w = 1; a.ioff_h = -1; a.ioff_w = -1; a.tstep_h = 1;
+  a.tstep_w = 1; a.OH = (int)H; a.OW = (int)W; a.ost_h = 1; a.ost_w = 1;
+  a.M = N * H * W;
+  pdt::conv_fwd_launch(a, dt, 256, 64, 64, cur_stream());
 }
 
 // ResNet stem forward (7x7/2, 3 -> 64) over the zero-padded NHWC4 image with window-row weights
@@ -370,7 +406,8 @@ bool wgrad_3x3c64_supported(int64_t C, int64_t Kout, int64_t T, int64_t U, int64
   return pdt::wgrad3x3_c64_supported((int)C, (int)Kout, (int)T, (int)U, (int)W, (int)stride, (int)pad, 0);
 }
 
-int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W) {
+int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W,
+                          const OptT& pre_coef) {
   const int dt = dt16(x, "x");
   TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad_3x3c64: mixed dtypes");
   TORCH_CHECK(pdt::wgrad3x3_c64_supported(64, 64, 3, 3, (int)W, 1, 1, 0), "conv_wgrad_3x3c64: needs W == 56");
@@ -383,6 +420,10 @@ int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t
   a.dy = p16(dy, "dy");
   a.ws = pf(ws, "ws");
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = 64; a.Kout = 64; a.T = 3; a.U = 3; a.ldw = 576;
+  if (pre_coef.has_value()) {
+    TORCH_CHECK(pre_coef->numel() >= 128, "conv_wgrad_3x3c64: pre_coef needs scale[64] | shift[64]");
+    a.pre_coef = pf(*pre_coef, "pre_coef");
+  }
   pdt::wgrad3x3_c64_launch(a, blocks, dt, cur_stream());
   return blocks;
 }
@@ -859,7 +900,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_reduce", &wgrad_reduce);
   m.def("wgrad_blocks_3x3c64", &wgrad_blocks_3x3c64);
   m.def("wgrad_3x3c64_supported", &wgrad_3x3c64_supported);
-  m.def("conv_wgrad_3x3c64", &conv_wgrad_3x3c64);
+  m.def("conv_wgrad_3x3c64", &conv_wgrad_3x3c64, py::arg("x"), py::arg("dy"), py::arg("ws"), py::arg("N"), py::arg("H"),
+        py::arg("W"), py::arg("pre_coef") = py::none());
+  m.def("conv_fwd_pre", &conv_fwd_pre);
+  m.def("conv_fwd_pre_supported", &conv_fwd_pre_supported);
   m.def("bn_slot_sum", &bn_slot_sum);
   m.def("stat_slots", &stat_slots);
   m.def("bn_finalize", &bn_finalize);

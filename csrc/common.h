@@ -40,6 +40,27 @@ template <> struct E16<kF16> {
 };
 
 
+// Producer BatchNorm + ReLU applied to a 16-byte chunk (8 channels) of an activation tile already staged in LDS
+// (the BN1 -> ReLU -> conv2 chain of a residual block without the materialised activation).
+// Bit-identical to bn_apply: the same fma(y, scale, shift) in fp32 and the same rounding; ReLU is taken on the
+// rounded 16-bit values (max as signed 16-bit integers against +0: every negative value, -0 included, has the
+// sign bit), which equals rounding after the fp32 max.
+typedef short pdt_s16x2 __attribute__((ext_vector_type(2)));
+template <int DT>
+PDT_DEVICE void pre_act_chunk(char* p, const float (&sc)[8], const float (&sh)[8]) {
+  using E = E16<DT>;
+  uint4 v = *(const uint4*)p;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float lo = E::to_f((uint16_t)(w[e] & 0xffff)) * sc[2 * e] + sh[2 * e];
+    const float hi = E::to_f((uint16_t)(w[e] >> 16)) * sc[2 * e + 1] + sh[2 * e + 1];
+    const uint32_t pk = (uint32_t)E::from_f(lo) | ((uint32_t)E::from_f(hi) << 16);
+    w[e] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(pdt_s16x2, pk), pdt_s16x2{0, 0}));
+  }
+  *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // 16-byte streaming (nontemporal) global load / store for the elementwise passes: the activations they
 // touch are hundreds of MB and are not re-read from L2 before eviction (tools/bw_probe.py:
 // 5.0 TB/s for grid-stride cached loops vs 6.2-6.5 TB/s for one-vector-per-thread streaming grids).

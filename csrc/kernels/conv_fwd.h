@@ -51,6 +51,9 @@ struct ConvFwdArgs {
   // a 3x3/2 dgrad and so is neither written nor read there).  -1: residual in dx's layout on every phase.
   int res_phase = -1;
   int stage_out = 0;  // epilogue writes the output tile through LDS as whole rows (set by the launcher)
+  // pre_coef != nullptr: x is the RAW output of a producer conv and the kernel applies that BatchNorm + ReLU
+  // (scale[C] | shift[C]) to the staged input tile itself (conv_l1 forward only; zero padding stays zero)
+  const float* pre_coef = nullptr;
   int pT[4], pU[4], pioff_h[4], pioff_w[4], pPm[4], pQm[4], pooff_h[4], pooff_w[4], pmt[4];
   int64_t pwoff[4];
   uint32_t ppq_mul[4], ppq_shift[4], pq1_mul[4], pq1_shift[4];

@@ -931,6 +931,9 @@ void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hi
     conv_l1_launch(a, flip, dtype, s);
     return;
   }
+  if (a.pre_coef)
+    pdt_hip_fail("conv_fwd: a fused producer BN (pre_coef) is only supported by the layer1 halo kernel",
+                 hipErrorInvalidValue, __FILE__, __LINE__);
   if (dtype == kBF16)
     launch_dt<kBF16>(a, bm, bn, bk, s);
   else

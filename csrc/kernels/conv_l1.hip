@@ -46,7 +46,9 @@ PDT_DEVICE int pix_of_lane(int fr) { return fr < 4 ? fr : (fr >= 12 ? fr - 8 : f
 PDT_DEVICE int wswz(int co, int c) { return (c & ~7) | ((c & 7) ^ ((co >> 1) & 7)); }  // weight chunk
 }  // namespace
 
-template <int DT, int EPI, bool RES>
+// PRE: the input is the raw output of the block's first conv; its BatchNorm + ReLU is applied to each staged
+// halo in LDS (one pass per tile, padding rows / columns left zero) instead of by a separate bn_apply pass.
+template <int DT, int EPI, bool RES, bool PRE = false>
 __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -126,6 +128,18 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
   if constexpr (EPI >= 2) cfl[tid] = a.bn_coef1[tid];  // published by the first tile's barrier
   auto coef = [&](int q, int i) { return *(const float4*)(cfl + q * 64 + i * 16 + 4 * fq); };
 
+  // PRE: thread tid transforms halo rows R = tid/8 + 32k at physical chunk tid%8, which always holds logical
+  // chunk (tid ^ (tid >> 3)) & 7 (the row swizzle is R & 7 and 32k keeps it): 8 fixed channels per thread
+  float pre_sc[8], pre_sh[8];
+  if constexpr (PRE) {
+    const int lc = (tid ^ (tid >> 3)) & 7;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pre_sc[e] = a.pre_coef[lc * 8 + e];
+      pre_sh[e] = a.pre_coef[64 + lc * 8 + e];
+    }
+  }
+
   int t = t_begin + lb;
   int buf = 0;
   // Stores this wave issued in the previous tile's epilogue: they are the only vector-memory operations
@@ -146,6 +160,21 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRE) {
+      const int n = t / TH, h0 = (t - n * TH) * 4;
+      char* sbw = stage0 + buf * kStageB;
+#pragma unroll
+      for (int k = 0; k < 11; ++k) {
+        const int R = (tid >> 3) + 32 * k;
+        const int hr = R / kXP, wc = R - (R / kXP) * kXP;
+        const int h = h0 - 1 + hr, w = wc - 1;
+        if (R < kXRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW)
+          pre_act_chunk<DT>(sbw + R * 128 + (tid & 7) * 16, pre_sc, pre_sh);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
     const char* sb = stage0 + buf * kStageB;
 
@@ -346,12 +375,18 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
   if (G > cap) G = cap;
   const bool rs = a.res != nullptr;
   const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
+  if (a.pre_coef && (epi != 1 || rs || flip))
+    pdt_hip_fail("conv_l1: the fused producer BN (pre_coef) needs a forward conv with statistics, no residual",
+                 hipErrorInvalidValue, __FILE__, __LINE__);
+  if (a.pre_coef) PDT_COUNT("conv_l1_fwd_fused_bn_relu");
   Scratch part(a.stats ? (size_t)G * 128 * sizeof(float) : 0, s);
   a.srows = part.as<float>();
 #define PDT_L1(DT_, E_, R_) hipLaunchKernelGGL((conv_l1_kernel<DT_, E_, R_>), dim3(G), dim3(256), 0, s, a, flip)
+#define PDT_L1P(DT_) hipLaunchKernelGGL((conv_l1_kernel<DT_, 1, false, true>), dim3(G), dim3(256), 0, s, a, flip)
 #define PDT_L1_DT(DT_)                                                                                 \
   if (epi == 0 && !rs) PDT_L1(DT_, 0, false);                                                          \
   else if (epi == 0 && rs) PDT_L1(DT_, 0, true);                                                       \
+  else if (epi == 1 && !rs && a.pre_coef) PDT_L1P(DT_);                                                 \
   else if (epi == 1 && !rs) PDT_L1(DT_, 1, false);                                                     \
   else if (epi == 2 && !rs) PDT_L1(DT_, 2, false);                                                     \
   else if (epi == 3 && rs) PDT_L1(DT_, 3, true);                                                       \
@@ -362,6 +397,7 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     PDT_L1_DT(kF16)
   }
 #undef PDT_L1_DT
+#undef PDT_L1P
 #undef PDT_L1
   if (a.stats) stat_rows_reduce_launch(a.srows, G, 128, a.stats, s);
 }

@@ -27,6 +27,9 @@ struct ConvWgradArgs {
   const float* f_coef = nullptr;
   const float* f_bcoef = nullptr;
   int f_OH = 0, f_OW = 0;
+  // layer1 3x3 kernel only: x is the RAW output of the producer conv; its BatchNorm + ReLU (scale[64] | shift[64])
+  // is applied to each staged input halo in LDS (see conv_l1.hip, PRE)
+  const float* pre_coef = nullptr;
 };
 
 int wgrad_tile(int C, int Kout, int win);  // 256 (ping-pong), 128 or 64

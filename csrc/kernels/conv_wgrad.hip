@@ -783,7 +783,9 @@ constexpr int kL1Stage = kL1XBytes + kL1YBytes;
 PDT_DEVICE int l1_swz(int row2d, int col) { return (((col >> 1) & 1) << 1) | ((row2d & 1) << 2); }
 }  // namespace
 
-template <int DT>
+// PRE: x is the raw output of the block's first conv; its BatchNorm + ReLU is applied to each staged X halo in
+// LDS (conv_l1.hip, PRE) -- the activation is never materialised.
+template <int DT, bool PRE = false>
 __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -851,12 +853,36 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
     return __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
+  // PRE: thread tid transforms logical chunk tid % 8 (8 fixed channels) of halo rows R = tid/8 + 32k; the
+  // physical chunk follows the row's swizzle, so each 8-thread group covers one whole 128-B row
+  float pre_sc[8], pre_sh[8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pre_sc[e] = a.pre_coef[(tid & 7) * 8 + e];
+      pre_sh[e] = a.pre_coef[64 + (tid & 7) * 8 + e];
+    }
+  }
+
   int t = t_begin + lb;
   int buf = 0;
   if (t < t_end) stage_tile(t, 0);
   for (; t < t_end; t += per_x) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (PRE) {
+      const int n = t / TH, h0 = (t - n * TH) * 4;
+      char* sxw = smem + buf * kL1Stage;
+#pragma unroll
+      for (int k = 0; k < 11; ++k) {
+        const int R = (tid >> 3) + 32 * k;
+        const int hr = R / kL1XP, wc = R - (R / kL1XP) * kL1XP;
+        const int h = h0 - 1 + hr, w = wc - 1;
+        if (R < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W)
+          pre_act_chunk<DT>(sxw + R * 128 + (((tid & 7) ^ l1_swz(hr, wc)) << 4), pre_sc, pre_sh);
+      }
+      __syncthreads();
+    }
     if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
     const char* sx = smem + buf * kL1Stage;
     const char* sy = sx + kL1XBytes;
@@ -916,10 +942,17 @@ int wgrad3x3_c64_blocks() {
 
 void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s) {
   PDT_COUNT("wgrad3x3_c64");
-  if (dtype == kBF16)
+  if (a.pre_coef) {
+    PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<kBF16, true>), dim3(blocks), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<kF16, true>), dim3(blocks), dim3(256), 0, s, a);
+  } else if (dtype == kBF16) {
     hipLaunchKernelGGL((wgrad3x3_c64_kernel<kBF16>), dim3(blocks), dim3(256), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL((wgrad3x3_c64_kernel<kF16>), dim3(blocks), dim3(256), 0, s, a);
+  }
 }
 
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)

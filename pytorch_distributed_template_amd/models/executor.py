@@ -124,6 +124,9 @@ class ResNetExecutor:
         self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
+        # a layer1 block's inner BN + ReLU applied by its consumers (conv2 forward and conv2 weight
+        # gradient) to their staged input tiles in LDS; the activation relu(bn(z1)) is never written or re-read
+        self.fuse_pre = os.environ.get("PDT_FUSE_PRE", "1") == "1"
         # stem backward: weight gradient with in-kernel dY (PDT_STEM_FUSED=0: separate apply pass + wgrad)
         self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
         # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad (PDT_COMPACT_DS=0: off)
@@ -303,7 +306,19 @@ class ResNetExecutor:
         return self.flat.grad[slot.offset:slot.offset + slot.numel]
 
     # ---------------------------------------------------------------------------------- conv ops
-    def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None):
+    def _pre_ok(self, nxt: _Conv, N: int, H: int, W: int, train: bool) -> bool:
+        """Can ``nxt`` (the conv consuming a block-internal BN + ReLU) apply that BN itself (conv_fwd_pre +
+        the fused layer1 weight gradient)?"""
+        return (self.fuse_pre and train and self.wgrad_l1 and hasattr(self.C, "conv_fwd_pre") and nxt.R == 3 and nxt.S == 3 and nxt.st == 1 and
+                nxt.pad == 1 and nxt.cin == 64 and nxt.cout == 64 and self.C.conv_fwd_pre_supported(N, H, W) and
+                self.C.wgrad_3x3c64_supported(64, 64, 3, 3, W, 1, 1))
+
+    def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None,
+                 pre=None):
+        if pre is not None:  # x is the producer conv's raw output; pre = its BN coefficients (layer1 only)
+            sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64)
+            self.C.conv_fwd_pre(x, self._w(c), y, sp, pre, N, H, W)
+            return H, W, sp, N * H * W
         cin = cin or c.cin
         R = R or c.R
         S = S or c.S
@@ -368,7 +383,7 @@ class ResNetExecutor:
                             bn.eps, bn.coef)
 
     def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None, bnb=None,
-                 res_phase: int = -1, compact: bool = False):
+                 res_phase: int = -1, compact: bool = False, pre=None):
         """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``.
 
         ``bnb`` = (mode, y1, coef1, y2, coef2, out_mask, slots): fuse the consuming BatchNorm's backward
@@ -383,7 +398,7 @@ class ResNetExecutor:
         else:
             xg, Hx, Wx, Cx, R, S, st, pad = wgrad_geom
         def wg():
-            self._wgrad(c.cout, xg, dy, N, Hx, Wx, Cx, R, S, P, Q, st, pad, self._g(c.slot), R * S * Cx)
+            self._wgrad(c.cout, xg, dy, N, Hx, Wx, Cx, R, S, P, Q, st, pad, self._g(c.slot), R * S * Cx, pre=pre)
             self.grad_ready(c.pid)
         self._side_wgrad(dy, wg)
         # --- dgrad
@@ -410,14 +425,19 @@ class ResNetExecutor:
         launch(bm, bn)
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
-               win=False, dil=1):
+               win=False, dil=1, pre=None):
         if not win and self.wgrad_l1 and self.C.wgrad_3x3c64_supported(C, cout, R, S, W, st, pad):
-            # ResNet layer1 3x3 convs: all 9 taps per block over staged 4-row tiles (csrc conv_wgrad.hip)
+            # ResNet layer1 3x3 convs: all 9 taps per block over staged 4-row tiles (csrc conv_wgrad.hip); with
+            # ``pre`` x is the producer's raw output and the kernel applies its BN + ReLU to each staged tile
             blocks = self.C.wgrad_blocks_3x3c64()
             ws = self._buf("ws", blocks * 64 * 576, torch.float32)
-            self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W)
+            if pre is None:
+                self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W)
+            else:
+                self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W, pre)
             self.C.wgrad_reduce(ws, blocks, 64, 576, 576, 64 * 576, gout, ldo, 1.0, False)
             return
+        assert pre is None, "fused producer BN only on the layer1 weight-gradient kernel"
         key = (cout, R, S, C, N * P * Q, win)
         plan = self._plans.get(key)
         if plan is None:
@@ -516,13 +536,14 @@ class ResNetExecutor:
         Hc, Wc, Cc = H1, W1, st.cout
         blk_saved = []
         for bi, b in enumerate(self.blocks):
-            rec = {"x": x, "H": Hc, "W": Wc, "C": Cc, "ys": [], "as": [], "hw": []}
+            rec = {"x": x, "H": Hc, "W": Wc, "C": Cc, "ys": [], "as": [], "pre": [], "hw": []}
             cur, h, w = x, Hc, Wc
             nconv = len(b["convs"])
+            pre = None  # BN coefficients the current conv applies to its (raw) input itself
             for ci, (c, bn) in enumerate(zip(b["convs"], b["bns"])):
                 P, Q = c.out_hw(h, w)
                 y = self._buf(("y", bi, ci), N * P * Q * c.cout)
-                _, _, sp, tiles = self.conv_fwd(c, cur, N, h, w, y, train)
+                _, _, sp, tiles = self.conv_fwd(c, cur, N, h, w, y, train, pre=pre)
                 if train:
                     self.bn_train_finalize(bn, sp, tiles, N * P * Q)
                 else:
@@ -530,9 +551,17 @@ class ResNetExecutor:
                 rec["ys"].append(y)
                 rec["hw"].append((h, w, P, Q))
                 if ci < nconv - 1:
+                    if self._pre_ok(b["convs"][ci + 1], N, P, Q, train):
+                        pre = bn.coef  # consumers apply BN + ReLU to their staged tiles: no bn_apply pass
+                        rec["as"].append(y)
+                        rec["pre"].append(bn.coef)
+                        cur, h, w = y, P, Q
+                        continue
+                    pre = None
                     a = self._buf(("a", bi, ci), N * P * Q * c.cout)
                     Cn.bn_apply(y, bn.coef, None, None, a, c.cout, 0, True, None)
                     rec["as"].append(a)
+                    rec["pre"].append(None)
                     cur, h, w = a, P, Q
                 else:
                     h, w = P, Q
@@ -674,6 +703,7 @@ class ResNetExecutor:
                 c = convs[ci]
                 h, w, P, Q = rec["hw"][ci]
                 xin = rec["as"][ci - 1] if ci > 0 else x
+                xpre = rec["pre"][ci - 1] if ci > 0 else None
                 if ci > 0:
                     # dgrad epilogue applies the ReLU mask (recomputed from the BN input) and reduces the
                     # inner BN's backward sums: da holds dz, no separate reduce pass
@@ -681,7 +711,8 @@ class ResNetExecutor:
                     bnp = bns[ci - 1]
                     yp = rec["ys"][ci - 1]
                     slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
-                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, da, bnb=(1, yp, bnp.coef, None, None, None, slots))
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, da, bnb=(1, yp, bnp.coef, None, None, None, slots),
+                                  pre=xpre)
                     self._bn_bwd_finish(slots, N * h * w, bnp)
                     dname = "dy_c" if dname == "dy_a" else "dy_a"
                     dyp = self._buf(bk_(dname), yp.numel())

@@ -107,7 +107,8 @@ def test_training_reduces_loss():
 # weight gradient, the ping-pong 256x256 conv and weight-gradient kernels, phased strided dgrad with the
 # compact downsample residual
 R18_224_KERNELS = ("stem_fwd", "conv_l1_fwd", "conv_l1_dgrad", "wgrad3x3_c64", "wgrad_stem_fused", "conv_pp_fwd",
-                   "conv_pp_dgrad", "conv_wgrad_pp", "conv_generic_dgrad_phased", "conv_dgrad_compact_residual")
+                   "conv_pp_dgrad", "conv_wgrad_pp", "conv_generic_dgrad_phased", "conv_dgrad_compact_residual",
+                   "conv_l1_fwd_fused_bn_relu", "wgrad3x3_c64_fused_bn_relu")
 
 
 @pytest.mark.parametrize("arch,N", [("resnet18", 16), ("resnet18", 32), ("resnet50", 8)])

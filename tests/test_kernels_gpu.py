@@ -619,3 +619,43 @@ def test_colsum_matches_torch(B, ld, ncols):
     native.C.colsum(d, B, ld, ncols, out, 0.5)
     ref = d[:, :ncols].float().sum(0) * 0.5
     assert torch.allclose(out, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_fused_producer_bn_relu_layer1(dtype):
+    """the layer1 conv forward and weight gradient applying the producer BN + ReLU to their staged
+    input tiles must equal the unfused chain (bn_apply -> conv / wgrad) BIT FOR BIT, including the zero padding
+    of image borders (BN(0) != 0: a transformed pad would show up on every border pixel)."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    C = native.C
+    torch.manual_seed(21)
+    N, H, W = 3, 12, 56
+    z = _rand16(N, H, W, 64, dtype=dtype)
+    w = _rand16(64, 3, 3, 64, dtype=dtype, scale=1.0 / 24)
+    coef = torch.cat([torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.5,
+                      torch.zeros(128, device=DEV)]).contiguous()
+    a = torch.empty_like(z)
+    C.bn_apply(z, coef, None, None, a, 64, 0, True, None)
+    ref_a = torch.relu(z.float() * coef[:64] + coef[64:128]).to(dtype)
+    assert _rel(a, ref_a) < 1e-2  # (bn_apply rounds one fma; torch rounds the product and the sum)
+    # forward with statistics: unfused (conv over a) vs fused (conv over z with pre_coef)
+    st_u = torch.zeros(C.stat_slots() * 64 * 2, dtype=torch.float64, device=DEV)
+    st_f = torch.zeros_like(st_u)
+    y_u, y_f = torch.empty_like(z), torch.empty_like(z)
+    C.conv_fwd(a, w, y_u, None, st_u, N, H, W, 64, 64, 3, 3, H, W, 1, 1, -1, -1, 1, 1, H, W, 1, 1, 0, 0, 256, 64, 64, 0)
+    assert C.conv_fwd_pre_supported(N, H, W)
+    C.conv_fwd_pre(z, w, y_f, st_f, coef, N, H, W)
+    assert torch.equal(y_u, y_f)
+    assert torch.equal(st_u, st_f)
+    ref = F.conv2d(ref_a.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert _rel(y_f, ref) < 2e-2
+    # weight gradient: unfused over a vs fused over z
+    dy = _rand16(N, H, W, 64, dtype=dtype)
+    blocks = C.wgrad_blocks_3x3c64()
+    ws_u = torch.empty(blocks * 64 * 576, device=DEV)
+    ws_f = torch.empty_like(ws_u)
+    C.conv_wgrad_3x3c64(a, dy, ws_u, N, H, W)
+    C.conv_wgrad_3x3c64(z, dy, ws_f, N, H, W, coef)
+    assert torch.equal(ws_u, ws_f)
+    # not eligible: H % 4 != 0 (partial row tiles go to the generic kernel, which has no fused producer BN)
+    assert not C.conv_fwd_pre_supported(N, 10, W)
