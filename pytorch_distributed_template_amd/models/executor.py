@@ -134,11 +134,12 @@ class ResNetExecutor:
         self.bwd_buf_per_block = os.environ.get("PDT_BWD_BUF_PER_BLOCK", "1") == "1"
         # backward-only derived weight layouts gathered on the side stream under the forward (PDT_SPLIT_DERIVED=0: off)
         self.split_derived = os.environ.get("PDT_SPLIT_DERIVED", "1") == "1"
-        # block-output BN-backward reduce fused into the next block's first dgrad epilogue only where dX has at
-        # most this many pixels per image (PDT_FUSE_BLOCK_BN_MAXHW; larger: plain dgrad + reduce pass).  The
-        # fused 2-branch / masked epilogues are VALU-heavy (conv_l1 dgrad 290 -> 756 us at layer1, rocprof
-        # r2): at 56x56 and 28x28 the separate bandwidth-bound reduce is cheaper (22.64 -> 22.54 ms/step A/B)
-        self.fuse_block_bn_maxhw = int(os.environ.get("PDT_FUSE_BLOCK_BN_MAXHW", "200"))
+        # block-output BN-backward reduce fused into the next block's first dgrad epilogue where dX has at most
+        # this many pixels per image (PDT_FUSE_BLOCK_BN_MAXHW; larger: plain dgrad + a separate reduce pass).
+        # Round 2 made the fused masked epilogues straight-line (tools/epi_bench.py: layer1 803 -> 598 us,
+        # layer2 2-branch 766 -> 508 us), after which fusing at every resolution measured equal or faster than
+        # the separate reduce (A/B 21.76 -> 21.71 ms/step), so it is the default everywhere.
+        self.fuse_block_bn_maxhw = int(os.environ.get("PDT_FUSE_BLOCK_BN_MAXHW", "1000000"))
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)

@@ -3,12 +3,13 @@
 # WRITE_SIZE (2 TCC counters) -- separate passes because one pass holds at most 4 TCC counters.  Summarise with
 # tools/pmc_bytes_summary.py.  BENCH_ARGS passes extra bench.py flags (e.g. "--arch resnet50 --dtype fp16").
 R="${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p "$R/gpurun_out/pmc_bytes"
+O="$R/gpurun_out/${PMC_OUT:-pmc_bytes}"   # PMC_OUT: output directory name (A/B runs)
+mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE GRBM_GUI_ACTIVE \
-  -d "$R/gpurun_out/pmc_bytes/fetch" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 ${BENCH_ARGS:-} \
-  > "$R/gpurun_out/pmc_bytes/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 1; }
+  -d "$O/fetch" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 ${BENCH_ARGS:-} \
+  > "$O/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 1; }
 timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE GRBM_GUI_ACTIVE \
-  -d "$R/gpurun_out/pmc_bytes/write" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 ${BENCH_ARGS:-} \
-  > "$R/gpurun_out/pmc_bytes/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 1; }
+  -d "$O/write" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 ${BENCH_ARGS:-} \
+  > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 1; }
 echo "pmc bytes ok"
