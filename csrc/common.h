@@ -47,9 +47,8 @@ template <> struct E16<kF16> {
 // sign bit), which equals rounding after the fp32 max.
 typedef short pdt_s16x2 __attribute__((ext_vector_type(2)));
 template <int DT>
-PDT_DEVICE void pre_act_chunk(char* p, const float (&sc)[8], const float (&sh)[8]) {
+PDT_DEVICE uint4 pre_act8(uint4 v, const float (&sc)[8], const float (&sh)[8]) {
   using E = E16<DT>;
-  uint4 v = *(const uint4*)p;
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -58,7 +57,21 @@ PDT_DEVICE void pre_act_chunk(char* p, const float (&sc)[8], const float (&sh)[8
     const uint32_t pk = (uint32_t)E::from_f(lo) | ((uint32_t)E::from_f(hi) << 16);
     w[e] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(pdt_s16x2, pk), pdt_s16x2{0, 0}));
   }
-  *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// The same over a thread's share of a staged tile: chunk k at base + off[k] when ok[k].  All reads are issued
+// before any write (the compiler cannot prove the chunks disjoint, so per-chunk read-modify-write would
+// serialise one LDS round trip per chunk).
+template <int DT, int NCH>
+PDT_DEVICE void pre_act_chunks(char* base, const int (&off)[NCH], const bool (&ok)[NCH], const float (&sc)[8],
+                               const float (&sh)[8]) {
+  uint4 v[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) v[k] = *(const uint4*)(base + off[k]);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+    if (ok[k]) *(uint4*)(base + off[k]) = pre_act8<DT>(v[k], sc, sh);
 }
 
 // 16-byte streaming (nontemporal) global load / store for the elementwise passes: the activations they

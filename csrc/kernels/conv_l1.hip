@@ -163,13 +163,21 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
     if constexpr (PRE) {
       const int n = t / TH, h0 = (t - n * TH) * 4;
       char* sbw = stage0 + buf * kStageB;
+      // two batches (6 + 5 chunks): all of a batch's LDS reads in flight together, register budget kept
 #pragma unroll
-      for (int k = 0; k < 11; ++k) {
-        const int R = (tid >> 3) + 32 * k;
-        const int hr = R / kXP, wc = R - (R / kXP) * kXP;
-        const int h = h0 - 1 + hr, w = wc - 1;
-        if (R < kXRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW)
-          pre_act_chunk<DT>(sbw + R * 128 + (tid & 7) * 16, pre_sc, pre_sh);
+      for (int k0 = 0; k0 < 11; k0 += 6) {
+        int off[6];
+        bool ok[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const int R = min((tid >> 3) + 32 * (k0 + k), kXRows - 1);
+          const int hr = R / kXP, wc = R - (R / kXP) * kXP;
+          const int h = h0 - 1 + hr, w = wc - 1;
+          ok[k] = k0 + k < 11 && (tid >> 3) + 32 * (k0 + k) < kXRows && (unsigned)h < (unsigned)a.H &&
+                  (unsigned)w < (unsigned)kW;
+          off[k] = R * 128 + (tid & 7) * 16;
+        }
+        pre_act_chunks<DT, 6>(sbw, off, ok, pre_sc, pre_sh);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

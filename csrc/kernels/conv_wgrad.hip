@@ -873,14 +873,17 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
     if constexpr (PRE) {
       const int n = t / TH, h0 = (t - n * TH) * 4;
       char* sxw = smem + buf * kL1Stage;
+      int off[11];
+      bool ok[11];
 #pragma unroll
       for (int k = 0; k < 11; ++k) {
-        const int R = (tid >> 3) + 32 * k;
+        const int R = min((tid >> 3) + 32 * k, kL1XRows - 1);
         const int hr = R / kL1XP, wc = R - (R / kL1XP) * kL1XP;
         const int h = h0 - 1 + hr, w = wc - 1;
-        if (R < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W)
-          pre_act_chunk<DT>(sxw + R * 128 + (((tid & 7) ^ l1_swz(hr, wc)) << 4), pre_sc, pre_sh);
+        ok[k] = (tid >> 3) + 32 * k < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W;
+        off[k] = R * 128 + (((tid & 7) ^ l1_swz(hr, wc)) << 4);
       }
+      pre_act_chunks<DT, 11>(sxw, off, ok, pre_sc, pre_sh);
       __syncthreads();
     }
     if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);

@@ -41,20 +41,27 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     float sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sc[e] = coef[c0 + e]; sh[e] = coef[C + c0 + e]; }
+    // all 9 window loads issued up front (branch-free: an out-of-image tap reads the clamped in-image pixel
+    // and is then ignored), so a thread pays one memory latency instead of one per in-bounds tap
+    uint4 q[9];
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int h = oh * 2 - 1 + kh;
-      if ((unsigned)h >= (unsigned)H) continue;
+    for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int w = ow * 2 - 1 + kw;
-        if ((unsigned)w >= (unsigned)W) continue;
-        const uint4 q = *(const uint4*)(y + ((uint32_t)(n * H + h) * W + w) * C + c0);
-        const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+        const int h = min(max(oh * 2 - 1 + kh, 0), H - 1), w = min(max(ow * 2 - 1 + kw, 0), W - 1);
+        q[kh * 3 + kw] = *(const uint4*)(y + ((uint32_t)(n * H + h) * W + w) * C + c0);
+      }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const bool hok = (unsigned)(oh * 2 - 1 + kh) < (unsigned)H;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const bool ok = hok && (unsigned)(ow * 2 - 1 + kw) < (unsigned)W;
+        const uint32_t qw[4] = {q[kh * 3 + kw].x, q[kh * 3 + kw].y, q[kh * 3 + kw].z, q[kh * 3 + kw].w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float val = fmaxf(E::to_f((uint16_t)(qw[e >> 1] >> (16 * (e & 1)))) * sc[e] + sh[e], 0.f);
-          if (val > best[e]) { best[e] = val; bi[e] = (uint8_t)(kh * 3 + kw); }
+          if (ok && val > best[e]) { best[e] = val; bi[e] = (uint8_t)(kh * 3 + kw); }
         }
       }
     }
