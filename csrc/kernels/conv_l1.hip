@@ -95,7 +95,11 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
         const int h = h0 - 1 + hr, w = wc - 1;
         const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW;
         const uint32_t off = ok ? (uint32_t)((((n * a.H + h) * kW + w) * 64 + (pch ^ hswz(R)) * 8) * 2) : kOOB;
-        buf_lds16(rx, sb + ii * 1024, off);
+        // PRE: opaque DMA, or the compiler drains it (vmcnt(0)) before the in-LDS transform of the other buffer
+        if constexpr (PRE)
+          buf_lds16_asm(rx, sb + ii * 1024, off);
+        else
+          buf_lds16(rx, sb + ii * 1024, off);
       }
     }
   };
@@ -160,6 +164,8 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
+    // PRE: transform this tile's halo while the next tile's DMA (into the other buffer) is in flight
     if constexpr (PRE) {
       const int n = t / TH, h0 = (t - n * TH) * 4;
       char* sbw = stage0 + buf * kStageB;
@@ -183,7 +189,6 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
     const char* sb = stage0 + buf * kStageB;
 
     // epilogue operands (residual, BN input, block output) of this tile, loaded now so their latency

@@ -870,6 +870,8 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
   for (; t < t_end; t += per_x) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
+    // PRE: transform this tile's X halo while the next tile's DMA (into the other buffer) is in flight
     if constexpr (PRE) {
       const int n = t / TH, h0 = (t - n * TH) * 4;
       char* sxw = smem + buf * kL1Stage;
@@ -886,7 +888,6 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
       pre_act_chunks<DT, 11>(sxw, off, ok, pre_sc, pre_sh);
       __syncthreads();
     }
-    if (t + per_x < t_end) stage_tile(t + per_x, buf ^ 1);
     const char* sx = smem + buf * kL1Stage;
     const char* sy = sx + kL1XBytes;
 #pragma unroll 1
