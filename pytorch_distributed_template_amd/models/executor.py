@@ -124,6 +124,7 @@ class ResNetExecutor:
         self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
+        self.bk32_short = os.environ.get("PDT_BK32_SHORT", "1") == "1"
         # a layer1 block's inner BN + ReLU applied by its consumers (conv2 forward and conv2 weight
         # gradient) to their staged input tiles in LDS; the activation relu(bn(z1)) is never written or re-read
         self.fuse_pre = os.environ.get("PDT_FUSE_PRE", "1") == "1"
@@ -327,6 +328,10 @@ class ResNetExecutor:
         pad = c.pad if pad is None else pad
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
         bk = 64 if cin % 64 == 0 else 32
+        if cin * R * S == 64 and c.cout >= 256 and self.bk32_short:
+            # a single 64-wide K-step: two 32-wide steps on the 3-stage ring overlap load and MFMA
+            # (tools/conv_bench.py --r50: ResNet-50 1x1 64->256 with statistics 162 vs 142 TF/s)
+            bk = 32
         M = N * P * Q
         sp = None
         if stats:

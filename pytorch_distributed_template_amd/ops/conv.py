@@ -12,11 +12,18 @@ buffers.  They are the unit-test surface of the kernels (tests/test_kernels_gpu.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
 
 from . import native
+
+
+# shortest reduction that goes to the ping-pong kernel: tools/conv_bench.py --r50 (forward + BN statistics) measured
+# it ahead of the 128x128 kernel from two K-steps on (ResNet-50 1x1 convs 128->512: 278 vs 251 TF/s, 256->1024:
+# 452 vs 392); PDT_PP_MIN_K overrides (the round-1 table used 512)
+_PP_MIN_K = int(os.environ.get("PDT_PP_MIN_K", "128"))
 
 
 def conv_tile(cout: int, kdim: int = 0) -> Tuple[int, int]:
@@ -27,7 +34,7 @@ def conv_tile(cout: int, kdim: int = 0) -> Tuple[int, int]:
     CU, counted-vmcnt DMA pipeline: +10-25 % over the 2-stage 128x128 kernel on ResNet layer3/4 shapes,
     tools/conv_bench.py); short ones (1x1 convs: 1-4 K-steps) stay on the 2-stage kernel, whose
     prologue/epilogue is cheaper."""
-    if cout % 256 == 0 and kdim >= 512 and kdim % 64 == 0:
+    if cout % 256 == 0 and kdim >= _PP_MIN_K and kdim % 64 == 0:
         return 256, 256
     if cout % 128 == 0:
         return 128, 128

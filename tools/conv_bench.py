@@ -20,6 +20,10 @@ SHAPES = [  # H, Cin, Cout, k, stride
     (28, 128, 256, 3, 2), (14, 256, 256, 3, 1), (28, 128, 256, 1, 2), (14, 256, 512, 3, 2),
     (7, 512, 512, 3, 1), (14, 256, 512, 1, 2),
 ]
+SHAPES_R50 = [  # ResNet-50 bottleneck 1x1 convs: H, Cin, Cout, k, stride
+    (56, 64, 256, 1, 1), (56, 256, 64, 1, 1), (28, 512, 128, 1, 1), (28, 128, 512, 1, 1), (14, 1024, 256, 1, 1),
+    (14, 256, 1024, 1, 1), (7, 2048, 512, 1, 1), (7, 512, 2048, 1, 1),
+]
 FWD_TILES = [(256, 256, 64), (512, 128, 64), (128, 128, 64), (256, 256, 32), (256, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64),
              (256, 64, 32), (128, 128, 32)]
 
@@ -77,6 +81,7 @@ def main():
     ap.add_argument("--only-stem", action="store_true")
     ap.add_argument("--skip-stem", action="store_true")
     ap.add_argument("--shapes", default="", help="comma-separated indices into SHAPES (default: all)")
+    ap.add_argument("--r50", action="store_true", help="ResNet-50 1x1 shapes (SHAPES_R50), forward with statistics")
     a = ap.parse_args()
     C = native.C
     dev = "cuda"
@@ -85,8 +90,9 @@ def main():
         stem_bench(C, a.batch, a.reps)
     if a.only_stem:
         return
-    sel = [int(v) for v in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
-    for (H, ci, co, k, st) in [SHAPES[i] for i in sel]:
+    table = SHAPES_R50 if a.r50 else SHAPES
+    sel = [int(v) for v in a.shapes.split(",")] if a.shapes else range(len(table))
+    for (H, ci, co, k, st) in [table[i] for i in sel]:
         pad = k // 2
         N = a.batch
         P = (H + 2 * pad - k) // st + 1
@@ -99,10 +105,15 @@ def main():
         for (bm, bn, bk) in FWD_TILES:
             if co % bn:
                 continue
-            def f(bm=bm, bn=bn, bk=bk):
-                C.conv_fwd(x, w, y, None, None, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1,
+            sp = torch.zeros(C.stat_slots() * co * 2, dtype=torch.float64, device=dev) if a.r50 else None
+
+            def f(bm=bm, bn=bn, bk=bk, sp=sp):
+                C.conv_fwd(x, w, y, None, sp, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1,
                            0, 0, bm, bn, bk, 0)
             row[f"fwd_{bm}x{bn}x{bk}"] = round(flops / timeit(f, a.reps) / 1e9, 1)
+        if a.r50:  # forward-with-statistics tiles only
+            print(json.dumps(row), flush=True)
+            continue
         dx = torch.empty(N, H, H, ci, device=dev, dtype=torch.bfloat16)
         pieces, phases, off = [], [], 0
         for ph, pw, rs, ss, ih, iw in conv.dgrad_phases(k, k, st, pad):
