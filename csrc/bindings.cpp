@@ -679,7 +679,7 @@ void im2col(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64
 void stem_pack(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t pad, int64_t Hp,
                int64_t Wp) {
   TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * Hp * Wp * 4 && C <= 4 && Hp >= H + 2 * pad &&
-                  Wp >= W + 2 * pad, "stem_pack: bad sizes");
+                  Wp >= W + 2 * pad && N * Hp * Wp < (int64_t(1) << 31), "stem_pack: bad sizes");
   pdt::stem_pack_launch(dt16(out, "out"), pf(x, "x"), p16(out, "out"), N, C, H, W, pad, Hp, Wp, cur_stream());
 }
 
@@ -689,7 +689,8 @@ void stem_pack_u8(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H,
   check_dev(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kByte, "stem_pack_u8: x must be uint8");
   TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * Hp * Wp * 4 && C <= 4 && Hp >= H + 2 * pad &&
-                  Wp >= W + 2 * pad && scale.numel() >= C && shift.numel() >= C, "stem_pack_u8: bad sizes");
+                  Wp >= W + 2 * pad && scale.numel() >= C && shift.numel() >= C && N * Hp * Wp < (int64_t(1) << 31),
+              "stem_pack_u8: bad sizes");
   pdt::stem_pack_u8_launch(dt16(out, "out"), x.data_ptr<uint8_t>(), p16(out, "out"), N, C, H, W, pad, Hp, Wp,
                            pf(scale, "scale"), pf(shift, "shift"), cur_stream());
 }

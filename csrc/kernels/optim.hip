@@ -182,26 +182,32 @@ template <int DT, typename TIN>
 __global__ __launch_bounds__(256) void stem_pack_kernel(const TIN* __restrict__ x, uint16_t* __restrict__ out, int N,
                                                         int C, int H, int W, int pad, int Hp, int Wp,
                                                         const float* __restrict__ scale,
-                                                        const float* __restrict__ shift) {
+                                                        const float* __restrict__ shift, FastDiv fwp, FastDiv fhp) {
   using E = E16<DT>;
-  const int64_t total = (int64_t)N * Hp * Wp;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
-    const int wp = (int)(v % Wp);
-    const int64_t t = v / Wp;
-    const int hp = (int)(t % Hp);
-    const int n = (int)(t / Hp);
+  // 32-bit index math (the host checks N*Hp*Wp < 2^31): 64-bit div/mod by the padded sizes made this pass
+  // ALU-bound at ~3 TB/s
+  const uint32_t total = (uint32_t)N * Hp * Wp;
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < total; v += gridDim.x * 256u) {
+    const uint32_t t = fdiv(v, fwp);
+    const int wp = (int)(v - t * (uint32_t)Wp);
+    const int n = (int)fdiv(t, fhp);
+    const int hp = (int)(t - (uint32_t)n * (uint32_t)Hp);
     const int h = hp - pad, w = wp - pad;
     uint16_t o[4] = {0, 0, 0, 0};
     if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
-      for (int c = 0; c < C && c < 4; ++c) {
-        const float v = (float)x[(((int64_t)n * C + c) * H + h) * W + w];
-        o[c] = E::from_f(scale ? v * scale[c] + shift[c] : v);
+      const TIN* px = x + ((size_t)n * C * H + h) * W + w;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c < C) {
+          const float v = (float)px[(size_t)c * H * W];
+          o[c] = E::from_f(scale ? v * scale[c] + shift[c] : v);
+        }
       }
     }
     uint2 q;
     q.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
     q.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-    *(uint2*)(out + v * 4) = q;
+    *(uint2*)(out + (size_t)v * 4) = q;
   }
 }
 
@@ -210,10 +216,10 @@ void stem_pack_launch(int dtype, const float* x, uint16_t* out, int N, int C, in
   const int64_t total = (int64_t)N * Hp * Wp;
   if (dtype == kBF16)
     hipLaunchKernelGGL((stem_pack_kernel<kBF16, float>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W,
-                       pad, Hp, Wp, nullptr, nullptr);
+                       pad, Hp, Wp, nullptr, nullptr, make_fastdiv((uint32_t)Wp), make_fastdiv((uint32_t)Hp));
   else
     hipLaunchKernelGGL((stem_pack_kernel<kF16, float>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H, W,
-                       pad, Hp, Wp, nullptr, nullptr);
+                       pad, Hp, Wp, nullptr, nullptr, make_fastdiv((uint32_t)Wp), make_fastdiv((uint32_t)Hp));
 }
 
 void stem_pack_u8_launch(int dtype, const uint8_t* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp,
@@ -221,10 +227,10 @@ void stem_pack_u8_launch(int dtype, const uint8_t* x, uint16_t* out, int N, int 
   const int64_t total = (int64_t)N * Hp * Wp;
   if (dtype == kBF16)
     hipLaunchKernelGGL((stem_pack_kernel<kBF16, uint8_t>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H,
-                       W, pad, Hp, Wp, scale, shift);
+                       W, pad, Hp, Wp, scale, shift, make_fastdiv((uint32_t)Wp), make_fastdiv((uint32_t)Hp));
   else
     hipLaunchKernelGGL((stem_pack_kernel<kF16, uint8_t>), dim3(ew_blocks(total)), dim3(256), 0, s, x, out, N, C, H,
-                       W, pad, Hp, Wp, scale, shift);
+                       W, pad, Hp, Wp, scale, shift, make_fastdiv((uint32_t)Wp), make_fastdiv((uint32_t)Hp));
 }
 
 __global__ __launch_bounds__(256) void gather32_kernel(const float* __restrict__ src, const int* __restrict__ idx,
