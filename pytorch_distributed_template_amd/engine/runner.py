@@ -16,6 +16,7 @@ from __future__ import annotations
 import datetime
 import os
 import random
+import sys
 import time
 import warnings
 from typing import Optional
@@ -88,6 +89,31 @@ class _DeviceMeter:
         return a[0], a[1]
 
 
+def _fault_spec():
+    """``PDT_FAULT_INJECT=rank:iteration[:exit|hang[:epoch]]`` -- the fault-injection hook of SURVEY §5 ("kill rank k
+    at step s"): global rank ``rank`` dies (``exit``: status 13 without any teardown, like a crashed process) or
+    stops making progress forever (``hang``: the other ranks block in the next collective until ``--dist-timeout``
+    / the comm watchdog fires) when it reaches training iteration ``iteration`` of epoch ``epoch`` (default 0).
+    Used by tests/test_distributed_cpu.py to check that the group is torn down instead of hanging."""
+    spec = os.environ.get("PDT_FAULT_INJECT")
+    if not spec:
+        return None
+    f = spec.split(":")
+    return int(f[0]), int(f[1]), (f[2] if len(f) > 2 else "exit"), (int(f[3]) if len(f) > 3 else 0)
+
+
+def _maybe_inject_fault(rank: int, epoch: int, it: int) -> None:
+    spec = _fault_spec()
+    if spec is None or (rank, it, epoch) != (spec[0], spec[1], spec[3]):
+        return
+    sys.stderr.write(f"[fault injection] rank {rank}: {spec[2]} at epoch {epoch} iteration {it}\n")
+    sys.stderr.flush()
+    if spec[2] == "hang":
+        while True:
+            time.sleep(3600)
+    os._exit(13)
+
+
 def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, device):
     batch_times = AverageMeter("Time", ":6.3f")
     data_times = AverageMeter("Data", ":6.3f")
@@ -102,6 +128,7 @@ def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, de
         if i >= n_iter:
             break
         data_times.update(time.time() - end)
+        _maybe_inject_fault(rank, epoch, i)
         if not getattr(trainer, "host_batches", False):  # native DP scatters host batches to every GPU itself
             images = images.to(device, non_blocking=True)
             target = target.to(device, non_blocking=True)

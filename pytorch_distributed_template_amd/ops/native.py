@@ -53,8 +53,27 @@ def available() -> bool:
 
 
 class _Proxy:
+    """``native.C``: attribute access on the extension.  With ``PDT_VALIDATE`` >= 1 (read once, at the first
+    access) extension functions come back wrapped by :mod:`.validate` (launch-checked / non-finite tracking)."""
+
+    def __init__(self):
+        self._wrapped = None  # None: not decided yet; False: validation off; dict: name -> checked wrapper
+
     def __getattr__(self, name):
-        return getattr(load(), name)
+        obj = getattr(load(), name)
+        if name.startswith("_"):
+            return obj
+        w = self._wrapped
+        if w is None:
+            from . import validate
+            w = self._wrapped = {} if validate.level_from_env() > 0 else False
+        if w is False:
+            return obj
+        f = w.get(name)
+        if f is None:
+            from . import validate
+            f = w[name] = validate.maybe_wrap(name, obj)
+        return f
 
 
 C = _Proxy()

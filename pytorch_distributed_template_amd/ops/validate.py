@@ -1,0 +1,128 @@
+"""Validation mode for the native ops (the debug / sanitizer counterpart of ``CUDA_LAUNCH_BLOCKING=1`` +
+``torch.autograd.detect_anomaly`` for our own kernels; SURVEY §5 "race detection / sanitizers").
+
+Enabled with ``PDT_VALIDATE=<level>`` before the extension is first used (``native.C`` then hands out
+checked wrappers of every extension *function*; classes such as the communicator pass through):
+
+* level 1 -- launch-checked: every native op is followed by a device synchronisation, so an asynchronous
+  HIP error (illegal address, invalid launch, a kernel trap) is raised AT the op that caused it, with the
+  op's name, its tensor arguments and the last ``PDT_VALIDATE_HISTORY`` (default 32) ops in the message.
+  ``PDT_VALIDATE_LOG=<file>`` also appends each op name to a file (flushed) BEFORE it launches: a fault the
+  HIP runtime turns into a process abort (GPU memory access fault) leaves the faulting op as the last line.
+* level 2 -- level 1 plus non-finite tracking: every floating-point tensor argument is scanned before and
+  after the op, and an op that turns a finite tensor into one holding NaN/Inf raises
+  :class:`NonFiniteError` naming the op and the argument.  (An fp16 AMP step that overflows on purpose --
+  the GradScaler then skips it -- trips this too, exactly like torch's anomaly mode.)
+
+Steps being captured into a HIP graph are not checked (nothing may synchronise inside a capture).
+Everything here costs a device round trip per op: it is a debugging mode, never on in a benchmark.
+"""
+from __future__ import annotations
+
+import collections
+import os
+import threading
+from typing import Any, Callable, Deque, List, Optional, Tuple
+
+import torch
+
+
+class ValidationError(RuntimeError):
+    """A native op failed (synchronous TORCH_CHECK or an asynchronous HIP error surfaced at its sync)."""
+
+
+class NonFiniteError(ValidationError):
+    """A native op produced NaN/Inf in a tensor argument that was finite before the op."""
+
+
+def _describe(args) -> str:
+    parts = []
+    for i, a in enumerate(args):
+        if isinstance(a, torch.Tensor):
+            parts.append(f"#{i}:{str(a.dtype).replace('torch.', '')}{list(a.shape)}")
+    return " ".join(parts) if parts else "(no tensors)"
+
+
+class Validator:
+    """Wraps extension functions; one instance per process (see :func:`validator`)."""
+
+    def __init__(self, level: int = 1, history: int = 32, log_path: Optional[str] = None,
+                 sync: Optional[Callable[[], None]] = None, capturing: Optional[Callable[[], bool]] = None):
+        self.level = int(level)
+        self.history: Deque[str] = collections.deque(maxlen=max(1, int(history)))
+        self.calls = 0
+        self._lock = threading.Lock()
+        self._log = open(log_path, "a", buffering=1) if log_path else None
+        self._sync = sync or (lambda: torch.cuda.synchronize() if torch.cuda.is_available() else None)
+        self._capturing = capturing or (lambda: torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+
+    def _recent(self) -> str:
+        return "\n  ".join(self.history)
+
+    @staticmethod
+    def _finite_args(args) -> List[Tuple[int, torch.Tensor, bool]]:
+        out = []
+        for i, a in enumerate(args):
+            if isinstance(a, torch.Tensor) and a.is_floating_point() and a.numel() > 0:
+                out.append((i, a, bool(torch.isfinite(a).all())))
+        return out
+
+    def wrap(self, name: str, fn: Callable[..., Any]) -> Callable[..., Any]:
+        def checked(*args, **kwargs):
+            if self._capturing():
+                return fn(*args, **kwargs)
+            entry = f"{name} {_describe(args)}"
+            with self._lock:
+                self.calls += 1
+                self.history.append(entry)
+                if self._log is not None:
+                    self._log.write(entry + "\n")
+            pre = self._finite_args(args) if self.level >= 2 else []
+            try:
+                res = fn(*args, **kwargs)
+                self._sync()
+            except Exception as e:  # TORCH_CHECK in the binding, or an async HIP error at the sync
+                raise ValidationError(f"native op `{name}` failed: {e}\n  args: {_describe(args)}\n"
+                                      f"  last native ops (oldest first):\n  {self._recent()}") from e
+            for i, t, was_finite in pre:
+                if was_finite and not bool(torch.isfinite(t).all()):
+                    bad = int((~torch.isfinite(t)).sum())
+                    raise NonFiniteError(f"native op `{name}` wrote {bad} non-finite value(s) into argument #{i} "
+                                         f"({str(t.dtype).replace('torch.', '')}{list(t.shape)}), finite before "
+                                         f"the op\n  last native ops (oldest first):\n  {self._recent()}")
+            return res
+        checked.__name__ = name
+        checked.__wrapped__ = fn
+        return checked
+
+
+_validator: Optional[Validator] = None
+_vlock = threading.Lock()
+
+
+def level_from_env() -> int:
+    try:
+        return int(os.environ.get("PDT_VALIDATE", "0") or 0)
+    except ValueError:
+        return 1
+
+
+def validator() -> Optional[Validator]:
+    """The process-wide validator, created on first use when ``PDT_VALIDATE`` >= 1, else None."""
+    global _validator
+    lvl = level_from_env()
+    if lvl <= 0:
+        return None
+    with _vlock:
+        if _validator is None or _validator.level != lvl:
+            _validator = Validator(lvl, int(os.environ.get("PDT_VALIDATE_HISTORY", "32")),
+                                   os.environ.get("PDT_VALIDATE_LOG") or None)
+        return _validator
+
+
+def maybe_wrap(name: str, obj: Any) -> Any:
+    """``obj`` unchanged unless validation is on and it is an extension function (not a class/constant)."""
+    v = validator()
+    if v is None or isinstance(obj, type) or not callable(obj):
+        return obj
+    return v.wrap(name, obj)

@@ -151,3 +151,24 @@ def test_bench_multi_gpu_request_fails_loudly_without_gpus():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=ROOT, capture_output=True, text=True,
                        timeout=300, env=dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.parametrize("mode,port", [("exit", 29621), ("hang", 29622)])
+def test_fault_injection_tears_down_group(tmp_path, mode, port):
+    """SURVEY §5 fault injection ("kill rank k at step s", PDT_FAULT_INJECT): rank 1 of a 2-rank DDP run dies
+    (exit) or stops making progress (hang) at iteration 1.  The group must end with a non-zero status instead of
+    hanging: the launcher tears it down when a child exits non-zero; for a hang, rank 0's next collective hits
+    --dist-timeout first."""
+    import time
+    out = str(tmp_path / f"output_fault_{mode}")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="1", PDT_FAULT_INJECT=f"1:1:{mode}")
+    cmd = [sys.executable, "-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=2",
+           "--master_addr=127.0.0.1", f"--master_port={port}", "--grace_s=2", "distributed.py", "--outpath", out,
+           "-b", "8", "--dist-timeout", "15"] + COMMON
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    log = r.stdout + r.stderr
+    assert r.returncode != 0, log[-3000:]
+    assert f"[fault injection] rank 1: {mode} at epoch 0 iteration 1" in log
+    assert "terminating the group" in log, log[-3000:]
+    assert time.time() - t0 < 240

@@ -226,3 +226,47 @@ def test_no_reads_of_unwritten_memory():
     assert not bad, bad[:10]
     assert torch.equal(d0, d1)
     assert torch.equal(b0, b1)
+
+
+_VALIDATE_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+from pytorch_distributed_template_amd.models import registry
+from pytorch_distributed_template_amd.ops import native, validate
+dev = torch.device("cuda:0")
+torch.manual_seed(0)
+tr = NativeTrainer(registry.create("resnet18"), dev, dtype=torch.bfloat16)
+x = torch.randn(8, 3, 64, 64, device=dev)
+t = torch.randint(0, 1000, (8,), device=dev)
+for _ in range(2):
+    tr.train_step(x, t)
+torch.cuda.synchronize()
+v = validate.validator()
+print("CLEAN_CALLS", v.calls, "WRAPPED", hasattr(native.C.conv_fwd, "__wrapped__"))
+x[0, 0, 5, 5] = float("nan")
+try:
+    tr.train_step(x, t)
+except validate.NonFiniteError as e:
+    print("CAUGHT", str(e).splitlines()[0])
+"""
+
+
+def test_validation_mode_localises_nonfinite(tmp_path):
+    """PDT_VALIDATE=2 over the real kernels: clean steps pass with every native op launch-checked and
+    scanned; a NaN pixel is attributed to the first op that spreads it (the stem input packing)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    log = tmp_path / "ops.log"
+    env = dict(os.environ, PDT_VALIDATE="2", PDT_VALIDATE_LOG=str(log))
+    r = subprocess.run([sys.executable, "-c", _VALIDATE_SCRIPT.format(root=root)], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    clean = [ln for ln in r.stdout.splitlines() if ln.startswith("CLEAN_CALLS")][0].split()
+    assert int(clean[1]) > 100 and clean[3] == "True", r.stdout
+    caught = [ln for ln in r.stdout.splitlines() if ln.startswith("CAUGHT")]
+    assert caught and "native op `stem_pack` wrote" in caught[0], r.stdout + r.stderr[-2000:]
+    ops = log.read_text().splitlines()
+    assert ops[-1].startswith("stem_pack ") and any(o.startswith("conv_fwd ") for o in ops)

@@ -1,0 +1,65 @@
+"""Validation mode (ops/validate.py): launch-checked native ops with an op history, non-finite tracking,
+and the pre-launch op log -- exercised on CPU with stand-in extension functions (the GPU test in
+tests/test_executor_gpu.py runs it over the real kernels)."""
+import pytest
+import torch
+
+from pytorch_distributed_template_amd.ops import validate
+
+
+def _v(level, **kw):
+    return validate.Validator(level, history=4, sync=lambda: None, capturing=lambda: False, **kw)
+
+
+def test_level1_names_the_failing_op_and_history():
+    v = _v(1)
+    ok = v.wrap("ok_op", lambda t: t.add_(1))
+    def boom(t):
+        raise RuntimeError("invalid device function")
+    bad = v.wrap("bad_op", boom)
+    t = torch.zeros(3)
+    for _ in range(5):
+        ok(t)
+    assert torch.equal(t, torch.full((3,), 5.0))
+    with pytest.raises(validate.ValidationError) as e:
+        bad(torch.ones(2, 2))
+    msg = str(e.value)
+    assert "`bad_op` failed: invalid device function" in msg and "float32[2, 2]" in msg
+    assert msg.count("ok_op") == 3  # history holds the last 4 ops: 3 x ok_op + bad_op
+    assert v.calls == 6
+
+
+def test_level2_flags_the_op_that_creates_nonfinite():
+    v = _v(2)
+    src = torch.tensor([1.0, float("nan"), 2.0])  # already non-finite: not this op's fault
+    out = torch.zeros(3)
+    copy = v.wrap("copy_op", lambda s, o: o.copy_(torch.nan_to_num(s)))
+    poison = v.wrap("poison_op", lambda s, o: o.copy_(s))
+    copy(src, out)
+    with pytest.raises(validate.NonFiniteError) as e:
+        poison(src, out)
+    assert "`poison_op` wrote 1 non-finite value(s) into argument #1" in str(e.value)
+    # level 1 does not scan
+    _v(1).wrap("poison_op", lambda s, o: o.copy_(s))(src, torch.zeros(3))
+
+
+def test_capture_and_log(tmp_path):
+    log = tmp_path / "ops.log"
+    v = validate.Validator(1, sync=lambda: (_ for _ in ()).throw(RuntimeError("sync inside capture")),
+                           capturing=lambda: True, log_path=str(log))
+    v.wrap("captured", lambda: 7)()  # no sync, no record while capturing
+    assert v.calls == 0
+    v2 = validate.Validator(1, sync=lambda: None, capturing=lambda: False, log_path=str(log))
+    v2.wrap("first", lambda: None)()
+    v2.wrap("second", lambda x: None)(torch.ones(1, dtype=torch.float16))
+    assert log.read_text().splitlines() == ["first (no tensors)", "second #0:float16[1]"]
+
+
+def test_env_wrapping(monkeypatch):
+    monkeypatch.setenv("PDT_VALIDATE", "0")
+    f = lambda: 1  # noqa: E731
+    assert validate.maybe_wrap("f", f) is f
+    monkeypatch.setenv("PDT_VALIDATE", "2")
+    w = validate.maybe_wrap("f", f)
+    assert w is not f and w.__wrapped__ is f and w() == 1
+    assert validate.maybe_wrap("T", torch.nn.Module) is torch.nn.Module  # classes pass through
