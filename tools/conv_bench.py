@@ -111,7 +111,18 @@ def main():
                 C.conv_fwd(x, w, y, None, sp, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1,
                            0, 0, bm, bn, bk, 0)
             row[f"fwd_{bm}x{bn}x{bk}"] = round(flops / timeit(f, a.reps) / 1e9, 1)
-        if a.r50:  # forward-with-statistics tiles only
+        if a.r50:  # forward-with-statistics tiles only; + the best tile's effective HBM rate (x + w + y bytes)
+            best = max(v for kk, v in row.items() if kk.startswith("fwd_"))
+            nbytes = 2.0 * (N * H * H * ci + co * k * k * ci + N * P * P * co)
+            row["best_TBps"] = round(best * 1e12 / flops * nbytes / 1e12, 2)
+            row["best_us"] = round(flops / (best * 1e12) * 1e6, 1)
+            bt = max((kk for kk in row if kk.startswith("fwd_")), key=lambda kk: row[kk])
+            bm, bn, bk = (int(v) for v in bt[4:].split("x"))
+            row["best_nostats_us"] = round(timeit(lambda: C.conv_fwd(
+                x, w, y, None, None, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1, 0, 0, bm, bn,
+                bk, 0), a.reps) * 1e3, 1)
+            row["copy_y_us"] = round(timeit(lambda: y.copy_(dy), a.reps) * 1e3, 1)  # read + write of y's bytes
+            row["fill_y_us"] = round(timeit(lambda: y.fill_(1.0), a.reps) * 1e3, 1)  # write-only
             print(json.dumps(row), flush=True)
             continue
         dx = torch.empty(N, H, H, ci, device=dev, dtype=torch.bfloat16)
