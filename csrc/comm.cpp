@@ -18,6 +18,9 @@
 //     unblocks a host thread stuck in RCCL) and ends the process with a non-zero status, so the launcher
 //     tears the group down instead of every rank hanging in a ring that will never complete.
 //     async_error()/abort() stay available for explicit polling.
+//   * HIP graphs: every call only enqueues work and orders streams with events, so a training step that
+//     issues its collectives through this class can be captured (the comm stream joins the capture through
+//     join_compute's event and leaves it through wait()); captured collectives are not watchdog-tracked.
 // RCCL is the copy PyTorch already loaded (same soname), so there is one RCCL instance per process.
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -124,8 +127,14 @@ class Communicator {
   double timeout_s() const { return timeout_s_; }
 
   // Watchdog bookkeeping: a completion event on the comm stream behind the collective just enqueued.
+  // Not while the caller's stream is being captured into a HIP graph: the collective is then a graph node
+  // (replayed later, possibly many times) and an event recorded now would never complete as a real event.
   void track(const char* what) {
     if (timeout_s_ <= 0) return;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(at::hip::getCurrentHIPStream().stream(), &cap) == hipSuccess &&
+        cap != hipStreamCaptureStatusNone)
+      return;
     std::lock_guard<std::mutex> lk(mu_);
     hipEvent_t ev;
     if (!free_evs_.empty()) {

@@ -85,8 +85,12 @@ class NativeTrainer:
         self.broadcast_buffers = broadcast_buffers and (self.distributed or self.ncomm is not None)
         self.reduce_metrics = reduce_metrics and (self.distributed or self.ncomm is not None)
         self._steps = 0
-        # whole-step HIP graph (launch-bound small batches): single-process only, collectives stay eager
-        self.use_graph = graph and not self.distributed and self.ncomm is None
+        # whole-step HIP graph (launch-bound small batches, e.g. the reference's -b 1200 split over 8 GPUs = 150
+        # per GPU): single process, or any world on the native communicator, whose collectives (buffer
+        # broadcast, gradient buckets, SyncBN statistics, metrics) are captured into the graph with the kernels
+        # (RCCL supports stream capture; every rank captures and replays the same sequence).  c10d's
+        # ProcessGroupNCCL collectives stay eager, so world > 1 on --comm torch runs without a graph.
+        self.use_graph = graph and (not self.distributed or self.ncomm is not None)
         self._graphs = {}
         self._graph_warm = 0
 

@@ -58,14 +58,20 @@ def test_native_bucketer_step_matches_default():
     assert torch.allclose(mn, mt)
 
 
-def test_graphed_training_step_matches_eager():
-    """Whole-step HIP graph replay == eager steps (same data, same updates), including an LR change."""
+@pytest.mark.parametrize("comm,sync_bn", [("torch", False), ("native", False), ("native", True)])
+def test_graphed_training_step_matches_eager(comm, sync_bn):
+    """Whole-step HIP graph replay == eager steps (same data, same updates), including an LR change.  With the
+    native communicator (a real RCCL communicator of one rank, watchdog on) the buffer broadcast, gradient
+    bucket all-reduces, metric all-reduce and SyncBN statistic all-reduces are captured into the graph too."""
     from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
     from pytorch_distributed_template_amd.models import registry
 
     def run(graph):
         torch.manual_seed(0)
-        tr = NativeTrainer(registry.create("resnet18", num_classes=100), DEV, dtype=torch.bfloat16, graph=graph)
+        kw = dict(comm="native", force_comm=True, comm_timeout_s=120.0, sync_bn=sync_bn) if comm == "native" else {}
+        tr = NativeTrainer(registry.create("resnet18", num_classes=100), DEV, dtype=torch.bfloat16, graph=graph,
+                           **kw)
+        assert tr.use_graph == graph and (tr.ncomm is not None) == (comm == "native")
         g = torch.Generator(device=DEV).manual_seed(3)
         batches = [(torch.randn(8, 3, 64, 64, device=DEV, generator=g),
                     torch.randint(0, 100, (8,), device=DEV, generator=g)) for _ in range(3)]
@@ -81,6 +87,12 @@ def test_graphed_training_step_matches_eager():
     tg, mg = run(True)
     te, me = run(False)
     assert len(tg._graphs) == 2 and tg.optimizer.step_count == te.optimizer.step_count == 6
+    if comm == "native":
+        # the watchdog drains every tracked collective (one recorded inside the capture would never complete
+        # as an event and would end the process with a false timeout)
+        import time
+        time.sleep(0.3)
+        assert tg.ncomm.comm.pending() == 0
     assert torch.allclose(mg, me, rtol=1e-3, atol=1e-3)
     assert ((tg.flat.data - te.flat.data).norm() / te.flat.data.norm()).item() < 1e-4
 
