@@ -36,7 +36,7 @@ def main():
         iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r) for r in st]
         t0 = iv[0][0] if si == 0 else int(steps[si - 1][-1]["End_Timestamp"])
         t1 = max(e for _, e, _ in iv)
-        busy, gaps, end, prev = 0, [], t0, None
+        busy, gaps, end, prev = 0, [], t0, (steps[si - 1][-1] if si else None)
         for s, e, r in iv:
             if s > end:
                 gaps.append((s - end, prev, r))
@@ -50,7 +50,7 @@ def main():
         if si == (a.step % len(steps)):
             gaps.sort(key=lambda g: -g[0])
             for d, p, r in gaps[:a.gaps]:
-                print(f"    gap {d / 1e3:8.1f} us  after {_name(p) if p else '<step start>':60s} before {_name(r)}")
+                print(f"    gap {d / 1e3:8.1f} us  after {_name(p) if p else '<trace start>':60s} before {_name(r)}")
 
 
 if __name__ == "__main__":
