@@ -14,6 +14,7 @@ The printed running averages are identical either way.
 from __future__ import annotations
 
 import datetime
+import functools
 import os
 import random
 import sys
@@ -89,6 +90,7 @@ class _DeviceMeter:
         return a[0], a[1]
 
 
+@functools.lru_cache(maxsize=None)
 def _fault_spec():
     """``PDT_FAULT_INJECT=rank:iteration[:exit|hang[:epoch]]`` -- the fault-injection hook of SURVEY §5 ("kill rank k
     at step s"): global rank ``rank`` dies (``exit``: status 13 without any teardown, like a crashed process) or
