@@ -60,6 +60,8 @@ def _parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the benchmark) or gloo (multi-rank rehearsal on fewer GPUs than ranks)")
     ap.add_argument("--comm-timeout", type=float, default=900.0, help="native comm watchdog timeout (s)")
+    ap.add_argument("--grad-compress", default="none", choices=["none", "bf16"],
+                    help="native comm: bf16 gradient all-reduce (default none: fp32, the reference's precision)")
     return ap.parse_args()
 
 
@@ -129,6 +131,7 @@ def main() -> int:
                        use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb,
                        graph=args.graph, autotune=args.autotune, comm=comm, force_comm=args.force_comm,
                        comm_timeout_s=args.comm_timeout, time_comm=True,
+                       grad_compress=args.grad_compress if comm == "native" else "none",
                        last_bucket_mb=args.last_bucket_mb if args.last_bucket_mb > 0 else None)
     nc = tr.ncomm
 
@@ -215,6 +218,7 @@ def main() -> int:
                        "comm_selftest": comm_ok,
                        "params_equal_across_ranks": params_equal,
                        "bucket_sizes_mb": [round(x, 3) for x in tr.bucketer.bucket_sizes_mb()] if world > 1 else [],
+                       "grad_compress": args.grad_compress if comm == "native" else "none",
                        "exposed_comm_ms_per_step": round(float(exp_t.item()), 3) if world > 1 or nc is not None
                        else None,
                        "last_loss": round(float(met[0].item()), 4) if met is not None else None}}), flush=True)

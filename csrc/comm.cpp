@@ -11,6 +11,9 @@
 //     launches that bucket's all-reduce (in place, SUM; 1/world is folded into the SGD kernel) as soon as
 //     its count reaches zero, so the reductions overlap the rest of backward; finish() launches leftover
 //     buckets (unused parameters) and joins the comm stream into the compute stream.
+//     Optional bf16 gradient compression (``compress``; upstream DDP's bf16_compress_hook, SURVEY §5 comm notes):
+//     a bucket is cast to a bf16 scratch, all-reduced in bf16 (half the xGMI bytes) and widened back into the
+//     fp32 gradient, all three on the comm stream.
 //   * Failure handling (the reference has none; c10d's ProcessGroupNCCL watchdog is the model): every
 //     collective records a completion event on the comm stream; a watchdog thread polls those events and
 //     ncclCommGetAsyncError.  A collective still pending after ``timeout_s`` (the trainer's
@@ -26,6 +29,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <torch/extension.h>
+
+#include "dtypes.h"
+#include "kernels/optim.h"
 
 #include <atomic>
 #include <chrono>
@@ -296,9 +302,11 @@ class Communicator {
 class Bucketer {
  public:
   Bucketer(std::shared_ptr<Communicator> comm, Tensor flat_grad, std::vector<int64_t> lo, std::vector<int64_t> hi,
-           std::vector<int64_t> param_bucket)
+           std::vector<int64_t> param_bucket, int64_t compress = 0)
       : comm_(std::move(comm)), grad_(std::move(flat_grad)), lo_(std::move(lo)), hi_(std::move(hi)),
-        param_bucket_(std::move(param_bucket)) {
+        param_bucket_(std::move(param_bucket)), compress_(compress) {
+    TORCH_CHECK(compress_ == 0 || compress_ == 1, "bucketer: compress must be 0 (fp32) or 1 (bf16)");
+    if (compress_) scratch_ = at::empty({grad_.numel()}, grad_.options().dtype(at::kBFloat16));
     TORCH_CHECK(grad_.is_cuda() && grad_.scalar_type() == at::kFloat && grad_.is_contiguous(),
                 "bucketer: flat gradient must be a contiguous fp32 GPU tensor");
     TORCH_CHECK(lo_.size() == hi_.size() && !lo_.empty(), "bucketer: bad bucket ranges");
@@ -333,7 +341,15 @@ class Bucketer {
   void launch(size_t b) {
     comm_->join_compute();
     float* p = grad_.data_ptr<float>() + lo_[b];
-    PDT_NCCL_CHECK(ncclAllReduce(p, p, hi_[b] - lo_[b], ncclFloat32, ncclSum, comm_->comm(), comm_->stream()));
+    const int64_t n = hi_[b] - lo_[b];
+    if (compress_) {
+      uint16_t* h = reinterpret_cast<uint16_t*>(scratch_.data_ptr()) + lo_[b];
+      pdt::cast16_launch(pdt::kBF16, p, h, n, comm_->stream());
+      PDT_NCCL_CHECK(ncclAllReduce(h, h, n, ncclBfloat16, ncclSum, comm_->comm(), comm_->stream()));
+      pdt::widen16_launch(pdt::kBF16, h, p, n, comm_->stream());
+    } else {
+      PDT_NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, comm_->comm(), comm_->stream()));
+    }
     comm_->track("gradient bucket all_reduce");
     launched_[b] = true;
   }
@@ -345,6 +361,8 @@ class Bucketer {
   Tensor grad_;
   std::vector<int64_t> lo_, hi_, param_bucket_, nparams_, pending_;
   std::vector<bool> launched_;
+  int64_t compress_ = 0;
+  Tensor scratch_;  // bf16 image of the flat gradient (compress_)
 };
 
 void register_comm(py::module& m) {
@@ -373,7 +391,9 @@ void register_comm(py::module& m) {
       .def("destroy", &Communicator::destroy);
   py::class_<Bucketer>(m, "Bucketer")
       .def(py::init<std::shared_ptr<Communicator>, Tensor, std::vector<int64_t>, std::vector<int64_t>,
-                    std::vector<int64_t>>())
+                    std::vector<int64_t>, int64_t>(),
+           py::arg("comm"), py::arg("flat_grad"), py::arg("lo"), py::arg("hi"), py::arg("param_bucket"),
+           py::arg("compress") = 0)
       .def("ready", &Bucketer::ready)
       .def("finish", &Bucketer::finish)
       .def("launched", &Bucketer::launched);

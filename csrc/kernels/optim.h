@@ -7,6 +7,7 @@ void sgd_launch(int dtype, float* p, const float* g, float* buf, uint16_t* shado
                 float lr, float momentum, float wd, float gscale, const float* loss_scale, const float* found_inf,
                 bool first, hipStream_t s);
 void cast16_launch(int dtype, const float* p, uint16_t* out, int64_t n, hipStream_t s);
+void widen16_launch(int dtype, const uint16_t* in, float* out, int64_t n, hipStream_t s);
 void amp_update_launch(float* scale, int* tracker, float* found_inf, float growth, float backoff, int interval,
                        hipStream_t s);
 void gather16_launch(const uint16_t* src, const int* idx, uint16_t* dst, int64_t n, hipStream_t s);

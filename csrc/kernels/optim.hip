@@ -84,6 +84,20 @@ void cast16_launch(int dtype, const float* p, uint16_t* out, int64_t n, hipStrea
     hipLaunchKernelGGL(cast16_kernel<kF16>, dim3(ew_blocks(n)), dim3(256), 0, s, p, out, n);
 }
 
+// 16-bit -> fp32 widening (gradient-compression epilogue of the native bucketer: bf16 all-reduce, fp32 grads)
+template <int DT>
+__global__ __launch_bounds__(256) void widen16_kernel(const uint16_t* __restrict__ in, float* __restrict__ out, int64_t n) {
+  using E = E16<DT>;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = E::to_f(in[i]);
+}
+
+void widen16_launch(int dtype, const uint16_t* in, float* out, int64_t n, hipStream_t s) {
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(widen16_kernel<kBF16>, dim3(ew_blocks(n)), dim3(256), 0, s, in, out, n);
+  else
+    hipLaunchKernelGGL(widen16_kernel<kF16>, dim3(ew_blocks(n)), dim3(256), 0, s, in, out, n);
+}
+
 // GradScaler._amp_update_scale_: scale *= backoff on inf (tracker = 0), else tracker += 1 and
 // scale *= growth when tracker reaches the interval (tracker = 0).  Resets found_inf for the next step.
 __global__ void amp_update_kernel(float* scale, int* tracker, float* found_inf, float growth, float backoff,

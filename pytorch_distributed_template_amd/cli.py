@@ -139,6 +139,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
                    help="native engine collectives: this framework's own RCCL communicator and C++ gradient "
                         "bucketer (default; torch.distributed then only provides the rendezvous store) or "
                         "torch.distributed (RCCL via c10d)")
+    g.add_argument("--grad-compress", default="none", choices=["none", "bf16"],
+                   help="native communicator: all-reduce the gradient buckets in bf16 (half the bytes; upstream "
+                        "DDP's bf16_compress_hook). Default none: fp32 like the reference")
     g.add_argument("--dist-timeout", type=float, default=1800.0,
                    help="collective timeout in seconds (a hung rank fails the job instead of hanging it)")
     g.add_argument("--profile", default=False, type=str2bool, nargs="?", const=True,

@@ -30,7 +30,8 @@ class NativeTrainer:
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
                  force_comm: bool = False, graph: bool = False, last_bucket_mb: Optional[float] = 1.0,
-                 comm_timeout_s: float = 0.0, time_comm: bool = False, eval_fp32: bool = False):
+                 comm_timeout_s: float = 0.0, time_comm: bool = False, eval_fp32: bool = False,
+                 grad_compress: str = "none"):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -53,7 +54,9 @@ class NativeTrainer:
                               last_bucket_mb=last_bucket_mb)
         if self.ncomm is not None:
             from ..parallel.comm import NativeBucketer
-            self.bucketer = NativeBucketer(layout, self.ncomm)
+            self.bucketer = NativeBucketer(layout, self.ncomm, compress=grad_compress)
+        elif grad_compress != "none":
+            raise ValueError("--grad-compress needs the native communicator (--comm native)")
         else:
             self.bucketer = layout
         # HIP events around bucketer.finish(): the time the compute stream waits for gradient all-reduces

@@ -243,6 +243,7 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
                              comm=getattr(args, "comm", "native"), graph=bool(getattr(args, "graph", False)),
                              last_bucket_mb=lb if lb > 0 else None,
                              comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)),
+                             grad_compress=getattr(args, "grad_compress", "none"),
                              eval_fp32=getattr(args, "eval_precision", "compute") == "fp32", **kw)
     from .torch_trainer import TorchTrainer
     return TorchTrainer(model, device, dtype=dtype, **kw, **torch_kw)

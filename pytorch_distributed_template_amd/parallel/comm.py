@@ -94,15 +94,21 @@ class NativeComm:
 class NativeBucketer:
     """Drop-in for :class:`~.ddp.GradBucketer` backed by the C++ bucketer (same bucket layout)."""
 
-    def __init__(self, layout, comm: NativeComm):
+    def __init__(self, layout, comm: NativeComm, compress: str = "none"):
+        """``compress="bf16"``: buckets are all-reduced in bf16 (cast on the comm stream, half the bytes on
+        xGMI, widened back into the fp32 gradient) -- upstream DDP's ``bf16_compress_hook``; off by default, as
+        the reference all-reduces fp32 gradients."""
+        if compress not in ("none", "bf16"):
+            raise ValueError(f"gradient compression must be 'none' or 'bf16', got {compress!r}")
         self.world = comm.world
         self.comm = comm
+        self.compress = compress
         self.buckets = layout.buckets
         pb: List[int] = [0] * len(layout.flat.slots)
         for pid, bid in layout.bucket_of.items():
             pb[pid] = bid
         self._impl = native.C.Bucketer(comm.comm, layout.flat.grad, [b["lo"] for b in self.buckets],
-                                       [b["hi"] for b in self.buckets], pb)
+                                       [b["hi"] for b in self.buckets], pb, 1 if compress == "bf16" else 0)
 
     def grad_ready(self, pid: int) -> None:
         self._impl.ready(pid)

@@ -58,6 +58,37 @@ def test_native_bucketer_step_matches_default():
     assert torch.allclose(mn, mt)
 
 
+def test_bucketer_bf16_gradient_compression():
+    """--grad-compress bf16: each bucket is cast to bf16 on the comm stream, all-reduced in bf16 and widened back,
+    so at a world of one the fp32 gradient comes back exactly bf16-rounded; a training step runs on it."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    torch.manual_seed(0)
+    tr = NativeTrainer(registry.create("resnet18", num_classes=100), DEV, dtype=torch.bfloat16, comm="native",
+                       force_comm=True, bucket_cap_mb=4.0, grad_compress="bf16")
+    assert tr.bucketer.compress == "bf16" and len(tr.bucketer.buckets) > 1
+    g = tr.flat.grad
+    g.copy_(torch.randn_like(g) * 1e-2)
+    ref = g.clone()
+    covered = torch.zeros(g.numel(), dtype=torch.bool, device=DEV)  # buckets skip the flat buffer's alignment pads
+    for b in tr.bucketer.buckets:
+        covered[b["lo"]:b["hi"]] = True
+    ref[covered] = ref[covered].to(torch.bfloat16).float()
+    assert not torch.equal(g, ref)
+    for pid in range(len(tr.flat.slots)):
+        tr.bucketer.grad_ready(pid)
+    tr.bucketer.finish()
+    torch.cuda.synchronize()
+    assert torch.equal(g, ref)
+    x = torch.randn(8, 3, 64, 64, device=DEV)
+    t = torch.randint(0, 100, (8,), device=DEV)
+    _, met = tr.train_step(x, t)
+    assert torch.isfinite(met).all() and torch.isfinite(tr.flat.data).all()
+    with pytest.raises(ValueError, match="native communicator"):
+        NativeTrainer(registry.create("resnet18", num_classes=100), DEV, dtype=torch.bfloat16, comm="torch",
+                      grad_compress="bf16")
+
+
 @pytest.mark.parametrize("comm,sync_bn", [("torch", False), ("native", False), ("native", True)])
 def test_graphed_training_step_matches_eager(comm, sync_bn):
     """Whole-step HIP graph replay == eager steps (same data, same updates), including an LR change.  With the
