@@ -316,9 +316,10 @@ class ResNetExecutor:
                 self.C.wgrad_3x3c64_supported(64, 64, 3, 3, W, 1, 1))
 
     def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None,
-                 pre=None):
+                 pre=None, stats_tag=None):
         if pre is not None:  # x is the producer conv's raw output; pre = its BN coefficients (layer1 only)
-            sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64)
+            key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
+            sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
             self.C.conv_fwd_pre(x, self._w(c), y, sp, pre, N, H, W)
             return H, W, sp, N * H * W
         cin = cin or c.cin
@@ -335,7 +336,8 @@ class ResNetExecutor:
         M = N * P * Q
         sp = None
         if stats:
-            sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64)
+            key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
+            sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
         wt = self._w(c) if w is None else w
 
         def launch(bm, bn):
@@ -383,6 +385,23 @@ class ResNetExecutor:
         count = count * self.syncbn_world
         self.C.bn_finalize(bn.sums, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
                            bn.mod.running_mean, bn.mod.running_var, bn.coef, True)
+
+    def bn_train_finalize_pair(self, bn_a: _BN, sp_a, count_a: int, bn_b: _BN, sp_b, count_b: int):
+        """Two BatchNorms whose statistics are ready together (a downsample block's main-branch and downsample
+        BN): with SyncBN, ONE all-reduce carries both layers' sums (one latency-bound collective fewer per
+        downsample block); without it, the plain per-layer finalize."""
+        if not self.syncbn:
+            self.bn_train_finalize(bn_a, sp_a, 0, count_a)
+            self.bn_train_finalize(bn_b, sp_b, 0, count_b)
+            return
+        ca, cb = bn_a.C, bn_b.C
+        pair = self._buf(("syncbn_pair", ca, cb), 2 * (ca + cb), torch.float64)
+        self.C.bn_slot_sum(sp_a, ca, 2, pair[:2 * ca])
+        self.C.bn_slot_sum(sp_b, cb, 2, pair[2 * ca:])
+        self._sync_sum(pair)
+        for bn, sums, cnt in ((bn_a, pair[:2 * ca], count_a), (bn_b, pair[2 * ca:], count_b)):
+            self.C.bn_finalize(sums, float(cnt * self.syncbn_world), self._p(bn.gslot), self._p(bn.bslot), bn.eps,
+                               bn.momentum, bn.mod.running_mean, bn.mod.running_var, bn.coef, True)
 
     def bn_eval(self, bn: _BN):
         self.C.bn_eval_coef(self._p(bn.gslot), self._p(bn.bslot), bn.mod.running_mean, bn.mod.running_var,
@@ -549,8 +568,14 @@ class ResNetExecutor:
             for ci, (c, bn) in enumerate(zip(b["convs"], b["bns"])):
                 P, Q = c.out_hw(h, w)
                 y = self._buf(("y", bi, ci), N * P * Q * c.cout)
-                _, _, sp, tiles = self.conv_fwd(c, cur, N, h, w, y, train, pre=pre)
-                if train:
+                # SyncBN + downsample block: the last BN's statistics wait for the downsample conv's and share
+                # its all-reduce (bn_train_finalize_pair); its partial rows get their own buffer meanwhile
+                defer = train and self.syncbn and ci == nconv - 1 and b["ds_conv"] is not None
+                _, _, sp, tiles = self.conv_fwd(c, cur, N, h, w, y, train, pre=pre,
+                                                stats_tag="deferred" if defer else None)
+                if defer:
+                    deferred = (bn, sp, N * P * Q)
+                elif train:
                     self.bn_train_finalize(bn, sp, tiles, N * P * Q)
                 else:
                     self.bn_eval(bn)
@@ -579,7 +604,9 @@ class ResNetExecutor:
                 dc, dbn = b["ds_conv"], b["ds_bn"]
                 yd = self._buf(("yd", bi), N * h * w * dc.cout)
                 _, _, sp, tiles = self.conv_fwd(dc, x, N, Hc, Wc, yd, train)
-                if train:
+                if train and self.syncbn:
+                    self.bn_train_finalize_pair(deferred[0], deferred[1], deferred[2], dbn, sp, N * h * w)
+                elif train:
                     self.bn_train_finalize(dbn, sp, tiles, N * h * w)
                 else:
                     self.bn_eval(dbn)
