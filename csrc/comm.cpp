@@ -135,12 +135,13 @@ class Communicator {
   // Watchdog bookkeeping: a completion event on the comm stream behind the collective just enqueued.
   // Not while the caller's stream is being captured into a HIP graph: the collective is then a graph node
   // (replayed later, possibly many times) and an event recorded now would never complete as a real event.
-  void track(const char* what) {
+  void track(const char* what, hipStream_t on = nullptr) {
     if (timeout_s_ <= 0) return;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(at::hip::getCurrentHIPStream().stream(), &cap) == hipSuccess &&
         cap != hipStreamCaptureStatusNone)
       return;
+    if (on == nullptr) on = stream_;
     std::lock_guard<std::mutex> lk(mu_);
     hipEvent_t ev;
     if (!free_evs_.empty()) {
@@ -149,7 +150,7 @@ class Communicator {
     } else {
       PDT_HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
-    PDT_HIP_OK(hipEventRecord(ev, stream_));
+    PDT_HIP_OK(hipEventRecord(ev, on));
     pending_.push_back({ev, std::chrono::steady_clock::now(), what});
   }
   // Test hook: a pending "collective" that never completes, enqueued ``age_s`` seconds ago.
@@ -183,6 +184,16 @@ class Communicator {
     PDT_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), nccl_op(op), comm(), stream_));
     track("all_reduce");
     if (!async_op) wait();
+  }
+  // In-place all-reduce enqueued on the CALLER's (compute) stream: no event hop to the comm stream and back.
+  // Only for collectives whose order relative to every comm-stream collective is fixed by the compute stream
+  // itself -- e.g. SyncBN forward statistics, issued while no gradient bucket is in flight -- since RCCL needs
+  // the same operation order on every rank.
+  void all_reduce_inline(Tensor& t, const std::string& op) {
+    check(t);
+    hipStream_t cs = at::hip::getCurrentHIPStream().stream();
+    PDT_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), nccl_op(op), comm(), cs));
+    track("all_reduce (compute stream)", cs);
   }
   void broadcast(Tensor& t, int root, bool async_op) {
     check(t);
@@ -382,6 +393,7 @@ void register_comm(py::module& m) {
       .def("pending", &Communicator::pending)
       .def("inject_stall", &Communicator::inject_stall)
       .def("all_reduce", &Communicator::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
+      .def("all_reduce_inline", &Communicator::all_reduce_inline, py::arg("t"), py::arg("op") = "sum")
       .def("broadcast", &Communicator::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
       .def("all_gather", &Communicator::all_gather, py::arg("inp"), py::arg("out"), py::arg("async_op") = false)
       .def("barrier", &Communicator::barrier)

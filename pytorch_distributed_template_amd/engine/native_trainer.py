@@ -12,6 +12,7 @@ two scalar all-reduces) and read by the caller only when it logs.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -65,9 +66,15 @@ class NativeTrainer:
         # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full
         # SyncBN path with identity all-reduces), else over torch.distributed at world > 1
         nsync = sync_bn and self.ncomm is not None
+        # forward statistics go straight onto the compute stream (no gradient bucket is in flight during the
+        # forward pass, so RCCL sees the same order on every rank); backward ones share the comm stream with the
+        # buckets.  PDT_SYNCBN_INLINE=0 keeps the forward on the comm stream too.
+        inline = nsync and os.environ.get("PDT_SYNCBN_INLINE", "1") != "0"
         sync_kw = dict(syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed and not nsync)
                        else None, syncbn_allreduce=self.ncomm.all_reduce if nsync else None,
                        syncbn_world=self.ncomm.world if nsync else 0)
+        if inline and dtype != torch.float32:
+            sync_kw["syncbn_allreduce_fwd"] = self.ncomm.all_reduce_inline
         if dtype == torch.float32:
             from ..models.executor32 import ResNetExecutor32
             self.executor = ResNetExecutor32(model, self.flat, self.device, grad_ready=self.bucketer.grad_ready,

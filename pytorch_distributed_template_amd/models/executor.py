@@ -81,7 +81,8 @@ class ResNetExecutor:
     def __init__(self, model: ResNet, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None,
                  syncbn_group=None, wgrad_blocks: int = 2048, wgrad_blocks_1x1: int = 512, autotune: bool = False,
-                 syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0):
+                 syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0,
+                 syncbn_allreduce_fwd: Optional[Callable[[torch.Tensor], None]] = None):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not isinstance(model, ResNet) or model.groups != 1:
@@ -113,7 +114,8 @@ class ResNetExecutor:
         if syncbn_allreduce is not None:
             self.syncbn_world = int(syncbn_world) if syncbn_world else 1
             self._sync_sum = syncbn_allreduce
-        elif syncbn_group is not None:
+        self._sync_sum_fwd = syncbn_allreduce_fwd  # forward statistics (None: same as _sync_sum)
+        if syncbn_group is not None and syncbn_allreduce is None:
             import torch.distributed as dist
             self.syncbn_world = dist.get_world_size(syncbn_group)
             self._sync_sum = lambda t: dist.all_reduce(t, group=syncbn_group)
@@ -381,7 +383,7 @@ class ResNetExecutor:
                                      bn.mod.running_mean, bn.mod.running_var, bn.coef, bn.sums, True)
             return
         self.C.bn_slot_sum(sp, C, 2, bn.sums)
-        self._sync_sum(bn.sums)
+        (self._sync_sum_fwd or self._sync_sum)(bn.sums)
         count = count * self.syncbn_world
         self.C.bn_finalize(bn.sums, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
                            bn.mod.running_mean, bn.mod.running_var, bn.coef, True)
@@ -398,7 +400,7 @@ class ResNetExecutor:
         pair = self._buf(("syncbn_pair", ca, cb), 2 * (ca + cb), torch.float64)
         self.C.bn_slot_sum(sp_a, ca, 2, pair[:2 * ca])
         self.C.bn_slot_sum(sp_b, cb, 2, pair[2 * ca:])
-        self._sync_sum(pair)
+        (self._sync_sum_fwd or self._sync_sum)(pair)
         for bn, sums, cnt in ((bn_a, pair[:2 * ca], count_a), (bn_b, pair[2 * ca:], count_b)):
             self.C.bn_finalize(sums, float(cnt * self.syncbn_world), self._p(bn.gslot), self._p(bn.bslot), bn.eps,
                                bn.momentum, bn.mod.running_mean, bn.mod.running_var, bn.coef, True)

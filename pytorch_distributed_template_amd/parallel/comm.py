@@ -64,6 +64,11 @@ class NativeComm:
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> None:
         self.comm.all_reduce(t, op, async_op)
 
+    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum") -> None:
+        """All-reduce on the caller's stream (no comm-stream round trip); the caller guarantees that no
+        comm-stream collective can be reordered against it (see csrc/comm.cpp)."""
+        self.comm.all_reduce_inline(t, op)
+
     def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False) -> None:
         self.comm.broadcast(t, src, async_op)
 
