@@ -195,6 +195,12 @@ class Communicator {
     PDT_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), nccl_op(op), comm(), cs));
     track("all_reduce (compute stream)", cs);
   }
+  void broadcast_inline(Tensor& t, int root) {  // on the caller's stream; same ordering contract as above
+    check(t);
+    hipStream_t cs = at::hip::getCurrentHIPStream().stream();
+    PDT_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), root, comm(), cs));
+    track("broadcast (compute stream)", cs);
+  }
   void broadcast(Tensor& t, int root, bool async_op) {
     check(t);
     join_compute();
@@ -394,6 +400,7 @@ void register_comm(py::module& m) {
       .def("inject_stall", &Communicator::inject_stall)
       .def("all_reduce", &Communicator::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
       .def("all_reduce_inline", &Communicator::all_reduce_inline, py::arg("t"), py::arg("op") = "sum")
+      .def("broadcast_inline", &Communicator::broadcast_inline, py::arg("t"), py::arg("root") = 0)
       .def("broadcast", &Communicator::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
       .def("all_gather", &Communicator::all_gather, py::arg("inp"), py::arg("out"), py::arg("async_op") = false)
       .def("barrier", &Communicator::barrier)

@@ -146,10 +146,12 @@ class NativeTrainer:
 
     def _sync_buffers(self) -> None:
         if self.ncomm is not None:
+            # start of a step: every earlier collective was joined into the compute stream, so the broadcasts
+            # go straight onto it (no comm-stream round trip; same RCCL order on every rank)
             if self.buffers.n_float:
-                self.ncomm.broadcast(self.buffers.fdata, 0)
+                self.ncomm.broadcast_inline(self.buffers.fdata, 0)
             if self.buffers.n_int:
-                self.ncomm.broadcast(self.buffers.idata, 0)
+                self.ncomm.broadcast_inline(self.buffers.idata, 0)
         else:
             sync_buffers(self.buffers, self.pg)
 

@@ -69,6 +69,10 @@ class NativeComm:
         comm-stream collective can be reordered against it (see csrc/comm.cpp)."""
         self.comm.all_reduce_inline(t, op)
 
+    def broadcast_inline(self, t: torch.Tensor, src: int = 0) -> None:
+        """Broadcast on the caller's stream (same ordering contract as :meth:`all_reduce_inline`)."""
+        self.comm.broadcast_inline(t, src)
+
     def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False) -> None:
         self.comm.broadcast(t, src, async_op)
 
