@@ -194,16 +194,9 @@ class NativeTrainer:
             # BatchNorm num_batches_tracked: issued ahead of the step so it is not a launch in the tail between the
             # last weight gradient and SGD (rocprof: ~20 us there)
             self.buffers.idata.add_(1)
-        # native communicator: the [loss, acc] all-reduce is enqueued on the comm stream between the loss and the
-        # backward (async: ahead of every gradient bucket, so it overlaps backward instead of trailing the last
-        # bucket); bucketer.finish() joins it like the buckets
-        early = self.reduce_metrics and self.ncomm is not None
         logits, met = self.executor.train_step(images, target, loss_scale=self.scaler.scale_tensor,
-                                               grad_div=float(images.shape[0]),
-                                               on_loss=(lambda m: self.ncomm.all_reduce(m, async_op=True))
-                                               if early else None)
-        if not early:
-            met = self._reduce(met)
+                                               grad_div=float(images.shape[0]))
+        met = self._reduce(met)
         if self._comm_events is not None and not torch.cuda.is_current_stream_capturing():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -212,8 +205,6 @@ class NativeTrainer:
             self._comm_events.append((e0, e1))
         else:
             self.bucketer.finish()
-        if early:
-            met.div_(self.world)  # after finish(): the compute stream has joined the comm stream
         self.scaler.unscale_check(self.flat.grad)
         self.optimizer.step(grad_scale=self.bucketer.grad_scale(), loss_scale=self.scaler.scale_tensor,
                             found_inf=self.scaler.found_inf)

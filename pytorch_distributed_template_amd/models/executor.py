@@ -648,15 +648,12 @@ class ResNetExecutor:
         return self._loss(saved, target, None, None, 1.0)
 
     @torch.no_grad()
-    def train_step(self, images, target, loss_scale: Optional[torch.Tensor] = None, grad_div: Optional[float] = None,
-                   on_loss=None):
+    def train_step(self, images, target, loss_scale: Optional[torch.Tensor] = None, grad_div: Optional[float] = None):
         """Forward + loss + backward.  Gradients (scaled by loss_scale / grad_div) land in flat.grad."""
         saved = self._forward(images, train=True)
         N = saved["N"]
         dlog = self._buf("dlogits", N * self.ncls_pad)
         logits, met = self._loss(saved, target, dlog, loss_scale, grad_div or N)
-        if on_loss is not None:  # e.g. the cross-rank metric all-reduce, issued ahead of every gradient bucket
-            on_loss(met)
         self._backward(saved, dlog)
         return logits, met
 

@@ -276,14 +276,11 @@ class ResNetExecutor32(ResNetExecutor):
         return out, met
 
     @torch.no_grad()
-    def train_step(self, images, target, loss_scale: Optional[torch.Tensor] = None, grad_div: Optional[float] = None,
-                   on_loss=None):
+    def train_step(self, images, target, loss_scale: Optional[torch.Tensor] = None, grad_div: Optional[float] = None):
         saved = self._forward(images, train=True)
         N = saved["N"]
         dlog = self._buf("dlogits32", N * self.ncls_pad, torch.float32)
         logits, met = self._loss(saved, target, dlog, loss_scale, grad_div or N)
-        if on_loss is not None:  # e.g. the cross-rank metric all-reduce, issued ahead of every gradient bucket
-            on_loss(met)
         self._backward(saved, dlog)
         return logits, met
 
