@@ -1,0 +1,41 @@
+"""Bitwise repeatability probe: N identically seeded native trainers (ResNet-18, 224 px, B = 16, 3 steps each) in
+one process must end with bit-identical fp32 parameters.
+
+    python tools/repeat_check.py [--reps 6]          (PDT_WGRAD_STREAM=0: single-stream schedule)
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import torch  # noqa: E402
+
+from _ddp_common import make_batch, make_model  # noqa: E402
+from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=6)
+    a = ap.parse_args()
+    X, T = make_batch(16, 224)
+    x, t = X.cuda(), T.cuda()
+    ref, bad = None, 0
+    for rep in range(a.reps):
+        tr = NativeTrainer(make_model(seed=0), "cuda:0", dtype=torch.bfloat16)
+        for _ in range(3):
+            tr.train_step(x, t)
+        torch.cuda.synchronize()
+        d = tr.flat.data.clone()
+        del tr
+        ref = d if ref is None else ref
+        eq = torch.equal(d, ref)
+        bad += not eq
+        print("rep", rep, "equal", eq, "maxdiff", (d - ref).abs().max().item(), flush=True)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
