@@ -19,13 +19,23 @@ from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--poison", action="store_true",
+                    help="before every trainer: fill the caching allocator's free memory with 0xFF bytes (NaN), "
+                         "so a read of memory no kernel wrote shows up as a difference")
+    ap.add_argument("--steps", type=int, default=3)
     a = ap.parse_args()
     X, T = make_batch(16, 224)
     x, t = X.cuda(), T.cuda()
     ref, bad = None, 0
     for rep in range(a.reps):
+        if a.poison and rep > 0:
+            torch.cuda.empty_cache()
+            big = torch.full((6 * 2 ** 30 // 4,), -1, dtype=torch.int32, device="cuda")
+            small = [torch.full((128 * 1024,), -1, dtype=torch.int32, device="cuda") for _ in range(1024)]
+            torch.cuda.synchronize()
+            del big, small
         tr = NativeTrainer(make_model(seed=0), "cuda:0", dtype=torch.bfloat16)
-        for _ in range(3):
+        for _ in range(a.steps):
             tr.train_step(x, t)
         torch.cuda.synchronize()
         d = tr.flat.data.clone()
