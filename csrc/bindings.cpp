@@ -706,6 +706,13 @@ void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
   pdt::gather32_launch(pf(src, "src"), idx.data_ptr<int>(), pf(dst, "dst"), dst.numel(), cur_stream());
 }
 
+// dst[idx[i]] = src[i]; the caller guarantees 0 <= idx < dst.numel() (checked where the index map is built)
+void scatter32(const Tensor& src, const Tensor& idx, Tensor& dst) {
+  check_dev(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == src.numel(), "scatter32: idx must be int32 like src");
+  pdt::scatter32_launch(pf(src, "src"), idx.data_ptr<int>(), pf(dst, "dst"), src.numel(), cur_stream());
+}
+
 // ------------------------------------------------------------------------------------------ fp32 path
 const float* pfc(const OptT& t, const char* name) { return t.has_value() ? pf(*t, name) : nullptr; }
 
@@ -939,6 +946,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_pack", &stem_pack);
   m.def("stem_pack_u8", &stem_pack_u8);
   m.def("gather32", &gather32);
+  m.def("scatter32", &scatter32);
   m.def("bw_probe", &bw_probe);
   m.def("conv32_fwd", &conv32_fwd);
   m.def("conv32_dgrad", &conv32_dgrad);

@@ -18,6 +18,7 @@ void stem_pack_launch(int dtype, const float* x, uint16_t* out, int N, int C, in
 void stem_pack_u8_launch(int dtype, const uint8_t* x, uint16_t* out, int N, int C, int H, int W, int pad, int Hp,
                          int Wp, const float* scale, const float* shift, hipStream_t s);
 void gather32_launch(const float* src, const int* idx, float* dst, int64_t n, hipStream_t s);
+void scatter32_launch(const float* src, const int* idx, float* dst, int64_t n, hipStream_t s);
 void bw_probe_launch(int mode, const uint16_t* x, const uint16_t* y, uint16_t* out, int64_t n, int blocks,
                      hipStream_t s);
 

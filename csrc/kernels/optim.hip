@@ -259,6 +259,18 @@ void gather32_launch(const float* src, const int* idx, float* dst, int64_t n, hi
   hipLaunchKernelGGL(gather32_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, src, idx, dst, n);
 }
 
+// dst[idx[i]] = src[i]: the inverse of gather32 over distinct indices (DataParallel replicas receive the fp32
+// values of the parameters the kernels read from the master copy -- BN affine, fc bias -- through a packed buffer)
+__global__ __launch_bounds__(256) void scatter32_kernel(const float* __restrict__ src, const int* __restrict__ idx,
+                                                        float* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[idx[i]] = src[i];
+}
+
+void scatter32_launch(const float* src, const int* idx, float* dst, int64_t n, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(scatter32_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, src, idx, dst, n);
+}
+
 }  // namespace pdt
 
 namespace pdt {

@@ -85,6 +85,7 @@ class NativeTrainer:
         # --eval-precision fp32: validation on the fp32 executor over the fp32 master weights (the reference
         # validates without autocast, `distributed_syncBN_amp.py:311-317`), whatever the training dtype
         self._eval32 = None
+        self._eval32_at = -1  # optimizer step count its derived layouts were gathered at
         if eval_fp32 and dtype != torch.float32:
             from ..models.executor32 import ResNetExecutor32
             self._eval32 = ResNetExecutor32(model, self.flat, self.device)
@@ -118,6 +119,7 @@ class NativeTrainer:
         """After ``model.load_state_dict`` (resume): re-derive the 16-bit shadow and the kernel weight layouts."""
         self.flat.refresh_shadow()
         self.executor.update_derived()
+        self._eval32_at = -1
 
     def exposed_comm_ms(self) -> Optional[float]:
         """Mean per-step exposed gradient-communication time since the last call (needs ``time_comm``)."""
@@ -217,7 +219,9 @@ class NativeTrainer:
         if self.broadcast_buffers and self._steps > 0:
             self._sync_buffers()
         if self._eval32 is not None:
-            self._eval32.update_derived()  # fp32 layouts of the current master weights
+            if self._eval32_at != self.optimizer.step_count:  # once per weight version, not per batch
+                self._eval32.update_derived()  # fp32 layouts of the current master weights
+                self._eval32_at = self.optimizer.step_count
             logits, met = self._eval32.eval_step(images, target)
         else:
             logits, met = self.executor.eval_step(images, target)

@@ -131,7 +131,7 @@ def train_epoch(loader, trainer, epoch: int, args, logger, writer, rank: int, de
             break
         data_times.update(time.time() - end)
         _maybe_inject_fault(rank, epoch, i)
-        if not getattr(trainer, "host_batches", False):  # native DP scatters host batches to every GPU itself
+        if not getattr(trainer, "host_batches", False):  # native DP: ShardedBatch, shard i already on GPU i
             images = images.to(device, non_blocking=True)
             target = target.to(device, non_blocking=True)
         with roctx_range("train_step", args.profile):
@@ -227,6 +227,8 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
         if engine == "native":
             from ..parallel.dp import NativeDataParallelTrainer
             ids = list(range(torch.cuda.device_count()))
+            if os.environ.get("PDT_DP_DEVICES"):  # rehearsal: e.g. "0,0" = two replicas sharing GPU 0
+                ids = [int(v) for v in os.environ["PDT_DP_DEVICES"].split(",")]
             return NativeDataParallelTrainer(model, ids, dtype=dtype, use_amp=use_amp, **common)
         from .torch_trainer import TorchTrainer
         # nn.DataParallel semantics on the torch engine too: the node-total batch is scattered over every
@@ -327,8 +329,9 @@ def main(mode: str, argv: Optional[list] = None) -> int:
     lr_scheduler = build_scheduler(args.lr_scheduler, optimizer, args.step, args.gamma)
     ddp_print("lr_scheduler: SGD MultiStepLR !!!", logger, rank)
 
+    shard_devices = [f"cuda:{i}" for i in trainer.device_ids] if getattr(trainer, "host_batches", False) else None
     train_loader, val_loader, train_sampler, val_sampler = build_loaders(args, world, rank, device, distributed,
-                                                                         args.batch_size)
+                                                                         args.batch_size, shard_devices=shard_devices)
     best_acc1, best_acc1_index = 0.0, 0
     start_epoch = args.start_epoch
     if args.resume:

@@ -277,7 +277,10 @@ class ResNetExecutor:
 
     def _side_wgrad(self, reads, fn) -> None:
         """Run ``fn`` (a weight gradient + its grad_ready) on the side stream behind the main stream's work
-        so far; later main-stream writes to ``reads`` (a tensor or a tuple of them) wait for it."""
+        so far; later main-stream writes to ``reads`` (a tensor or a tuple of them) wait for it.  ``reads`` must
+        list EVERY tensor ``fn`` reads that the main stream could rewrite before the end of backward: its dY, its
+        input activation, the producer-BN coefficients it applies (layer1), the stem's packed image / argmax /
+        pre-BN output; a buffer taken from ``_buf`` for writing then waits for the pending read."""
         if self.side is None:
             fn()
             return
@@ -427,7 +430,7 @@ class ResNetExecutor:
         def wg():
             self._wgrad(c.cout, xg, dy, N, Hx, Wx, Cx, R, S, P, Q, st, pad, self._g(c.slot), R * S * Cx, pre=pre)
             self.grad_ready(c.pid)
-        self._side_wgrad(dy, wg)
+        self._side_wgrad((dy, xg) + ((pre,) if pre is not None else ()), wg)
         # --- dgrad
         if dx is None:
             return
@@ -669,7 +672,7 @@ class ResNetExecutor:
             self._wgrad(self.ncls_pad, saved["feat"], dlog, N, 1, 1, self.feat, 1, 1, 1, 1, 1, 0,
                         self._g(self.fc_slot), self.feat, rows=self.ncls, cols=self.feat)
             self.grad_ready(self.fc_slot.index)
-        self._side_wgrad(dlog, fc_wg)
+        self._side_wgrad((dlog, saved["feat"]), fc_wg)
         dfeat = self._buf("dfeat", N * self.feat)
         wt = self.derived[self.fc_wt_off:self.fc_wt_off + self.ncls_pad * self.feat]
         bm, bn = _conv_tile(self.feat)
@@ -796,7 +799,7 @@ class ResNetExecutor:
                 Cn.wgrad_reduce(ws, splits, st.cout, ldw, ldw, st.cout * ldw, tmp, ldw, 1.0, False)
                 Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
                 self.grad_ready(st.pid)
-            self._side_wgrad(g, stem_wg)
+            self._side_wgrad((g, saved["xp"], saved["idx"], saved["y0"], sbn.coef, sbn.bcoef), stem_wg)
         else:
             dy0 = self._buf("dy0", N * P0 * Q0 * st.cout)
             Cn.stem_pool_bwd_apply(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
@@ -807,5 +810,5 @@ class ResNetExecutor:
                             st.st, 0, tmp, ldw, cs=4, win=True, dil=2)
                 Cn.gather32(tmp, self.stem_gidx, self._g(st.slot))
                 self.grad_ready(st.pid)
-            self._side_wgrad(dy0, stem_wg)
+            self._side_wgrad((dy0, saved["xp"]), stem_wg)
         self._join_side()

@@ -53,6 +53,9 @@ class ResNetExecutor32(ResNetExecutor):
         self._pending_reads = {}
         self.syncbn_group = syncbn_group
         self.syncbn = syncbn_allreduce is not None or syncbn_group is not None
+        # the inherited bn_train_finalize / _pair use the forward-statistics hook when one is set; this executor
+        # issues every SyncBN all-reduce through _sync_sum
+        self._sync_sum_fwd = None
         if syncbn_allreduce is not None:
             self.syncbn_world = int(syncbn_world) if syncbn_world else 1
             self._sync_sum = syncbn_allreduce

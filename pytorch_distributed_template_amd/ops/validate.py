@@ -13,6 +13,18 @@ checked wrappers of every extension *function*; classes such as the communicator
   after the op, and an op that turns a finite tensor into one holding NaN/Inf raises
   :class:`NonFiniteError` naming the op and the argument.  (An fp16 AMP step that overflows on purpose --
   the GradScaler then skips it -- trips this too, exactly like torch's anomaly mode.)
+* level 3 -- level 1 plus replay determinism (an intra-kernel race detector): before each op every tensor
+  argument is snapshotted; after it ran, the op is re-run ``PDT_VALIDATE_REPLAYS`` (default 3) times from the
+  snapshot and every argument must come out BIT-identical to the first run.  A kernel whose result depends on
+  wave timing (a missing barrier / ``s_waitcnt``, an LDS read racing an LDS-DMA, an order-dependent reduction)
+  raises :class:`NondeterminismError` naming the op, the argument, and how many elements differed
+  (``PDT_VALIDATE_COLLECT=1``: record in ``Validator.findings`` and continue instead).
+
+Guard bands (any level, ``PDT_VALIDATE_GUARD=<elements>``): :class:`~..optim.flat.FlatParams` leaves that many
+extra elements after every parameter slot and fills them in the GRADIENT buffer with a finite canary; after every
+op the canaries are checked, and an op that wrote past the end of a gradient slice (e.g. a side-stream weight
+gradient spilling into the BN-gradient slot a main-stream kernel writes concurrently) raises
+:class:`GuardBandError` naming the op and the parameter whose guard it hit.
 
 Steps being captured into a HIP graph are not checked (nothing may synchronise inside a capture).
 Everything here costs a device round trip per op: it is a debugging mode, never on in a benchmark.
@@ -35,6 +47,29 @@ class NonFiniteError(ValidationError):
     """A native op produced NaN/Inf in a tensor argument that was finite before the op."""
 
 
+class NondeterminismError(ValidationError):
+    """Re-running a native op from identical inputs produced different bits (level 3)."""
+
+
+class GuardBandError(ValidationError):
+    """A native op wrote into a canary guard band after a flat-buffer slot."""
+
+
+CANARY_BITS = 0x0BADC0DE  # a finite fp32 (~7e-32): harmless if a whole-buffer op reads it, unmistakable if overwritten
+
+
+def _bits(t: torch.Tensor) -> torch.Tensor:
+    """Bitwise view for comparisons (NaN payloads compare equal to themselves)."""
+    t = t.detach().contiguous().reshape(-1)
+    if t.dtype in (torch.float64, torch.int64):
+        return t.view(torch.int64)
+    if t.dtype in (torch.float32, torch.int32):
+        return t.view(torch.int32)
+    if t.dtype in (torch.float16, torch.bfloat16, torch.int16):
+        return t.view(torch.int16)
+    return t.view(torch.uint8)
+
+
 def _describe(args) -> str:
     parts = []
     for i, a in enumerate(args):
@@ -55,6 +90,60 @@ class Validator:
         self._log = open(log_path, "a", buffering=1) if log_path else None
         self._sync = sync or (lambda: torch.cuda.synchronize() if torch.cuda.is_available() else None)
         self._capturing = capturing or (lambda: torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+        self.replays = int(os.environ.get("PDT_VALIDATE_REPLAYS", "3"))
+        self.collect = os.environ.get("PDT_VALIDATE_COLLECT", "0") == "1"
+        self.findings: List[str] = []
+        self.replayed = 0
+        self.replay_host = False  # replay host-tensor ops too (CPU tests of the mechanism)
+        self._guards: List[Tuple[torch.Tensor, torch.Tensor, List[Tuple[int, str]]]] = []
+
+    def register_guard(self, buf: torch.Tensor, idx: torch.Tensor, owners: List[Tuple[int, str]]) -> None:
+        """``buf[idx]`` holds canaries; ``owners`` = (first position in idx, parameter name) per slot guard."""
+        self._guards.append((buf, idx, owners))
+
+    def _check_guards(self, name: str, args) -> None:
+        for buf, idx, owners in self._guards:
+            v = buf.view(torch.int32)[idx]
+            bad = (v != CANARY_BITS).nonzero()
+            if bad.numel():
+                pos = int(bad[0])
+                who = [n for start, n in owners if start <= pos][-1]
+                raise GuardBandError(f"native op `{name}` wrote into the guard band after parameter `{who}` "
+                                     f"({int(bad.numel())} canary element(s) overwritten)\n  args: {_describe(args)}"
+                                     f"\n  last native ops (oldest first):\n  {self._recent()}")
+
+    def _replay(self, name: str, fn, args, kwargs):
+        """Run ``fn`` once, then ``self.replays`` more times from the same inputs; returns the first result."""
+        ts = [(i, a) for i, a in enumerate(args) if isinstance(a, torch.Tensor) and a.numel() > 0]
+        if not ts or not (self.replay_host or any(a.is_cuda for _, a in ts)):
+            res = fn(*args, **kwargs)
+            self._sync()
+            return res
+        pre = [a.clone() for _, a in ts]
+        res = fn(*args, **kwargs)
+        self._sync()
+        post = [_bits(a).clone() for _, a in ts]
+        self.replayed += 1
+        for r in range(self.replays):
+            for (_, a), p in zip(ts, pre):
+                a.copy_(p)
+            fn(*args, **kwargs)
+            self._sync()
+            for (i, a), want in zip(ts, post):
+                got = _bits(a)
+                if torch.equal(got, want):
+                    continue
+                nd = int((got != want).sum())
+                msg = (f"native op `{name}` is not deterministic: replay {r + 1} changed {nd} of {a.numel()} "
+                       f"element(s) of argument #{i} ({str(a.dtype).replace('torch.', '')}{list(a.shape)})")
+                for (_, a2), w2 in zip(ts, post):  # keep the first run's result so the step can go on
+                    a2.copy_(w2.view(a2.dtype).view(a2.shape))
+                if self.collect:
+                    self.findings.append(msg)
+                    return res
+                raise NondeterminismError(msg + f"\n  args: {_describe(args)}\n  last native ops (oldest first):"
+                                          f"\n  {self._recent()}")
+        return res
 
     def _recent(self) -> str:
         return "\n  ".join(self.history)
@@ -77,13 +166,20 @@ class Validator:
                 self.history.append(entry)
                 if self._log is not None:
                     self._log.write(entry + "\n")
-            pre = self._finite_args(args) if self.level >= 2 else []
+            pre = self._finite_args(args) if self.level == 2 else []
             try:
-                res = fn(*args, **kwargs)
-                self._sync()
+                if self.level >= 3:
+                    res = self._replay(name, fn, args, kwargs)
+                else:
+                    res = fn(*args, **kwargs)
+                    self._sync()
+            except ValidationError:
+                raise
             except Exception as e:  # TORCH_CHECK in the binding, or an async HIP error at the sync
                 raise ValidationError(f"native op `{name}` failed: {e}\n  args: {_describe(args)}\n"
                                       f"  last native ops (oldest first):\n  {self._recent()}") from e
+            if self._guards:
+                self._check_guards(name, args)
             for i, t, was_finite in pre:
                 if was_finite and not bool(torch.isfinite(t).all()):
                     bad = int((~torch.isfinite(t)).sum())

@@ -12,6 +12,7 @@ are untouched.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -49,6 +50,10 @@ class FlatParams:
         self.slots: List[ParamSlot] = []
         self.params: List[nn.Parameter] = []
         self.by_param: Dict[int, ParamSlot] = {}
+        # PDT_VALIDATE guard bands (ops/validate.py): extra canary elements after every slot of the gradient buffer
+        from ..ops import validate
+        guard = int(os.environ.get("PDT_VALIDATE_GUARD", "0") or 0) if validate.level_from_env() > 0 else 0
+        self.guard = guard
         off = 0
         for name, p in model.named_parameters():
             if not p.requires_grad:
@@ -58,7 +63,7 @@ class FlatParams:
             self.slots.append(s)
             self.params.append(p)
             self.by_param[id(p)] = s
-            off += (p.numel() + align - 1) // align * align
+            off += (p.numel() + guard + align - 1) // align * align
         self.total = off
         self.data = torch.zeros(self.total, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
@@ -72,6 +77,26 @@ class FlatParams:
                 p.grad = _phys_view(self.grad, s.offset, s.shape, s.channels_last)
         # parameters that receive weight decay: all of them, like the reference (SURVEY §2.2 --wd)
         self.refresh_shadow()
+        if guard and self.device.type == "cuda":
+            self._install_guards(validate)
+
+    def _install_guards(self, validate) -> None:
+        """Canary-fill every gap between slots in ``grad`` and register it with the validator."""
+        idx, owners = [], []
+        n = 0
+        for i, s in enumerate(self.slots):
+            end = self.slots[i + 1].offset if i + 1 < len(self.slots) else self.total
+            if end > s.offset + s.numel:
+                owners.append((n, s.name))
+                idx.append(torch.arange(s.offset + s.numel, end, dtype=torch.int64))
+                n += end - s.offset - s.numel
+        if not idx:
+            return
+        gi = torch.cat(idx).to(self.device)
+        self.grad.view(torch.int32)[gi] = validate.CANARY_BITS
+        v = validate.validator()
+        if v is not None:
+            v.register_guard(self.grad, gi, owners)
 
     # -- views -----------------------------------------------------------------------------------
     def slot(self, p: torch.Tensor) -> ParamSlot:
@@ -98,6 +123,15 @@ class FlatParams:
             native.C.cast16(self.data, self.shadow)
         else:
             self.shadow.copy_(self.data)
+
+    def master_read_index(self) -> torch.Tensor:
+        """int32 flat offsets of every element of the 1-D parameters (BatchNorm gamma/beta, biases): the values the
+        16-bit executor reads from the fp32 MASTER rather than from the shadow.  A DataParallel replica needs the
+        shadow plus exactly these (``parallel/dp.py``)."""
+        idx = [torch.arange(s.offset, s.offset + s.numel, dtype=torch.int64) for s in self.slots if len(s.shape) < 2]
+        out = torch.cat(idx) if idx else torch.zeros(0, dtype=torch.int64)
+        assert out.numel() == 0 or int(out.max()) < self.total
+        return out.to(torch.int32)
 
     def zero_grad(self) -> None:
         self.grad.zero_()

@@ -22,6 +22,20 @@ N replicas would wait on one launching thread.  With ``graph=True`` (the default
 replica's forward + backward (plus its derived weight layouts) is captured once per input shape as a HIP
 graph on its own device and replayed: per step the host issues the broadcast, N graph launches, the
 gradient reduce and the SGD -- the devices' work overlaps instead of queueing behind the host.
+
+What a replica receives each forward (``_replicate``): the 16-bit shadow (conv / fc weights as the kernels read
+them), the fp32 values of the 1-D parameters that the executor reads from the MASTER copy (BatchNorm gamma / beta
+in every finalize / eval / backward coefficient, the fc bias in the loss kernel; ``FlatParams.master_read_index``,
+~10 K floats for ResNet-18) packed into one buffer, and the BN running statistics.  On the fp32 path the master
+itself is the compute copy and is broadcast whole.
+
+Replicas may share a device (``device_ids=[0, 0]``): their collectives are then plain device copies / adds in a
+fixed order (:class:`_LocalGroup`), which rehearses the whole multi-replica step -- scatter, replication, per-
+replica BN statistics, gradient reduce -- on one GPU, bit-comparable with a single-executor oracle.
+
+Host batches: when the loader yields :class:`ShardedBatch` objects (``data/loader.py`` builds them for native DP
+on > 1 device), each shard was copied host -> its own GPU already and ``_scatter`` only hands them out; a plain
+tensor batch is split and copied from wherever it lives (``nn.DataParallel``'s scatter).
 """
 from __future__ import annotations
 
@@ -31,9 +45,26 @@ from typing import List, Optional
 import torch
 
 from ..amp.scaler import DeviceGradScaler
+from ..data.loader import ShardedBatch
 from ..models.executor import ResNetExecutor
 from ..optim.flat import FlatBuffers, FlatParams
 from ..optim.sgd import FusedSGD
+
+
+class _LocalGroup:
+    """DataParallel collectives when replicas share a device (RCCL refuses duplicate GPUs): device copies and
+    adds on the current streams, reduced in replica order (deterministic)."""
+
+    def broadcast(self, ts, root: int) -> None:
+        for i, t in enumerate(ts):
+            if i != root:
+                t.copy_(ts[root], non_blocking=True)
+
+    def reduce(self, ts, root: int) -> None:
+        acc = ts[root]
+        for i, t in enumerate(ts):
+            if i != root:
+                acc.add_(t.to(acc.device, non_blocking=True))
 
 
 class NativeDataParallelTrainer:
@@ -41,8 +72,9 @@ class NativeDataParallelTrainer:
                  momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False,
                  graph: Optional[bool] = None):
         self.device_ids = list(device_ids)
+        distinct = len(set(self.device_ids))
         # per-replica HIP graphs (see module doc); two eager warm-up steps settle buffers and tile choices
-        self.use_graph = (len(self.device_ids) > 1) if graph is None else bool(graph)
+        self.use_graph = (distinct > 1) if graph is None else bool(graph)
         self._graphs = {}
         self._graph_warm = 0
         self.devices = [torch.device("cuda", i) for i in self.device_ids]
@@ -67,26 +99,46 @@ class NativeDataParallelTrainer:
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executors[0].update_derived)
         self.scaler = DeviceGradScaler(self.devices[0], enabled=use_amp and dtype == torch.float16)
+        # fp32 values the 16-bit executors read from the master (BN affine, fc bias): packed on GPU 0, broadcast,
+        # unpacked into each replica's master (see module doc)
+        self._aux_idx, self._aux = [], []
+        if dtype != torch.float32 and len(self.devices) > 1:
+            idx = self.flat.master_read_index()
+            for d in self.devices:
+                self._aux_idx.append(idx.to(d))
+                self._aux.append(torch.zeros(idx.numel(), dtype=torch.float32, device=d))
         self.group = None
-        # the runner hands host (pinned) batches straight to _scatter: each shard is copied host -> its own
-        # GPU, instead of the whole batch going to GPU 0 first (nn.DataParallel's scatter from GPU 0)
+        # the runner hands batches over as they come from the loader: ShardedBatch (already on every GPU) or a
+        # tensor that _scatter splits; no copy to the runner's device first
         self.host_batches = len(self.devices) > 1
         if len(self.devices) > 1:
-            from ..ops import native
-            self.group = native.C.DeviceGroup(self.device_ids)
+            if distinct == len(self.devices):
+                from ..ops import native
+                self.group = native.C.DeviceGroup(self.device_ids)
+            else:
+                self.group = _LocalGroup()
 
     def on_state_loaded(self) -> None:
-        """After ``model.load_state_dict`` (resume): GPU 0's shadow and derived layouts; the other replicas
-        receive them with the next forward's replication."""
+        """After ``model.load_state_dict`` (resume): GPU 0's shadow and derived layouts, then every replica's full
+        compute state (shadow, master-read parameters, BN buffers, derived layouts)."""
         with torch.cuda.device(self.devices[0]):
             self.flat.refresh_shadow()
             self.executors[0].update_derived()
+        self._replicate(derived=True)
 
     def _replicate(self, derived: bool = True) -> None:
         if len(self.devices) == 1:
             return
         # the compute copy: the 16-bit shadow, or the fp32 master itself on the fp32 path
         self.group.broadcast([f.shadow if f.shadow is not None else f.data for f in self.flats], 0)
+        if self._aux:
+            from ..ops import native
+            with torch.cuda.device(self.devices[0]):
+                native.C.gather32(self.flat.data, self._aux_idx[0], self._aux[0])
+            self.group.broadcast(self._aux, 0)
+            for i in range(1, len(self.devices)):
+                with torch.cuda.device(self.devices[i]):
+                    native.C.scatter32(self._aux[i], self._aux_idx[i], self.flats[i].data)
         if self.buffers[0].n_float:
             self.group.broadcast([b.fdata for b in self.buffers], 0)
         if derived:
@@ -115,6 +167,10 @@ class NativeDataParallelTrainer:
                     res.append(self._replica_step(i, x, t, ls, B, derived=False))
                     continue
                 key = (i, tuple(x.shape), x.dtype, B)
+                # executor 0's derived layouts are gathered eagerly by the post-step hook (on its side stream when
+                # split): order them before the capture / replay here, never through an event waited on inside
+                # the capture (a capture-time wait on an outside event does not order a later replay)
+                self.executors[i]._wait_derived()
                 ent = self._graphs.get(key)
                 if ent is None:
                     sx, st = x.clone(), t.clone()
@@ -135,6 +191,9 @@ class NativeDataParallelTrainer:
         return res, warm
 
     def _scatter(self, images, target):
+        if isinstance(images, ShardedBatch):  # the loader already put shard i on device i
+            assert len(images.parts) == len(self.devices), "ShardedBatch built for another device list"
+            return list(images.parts), list(target.parts)
         n = len(self.devices)
         chunks = torch.tensor_split(torch.arange(images.shape[0]), n)
         xs, ts = [], []
@@ -145,7 +204,7 @@ class NativeDataParallelTrainer:
         return xs, ts
 
     def train_step(self, images, target):
-        B = images.shape[0]
+        B = images.size(0)
         warm = self.use_graph and self._graph_warm >= 2
         self._replicate(derived=not warm)  # graphed replicas gather their derived layouts inside the graph
         xs, ts = self._scatter(images, target)
@@ -170,7 +229,7 @@ class NativeDataParallelTrainer:
 
     @torch.no_grad()
     def eval_step(self, images, target):
-        B = images.shape[0]
+        B = images.size(0)
         self._replicate()
         xs, ts = self._scatter(images, target)
         outs, mets = [], []

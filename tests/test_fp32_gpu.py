@@ -183,3 +183,22 @@ def test_entry_script_fp32_native(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     log = open(os.path.join(out + "_resnet18", "experiment.log")).read()
     assert "=> engine: native | compute dtype: float32" in log
+
+
+def test_fp32_syncbn_native_comm_world1_equals_plain_bn():
+    """--precision fp32 with --sync_batchnorm on the native communicator (forced at world 1, identity all-reduces):
+    the fp32 executor's SyncBN path runs (it used to raise AttributeError on _sync_sum_fwd) and matches plain BN."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    x = torch.randn(8, 3, 64, 64, device=DEV)
+    t = torch.randint(0, 1000, (8,), device=DEV)
+    out = []
+    for sync in (True, False):
+        torch.manual_seed(0)
+        tr = NativeTrainer(registry.create("resnet18"), DEV, dtype=torch.float32, comm="native", force_comm=True,
+                           sync_bn=sync)
+        for _ in range(2):
+            tr.train_step(x, t)
+        torch.cuda.synchronize()
+        out.append(tr.flat.data.clone())
+    assert _rel(out[0], out[1]) < 1e-5

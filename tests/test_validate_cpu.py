@@ -63,3 +63,60 @@ def test_env_wrapping(monkeypatch):
     w = validate.maybe_wrap("f", f)
     assert w is not f and w.__wrapped__ is f and w() == 1
     assert validate.maybe_wrap("T", torch.nn.Module) is torch.nn.Module  # classes pass through
+
+
+def test_level3_replay_flags_a_timing_dependent_op():
+    """Replay determinism: an op whose output depends on something other than its inputs (here a call counter,
+    standing in for wave timing) is named; a pure op passes and keeps its first result."""
+    v = _v(3)
+    v.replay_host = True
+    pure = v.wrap("pure_op", lambda a, o: o.copy_(a * 2 + 1))
+    a, o = torch.arange(6.0), torch.zeros(6)
+    pure(a, o)
+    assert torch.equal(o, torch.arange(6.0) * 2 + 1) and v.replayed == 1
+    calls = [0]
+
+    def racy(a, o):
+        calls[0] += 1
+        o.copy_(a)
+        if calls[0] == 3:  # the second replay differs in one element
+            o[4] += 1e-3
+    with pytest.raises(validate.NondeterminismError) as e:
+        v.wrap("racy_op", racy)(torch.arange(6.0), torch.zeros(6))
+    assert "`racy_op` is not deterministic: replay 2 changed 1 of 6 element(s) of argument #1" in str(e.value)
+    # accumulate-style ops are replayed from the snapshot, so they are not falsely flagged
+    acc = v.wrap("acc_op", lambda a, o: o.add_(a))
+    o2 = torch.ones(3)
+    acc(torch.ones(3), o2)
+    assert torch.equal(o2, torch.full((3,), 2.0))
+    # collect mode: recorded, the first run's result kept
+    v.collect = True
+    calls[0] = 0
+    o3 = torch.zeros(6)
+    v.wrap("racy_op", racy)(torch.arange(6.0), o3)
+    assert len(v.findings) == 1 and torch.equal(o3, torch.arange(6.0))
+
+
+def test_guard_band_names_the_overrunning_op():
+    v = _v(1)
+    buf = torch.zeros(16)
+    gi = torch.tensor([4, 5, 6, 7, 12, 13, 14, 15])  # guards after slot "a" [0,4) and slot "b" [8,12)
+    buf.view(torch.int32)[gi] = validate.CANARY_BITS
+    v.register_guard(buf, gi, [(0, "a"), (4, "b")])
+    v.wrap("in_bounds", lambda t: t[8:12].fill_(3.0))(buf)
+    with pytest.raises(validate.GuardBandError) as e:
+        v.wrap("overrun", lambda t: t[8:13].fill_(3.0))(buf)
+    assert "`overrun` wrote into the guard band after parameter `b`" in str(e.value)
+
+
+def test_flat_params_guard_layout(monkeypatch):
+    """PDT_VALIDATE_GUARD leaves a canary gap after every slot (CPU: layout only)."""
+    from pytorch_distributed_template_amd.optim.flat import FlatParams
+    monkeypatch.setenv("PDT_VALIDATE", "1")
+    monkeypatch.setenv("PDT_VALIDATE_GUARD", "16")
+    m = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.BatchNorm1d(8))
+    f = FlatParams(m, "cpu")
+    for a, b in zip(f.slots, f.slots[1:]):
+        assert b.offset - (a.offset + a.numel) >= 16
+    idx = f.master_read_index()
+    assert idx.numel() == 8 + 8 + 8  # linear bias, bn weight, bn bias
