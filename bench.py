@@ -60,6 +60,8 @@ def _parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the benchmark) or gloo (multi-rank rehearsal on fewer GPUs than ranks)")
     ap.add_argument("--comm-timeout", type=float, default=900.0, help="native comm watchdog timeout (s)")
+    ap.add_argument("--comm-transport", default="auto", choices=["auto", "rccl", "host"],
+                    help="native comm transport: rccl (one rank per GPU), host (shared memory; ranks sharing a GPU)")
     ap.add_argument("--grad-compress", default="none", choices=["none", "bf16"],
                     help="native comm: bf16 gradient all-reduce (default none: fp32, the reference's precision)")
     return ap.parse_args()
@@ -86,6 +88,9 @@ def _spawn(args) -> int:
            "--master_addr=127.0.0.1", f"--master_port={_free_port()}", "--no_local_rank",
            os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
+    # ROCm IPC: hosts whose amdgpu driver only supports dmabuf-based IPC need the non-legacy mode, otherwise RCCL's
+    # intra-node transport (and CUDA-tensor sharing between processes) fails with `hipIpcGetMemHandle: invalid
+    # argument`.  setdefault: an explicit user setting wins.
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, cwd=ROOT, env=env)
 
@@ -113,9 +118,11 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     shared_gpus = args.dist_backend == "gloo" and world > torch.cuda.device_count()
-    if shared_gpus:  # rehearsal: ranks share GPUs, so RCCL (which refuses duplicate GPUs) is out
+    if shared_gpus:
+        # rehearsal: ranks share GPUs, so RCCL (which refuses duplicate GPUs) is out; --comm native then runs the
+        # SAME C++ communicator + bucketer over the host shared-memory transport (csrc/shm_group.h)
         local_rank %= torch.cuda.device_count()
-    comm = args.comm if not shared_gpus else "torch"
+    comm = args.comm
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -130,7 +137,7 @@ def main() -> int:
     tr = NativeTrainer(model, dev, dtype=dtype, lr=0.1, momentum=0.9, weight_decay=1e-4,
                        use_amp=(args.dtype == "fp16"), sync_bn=args.sync_bn, bucket_cap_mb=args.bucket_cap_mb,
                        graph=args.graph, autotune=args.autotune, comm=comm, force_comm=args.force_comm,
-                       comm_timeout_s=args.comm_timeout, time_comm=True,
+                       comm_timeout_s=args.comm_timeout, time_comm=True, comm_transport=args.comm_transport,
                        grad_compress=args.grad_compress if comm == "native" else "none",
                        last_bucket_mb=args.last_bucket_mb if args.last_bucket_mb > 0 else None)
     nc = tr.ncomm
@@ -213,8 +220,9 @@ def main() -> int:
                        "per_gpu_batch": B, "sync_bn": args.sync_bn, "engine": "native-hip",
                        "comm": (comm if world > 1 or nc is not None else "none"),
                        "dist_backend": args.dist_backend if world > 1 else None,
-                       "rccl_world": nc.count() if nc is not None else (world if world > 1 and not shared_gpus
-                                                                        else None),
+                       "rccl_world": (nc.count() if nc is not None and nc.transport == "rccl" else
+                                      (world if world > 1 and nc is None and not shared_gpus else None)),
+                       "comm_transport": nc.transport if nc is not None else None,
                        "comm_selftest": comm_ok,
                        "params_equal_across_ranks": params_equal,
                        "bucket_sizes_mb": [round(x, 3) for x in tr.bucketer.bucket_sizes_mb()] if world > 1 else [],
@@ -225,7 +233,7 @@ def main() -> int:
     if world > 1:
         barrier()
     if nc is not None:
-        nc.destroy()
+        tr.close()
     if world > 1:
         dist.destroy_process_group()
     return 0 if params_equal else 4

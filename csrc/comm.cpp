@@ -23,7 +23,15 @@
 //     async_error()/abort() stay available for explicit polling.
 //   * HIP graphs: every call only enqueues work and orders streams with events, so a training step that
 //     issues its collectives through this class can be captured (the comm stream joins the capture through
-//     join_compute's event and leaves it through wait()); captured collectives are not watchdog-tracked.
+//     join_compute's event and leaves it through wait()); captured collectives are not watchdog-tracked, so the
+//     trainer records one tracked event on the compute stream after every graph replay (track_compute).
+//   * Transports: the Communicator / Bucketer logic sits on a Transport interface with two implementations --
+//     RcclTransport (ncclComm_t, the production path over xGMI) and HostTransport (csrc/shm_group.h: a POSIX
+//     shared-memory group, fixed rank-order reductions).  The host transport runs the SAME multi-rank C++ code
+//     where RCCL cannot: ranks sharing one GPU (RCCL refuses duplicate devices; the 1-GPU DDP rehearsals) and
+//     CPU-only processes with host tensors (the CPU test suite, world 2 / 4).  Its collectives are synchronous
+//     (device buffers are staged through host memory behind a stream synchronisation), so it is a correctness
+//     transport, not a fast one.
 // RCCL is the copy PyTorch already loaded (same soname), so there is one RCCL instance per process.
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -32,6 +40,7 @@
 
 #include "dtypes.h"
 #include "kernels/optim.h"
+#include "shm_group.h"
 
 #include <atomic>
 #include <chrono>
@@ -89,25 +98,186 @@ py::bytes unique_id() {
   return py::bytes(id.internal, sizeof(id.internal));
 }
 
-class Communicator {
+static pdt_shm::Dt shm_type(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return pdt_shm::Dt::F32;
+    case at::kDouble: return pdt_shm::Dt::F64;
+    case at::kHalf: return pdt_shm::Dt::F16;
+    case at::kBFloat16: return pdt_shm::Dt::BF16;
+    case at::kInt: return pdt_shm::Dt::I32;
+    case at::kLong: return pdt_shm::Dt::I64;
+    case at::kByte: return pdt_shm::Dt::U8;
+    default: TORCH_CHECK(false, "host transport: unsupported dtype ", t.scalar_type());
+  }
+}
+
+static pdt_shm::Op shm_op(const std::string& op) {
+  if (op == "sum") return pdt_shm::Op::Sum;
+  if (op == "max") return pdt_shm::Op::Max;
+  if (op == "min") return pdt_shm::Op::Min;
+  if (op == "prod") return pdt_shm::Op::Prod;
+  TORCH_CHECK(false, "host transport: unsupported reduction ", op);
+}
+
+// A collective backend.  Buffers are raw pointers with their element type taken from a tensor of that type
+// (``proto``), so both transports see the same call; ``s`` is the stream the collective is ordered on
+// (ignored by a host-memory group).
+class Transport {
  public:
-  Communicator(const std::string& id, int world, int rank, int device, double timeout_s = 0.0, int exit_code = 75)
-      : world_(world), rank_(rank), device_(device), timeout_s_(timeout_s), exit_code_(exit_code) {
+  virtual ~Transport() = default;
+  virtual const char* name() const = 0;
+  virtual bool synchronous() const = 0;  // the call has completed when it returns (no watchdog tracking needed)
+  virtual void all_reduce(void* buf, int64_t n, const Tensor& proto, const std::string& op, hipStream_t s) = 0;
+  virtual void broadcast(void* buf, int64_t n, const Tensor& proto, int root, hipStream_t s) = 0;
+  virtual void all_gather(const void* in, void* out, int64_t n, const Tensor& proto, hipStream_t s) = 0;
+  virtual int count() = 0;
+  virtual std::string async_error() = 0;
+  virtual void abort() = 0;
+  virtual void destroy(hipStream_t s) = 0;
+};
+
+class RcclTransport final : public Transport {
+ public:
+  RcclTransport(const std::string& id, int world, int rank) {
     TORCH_CHECK(id.size() == sizeof(ncclUniqueId::internal), "rccl: unique id must be ", sizeof(ncclUniqueId::internal),
                 " bytes");
-    TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rccl: bad rank / world");
     ncclUniqueId uid;
     std::memcpy(uid.internal, id.data(), sizeof(uid.internal));
-    PDT_HIP_OK(hipSetDevice(device));
-    PDT_HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    PDT_HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
-    PDT_HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     PDT_NCCL_CHECK(ncclCommInitRank(&comm_, world, uid, rank));
+  }
+  ~RcclTransport() override {
+    if (comm_ && !aborted_.load()) ncclCommDestroy(comm_);
+  }
+  const char* name() const override { return "rccl"; }
+  bool synchronous() const override { return false; }
+  ncclComm_t comm() const {
+    TORCH_CHECK(comm_ != nullptr && !aborted_.load(), "rccl: communicator was aborted");
+    return comm_;
+  }
+  void all_reduce(void* buf, int64_t n, const Tensor& proto, const std::string& op, hipStream_t s) override {
+    PDT_NCCL_CHECK(ncclAllReduce(buf, buf, n, nccl_type(proto), nccl_op(op), comm(), s));
+  }
+  void broadcast(void* buf, int64_t n, const Tensor& proto, int root, hipStream_t s) override {
+    PDT_NCCL_CHECK(ncclBroadcast(buf, buf, n, nccl_type(proto), root, comm(), s));
+  }
+  void all_gather(const void* in, void* out, int64_t n, const Tensor& proto, hipStream_t s) override {
+    PDT_NCCL_CHECK(ncclAllGather(in, out, n, nccl_type(proto), comm(), s));
+  }
+  int count() override {
+    int n = 0;
+    PDT_NCCL_CHECK(ncclCommCount(comm(), &n));
+    return n;
+  }
+  std::string async_error() override {
+    if (!comm_ || aborted_.load()) return "aborted";
+    ncclResult_t e = ncclSuccess;
+    PDT_NCCL_CHECK(ncclCommGetAsyncError(comm_, &e));
+    return (e == ncclSuccess || e == ncclInProgress) ? std::string() : std::string(ncclGetErrorString(e));
+  }
+  void abort() override {
+    if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+  }
+  void destroy(hipStream_t s) override {
+    if (comm_ && !aborted_.load()) {
+      if (s) PDT_HIP_OK(hipStreamSynchronize(s));
+      PDT_NCCL_CHECK(ncclCommDestroy(comm_));
+    }
+    comm_ = nullptr;
+  }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  std::atomic<bool> aborted_{false};
+};
+
+// Shared-memory group over host memory.  ``device >= 0``: buffers are device memory, staged through host memory
+// (D2H on the collective's stream + synchronise, host collective, H2D + synchronise).
+class HostTransport final : public Transport {
+ public:
+  HostTransport(const std::string& name, int world, int rank, bool create, int64_t slot_bytes, double timeout_s,
+                int device)
+      : grp_(name, world, rank, create, (size_t)slot_bytes, timeout_s > 0 ? timeout_s : 600.0), device_(device) {
+    grp_.barrier();  // every rank has mapped the segment: its name can go (no leak if a rank dies later)
+    if (rank == 0) grp_.unlink();
+  }
+  const char* name() const override { return "host"; }
+  bool synchronous() const override { return true; }
+  void all_reduce(void* buf, int64_t n, const Tensor& proto, const std::string& op, hipStream_t s) override {
+    const size_t bytes = (size_t)n * proto.element_size();
+    void* h = stage_in(buf, bytes, s);
+    run([&] { grp_.all_reduce(h, n, shm_type(proto), shm_op(op)); });
+    stage_out(buf, h, bytes, s);
+  }
+  void broadcast(void* buf, int64_t n, const Tensor& proto, int root, hipStream_t s) override {
+    const size_t bytes = (size_t)n * proto.element_size();
+    void* h = stage_in(buf, bytes, s);
+    run([&] { grp_.broadcast(h, n, shm_type(proto), root); });
+    stage_out(buf, h, bytes, s);
+  }
+  void all_gather(const void* in, void* out, int64_t n, const Tensor& proto, hipStream_t s) override {
+    const size_t bytes = (size_t)n * proto.element_size();
+    if (device_ < 0) {
+      run([&] { grp_.all_gather(in, out, n, shm_type(proto)); });
+      return;
+    }
+    std::vector<uint8_t> hin(bytes), hout(bytes * grp_.world());
+    PDT_HIP_OK(hipMemcpyAsync(hin.data(), in, bytes, hipMemcpyDeviceToHost, s));
+    PDT_HIP_OK(hipStreamSynchronize(s));
+    run([&] { grp_.all_gather(hin.data(), hout.data(), n, shm_type(proto)); });
+    PDT_HIP_OK(hipMemcpyAsync(out, hout.data(), hout.size(), hipMemcpyHostToDevice, s));
+    PDT_HIP_OK(hipStreamSynchronize(s));
+  }
+  int count() override { return grp_.world(); }
+  std::string async_error() override { return grp_.aborted() ? "host group aborted by a peer" : std::string(); }
+  void abort() override { grp_.abort(); }
+  void destroy(hipStream_t) override {}
+
+ private:
+  template <typename F>
+  void run(F&& f) {
+    try {
+      f();
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, "host transport: ", e.what());
+    }
+  }
+  void* stage_in(void* buf, size_t bytes, hipStream_t s) {
+    if (device_ < 0) return buf;
+    if (stage_.size() < bytes) stage_.resize(bytes);
+    PDT_HIP_OK(hipMemcpyAsync(stage_.data(), buf, bytes, hipMemcpyDeviceToHost, s));
+    PDT_HIP_OK(hipStreamSynchronize(s));
+    return stage_.data();
+  }
+  void stage_out(void* buf, void* h, size_t bytes, hipStream_t s) {
+    if (device_ < 0) return;
+    PDT_HIP_OK(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
+    PDT_HIP_OK(hipStreamSynchronize(s));  // the staging buffer is reused by the next collective
+  }
+  pdt_shm::ShmGroup grp_;
+  int device_;
+  std::vector<uint8_t> stage_;
+};
+
+class Communicator {
+ public:
+  // RCCL over the devices of the job (one rank per GPU)
+  Communicator(const std::string& id, int world, int rank, int device, double timeout_s = 0.0, int exit_code = 75)
+      : world_(world), rank_(rank), device_(device), timeout_s_(timeout_s), exit_code_(exit_code) {
+    TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rccl: bad rank / world");
+    TORCH_CHECK(device >= 0, "rccl: a device is required");
+    make_streams();
+    transport_ = std::make_unique<RcclTransport>(id, world, rank);
     if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });
+  }
+  // Host shared-memory group (``device`` < 0: host tensors only; >= 0: device tensors staged through the host)
+  Communicator(std::unique_ptr<Transport> t, int world, int rank, int device, double timeout_s)
+      : world_(world), rank_(rank), device_(device), timeout_s_(timeout_s), exit_code_(75) {
+    if (device_ >= 0) make_streams();
+    transport_ = std::move(t);
   }
   ~Communicator() {
     stop_watchdog();
-    if (comm_) ncclCommDestroy(comm_);
+    transport_.reset();
     for (auto& p : pending_)
       if (p.ev) (void)hipEventDestroy(p.ev);
     for (hipEvent_t e : free_evs_) (void)hipEventDestroy(e);
@@ -120,23 +290,22 @@ class Communicator {
 
   int rank() const { return rank_; }
   int world() const { return world_; }
+  int device() const { return device_; }
   hipStream_t stream() const { return stream_; }
-  ncclComm_t comm() const {
-    TORCH_CHECK(comm_ != nullptr && !aborted_.load(), "rccl: communicator was aborted");
-    return comm_;
+  Transport& transport() {
+    TORCH_CHECK(transport_ != nullptr, "comm: communicator was destroyed");
+    return *transport_;
   }
-  int count() const {
-    int n = 0;
-    PDT_NCCL_CHECK(ncclCommCount(comm(), &n));
-    return n;
-  }
+  std::string transport_name() const { return transport_ ? transport_->name() : "destroyed"; }
+  int count() { return transport().count(); }
   double timeout_s() const { return timeout_s_; }
 
   // Watchdog bookkeeping: a completion event on the comm stream behind the collective just enqueued.
   // Not while the caller's stream is being captured into a HIP graph: the collective is then a graph node
   // (replayed later, possibly many times) and an event recorded now would never complete as a real event.
+  // Synchronous transports have nothing in flight to watch.
   void track(const char* what, hipStream_t on = nullptr) {
-    if (timeout_s_ <= 0) return;
+    if (timeout_s_ <= 0 || device_ < 0 || transport().synchronous()) return;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(at::hip::getCurrentHIPStream().stream(), &cap) == hipSuccess &&
         cap != hipStreamCaptureStatusNone)
@@ -153,6 +322,13 @@ class Communicator {
     PDT_HIP_OK(hipEventRecord(ev, on));
     pending_.push_back({ev, std::chrono::steady_clock::now(), what});
   }
+  // After a HIP-graph replay whose captured collectives the watchdog cannot see: one tracked event on the
+  // compute stream, completing when the replayed step (and its collectives) did.
+  void track_compute(const std::string& what) {
+    if (device_ < 0) return;
+    replay_what_ = what;
+    track(replay_what_.c_str(), at::hip::getCurrentHIPStream().stream());
+  }
   // Test hook: a pending "collective" that never completes, enqueued ``age_s`` seconds ago.
   void inject_stall(double age_s) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -167,12 +343,14 @@ class Communicator {
 
   // comm stream <- everything already enqueued on the caller's compute stream
   void join_compute() {
+    if (device_ < 0) return;
     hipStream_t cs = at::hip::getCurrentHIPStream().stream();
     PDT_HIP_OK(hipEventRecord(ev_in_, cs));
     PDT_HIP_OK(hipStreamWaitEvent(stream_, ev_in_, 0));
   }
   // compute stream <- every collective enqueued so far
   void wait() {
+    if (device_ < 0) return;
     hipStream_t cs = at::hip::getCurrentHIPStream().stream();
     PDT_HIP_OK(hipEventRecord(ev_out_, stream_));
     PDT_HIP_OK(hipStreamWaitEvent(cs, ev_out_, 0));
@@ -181,7 +359,7 @@ class Communicator {
   void all_reduce(Tensor& t, const std::string& op, bool async_op) {
     check(t);
     join_compute();
-    PDT_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), nccl_op(op), comm(), stream_));
+    transport().all_reduce(t.data_ptr(), t.numel(), t, op, stream_);
     track("all_reduce");
     if (!async_op) wait();
   }
@@ -191,20 +369,20 @@ class Communicator {
   // the same operation order on every rank.
   void all_reduce_inline(Tensor& t, const std::string& op) {
     check(t);
-    hipStream_t cs = at::hip::getCurrentHIPStream().stream();
-    PDT_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), nccl_op(op), comm(), cs));
+    hipStream_t cs = compute_stream();
+    transport().all_reduce(t.data_ptr(), t.numel(), t, op, cs);
     track("all_reduce (compute stream)", cs);
   }
   void broadcast_inline(Tensor& t, int root) {  // on the caller's stream; same ordering contract as above
     check(t);
-    hipStream_t cs = at::hip::getCurrentHIPStream().stream();
-    PDT_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), root, comm(), cs));
+    hipStream_t cs = compute_stream();
+    transport().broadcast(t.data_ptr(), t.numel(), t, root, cs);
     track("broadcast (compute stream)", cs);
   }
   void broadcast(Tensor& t, int root, bool async_op) {
     check(t);
     join_compute();
-    PDT_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_type(t), root, comm(), stream_));
+    transport().broadcast(t.data_ptr(), t.numel(), t, root, stream_);
     track("broadcast");
     if (!async_op) wait();
   }
@@ -212,36 +390,31 @@ class Communicator {
     check(in);
     check(out);
     TORCH_CHECK(out.numel() == in.numel() * world_ && out.scalar_type() == in.scalar_type(),
-                "rccl all_gather: out must hold world x in");
+                "comm all_gather: out must hold world x in");
     join_compute();
-    PDT_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_type(in), comm(), stream_));
+    transport().all_gather(in.data_ptr(), out.data_ptr(), in.numel(), in, stream_);
     track("all_gather");
     if (!async_op) wait();
   }
   void barrier() {
-    auto t = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_));
+    auto opts = at::TensorOptions().dtype(at::kFloat);
+    auto t = device_ >= 0 ? at::zeros({1}, opts.device(at::kCUDA, device_)) : at::zeros({1}, opts);
     all_reduce(t, "sum", false);
-    PDT_HIP_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
+    if (device_ >= 0) PDT_HIP_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
   }
   std::string async_error() {
-    if (!comm_) return "aborted";
-    ncclResult_t e = ncclSuccess;
-    PDT_NCCL_CHECK(ncclCommGetAsyncError(comm_, &e));
-    return e == ncclSuccess ? std::string() : std::string(ncclGetErrorString(e));
+    if (!transport_) return "aborted";
+    return transport_->async_error();
   }
   // Collective teardown: every rank calls it at the same point (after a barrier).
   void destroy() {
     stop_watchdog();
-    if (comm_ && !aborted_.load()) {
-      PDT_HIP_OK(hipStreamSynchronize(stream_));
-      PDT_NCCL_CHECK(ncclCommDestroy(comm_));
-    }
-    comm_ = nullptr;
+    if (transport_ && !aborted_.load()) transport_->destroy(stream_);
+    transport_.reset();
   }
   void abort() {
     stop_watchdog();
-    if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
-    comm_ = nullptr;
+    if (transport_ && !aborted_.exchange(true)) transport_->abort();
   }
 
  private:
@@ -250,6 +423,16 @@ class Communicator {
     std::chrono::steady_clock::time_point t;
     const char* what;
   };
+
+  void make_streams() {
+    PDT_HIP_OK(hipSetDevice(device_));
+    PDT_HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    PDT_HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+    PDT_HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  }
+  hipStream_t compute_stream() const {
+    return device_ >= 0 ? at::hip::getCurrentHIPStream().stream() : nullptr;
+  }
 
   void stop_watchdog() {
     if (!watchdog_.joinable()) return;
@@ -262,14 +445,14 @@ class Communicator {
   }
 
   [[noreturn]] void fail(const std::string& why) {
-    std::fprintf(stderr, "[pdt comm watchdog] rank %d/%d: %s; aborting the RCCL communicator and exiting (%d)\n",
+    std::fprintf(stderr, "[pdt comm watchdog] rank %d/%d: %s; aborting the communicator and exiting (%d)\n",
                  rank_, world_, why.c_str(), exit_code_);
     std::fflush(stderr);
-    if (!aborted_.exchange(true)) ncclCommAbort(comm_);
+    if (!aborted_.exchange(true) && transport_) transport_->abort();
     std::_Exit(exit_code_);
   }
 
-  // Poll the oldest pending collective and RCCL's async error every 50 ms.
+  // Poll the oldest pending collective and the transport's async error every 50 ms.
   void watch() {
     (void)hipSetDevice(device_);
     const auto limit = std::chrono::duration<double>(timeout_s_);
@@ -290,21 +473,26 @@ class Communicator {
           fail(std::string(p.what) + " did not complete within " + std::to_string(timeout_s_) + " s");
         break;
       }
-      ncclResult_t e = ncclSuccess;
-      if (comm_ && !aborted_ && ncclCommGetAsyncError(comm_, &e) == ncclSuccess && e != ncclSuccess &&
-          e != ncclInProgress)
-        fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(e));
+      if (transport_ && !aborted_) {
+        const std::string e = transport_->async_error();
+        if (!e.empty()) fail(std::string("asynchronous transport error: ") + e);
+      }
     }
   }
 
   void check(const Tensor& t) const {
-    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl: expected a contiguous GPU tensor");
-    TORCH_CHECK(t.get_device() == device_, "rccl: tensor on device ", t.get_device(), ", communicator on ", device_);
+    TORCH_CHECK(t.is_contiguous(), "comm: expected a contiguous tensor");
+    if (device_ < 0) {
+      TORCH_CHECK(!t.is_cuda(), "comm: host communicator got a GPU tensor");
+      return;
+    }
+    TORCH_CHECK(t.is_cuda(), "comm: expected a GPU tensor");
+    TORCH_CHECK(t.get_device() == device_, "comm: tensor on device ", t.get_device(), ", communicator on ", device_);
   }
   int world_, rank_, device_;
   double timeout_s_;
   int exit_code_;
-  ncclComm_t comm_ = nullptr;
+  std::unique_ptr<Transport> transport_;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
   std::atomic<bool> aborted_{false};
@@ -314,7 +502,23 @@ class Communicator {
   std::deque<Pending> pending_;
   std::vector<hipEvent_t> free_evs_;
   std::thread watchdog_;
+  std::string replay_what_;
 };
+
+std::shared_ptr<Communicator> make_host_communicator(const std::string& name, int world, int rank, int device,
+                                                     bool create, int64_t slot_bytes, double timeout_s) {
+  TORCH_CHECK(slot_bytes >= 64 && slot_bytes % 64 == 0, "host transport: slot_bytes must be a multiple of 64");
+  if (device >= 0) PDT_HIP_OK(hipSetDevice(device));
+  std::unique_ptr<Transport> t;
+  try {
+    t = std::make_unique<HostTransport>(name, world, rank, create, slot_bytes, timeout_s, device);
+  } catch (const c10::Error&) {
+    throw;
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, "host transport: ", e.what());
+  }
+  return std::make_shared<Communicator>(std::move(t), world, rank, device, timeout_s);
+}
 
 class Bucketer {
  public:
@@ -323,9 +527,11 @@ class Bucketer {
       : comm_(std::move(comm)), grad_(std::move(flat_grad)), lo_(std::move(lo)), hi_(std::move(hi)),
         param_bucket_(std::move(param_bucket)), compress_(compress) {
     TORCH_CHECK(compress_ == 0 || compress_ == 1, "bucketer: compress must be 0 (fp32) or 1 (bf16)");
+    const bool on_dev = comm_->device() >= 0;
+    TORCH_CHECK(grad_.scalar_type() == at::kFloat && grad_.is_contiguous() && grad_.is_cuda() == on_dev,
+                "bucketer: flat gradient must be a contiguous fp32 tensor on the communicator's device");
+    TORCH_CHECK(!compress_ || on_dev, "bucketer: bf16 compression needs a GPU communicator");
     if (compress_) scratch_ = at::empty({grad_.numel()}, grad_.options().dtype(at::kBFloat16));
-    TORCH_CHECK(grad_.is_cuda() && grad_.scalar_type() == at::kFloat && grad_.is_contiguous(),
-                "bucketer: flat gradient must be a contiguous fp32 GPU tensor");
     TORCH_CHECK(lo_.size() == hi_.size() && !lo_.empty(), "bucketer: bad bucket ranges");
     nparams_.assign(lo_.size(), 0);
     for (int64_t b : param_bucket_) {
@@ -353,33 +559,43 @@ class Bucketer {
     for (bool l : launched_) n += l;
     return n;
   }
+  // bucket ids in the order their all-reduces were launched this step (tests: production order, lock-step)
+  std::vector<int64_t> launch_order() const { return order_; }
 
  private:
   void launch(size_t b) {
     comm_->join_compute();
     float* p = grad_.data_ptr<float>() + lo_[b];
     const int64_t n = hi_[b] - lo_[b];
+    Transport& tr = comm_->transport();
     if (compress_) {
       uint16_t* h = reinterpret_cast<uint16_t*>(scratch_.data_ptr()) + lo_[b];
       pdt::cast16_launch(pdt::kBF16, p, h, n, comm_->stream());
-      PDT_NCCL_CHECK(ncclAllReduce(h, h, n, ncclBfloat16, ncclSum, comm_->comm(), comm_->stream()));
+      tr.all_reduce(h, n, scratch_, "sum", comm_->stream());
       pdt::widen16_launch(pdt::kBF16, h, p, n, comm_->stream());
     } else {
-      PDT_NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, comm_->comm(), comm_->stream()));
+      tr.all_reduce(p, n, grad_, "sum", comm_->stream());
     }
     comm_->track("gradient bucket all_reduce");
     launched_[b] = true;
+    order_.push_back((int64_t)b);
   }
   void reset() {
     pending_ = nparams_;
     launched_.assign(lo_.size(), false);
+    last_order_ = order_;
+    order_.clear();
   }
   std::shared_ptr<Communicator> comm_;
   Tensor grad_;
   std::vector<int64_t> lo_, hi_, param_bucket_, nparams_, pending_;
   std::vector<bool> launched_;
+  std::vector<int64_t> order_, last_order_;
   int64_t compress_ = 0;
   Tensor scratch_;  // bf16 image of the flat gradient (compress_)
+
+ public:
+  std::vector<int64_t> last_launch_order() const { return last_order_; }
 };
 
 void register_comm(py::module& m) {
@@ -394,7 +610,10 @@ void register_comm(py::module& m) {
            py::arg("rank"), py::arg("device"), py::arg("timeout_s") = 0.0, py::arg("exit_code") = 75)
       .def_property_readonly("rank", &Communicator::rank)
       .def_property_readonly("world", &Communicator::world)
+      .def_property_readonly("device", &Communicator::device)
+      .def_property_readonly("transport", &Communicator::transport_name)
       .def_property_readonly("timeout_s", &Communicator::timeout_s)
+      .def("track_compute", &Communicator::track_compute, py::arg("what") = "graph replay")
       .def("count", &Communicator::count)
       .def("pending", &Communicator::pending)
       .def("inject_stall", &Communicator::inject_stall)
@@ -415,7 +634,11 @@ void register_comm(py::module& m) {
            py::arg("compress") = 0)
       .def("ready", &Bucketer::ready)
       .def("finish", &Bucketer::finish)
-      .def("launched", &Bucketer::launched);
+      .def("launched", &Bucketer::launched)
+      .def("launch_order", &Bucketer::launch_order)
+      .def("last_launch_order", &Bucketer::last_launch_order);
+  m.def("host_communicator", &make_host_communicator, py::arg("name"), py::arg("world"), py::arg("rank"),
+        py::arg("device"), py::arg("create"), py::arg("slot_bytes") = 8 << 20, py::arg("timeout_s") = 600.0);
 }
 
 }  // namespace pdt_comm

@@ -32,7 +32,7 @@ class NativeTrainer:
                  process_group=None, reduce_metrics: bool = True, autotune: bool = False, comm: str = "torch",
                  force_comm: bool = False, graph: bool = False, last_bucket_mb: Optional[float] = 1.0,
                  comm_timeout_s: float = 0.0, time_comm: bool = False, eval_fp32: bool = False,
-                 grad_compress: str = "none"):
+                 grad_compress: str = "none", comm_transport: str = "auto"):
         self.device = torch.device(device)
         self.dtype = dtype
         self.model = model
@@ -49,7 +49,7 @@ class NativeTrainer:
         self.ncomm = None
         if comm == "native" and (self.distributed or force_comm):
             from ..parallel.comm import NativeComm
-            self.ncomm = NativeComm(self.device, process_group, timeout_s=comm_timeout_s)
+            self.ncomm = NativeComm(self.device, process_group, timeout_s=comm_timeout_s, transport=comm_transport)
         self._broadcast_initial()
         layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed,
                               last_bucket_mb=last_bucket_mb)
@@ -63,18 +63,28 @@ class NativeTrainer:
         # HIP events around bucketer.finish(): the time the compute stream waits for gradient all-reduces
         # that backward did not hide (exposed communication)
         self._comm_events = [] if time_comm else None
-        # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full
-        # SyncBN path with identity all-reduces), else over torch.distributed at world > 1
+        # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full SyncBN path
+        # with identity all-reduces), else over torch.distributed at world > 1.
+        # Native: the statistics get a communicator of their OWN (PDT_SYNCBN_COMM=own, default) and are all-reduced
+        # inline on the compute stream, forward and backward.  They are tiny and latency-bound and sit on the critical
+        # path (dgrad -> BN sums -> all-reduce -> finalize -> apply -> next dgrad), so they must never queue behind a
+        # 25 MiB gradient bucket on the bucket communicator's stream; RCCL orders collectives per communicator, so
+        # two communicators issued in the same host order on every rank keep both sequences consistent.
+        # PDT_SYNCBN_COMM=shared: one communicator (forward inline, backward on the comm stream behind the buckets).
         nsync = sync_bn and self.ncomm is not None
-        # forward statistics go straight onto the compute stream (no gradient bucket is in flight during the
-        # forward pass, so RCCL sees the same order on every rank); backward ones share the comm stream with the
-        # buckets.  PDT_SYNCBN_INLINE=0 keeps the forward on the comm stream too.
-        inline = nsync and os.environ.get("PDT_SYNCBN_INLINE", "1") != "0"
+        self.ncomm_bn = None
+        if nsync and os.environ.get("PDT_SYNCBN_COMM", "own") == "own":
+            from ..parallel.comm import NativeComm
+            self.ncomm_bn = NativeComm(self.device, process_group, timeout_s=comm_timeout_s, transport=comm_transport)
         sync_kw = dict(syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed and not nsync)
-                       else None, syncbn_allreduce=self.ncomm.all_reduce if nsync else None,
-                       syncbn_world=self.ncomm.world if nsync else 0)
-        if inline and dtype != torch.float32:
-            sync_kw["syncbn_allreduce_fwd"] = self.ncomm.all_reduce_inline
+                       else None)
+        if self.ncomm_bn is not None:
+            sync_kw.update(syncbn_allreduce=self.ncomm_bn.all_reduce_inline, syncbn_world=self.ncomm_bn.world)
+        elif nsync:
+            sync_kw.update(syncbn_allreduce=self.ncomm.all_reduce, syncbn_world=self.ncomm.world)
+            if dtype != torch.float32 and os.environ.get("PDT_SYNCBN_INLINE", "1") != "0":
+                # forward statistics straight onto the compute stream (no bucket is in flight during the forward)
+                sync_kw["syncbn_allreduce_fwd"] = self.ncomm.all_reduce_inline
         if dtype == torch.float32:
             from ..models.executor32 import ResNetExecutor32
             self.executor = ResNetExecutor32(model, self.flat, self.device, grad_ready=self.bucketer.grad_ready,
@@ -101,7 +111,9 @@ class NativeTrainer:
         # broadcast, gradient buckets, SyncBN statistics, metrics) are captured into the graph with the kernels
         # (RCCL supports stream capture; every rank captures and replays the same sequence).  c10d's
         # ProcessGroupNCCL collectives stay eager, so world > 1 on --comm torch runs without a graph.
-        self.use_graph = graph and (not self.distributed or self.ncomm is not None)
+        # (the host shared-memory transport synchronises the host inside every collective: not capturable)
+        self.use_graph = graph and (self.ncomm is None or self.ncomm.transport == "rccl") and (
+            not self.distributed or self.ncomm is not None)
         self._graphs = {}
         self._graph_warm = 0
 
@@ -114,6 +126,13 @@ class NativeTrainer:
             self.ncomm.broadcast(self.flat.data, 0)
             self._sync_buffers()
             self.flat.refresh_shadow()
+
+    def close(self) -> None:
+        """Collective teardown of the native communicators (every rank, same point)."""
+        for c in (self.ncomm_bn, self.ncomm):
+            if c is not None:
+                c.destroy()
+        self.ncomm_bn = None
 
     def on_state_loaded(self) -> None:
         """After ``model.load_state_dict`` (resume): re-derive the 16-bit shadow and the kernel weight layouts."""
@@ -185,6 +204,8 @@ class NativeTrainer:
         sx.copy_(images)
         st.copy_(target)
         g.replay()
+        if self.ncomm is not None:
+            self.ncomm.track_compute("graph replay of a training step")
         self._steps += 1
         self.optimizer.step_count += 1
         return out

@@ -248,7 +248,11 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
                              grad_compress=getattr(args, "grad_compress", "none"),
                              eval_fp32=getattr(args, "eval_precision", "compute") == "fp32", **kw)
     from .torch_trainer import TorchTrainer
-    return TorchTrainer(model, device, dtype=dtype, **kw, **torch_kw)
+    # CPU ranks: --comm native routes buckets / buffer broadcasts / metrics through the C++ communicator and bucketer
+    # over the host shared-memory transport (on GPUs the torch engine keeps c10d, whose RCCL it already set up)
+    tcomm = getattr(args, "comm", "native") if device.type == "cpu" else "torch"
+    return TorchTrainer(model, device, dtype=dtype, comm=tcomm, comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)),
+                        **kw, **torch_kw)
 
 
 def main(mode: str, argv: Optional[list] = None) -> int:

@@ -30,7 +30,8 @@ class TorchTrainer:
                  momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False, sync_bn: bool = False,
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, channels_last: bool = True,
-                 aux_loss_weight: float = 0.3, dp_device_ids=None):
+                 aux_loss_weight: float = 0.3, dp_device_ids=None, comm: str = "torch",
+                 comm_timeout_s: float = 0.0):
         self.device = torch.device(device)
         self.pg = process_group
         self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
@@ -48,8 +49,18 @@ class TorchTrainer:
         self.net = nn.DataParallel(model, device_ids=list(dp_device_ids)) if dp_device_ids else model
         self.buffers = FlatBuffers(model, self.device)
         broadcast_parameters(self.flat, self.buffers, process_group)
-        self.bucketer = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
-        self.bucketer.register_autograd_hooks()
+        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
+        # --comm native: gradient buckets, buffer broadcasts and metric all-reduces through this framework's C++
+        # communicator + bucketer (host shared-memory transport on the CPU, csrc/comm.cpp) instead of c10d
+        self.ncomm = None
+        if comm == "native" and self.distributed:
+            from ..parallel.comm import NativeBucketer, NativeComm
+            self.ncomm = NativeComm(self.device, process_group, timeout_s=comm_timeout_s)
+            self.bucketer = NativeBucketer(layout, self.ncomm)
+        else:
+            self.bucketer = layout
+        for s_, p_ in zip(self.flat.slots, self.flat.params):
+            p_.register_post_accumulate_grad_hook(lambda _p, i=s_.index: self.bucketer.grad_ready(i))
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.scaler = DeviceGradScaler(self.device, enabled=use_amp and dtype == torch.float16)
         self.broadcast_buffers = broadcast_buffers and self.distributed
@@ -66,9 +77,21 @@ class TorchTrainer:
             return contextlib.nullcontext()
         return torch.autocast(self.device.type, dtype=self.dtype)
 
+    def _sync_buffers(self) -> None:
+        if self.ncomm is None:
+            sync_buffers(self.buffers, self.pg)
+            return
+        if self.buffers.n_float:
+            self.ncomm.broadcast(self.buffers.fdata, 0)
+        if self.buffers.n_int:
+            self.ncomm.broadcast(self.buffers.idata, 0)
+
     def _reduce(self, met):
         if self.reduce_metrics:
-            dist.all_reduce(met, group=self.pg)
+            if self.ncomm is not None:
+                self.ncomm.all_reduce(met)
+            else:
+                dist.all_reduce(met, group=self.pg)
             met.div_(self.world)
         return met
 
@@ -80,7 +103,7 @@ class TorchTrainer:
     def train_step(self, images, target):
         self.model.train()
         if self.broadcast_buffers and self._steps > 0:
-            sync_buffers(self.buffers, self.pg)
+            self._sync_buffers()
         self.optimizer.zero_grad()
         with self._autocast():
             out, aux = split_outputs(self.net(self._inputs(images)))
@@ -102,7 +125,7 @@ class TorchTrainer:
     def eval_step(self, images, target):
         self.model.eval()
         if self.broadcast_buffers and self._steps > 0:
-            sync_buffers(self.buffers, self.pg)
+            self._sync_buffers()
         out = self.net(self._inputs(images)).float()  # validation runs without autocast (`:316-317`)
         loss = F.cross_entropy(out, target)
         acc = accuracy(out, target, 1)

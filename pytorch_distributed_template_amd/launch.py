@@ -50,6 +50,9 @@ def _spawn(a) -> List[subprocess.Popen]:
         env = dict(os.environ, MASTER_ADDR=a.master_addr, MASTER_PORT=str(a.master_port), WORLD_SIZE=str(world),
                    RANK=str(rank), LOCAL_RANK=str(local), LOCAL_WORLD_SIZE=str(a.nproc_per_node),
                    GROUP_RANK=str(a.node_rank))
+        # ROCm IPC: hosts whose amdgpu driver only supports dmabuf-based IPC need the non-legacy mode, otherwise RCCL's
+        # intra-node transport (and CUDA-tensor sharing between processes) fails with `hipIpcGetMemHandle: invalid
+        # argument`.  setdefault: an explicit user setting wins.
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         cmd = [sys.executable, "-u"] + (["-m", a.script] if a.module else [a.script])
         if not a.no_local_rank:

@@ -7,6 +7,12 @@ the compute stream (no host synchronisation), and the bucketed gradient all-redu
 (``Bucketer.ready`` launches a bucket's in-place SUM all-reduce the moment its last gradient is written).
 Reference counterparts: c10d ``ProcessGroupNCCL`` + ``TCPStore`` and the DDP ``Reducer`` (SURVEY §2.7,
 X1-X9; `distributed.py:124,144`).
+
+Transports (csrc/comm.cpp): ``rccl`` (the production path: one rank per GPU over xGMI) or ``host`` (a POSIX
+shared-memory group, csrc/shm_group.h) for ranks that share a GPU -- RCCL refuses duplicate devices -- or run on
+the CPU.  The host transport runs the same C++ Communicator / Bucketer code, synchronously, so the multi-rank
+bucketer logic is exercised by the CPU test suite (world 2 / 4, host tensors) and by 1-GPU DDP rehearsals
+(``bench.py --gpus 2 --dist-backend gloo``).  ``auto`` = host on the CPU or when ranks share a GPU, else rccl.
 """
 from __future__ import annotations
 
@@ -23,18 +29,27 @@ from .store import NativeStore
 _COUNTER = itertools.count()
 
 
+def _gpus_shared(world: int) -> bool:
+    """More ranks on this node than visible GPUs (a rehearsal with ranks sharing devices)."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    return torch.cuda.is_available() and local > torch.cuda.device_count()
+
+
 class NativeComm:
     """A process-group-like wrapper over :class:`_C.Communicator`."""
 
-    def __init__(self, device: torch.device, process_group=None, store=None, timeout_s: float = 0.0):
-        """The RCCL unique id travels through ``store``: c10d's store when torch.distributed is up,
-        otherwise (or when given) our native TCP store (:class:`~.store.NativeStore`, env://).
+    def __init__(self, device: torch.device, process_group=None, store=None, timeout_s: float = 0.0,
+                 transport: str = "auto"):
+        """The RCCL unique id (or the host group's segment name) travels through ``store``: c10d's store when
+        torch.distributed is up, otherwise (or when given) our native TCP store (:class:`~.store.NativeStore`).
 
         ``timeout_s > 0`` starts the C++ watchdog (csrc/comm.cpp): a collective pending longer than that, or
         an asynchronous RCCL error, aborts the communicator and exits the process non-zero (the launcher
-        then tears the group down) -- the counterpart of ProcessGroupNCCL's watchdog + ``timeout``."""
+        then tears the group down) -- the counterpart of ProcessGroupNCCL's watchdog + ``timeout``.  On the host
+        transport a barrier waiting longer than ``timeout_s`` raises (and aborts the group for every rank)."""
         self.device = torch.device(device)
-        key = f"pdt_rccl_uid_{next(_COUNTER)}"
+        seq = next(_COUNTER)
+        key = f"pdt_rccl_uid_{seq}"
         if store is None and dist.is_initialized():
             store = dist.distributed_c10d._get_default_store()
         elif store is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -45,21 +60,48 @@ class NativeComm:
             else:
                 self.rank = dist.get_rank(process_group)
                 self.world = dist.get_world_size(process_group)
+        else:
+            self.rank, self.world = 0, 1
+        self.store = store
+        if transport == "auto":
+            transport = "host" if self.device.type != "cuda" or _gpus_shared(self.world) else "rccl"
+        if transport not in ("rccl", "host"):
+            raise ValueError(f"comm transport must be auto, rccl or host, got {transport!r}")
+        if transport == "rccl" and self.device.type != "cuda":
+            raise ValueError("the rccl transport needs GPU tensors; use transport='host' on the CPU")
+        self.transport = transport
+        dev_index = (self.device.index or 0) if self.device.type == "cuda" else -1
+        if transport == "host":
+            # rank 0 publishes a fresh segment name and creates it; the others open it (retrying until it exists);
+            # the constructor's barrier returns once every rank mapped it, and rank 0 then unlinks the name
+            if self.rank == 0:
+                name = f"/pdt_comm_{os.getpid()}_{seq}_{os.urandom(4).hex()}"
+                if store is not None:
+                    store.set(key, name.encode())
+            else:
+                name = bytes(store.get(key)).decode()
+            slot = int(os.environ.get("PDT_HOST_COMM_SLOT_MB", "8")) << 20
+            self.comm = native.C.host_communicator(name, self.world, self.rank, dev_index, self.rank == 0, slot,
+                                                   float(timeout_s) if timeout_s and timeout_s > 0 else 600.0)
+            return
+        if store is not None:
             if self.rank == 0:
                 uid = native.C.rccl_unique_id()
                 store.set(key, uid)
             else:
                 uid = store.get(key)
         else:
-            self.rank, self.world = 0, 1
             uid = native.C.rccl_unique_id()
-        self.store = store
-        self.comm = native.C.Communicator(bytes(uid), self.world, self.rank, self.device.index or 0,
-                                          float(timeout_s))
+        self.comm = native.C.Communicator(bytes(uid), self.world, self.rank, dev_index, float(timeout_s))
 
     def count(self) -> int:
-        """Ranks in the RCCL communicator (``ncclCommCount``)."""
+        """Ranks in the communicator (``ncclCommCount`` on RCCL)."""
         return self.comm.count()
+
+    def track_compute(self, what: str = "graph replay") -> None:
+        """Watchdog: one tracked event on the compute stream (after a HIP-graph replay, whose captured
+        collectives are otherwise invisible to the timeout)."""
+        self.comm.track_compute(what)
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> None:
         self.comm.all_reduce(t, op, async_op)

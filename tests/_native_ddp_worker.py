@@ -62,11 +62,13 @@ def main():
     if rank == 0:
         torch.save({"data": tr.flat.data.cpu(), "fbuf": tr.buffers.fdata.cpu(), "ibuf": tr.buffers.idata.cpu(),
                     "met": torch.stack(mets).cpu(), "buckets": len(tr.bucketer.buckets),
-                    "grad": tr.flat.grad.cpu()},
+                    "grad": tr.flat.grad.cpu(), "bucketer": type(tr.bucketer).__name__,
+                    "transport": tr.ncomm.transport if tr.ncomm is not None else None},
                    os.environ["PDT_TEST_OUT"])
     dist.barrier()
     if tr.ncomm is not None:
-        tr.ncomm.destroy()
+        tr.ncomm.barrier()
+        tr.close()
     dist.destroy_process_group()
 
 

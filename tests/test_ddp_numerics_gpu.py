@@ -73,25 +73,35 @@ def _compare_updates(tr, before, data, per_tensor_tol, total_tol):
     assert total < total_tol, total
 
 
-def test_native_ddp_equals_averaged_half_batches(tmp_path):
-    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=1)
-    X, T = make_batch(2 * B, HW)
-    xa, ta = X[:B].cuda(), T[:B].cuda()
-    xb, tb = X[B:].cuda(), T[B:].cuda()
+@pytest.mark.parametrize("comm,nproc", [("torch", 2), ("native", 2), ("native", 4)])
+def test_native_ddp_equals_averaged_half_batches(tmp_path, comm, nproc):
+    """DDP at world ``nproc`` == one process averaging the ranks' gradients, bit for bit.  ``native`` runs this
+    framework's C++ communicator + bucketer (ranks share cuda:0, so it selects the host shared-memory transport,
+    which sums in rank order -- the order the oracle accumulates in)."""
+    res = _run_ranks(tmp_path, nproc=nproc, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=1, PDT_TEST_COMM=comm)
+    if comm == "native":
+        assert res["transport"] == "host" and res["bucketer"] == "NativeBucketer"
+    X, T = make_batch(nproc * B, HW)
     box = {}
 
     def steps(tr):
-        _, ma = tr.executor.train_step(xa, ta, grad_div=float(B))
-        ga = tr.flat.grad.clone()
-        box["fbuf"] = tr.buffers.fdata.clone()  # rank 0's running stats come from its own half only
-        _, mb = tr.executor.train_step(xb, tb, grad_div=float(B))
-        tr.flat.grad.add_(ga)
-        tr.optimizer.step(grad_scale=0.5)
-        box["met"] = (ma + mb) / 2
+        acc = None
+        for r in range(nproc):
+            _, m = tr.executor.train_step(X[r * B:(r + 1) * B].cuda(), T[r * B:(r + 1) * B].cuda(), grad_div=float(B))
+            if r == 0:
+                box["fbuf"] = tr.buffers.fdata.clone()  # rank 0's running stats come from its own batch only
+                acc = tr.flat.grad.clone()
+                box["met"] = m.clone()
+            else:
+                acc.add_(tr.flat.grad)
+                box["met"] = box["met"] + m
+        tr.flat.grad.copy_(acc)
+        tr.optimizer.step(grad_scale=1.0 / nproc)
+        box["met"] = box["met"] / nproc
 
     tr, before = _single(steps)
     # the statistics path is deterministic (per-block partial rows + fixed-order reduction, conv_fwd.h) and the
-    # all-reduce of two fp32 addends is exact and commutative: gradients and the update are BIT-identical
+    # all-reduce sums in the oracle's order (two addends: any order): gradients and the update are BIT-identical
     grad = tr.flat.grad.cpu()
     bad = [s.name for s in tr.flat.slots
            if not torch.equal(res["grad"][s.offset:s.offset + s.numel], grad[s.offset:s.offset + s.numel])]
@@ -112,15 +122,15 @@ def _update_errors(tr, before, a, b):
     return out
 
 
-@pytest.mark.parametrize("steps", [1, 2])
-def test_native_syncbn_equals_full_batch(tmp_path, steps):
+@pytest.mark.parametrize("steps,comm", [(1, "torch"), (2, "torch"), (2, "native")])
+def test_native_syncbn_equals_full_batch(tmp_path, steps, comm):
     """A random-init ResNet's gradient is chaotic in 16-bit arithmetic: nudging the INPUT by one part in 1e6
     already moves the parameter updates by 10-60 % (the "floor", measured here).  SyncBN(2 x B/2) must
     agree with the full batch within that floor, and far better than plain DDP(2 x B/2), whose per-rank
     BN statistics genuinely differ; a scale error on any tensor (e.g. gamma/beta gradients world x) is
     >= 100 % and fails.  Running statistics, num_batches_tracked and the loss must match closely."""
-    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=steps)
-    nosync = _run_ranks(tmp_path, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=steps)["data"]
+    res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=steps, PDT_TEST_COMM=comm)
+    nosync = _run_ranks(tmp_path, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=steps, PDT_TEST_COMM=comm)["data"]
     X, T = make_batch(2 * B, HW)
     x, t = X.cuda(), T.cuda()
     mets = []
