@@ -64,6 +64,34 @@ for stage in "$@"; do
       timeout -k 10 600 python bench.py --steps 20 --warmup 5 --autotune > gpurun_out/bench_autotune.log 2>&1; rc=$?
       grep metric gpurun_out/bench_autotune.log
       [ $rc -eq 0 ] || { echo "autotune bench failed rc=$rc"; exit $rc; } ;;
+    dp)
+      timeout -k 10 600 python -u -m pytest tests/test_dp_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_dp.log 2>&1; rc=$?
+      tail -15 gpurun_out/pytest_dp.log
+      ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
+    replay)
+      # intra-kernel race detector: every native op of 2 training steps re-run 3x from a snapshot (PDT_VALIDATE=3)
+      timeout -k 10 600 python -u tools/repeat_check.py --replay --steps 2 > gpurun_out/replay.log 2>&1; rc=$?
+      tail -8 gpurun_out/replay.log
+      ok_rc $rc || { echo "replay crashed rc=$rc"; exit $rc; } ;;
+    repeat)
+      timeout -k 10 600 python -u tools/repeat_check.py --reps 6 > gpurun_out/repeat.log 2>&1; rc=$?
+      tail -8 gpurun_out/repeat.log
+      ok_rc $rc || { echo "repeat crashed rc=$rc"; exit $rc; } ;;
+    rehearse4)
+      # 4 DDP ranks sharing the GPU: the native C++ communicator + bucketer over the host shared-memory transport
+      timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29613 bench.py --gpus 4 --steps 3 --warmup 2 --dist-backend gloo --batch-per-gpu 128 \
+        > gpurun_out/rehearse4.log 2>&1; rc=$?
+      grep metric gpurun_out/rehearse4.log
+      [ $rc -eq 0 ] || { tail -30 gpurun_out/rehearse4.log; echo "rehearse4 failed rc=$rc"; exit $rc; } ;;
+    bench50)
+      timeout -k 10 600 python bench.py --arch resnet50 --dtype fp16 --steps 10 --warmup 3 > gpurun_out/bench50.log 2>&1; rc=$?
+      grep metric gpurun_out/bench50.log
+      [ $rc -eq 0 ] || { echo "bench50 failed rc=$rc"; exit $rc; } ;;
+    bench32)
+      timeout -k 10 600 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32.log 2>&1; rc=$?
+      grep metric gpurun_out/bench32.log
+      [ $rc -eq 0 ] || { echo "bench32 failed rc=$rc"; exit $rc; } ;;
     rehearse2)
       # 2 DDP ranks sharing the one GPU over gloo: exercises the world>1 native-trainer path
       # (bucketer, buffer broadcast, metric all-reduce, side-stream ordering) without a second GPU
