@@ -779,13 +779,15 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
 
 void wgrad32(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
              int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw, int64_t splits,
-             int64_t pix_per_split) {
-  TORCH_CHECK(C % 64 == 0 && Kout % 64 == 0, "wgrad32: C and Kout must be multiples of 64");
+             int64_t pix_per_split, int64_t tile) {
+  TORCH_CHECK(tile == 64 || tile == 128, "wgrad32: tile must be 64 or 128");
+  TORCH_CHECK(C % tile == 0 && Kout % tile == 0, "wgrad32: C and Kout must be multiples of the tile");
   TORCH_CHECK(x.numel() == N * H * W * C && dy.numel() == N * Pm * Qm * Kout, "wgrad32: size mismatch");
   TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30), "wgrad32: operands too large");
   TORCH_CHECK(ldw >= T * U * C && ws.numel() >= splits * Kout * ldw, "wgrad32: workspace too small");
   TORCH_CHECK(pix_per_split % 64 == 0 && splits * pix_per_split >= N * Pm * Qm, "wgrad32: bad split plan");
   pdt::Wgrad32Args a{};
+  a.tile = (int)tile;
   a.x = pf(x, "x"); a.dy = pf(dy, "dy"); a.ws = pf(ws, "ws");
   a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
   a.stride = stride; a.pad = pad; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;

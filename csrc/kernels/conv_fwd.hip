@@ -23,8 +23,9 @@
 // wave-instruction and XOR-swizzled through the SOURCE address (chunk ^= (row>>1)&(chunks-1)), which
 // makes the ds_read_b128 fragment reads bank-conflict free.  Optional epilogues: residual add (used
 // to fuse the identity-gradient add of a residual block into dgrad) and per-channel BatchNorm
-// statistics (sum, sum of squares of the rounded outputs), reduced per block and accumulated with
-// fp64 atomics into kStatSlots slot copies (so no separate statistics pass over the output).
+// statistics (sum, sum of squares of the rounded outputs), reduced per block and written with plain stores to
+// the block's own partial row, then summed in a fixed order by stat_rows_reduce into kStatSlots slots
+// (deterministic, no atomics; conv_fwd.h) -- so no separate statistics pass over the output.
 #include <cstdlib>
 
 #include "../common.h"

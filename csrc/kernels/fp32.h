@@ -35,6 +35,7 @@ struct Wgrad32Args {
   float* ws;
   int N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, ldw, splits, pix_per_split;
   int64_t P;
+  int tile = 64;  // 64: 64x64 output tile, 4 waves | 128: 128x128, 8 waves (C, Kout % 128 == 0)
 };
 void wgrad32_launch(const Wgrad32Args& a, hipStream_t s);
 

@@ -38,12 +38,17 @@ PDT_DEVICE void zero_stat_row32(const Conv32Args& a) {
   if constexpr (EPI != 0) {
     const int tm = (int)blockIdx.x / a.n_tiles, tn = (int)blockIdx.x - tm * a.n_tiles;
     float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * 2 + (int64_t)tn * BN_ * 2;
-    for (int i = threadIdx.x; i < BN_ * 2; i += 256) dst[i] = 0.f;
+    for (int i = threadIdx.x; i < BN_ * 2; i += blockDim.x) dst[i] = 0.f;
   }
 }
 
-template <int BM, int BN, int EPI, bool RES>
-__global__ __launch_bounds__(256) void conv32_kernel(Conv32Args args) {
+// WAVES_M x WAVES_N waves, each owning a (BM / WAVES_M) x (BN / WAVES_N) accumulator block.  128 x 128 / 4 waves
+// needs 32 FLOP per staged byte: at the fp32 MFMA rate that is ~5 TB/s of L2 traffic for the whole chip, which
+// the 4-wave tile does not get (52 % of fp32 MFMA peak, profiles/r2_fp32_path.md).  256 x 256 / 8 waves (and
+// 256 x 128 / 8 waves for 128-channel GEMMs) double / 1.3x that intensity; one 128 KB-LDS block per CU with two
+// waves per SIMD, each wave running 256 MFMAs (8192 cycles) per K-step behind the next stage's DMA.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool RES>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Args args) {
   Conv32Args a = args;
   if (args.nphase > 0) {  // multi-phase launch (strided backward-data): this block's phase geometry
     const int ph = blockIdx.y;
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(256) void conv32_kernel(Conv32Args args) {
       return;
     }
   }
-  constexpr int NW = 4, WAVES_N = 2, WAVES_M = 2;
+  constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WN = BN / WAVES_N, WM = BM / WAVES_M;
   constexpr int FN = WN / 16, FM = WM / 16;
   constexpr int ROWB = 128;               // 32 fp32 K-elements per LDS row
@@ -231,8 +236,8 @@ __global__ __launch_bounds__(256) void conv32_kernel(Conv32Args args) {
         }
     }
     __syncthreads();
-    if (tid < BN * 2) {
-      const int nl = tid >> 1, k = tid & 1;
+    for (int idx = tid; idx < BN * 2; idx += 64 * NW) {
+      const int nl = idx >> 1, k = idx & 1;
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < WAVES_M; ++w) t += red[(w * BN + nl) * 2 + k];
@@ -271,21 +276,24 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
   PDT_COUNT(a.nphase > 0 ? "conv32_dgrad" : "conv32_fwd");
   Scratch part(a.stats ? (size_t)srows * a.Kout * 2 * sizeof(float) : 0, s);
   a.srows = part.as<float>();
-  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(256);
   const bool st = a.stats != nullptr, rs = a.res != nullptr;
-#define PDT_C32(BM_, BN_)                                                                                  \
+#define PDT_C32(BM_, BN_, WM_, WN_)                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                          \
-    if (st && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 1, true>), grid, block, 0, s, a);           \
-    else if (st) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 1, false>), grid, block, 0, s, a);           \
-    else if (rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 0, true>), grid, block, 0, s, a);            \
-    else hipLaunchKernelGGL((conv32_kernel<BM_, BN_, 0, false>), grid, block, 0, s, a);                   \
+    dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(64 * WM_ * WN_);                                   \
+    if (st && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, true>), grid, block, 0, s, a); \
+    else if (st) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, false>), grid, block, 0, s, a); \
+    else if (rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, true>), grid, block, 0, s, a);  \
+    else hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, false>), grid, block, 0, s, a);         \
     if (st) stat_rows_reduce_launch(a.srows, srows, a.Kout * 2, a.stats, s);                               \
     return;                                                                                              \
   }
-  PDT_C32(128, 128)
-  PDT_C32(128, 64)
+  PDT_C32(128, 128, 2, 2)
+  PDT_C32(128, 64, 2, 2)
+  PDT_C32(256, 256, 2, 4)
+  PDT_C32(256, 128, 4, 2)
 #undef PDT_C32
-  pdt_hip_fail("conv32: unsupported tile (128x128 or 128x64)", hipErrorInvalidValue, __FILE__, __LINE__);
+  pdt_hip_fail("conv32: unsupported tile (128x128, 128x64, 256x256 or 256x128)", hipErrorInvalidValue, __FILE__,
+               __LINE__);
 }
 
 // ----------------------------------------------------------------------------------------------- wgrad32
@@ -390,7 +398,119 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(Wgrad32Args a) {
       }
 }
 
+// Wide variant: 128 (Kout) x 128 (C) output tile of one tap, 8 waves as 2 (k) x 4 (c), each 64 x 32 (4 x 2 MFMA
+// tiles), 32-pixel chunks (dY and X tiles 16 KB each, 512-byte rows, 2-deep LDS-DMA ring: 64 KB, two blocks per
+// CU).  32 FLOP per staged byte against the 64 x 64 kernel's 16: the 64 x 64 tile needs ~10 TB/s of L2 traffic at
+// the fp32 MFMA rate, this one half that.  Rows are 32 chunks of 16 B; source chunk = LDS chunk ^ ((row & 3) << 2),
+// so the 4 pixel rows one MFMA reads (lane / 16) land on 4 disjoint 16-bank groups (ds_read_b32 conflict free).
+__global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
+  constexpr int PIX = 32;
+  constexpr int ROW = 512;              // 128 fp32 channels
+  constexpr int TILE = PIX * ROW;       // 16 KiB per operand tile
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave >> 2, wc = wave & 3;
+  const int split = blockIdx.x, k0 = blockIdx.y * 128;
+  const int cblocks = a.C / 128;
+  const int tap = blockIdx.z / cblocks, c0 = (blockIdx.z - tap * cblocks) * 128;
+  const int t = tap / a.U, u = tap - t * a.U;
+  const int64_t p_begin = (int64_t)split * a.pix_per_split;
+  const int64_t p_end = p_begin + a.pix_per_split < a.P ? p_begin + a.pix_per_split : a.P;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * a.C * 4u));
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (uint32_t)((uint64_t)a.P * a.Kout * 4u));
+  // DMA lane geometry: one wave-instruction = 2 rows x 32 chunks of 16 B; 16 instructions per tile, 2 per wave
+  const int lrow = lane >> 5, pc = lane & 31;
+  const int PQ = a.Pm * a.Qm;
+  auto stage = [&](int64_t p0, int buf) {
+    char* dyb = smem + buf * 2 * TILE;
+    char* xb = dyb + TILE;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ins = wave * 2 + q;
+      const int row = ins * 2 + lrow;
+      const int sc = pc ^ ((row & 3) << 2);
+      const int64_t p = p0 + row;
+      uint32_t od = kOOB, ox = kOOB;
+      if (p < p_end) {
+        od = (uint32_t)((p * a.Kout + k0 + sc * 4) * 4);
+        const int n = (int)(p / PQ);
+        const int rem = (int)(p - (int64_t)n * PQ);
+        const int i = rem / a.Qm, j = rem - (rem / a.Qm) * a.Qm;
+        const int ih = i * a.stride - a.pad + t, iw = j * a.stride - a.pad + u;
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+          ox = (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0 + sc * 4) * 4);
+      }
+      buf_lds16(rd, dyb + ins * 1024, od);
+      buf_lds16(rx, xb + ins * 1024, ox);
+    }
+  };
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  // element (row, col) lives at row*512 + (((col >> 2) ^ ((row & 3) << 2)) << 4) + (col & 3)*4; rows read
+  // together are 4*s4 + fq, so (row & 3) == fq
+  int aoff[4], boff[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = wk * 64 + i * 16 + fr;
+    aoff[i] = fq * ROW + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wc * 32 + j * 16 + fr;
+    boff[j] = TILE + fq * ROW + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+  const int nchunks = p_end > p_begin ? (int)((p_end - p_begin + PIX - 1) / PIX) : 0;
+  if (nchunks > 0) {
+    stage(p_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const int cur = ch & 1;
+      if (ch + 1 < nchunks) stage(p_begin + (int64_t)(ch + 1) * PIX, cur ^ 1);
+      const char* base = smem + cur * 2 * TILE;
+#pragma unroll
+      for (int s4 = 0; s4 < PIX / 4; ++s4) {
+        const char* sb = base + s4 * 4 * ROW;
+        float av[4], bv[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = *(const float*)(sb + aoff[i]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = *(const float*)(sb + boff[j]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // lane holds dW[k = k0 + wk*64 + i*16 + 4*fq + r][c = c0 + wc*32 + j*16 + fr]
+  float* out = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + wk * 64 + i * 16 + 4 * fq + r;
+        const int c = c0 + wc * 32 + j * 16 + fr;
+        out[(int64_t)k * a.ldw + tap * a.C + c] = acc[i][j][r];
+      }
+}
+
 void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
+  if (a.tile == 128) {
+    PDT_COUNT("wgrad32_wide");
+    dim3 grid(a.splits, a.Kout / 128, a.T * a.U * (a.C / 128)), block(512);
+    hipLaunchKernelGGL(wgrad32w_kernel, grid, block, 0, s, a);
+    return;
+  }
   PDT_COUNT("wgrad32");
   dim3 grid(a.splits, a.Kout / 64, a.T * a.U * (a.C / 64)), block(256);
   hipLaunchKernelGGL(wgrad32_kernel, grid, block, 0, s, a);

@@ -21,6 +21,7 @@ tests/test_fp32_gpu.py judges against the fp64 gradients' own sensitivity to an 
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional
 
 import torch
@@ -137,11 +138,24 @@ class ResNetExecutor32(ResNetExecutor):
     def _bn_tile(n: int) -> int:
         return 128 if n % 128 == 0 else 64
 
+    _WIDE = os.environ.get("PDT_FP32_TILE", "wide") == "wide"
+
+    def _tile32(self, n: int, m: int):
+        """(BM, BN) of the fp32 implicit GEMM: 8-wave 256-row tiles (256x256 / 256x128, twice / 1.3x the FLOP per
+        staged byte of 128x128) when the GEMM has enough rows to fill the chip, else the 4-wave 128-row tiles.
+        PDT_FP32_TILE=legacy: always the 128-row tiles (A/B)."""
+        if self._WIDE and m >= 256 * 256:
+            if n % 256 == 0:
+                return 256, 256
+            if n % 128 == 0:
+                return 256, 128
+        return 128, self._bn_tile(n)
+
     def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool):
         P, Q = c.out_hw(H, W)
         sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
-        self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, 128,
-                          self._bn_tile(c.cout))
+        self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad,
+                          *self._tile32(c.cout, N * P * Q))
         return P, Q, sp
 
     def _dgrad(self, c: _Conv, dy, N, H, W, P, Q, dx, res=None):
@@ -149,24 +163,27 @@ class ResNetExecutor32(ResNetExecutor):
         # runs zero K-steps and writes zeros (+ the residual)
         phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
                   if H - ph > 0 and W - pw > 0]
-        self.C.conv32_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases, 128,
-                            self._bn_tile(c.cin))
+        self.C.conv32_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases,
+                            *self._tile32(c.cin, N * P * Q))
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
                accumulate=False):
         ldw = R * S * C
         npix = N * P * Q
-        key = (cout, R, S, C, npix)
+        # 128 x 128 / 8-wave tiles when both channel counts allow (twice the FLOP per staged byte, fp32.hip)
+        tile = 128 if (self._WIDE and C % 128 == 0 and cout % 128 == 0) else 64
+        key = (cout, R, S, C, npix, tile)
         plan = self._plans.get(key)
         if plan is None:
-            per_split = (cout // 64) * R * S * (C // 64)
-            splits = max(1, min(self.wgrad_blocks // max(per_split, 1), (npix + 63) // 64))
+            per_split = (cout // tile) * R * S * (C // tile)
+            target = self.wgrad_blocks if tile == 64 else self.wgrad_blocks // 2  # 2 wide blocks per CU
+            splits = max(1, min(target // max(per_split, 1), (npix + 63) // 64))
             pps = ((npix + splits - 1) // splits + 63) // 64 * 64
             splits = (npix + pps - 1) // pps
             plan = self._plans[key] = (splits, pps)
         splits, pps = plan
         ws = self._buf("ws", splits * cout * ldw, torch.float32)
-        self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps)
+        self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile)
         self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, accumulate)
 
     def _stem_chunk(self, N: int) -> int:

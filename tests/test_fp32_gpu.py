@@ -34,6 +34,16 @@ SHAPES = [  # N, H, Cin, Cout, k, stride
 ]
 
 
+def _tiles(n):
+    """every (BM, BN) tile the fp32 conv kernel has for a GEMM-N of n: the 4-wave 128-row and 8-wave 256-row ones"""
+    out = [(128, 128 if n % 128 == 0 else 64)]
+    if n % 256 == 0:
+        out.append((256, 256))
+    if n % 128 == 0:
+        out.append((256, 128))
+    return out
+
+
 @pytest.mark.parametrize("shape", SHAPES)
 def test_conv32_fwd_dgrad_wgrad_match_torch(shape):
     from pytorch_distributed_template_amd.ops import native
@@ -51,17 +61,17 @@ def test_conv32_fwd_dgrad_wgrad_match_torch(shape):
     P = y.shape[2]
     xh = x.detach().permute(0, 2, 3, 1).contiguous()
     wk = w.detach().permute(0, 2, 3, 1).contiguous()  # KRSC
-    bn = 128 if cout % 128 == 0 else 64
-    # forward + BN statistics + residual
-    out = torch.empty(N, P, P, cout, device=DEV)
-    sp = torch.empty(C.stat_slots() * cout * 2, dtype=torch.float64, device=DEV)
+    # forward + BN statistics + residual, every tile configuration
     resh = res_nchw.permute(0, 2, 3, 1).contiguous()
-    C.conv32_fwd(xh, wk.reshape(-1), out, resh, sp, N, H, H, cin, cout, k, k, P, P, st, pad, 128, bn)
     ref = (y.detach() + res_nchw).permute(0, 2, 3, 1)
-    assert _rel(out, ref) < 1e-5
-    s = sp.view(C.stat_slots(), cout, 2).sum(0)
-    assert _rel(s[:, 0], ref.reshape(-1, cout).double().sum(0)) < 1e-6
-    assert _rel(s[:, 1], (ref.reshape(-1, cout).double() ** 2).sum(0)) < 1e-6
+    for bm, bn in _tiles(cout):
+        out = torch.empty(N, P, P, cout, device=DEV)
+        sp = torch.empty(C.stat_slots() * cout * 2, dtype=torch.float64, device=DEV)
+        C.conv32_fwd(xh, wk.reshape(-1), out, resh, sp, N, H, H, cin, cout, k, k, P, P, st, pad, bm, bn)
+        assert _rel(out, ref) < 1e-5, (bm, bn)
+        s = sp.view(C.stat_slots(), cout, 2).sum(0)
+        assert _rel(s[:, 0], ref.reshape(-1, cout).double().sum(0)) < 1e-6
+        assert _rel(s[:, 1], (ref.reshape(-1, cout).double() ** 2).sum(0)) < 1e-6
     # backward-data: every sub-pixel phase in one launch
     wflat = wk.reshape(-1)
     pieces, phases, off = [], [], 0
@@ -72,20 +82,22 @@ def test_conv32_fwd_dgrad_wgrad_match_torch(shape):
         phases.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, off])
         off += idx.numel()
     wt = torch.cat(pieces)
-    dx = torch.empty(N, H, H, cin, device=DEV)
     gyh = gy.permute(0, 2, 3, 1).contiguous()
-    C.conv32_dgrad(gyh, wt, dx, None, N, P, P, cout, cin, H, H, st, phases, 128, 128 if cin % 128 == 0 else 64)
-    assert _rel(dx, x.grad.permute(0, 2, 3, 1)) < 1e-5
+    for bm, bn in _tiles(cin):
+        dx = torch.empty(N, H, H, cin, device=DEV)
+        C.conv32_dgrad(gyh, wt, dx, None, N, P, P, cout, cin, H, H, st, phases, bm, bn)
+        assert _rel(dx, x.grad.permute(0, 2, 3, 1)) < 1e-5, (bm, bn)
     # weight gradient (split-K over pixels + fixed-order split reduction)
     ldw = k * k * cin
     npix = N * P * P
     pps = ((npix + 2) // 3 + 63) // 64 * 64
     splits = (npix + pps - 1) // pps
-    ws = torch.empty(splits * cout * ldw, device=DEV)
-    C.wgrad32(xh, gyh, ws, N, H, H, cin, cout, k, k, P, P, st, pad, ldw, splits, pps)
-    dw = torch.empty(cout * ldw, device=DEV)
-    C.wgrad_reduce(ws, splits, cout, ldw, ldw, cout * ldw, dw, ldw, 1.0, False)
-    assert _rel(dw.view(cout, k, k, cin), w.grad.permute(0, 2, 3, 1)) < 1e-5
+    for tile in (64, 128) if cin % 128 == 0 and cout % 128 == 0 else (64,):
+        ws = torch.empty(splits * cout * ldw, device=DEV)
+        C.wgrad32(xh, gyh, ws, N, H, H, cin, cout, k, k, P, P, st, pad, ldw, splits, pps, tile)
+        dw = torch.empty(cout * ldw, device=DEV)
+        C.wgrad_reduce(ws, splits, cout, ldw, ldw, cout * ldw, dw, ldw, 1.0, False)
+        assert _rel(dw.view(cout, k, k, cin), w.grad.permute(0, 2, 3, 1)) < 1e-5, tile
 
 
 def _setup(arch, N, HW, seed=0):

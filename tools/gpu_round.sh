@@ -88,6 +88,16 @@ for stage in "$@"; do
       timeout -k 10 600 python bench.py --arch resnet50 --dtype fp16 --steps 10 --warmup 3 > gpurun_out/bench50.log 2>&1; rc=$?
       grep metric gpurun_out/bench50.log
       [ $rc -eq 0 ] || { echo "bench50 failed rc=$rc"; exit $rc; } ;;
+    fp32)
+      timeout -k 10 600 python -u -m pytest tests/test_fp32_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_fp32.log 2>&1; rc=$?
+      tail -5 gpurun_out/pytest_fp32.log
+      ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; }
+      timeout -k 10 600 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32.log 2>&1; rc=$?
+      grep metric gpurun_out/bench32.log
+      [ $rc -eq 0 ] || { echo "bench32 failed rc=$rc"; exit $rc; }
+      PDT_FP32_TILE=legacy timeout -k 10 600 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32_legacy.log 2>&1; rc=$?
+      grep metric gpurun_out/bench32_legacy.log
+      [ $rc -eq 0 ] || { echo "bench32 legacy failed rc=$rc"; exit $rc; } ;;
     bench32)
       timeout -k 10 600 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32.log 2>&1; rc=$?
       grep metric gpurun_out/bench32.log
