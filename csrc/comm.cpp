@@ -463,6 +463,13 @@ class Communicator {
       while (!pending_.empty()) {
         Pending& p = pending_.front();
         hipError_t q = p.ev ? hipEventQuery(p.ev) : hipErrorNotReady;
+        // another thread is capturing a HIP graph (the trainer captures in thread-local mode, but be safe): the
+        // query is refused, not failed -- poll again later
+        if (q == hipErrorStreamCaptureUnsupported || q == hipErrorStreamCaptureImplicit ||
+            q == hipErrorStreamCaptureInvalidated || q == hipErrorCapturedEvent) {
+          (void)hipGetLastError();
+          break;
+        }
         if (q == hipSuccess) {
           free_evs_.push_back(p.ev);
           pending_.pop_front();

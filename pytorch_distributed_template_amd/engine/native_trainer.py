@@ -196,7 +196,7 @@ class NativeTrainer:
             sx, st = images.clone(), target.clone()
             g = torch.cuda.CUDAGraph()
             steps, sc = self._steps, self.optimizer.step_count
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 out = self._train_step_eager(sx, st)
             self._steps, self.optimizer.step_count = steps, sc  # capture does not run the step
             ent = self._graphs[key] = (g, sx, st, out)

@@ -176,7 +176,7 @@ class NativeDataParallelTrainer:
                     sx, st = x.clone(), t.clone()
                     sls = ls.clone() if ls is not None else None
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
                         out = self._replica_step(i, sx, st, sls, B, derived=True)
                     ent = self._graphs[key] = (g, sx, st, sls, out)
                 g, sx, st, sls, out = ent

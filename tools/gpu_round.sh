@@ -30,6 +30,13 @@ for stage in "$@"; do
       cd "${GRAFT_REPO_ROOT:-/root/repo}"
       tail -5 gpurun_out/prof.log
       [ $rc -eq 0 ] || { echo "prof failed rc=$rc"; exit $rc; } ;;
+    prof32)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof32" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --dtype fp32 --steps 3 --warmup 1 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof32.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      tail -2 gpurun_out/prof32.log
+      [ $rc -eq 0 ] || { echo "prof32 failed rc=$rc"; exit $rc; } ;;
     profserial)
       # one stream (PDT_WGRAD_STREAM=0) so per-kernel durations are not inflated by concurrency
       cd /tmp && export TMPDIR=/tmp
