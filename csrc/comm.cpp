@@ -200,6 +200,9 @@ class HostTransport final : public Transport {
     grp_.barrier();  // every rank has mapped the segment: its name can go (no leak if a rank dies later)
     if (rank == 0) grp_.unlink();
   }
+  ~HostTransport() override {
+    if (stage_) (void)hipHostFree(stage_);
+  }
   const char* name() const override { return "host"; }
   bool synchronous() const override { return true; }
   void all_reduce(void* buf, int64_t n, const Tensor& proto, const std::string& op, hipStream_t s) override {
@@ -220,11 +223,14 @@ class HostTransport final : public Transport {
       run([&] { grp_.all_gather(in, out, n, shm_type(proto)); });
       return;
     }
-    std::vector<uint8_t> hin(bytes), hout(bytes * grp_.world());
-    PDT_HIP_OK(hipMemcpyAsync(hin.data(), in, bytes, hipMemcpyDeviceToHost, s));
+    reserve(bytes * (1 + grp_.world()));
+    uint8_t* hin = static_cast<uint8_t*>(stage_);
+    uint8_t* hout = hin + bytes;
     PDT_HIP_OK(hipStreamSynchronize(s));
-    run([&] { grp_.all_gather(hin.data(), hout.data(), n, shm_type(proto)); });
-    PDT_HIP_OK(hipMemcpyAsync(out, hout.data(), hout.size(), hipMemcpyHostToDevice, s));
+    PDT_HIP_OK(hipMemcpyAsync(hin, in, bytes, hipMemcpyDeviceToHost, s));
+    PDT_HIP_OK(hipStreamSynchronize(s));
+    run([&] { grp_.all_gather(hin, hout, n, shm_type(proto)); });
+    PDT_HIP_OK(hipMemcpyAsync(out, hout, bytes * grp_.world(), hipMemcpyHostToDevice, s));
     PDT_HIP_OK(hipStreamSynchronize(s));
   }
   int count() override { return grp_.world(); }
@@ -241,21 +247,34 @@ class HostTransport final : public Transport {
       TORCH_CHECK(false, "host transport: ", e.what());
     }
   }
+  // Device buffers cross through PINNED host staging.  The stream is drained BEFORE the device-to-host copy: a copy
+  // into pageable memory was observed (tests/test_ddp_numerics_gpu.py, native-2) to read the gradient before the
+  // kernels the stream had been made to wait for (join_compute's event) had written it -- stale bucket contents,
+  // bit-identical on every rank, so only the single-process oracle caught it.
   void* stage_in(void* buf, size_t bytes, hipStream_t s) {
     if (device_ < 0) return buf;
-    if (stage_.size() < bytes) stage_.resize(bytes);
-    PDT_HIP_OK(hipMemcpyAsync(stage_.data(), buf, bytes, hipMemcpyDeviceToHost, s));
+    reserve(bytes);
     PDT_HIP_OK(hipStreamSynchronize(s));
-    return stage_.data();
+    PDT_HIP_OK(hipMemcpyAsync(stage_, buf, bytes, hipMemcpyDeviceToHost, s));
+    PDT_HIP_OK(hipStreamSynchronize(s));
+    return stage_;
   }
   void stage_out(void* buf, void* h, size_t bytes, hipStream_t s) {
     if (device_ < 0) return;
     PDT_HIP_OK(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
     PDT_HIP_OK(hipStreamSynchronize(s));  // the staging buffer is reused by the next collective
   }
+  void reserve(size_t bytes) {
+    if (bytes <= stage_bytes_) return;
+    if (stage_) PDT_HIP_OK(hipHostFree(stage_));
+    stage_ = nullptr;
+    PDT_HIP_OK(hipHostMalloc(&stage_, bytes, hipHostMallocDefault));
+    stage_bytes_ = bytes;
+  }
   pdt_shm::ShmGroup grp_;
   int device_;
-  std::vector<uint8_t> stage_;
+  void* stage_ = nullptr;  // pinned host staging for device buffers
+  size_t stage_bytes_ = 0;
 };
 
 class Communicator {

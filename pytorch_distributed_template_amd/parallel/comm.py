@@ -155,6 +155,7 @@ class NativeBucketer:
         self.comm = comm
         self.compress = compress
         self.buckets = layout.buckets
+        self.bucket_of = layout.bucket_of
         pb: List[int] = [0] * len(layout.flat.slots)
         for pid, bid in layout.bucket_of.items():
             pb[pid] = bid

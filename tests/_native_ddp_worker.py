@@ -36,15 +36,21 @@ def main():
     tr = NativeTrainer(model, dev, dtype=dtype, sync_bn=sync_bn, bucket_cap_mb=4, comm=comm,
                        comm_timeout_s=300.0)
     local = None
+    init = tr.flat.data.clone()
     if os.environ.get("PDT_TEST_SAVE_LOCAL") == "1":  # diagnostics: each bucket's local gradient before its all-reduce
         local = torch.zeros_like(tr.flat.grad)
         bk = tr.bucketer
         orig = bk.grad_ready
+        pending = {b["id"]: len(b["params"]) for b in bk.buckets}
 
         def grad_ready(pid):
             b = bk.buckets[bk.bucket_of[pid]]
-            if bk._pending[b["id"]] == 1:
+            pending[b["id"]] -= 1
+            if pending[b["id"]] == 0:
+                torch.cuda.synchronize()
                 local[b["lo"]:b["hi"]].copy_(tr.flat.grad[b["lo"]:b["hi"]])
+                torch.cuda.synchronize()
+                pending[b["id"]] = len(b["params"])
             orig(pid)
         bk.grad_ready = grad_ready
         tr.executor._user_grad_ready = grad_ready
@@ -58,7 +64,8 @@ def main():
     torch.cuda.synchronize()
     torch.cuda.synchronize()
     if local is not None:
-        torch.save({"local": local.cpu(), "grad": tr.flat.grad.cpu()}, os.environ["PDT_TEST_OUT"] + f".r{rank}")
+        torch.save({"local": local.cpu(), "grad": tr.flat.grad.cpu(), "init": init.cpu()},
+                   os.environ["PDT_TEST_OUT"] + f".r{rank}")
     if rank == 0:
         torch.save({"data": tr.flat.data.cpu(), "fbuf": tr.buffers.fdata.cpu(), "ibuf": tr.buffers.idata.cpu(),
                     "met": torch.stack(mets).cpu(), "buckets": len(tr.bucketer.buckets),
