@@ -883,33 +883,61 @@ void colsum32_launch(const float* d, int B, int ld, int ncols, float* out, float
 }
 
 // fp32 NCHW images -> im2col rows [N*OH*OW][ldk], column k = (r*S + s)*C + c (zero beyond R*S*C / outside)
-__global__ __launch_bounds__(256) void im2col32_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int C,
-                                                       int H, int W, int R, int S, int stride, int pad, int OH, int OW,
-                                                       int ldk) {
+// One thread per (output pixel, 4 consecutive columns): the KRSC column order k = (r*S + s)*C + c, zero past R*S*C,
+// written as one 16-byte store (a wave writes 1 KB contiguous); the 4 gathered inputs come from NCHW rows that
+// neighbouring pixels share (L2 hits).  32-bit index math with FastDiv (the old version did two 64-bit divisions
+// and modulos per element and streamed at ~1.3 TB/s: 18.5 ms of a 155 ms fp32 ResNet-18 step).
+template <int CT, int ST>
+__global__ __launch_bounds__(256) void im2col32_kernel(const float* __restrict__ x, float* __restrict__ out, int C_,
+                                                       int H, int W, int R, int S_, int stride, int pad, int OH, int OW,
+                                                       int ldk, uint32_t nchunk, FastDiv fd_cpp, FastDiv fd_ow,
+                                                       FastDiv fd_oh) {
+  const int C = CT > 0 ? CT : C_, S = ST > 0 ? ST : S_;
   const int KK = R * S * C;
-  const int64_t total = (int64_t)N * OH * OW * ldk;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
-    const int k = (int)(v % ldk);
-    const int64_t pix = v / ldk;
-    float val = 0.f;
-    if (k < KK) {
-      const int c = k % C, rs = k / C;
-      const int r = rs / S, s_ = rs - r * S;
-      const int ow = (int)(pix % OW);
-      const int64_t tq = pix / OW;
-      const int oh = (int)(tq % OH), n = (int)(tq / OH);
-      const int h = oh * stride - pad + r, w = ow * stride - pad + s_;
-      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) val = x[(((int64_t)n * C + c) * H + h) * W + w];
+  const uint32_t cpp = (uint32_t)ldk / 4u;
+  for (uint32_t v = blockIdx.x * 256u + threadIdx.x; v < nchunk; v += gridDim.x * 256u) {
+    const uint32_t pix = fdiv(v, fd_cpp);
+    const int j = (int)(v - pix * cpp);
+    const uint32_t t1 = fdiv(pix, fd_ow);
+    const int ow = (int)(pix - t1 * (uint32_t)OW);
+    const uint32_t n = fdiv(t1, fd_oh);
+    const int oh = (int)(t1 - n * (uint32_t)OH);
+    const int h0 = oh * stride - pad, w0 = ow * stride - pad;
+    const float* xn = x + (int64_t)n * C * H * W;
+    float4 o;
+    float* op = reinterpret_cast<float*>(&o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * j + e;
+      float val = 0.f;
+      if (k < KK) {
+        const int c = k % C, rs = k / C;
+        const int r = rs / S, s_ = rs - r * S;
+        const int h = h0 + r, w = w0 + s_;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) val = xn[((int64_t)c * H + h) * W + w];
+      }
+      op[e] = val;
     }
-    out[v] = val;
+    *reinterpret_cast<float4*>(out + (int64_t)v * 4) = o;
   }
 }
 
 void im2col32_launch(const float* x, float* out, int N, int C, int H, int W, int R, int S, int stride, int pad, int ldk,
                      hipStream_t s) {
   const int OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
-  hipLaunchKernelGGL(im2col32_kernel, dim3(ew_blocks((int64_t)N * OH * OW * ldk)), dim3(256), 0, s, x, out, N, C, H, W,
-                     R, S, stride, pad, OH, OW, ldk);
+  const int64_t nchunk = (int64_t)N * OH * OW * (ldk / 4);
+  if (nchunk <= 0) return;
+  if (ldk % 4 != 0 || nchunk >= (int64_t(1) << 31))
+    pdt_hip_fail("im2col32: ldk % 4 != 0 or more than 2^31 output chunks", hipErrorInvalidValue, __FILE__, __LINE__);
+  const FastDiv fc = make_fastdiv((uint32_t)(ldk / 4)), fw = make_fastdiv((uint32_t)OW), fh = make_fastdiv((uint32_t)OH);
+  const int64_t blocks64 = (nchunk + 255) / 256;
+  const unsigned blocks = (unsigned)(blocks64 < 65536 ? blocks64 : 65536);
+  if (C == 3 && S == 7)  // the ResNet stem: constant divisors
+    hipLaunchKernelGGL((im2col32_kernel<3, 7>), dim3(blocks), dim3(256), 0, s, x, out, C, H, W, R, S, stride, pad, OH,
+                       OW, ldk, (uint32_t)nchunk, fc, fw, fh);
+  else
+    hipLaunchKernelGGL((im2col32_kernel<0, 0>), dim3(blocks), dim3(256), 0, s, x, out, C, H, W, R, S, stride, pad, OH,
+                       OW, ldk, (uint32_t)nchunk, fc, fw, fh);
 }
 
 }  // namespace pdt

@@ -217,6 +217,9 @@ class ResNetExecutor:
         self.derived = torch.zeros(off[0], dtype=dtype, device=self.device)
         self._bufs: Dict[Tuple, torch.Tensor] = {}
         self._plans: Dict[Tuple, Tuple[int, int]] = {}
+        from ..ops import validate
+        self._buf_guard = (int(os.environ.get("PDT_VALIDATE_GUARD", "0") or 0)
+                           if validate.level_from_env() > 0 and self.device.type == "cuda" else 0)
         self.update_derived()
 
     # ---------------------------------------------------------------------------------- helpers
@@ -254,7 +257,14 @@ class ResNetExecutor:
         k = (key, dtype)
         t = self._bufs.get(k)
         if t is None or t.numel() < numel:
-            t = torch.empty(numel, dtype=dtype, device=self.device)
+            if getattr(self, "_buf_guard", 0):  # PDT_VALIDATE_GUARD: a canary tail behind every work buffer (ops/validate.py)
+                from ..ops import validate
+                full = torch.empty(numel + self._buf_guard, dtype=dtype, device=self.device)
+                validate.fill_canary(full[numel:])
+                validate.validator().register_tail_guard(f"{key}/{str(dtype).replace('torch.', '')}", full[numel:])
+                t = full[:numel]
+            else:
+                t = torch.empty(numel, dtype=dtype, device=self.device)
             self._bufs[k] = t
         if self._pending_reads:  # the caller is about to overwrite it: wait for side-stream readers
             ev = self._pending_reads.pop(t.data_ptr(), None)

@@ -58,6 +58,20 @@ class GuardBandError(ValidationError):
 CANARY_BITS = 0x0BADC0DE  # a finite fp32 (~7e-32): harmless if a whole-buffer op reads it, unmistakable if overwritten
 
 
+def canary_bits(t: torch.Tensor) -> torch.Tensor:
+    """Integer view of a guard tail for canary comparisons."""
+    return _bits(t)
+
+
+def canary_value(t: torch.Tensor) -> int:
+    return {8: 0x0BADC0DE0BADC0DE, 4: CANARY_BITS, 2: 0x0BAD, 1: 0xA5}[t.element_size()] if t.element_size() != 1 \
+        else (0xA5 if t.dtype == torch.uint8 else -91)
+
+
+def fill_canary(t: torch.Tensor) -> None:
+    canary_bits(t).fill_(canary_value(t))
+
+
 def _bits(t: torch.Tensor) -> torch.Tensor:
     """Bitwise view for comparisons (NaN payloads compare equal to themselves)."""
     t = t.detach().contiguous().reshape(-1)
@@ -96,10 +110,25 @@ class Validator:
         self.replayed = 0
         self.replay_host = False  # replay host-tensor ops too (CPU tests of the mechanism)
         self._guards: List[Tuple[torch.Tensor, torch.Tensor, List[Tuple[int, str]]]] = []
+        self._tails = {}
 
     def register_guard(self, buf: torch.Tensor, idx: torch.Tensor, owners: List[Tuple[int, str]]) -> None:
         """``buf[idx]`` holds canaries; ``owners`` = (first position in idx, parameter name) per slot guard."""
         self._guards.append((buf, idx, owners))
+
+    def register_tail_guard(self, name: str, tail: torch.Tensor) -> None:
+        """``tail`` (the guard elements allocated behind a work buffer, any dtype) was canary-filled by
+        :func:`fill_canary`; an op writing past the end of the buffer in front of it overwrites them."""
+        self._tails[name] = tail
+
+    def _check_tails(self, name: str, args) -> None:
+        for owner, tail in self._tails.items():
+            b = canary_bits(tail)
+            if not bool((b == canary_value(tail)).all()):
+                n = int((b != canary_value(tail)).sum())
+                raise GuardBandError(f"native op `{name}` wrote past the end of work buffer `{owner}` ({n} guard "
+                                     f"element(s) overwritten)\n  args: {_describe(args)}\n  last native ops "
+                                     f"(oldest first):\n  {self._recent()}")
 
     def _check_guards(self, name: str, args) -> None:
         for buf, idx, owners in self._guards:
@@ -180,6 +209,8 @@ class Validator:
                                       f"  last native ops (oldest first):\n  {self._recent()}") from e
             if self._guards:
                 self._check_guards(name, args)
+            if self._tails:
+                self._check_tails(name, args)
             for i, t, was_finite in pre:
                 if was_finite and not bool(torch.isfinite(t).all()):
                     bad = int((~torch.isfinite(t)).sum())

@@ -77,7 +77,8 @@ class FlatParams:
                 p.grad = _phys_view(self.grad, s.offset, s.shape, s.channels_last)
         # parameters that receive weight decay: all of them, like the reference (SURVEY §2.2 --wd)
         self.refresh_shadow()
-        if guard and self.device.type == "cuda":
+        # (single process only: a multi-rank run all-reduces whole bucket ranges, canaries included)
+        if guard and self.device.type == "cuda" and int(os.environ.get("WORLD_SIZE", "1")) == 1:
             self._install_guards(validate)
 
     def _install_guards(self, validate) -> None:

@@ -63,8 +63,9 @@ def main():
         mets.append(met.clone())
     torch.cuda.synchronize()
     torch.cuda.synchronize()
-    if local is not None:
-        torch.save({"local": local.cpu(), "grad": tr.flat.grad.cpu(), "init": init.cpu()},
+    if local is not None or os.environ.get("PDT_TEST_SAVE_RANKS") == "1":
+        torch.save({"local": local.cpu() if local is not None else None, "grad": tr.flat.grad.cpu(),
+                    "init": init.cpu(), "data": tr.flat.data.cpu(), "fbuf": tr.buffers.fdata.cpu()},
                    os.environ["PDT_TEST_OUT"] + f".r{rank}")
     if rank == 0:
         torch.save({"data": tr.flat.data.cpu(), "fbuf": tr.buffers.fdata.cpu(), "ibuf": tr.buffers.idata.cpu(),
@@ -72,6 +73,12 @@ def main():
                     "grad": tr.flat.grad.cpu(), "bucketer": type(tr.bucketer).__name__,
                     "transport": tr.ncomm.transport if tr.ncomm is not None else None},
                    os.environ["PDT_TEST_OUT"])
+    from pytorch_distributed_template_amd.ops import validate
+    v = validate.validator()
+    if v is not None:  # PDT_VALIDATE runs (tools/diag_run.sh): report replay-determinism findings of this rank
+        print(f"[rank {rank}] validator: {v.replayed} launches replayed, {len(v.findings)} findings", flush=True)
+        for f in v.findings:
+            print(f"[rank {rank}] NONDETERMINISTIC: {f}", flush=True)
     dist.barrier()
     if tr.ncomm is not None:
         tr.ncomm.barrier()

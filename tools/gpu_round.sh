@@ -105,6 +105,15 @@ for stage in "$@"; do
       PDT_FP32_TILE=legacy timeout -k 10 600 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32_legacy.log 2>&1; rc=$?
       grep metric gpurun_out/bench32_legacy.log
       [ $rc -eq 0 ] || { echo "bench32 legacy failed rc=$rc"; exit $rc; } ;;
+    table)
+      # BASELINE.md's 1-GPU cells: ResNet-18 bf16, ResNet-18 fp16 AMP + SyncBN (native comm forced at world 1:
+      # the whole SyncBN path with identity all-reduces), ResNet-50 fp16 AMP
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/t_r18.log 2>&1 || exit $?
+      grep metric gpurun_out/t_r18.log
+      timeout -k 10 600 python bench.py --steps 20 --warmup 5 --dtype fp16 --sync-bn --force-comm > gpurun_out/t_r18sbn.log 2>&1 || exit $?
+      grep metric gpurun_out/t_r18sbn.log
+      timeout -k 10 600 python bench.py --steps 10 --warmup 3 --arch resnet50 --dtype fp16 > gpurun_out/t_r50.log 2>&1 || exit $?
+      grep metric gpurun_out/t_r50.log ;;
     bench32)
       timeout -k 10 600 python bench.py --dtype fp32 --steps 5 --warmup 2 > gpurun_out/bench32.log 2>&1; rc=$?
       grep metric gpurun_out/bench32.log
