@@ -68,7 +68,18 @@ long long* dispatch_counter(const char* name) {
 }
 
 void* scratch_alloc(size_t bytes, hipStream_t s) {
-  return c10::hip::HIPCachingAllocator::raw_alloc_with_stream(bytes, s);
+  void* p = c10::hip::HIPCachingAllocator::raw_alloc_with_stream(bytes, s);
+  // PDT_SCRATCH_POISON=1 (debugging): fill every internal scratch buffer with 0xFF bytes (NaN) before the kernels
+  // that are meant to write all of it -- any element they leave unwritten then surfaces as NaN downstream
+  static const bool poison = [] {
+    const char* e = getenv("PDT_SCRATCH_POISON");
+    return e && e[0] == '1';
+  }();
+  if (poison && p && bytes) {
+    hipError_t e = hipMemsetAsync(p, 0xFF, bytes, s);
+    if (e != hipSuccess) pdt_hip_fail("hipMemsetAsync(scratch poison)", e, __FILE__, __LINE__);
+  }
+  return p;
 }
 void scratch_free(void* p) { c10::hip::HIPCachingAllocator::raw_delete(p); }
 }  // namespace pdt

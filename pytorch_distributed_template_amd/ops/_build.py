@@ -84,8 +84,14 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     hdr = _headers_digest()
     jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
 
+    # -packed-fp32-ops: no v_pk_{fma,mul,add}_f32 in device code.  With them, the compiler issued a packed FP32
+    # op and, right behind it, an LDS load overwriting that op's source VGPRs; under GPU contention the last
+    # quarter-wave (lanes 48-63) intermittently read the NEW values (a register WAR race): the fused
+    # BN-backward statistics of conv_dgrad_bn changed between identical runs (tools/dgrad_bn_probe.py,
+    # profiles/r3_nondeterminism_root_cause.md) -- the long-standing non-repeatability.  (The host half of the
+    # compile ignores the feature with a warning.)
     hip_flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-                 "-munsafe-fp-atomics", f"-I{CSRC}"]
+                 "-munsafe-fp-atomics", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", f"-I{CSRC}"]
     py_inc = sysconfig.get_paths()["include"]
     cxx_flags = ["-O2", "-std=c++17", "-fPIC", f"-I{CSRC}", f"-I{py_inc}", "-D__HIP_PLATFORM_AMD__=1",
                  "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
