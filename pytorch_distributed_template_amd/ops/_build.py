@@ -22,8 +22,8 @@ import sysconfig
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
-BUILD = os.path.join(REPO, "build", "native")
-OUT = os.path.join(PKG_DIR, "_C.so")
+BUILD = os.environ.get("PDT_BUILD_DIR") or os.path.join(REPO, "build", "native")  # A/B builds: another object dir
+OUT = os.environ.get("PDT_BUILD_OUT") or os.path.join(PKG_DIR, "_C.so")             # ... and another .so
 ARCH = os.environ.get("PDT_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -90,8 +90,10 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     # BN-backward statistics of conv_dgrad_bn changed between identical runs (tools/dgrad_bn_probe.py,
     # profiles/r3_nondeterminism_root_cause.md) -- the long-standing non-repeatability.  (The host half of the
     # compile ignores the feature with a warning.)
+    no_pk = [] if os.environ.get("PDT_PACKED_FP32") == "1" else ["-Xclang", "-target-feature", "-Xclang",
+                                                                  "-packed-fp32-ops"]  # PDT_PACKED_FP32=1: A/B only
     hip_flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-                 "-munsafe-fp-atomics", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", f"-I{CSRC}"]
+                 "-munsafe-fp-atomics"] + no_pk + [f"-I{CSRC}"]
     py_inc = sysconfig.get_paths()["include"]
     cxx_flags = ["-O2", "-std=c++17", "-fPIC", f"-I{CSRC}", f"-I{py_inc}", "-D__HIP_PLATFORM_AMD__=1",
                  "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
