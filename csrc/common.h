@@ -33,7 +33,13 @@ template <> struct E16<kBF16> {
 template <> struct E16<kF16> {
   typedef f16x8_t vec8;
   static PDT_DEVICE float to_f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
-  static PDT_DEVICE uint16_t from_f(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+  static PDT_DEVICE uint16_t from_f(float f) {
+    // round the fp32 value itself: the opaque asm keeps the compiler from fusing the fma that produced f into a
+    // v_fma_mixlo_f16 (one rounding straight to f16) in some kernels and not in others -- two kernels rounding
+    // the same fp32 expression (bn_apply vs the fused producer BN of conv_l1) must agree bit for bit
+    asm("" : "+v"(f));
+    return __builtin_bit_cast(uint16_t, (_Float16)f);
+  }
   static PDT_DEVICE f32x4_t mfma16x16x32(vec8 a, vec8 b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
