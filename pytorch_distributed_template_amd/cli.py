@@ -139,6 +139,9 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
                    help="native engine collectives: this framework's own RCCL communicator and C++ gradient "
                         "bucketer (default; torch.distributed then only provides the rendezvous store) or "
                         "torch.distributed (RCCL via c10d)")
+    g.add_argument("--comm-transport", default="auto", choices=["auto", "rccl", "host"],
+                   help="native communicator transport: rccl (one rank per GPU) | host (shared memory: ranks sharing a "
+                        "GPU, CPU ranks) | auto")
     g.add_argument("--grad-compress", default="none", choices=["none", "bf16"],
                    help="native communicator: all-reduce the gradient buckets in bf16 (half the bytes; upstream "
                         "DDP's bf16_compress_hook). Default none: fp32 like the reference")

@@ -246,6 +246,7 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
                              last_bucket_mb=lb if lb > 0 else None,
                              comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)),
                              grad_compress=getattr(args, "grad_compress", "none"),
+                             comm_transport=getattr(args, "comm_transport", "auto"),
                              eval_fp32=getattr(args, "eval_precision", "compute") == "fp32", **kw)
     from .torch_trainer import TorchTrainer
     # CPU ranks: --comm native routes buckets / buffer broadcasts / metrics through the C++ communicator and bucketer
