@@ -791,12 +791,18 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
 void wgrad32(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
              int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw, int64_t splits,
              int64_t pix_per_split, int64_t tile) {
-  TORCH_CHECK(tile == 64 || tile == 128, "wgrad32: tile must be 64 or 128");
-  TORCH_CHECK(C % tile == 0 && Kout % tile == 0, "wgrad32: C and Kout must be multiples of the tile");
+  TORCH_CHECK(tile == 64 || tile == 128 || tile == 3, "wgrad32: tile must be 64, 128 or 3 (3x3 halo kernel)");
+  const int64_t cb = tile == 3 ? 64 : tile;
+  TORCH_CHECK(C % cb == 0 && Kout % cb == 0, "wgrad32: C and Kout must be multiples of the tile");
   TORCH_CHECK(x.numel() == N * H * W * C && dy.numel() == N * Pm * Qm * Kout, "wgrad32: size mismatch");
   TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30), "wgrad32: operands too large");
   TORCH_CHECK(ldw >= T * U * C && ws.numel() >= splits * Kout * ldw, "wgrad32: workspace too small");
-  TORCH_CHECK(pix_per_split % 64 == 0 && splits * pix_per_split >= N * Pm * Qm, "wgrad32: bad split plan");
+  if (tile == 3) {  // halo kernel: splits over OUTPUT ROWS (N * Pm of them)
+    TORCH_CHECK(pix_per_split > 0 && splits * pix_per_split >= N * Pm && T == 3 && U == 3 && stride == 1 && pad == 1 &&
+                    Pm == H && Qm == W && Qm <= 62, "wgrad32: bad halo plan / geometry");
+  } else {
+    TORCH_CHECK(pix_per_split % 64 == 0 && splits * pix_per_split >= N * Pm * Qm, "wgrad32: bad split plan");
+  }
   pdt::Wgrad32Args a{};
   a.tile = (int)tile;
   a.x = pf(x, "x"); a.dy = pf(dy, "dy"); a.ws = pf(ws, "ws");

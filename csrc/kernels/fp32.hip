@@ -291,9 +291,11 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
   PDT_C32(128, 64, 2, 2)
   PDT_C32(256, 256, 2, 4)
   PDT_C32(256, 128, 4, 2)
+  PDT_C32(256, 64, 4, 1)
+  PDT_C32(512, 64, 8, 1)
 #undef PDT_C32
-  pdt_hip_fail("conv32: unsupported tile (128x128, 128x64, 256x256 or 256x128)", hipErrorInvalidValue, __FILE__,
-               __LINE__);
+  pdt_hip_fail("conv32: unsupported tile (128x128, 128x64, 256x256, 256x128, 256x64 or 512x64)", hipErrorInvalidValue,
+               __FILE__, __LINE__);
 }
 
 // ----------------------------------------------------------------------------------------------- wgrad32
@@ -504,7 +506,131 @@ __global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
       }
 }
 
+// Halo variant for 3x3 / stride 1 / pad 1 convs over 64-channel blocks (ResNet layer1): a block owns ONE kernel row
+// r_tap and computes all three taps s of it -- a 64 (Kout) x 192 (s, C) tile -- over whole output rows.  Per output
+// row it stages the dY row (Q pixels) and the input row h + r_tap - 1 with a one-pixel halo (Q + 2 pixels, the
+// image padding as zeros), and tap s reads the input tile shifted by s rows: 48 FLOP per staged byte instead of the
+// 64 x 64 kernel's 16.  4 waves, each 64 (k) x 48 (s, c) = 4 x 3 MFMA 16x16 tiles; 2-deep LDS-DMA ring of
+// (Q + Q + 2 + 2) x 256 B.  Rows: the pixel-row swizzle of wgrad32 (chunk ^ (row & 3) << 2) keeps the four rows one
+// MFMA reads (lane / 16, plus the tap shift) on distinct bank groups.
+constexpr int kHaloMaxQ = 62;
+__global__ __launch_bounds__(256) void wgrad32_halo_kernel(Wgrad32Args a) {
+  constexpr int ROW = 256;                       // 64 fp32 channels
+  constexpr int XR = kHaloMaxQ + 2;               // staged input rows (halo included), 64
+  constexpr int DR = kHaloMaxQ + 2;               // staged dY rows (multiple of 4 for the DMA), 64
+  constexpr int TILE_D = DR * ROW, TILE_X = XR * ROW;
+  constexpr int STAGE = TILE_D + TILE_X;          // 32 KB
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int split = blockIdx.x, rt = blockIdx.y;
+  const int cblocks = a.C / 64;
+  const int k0 = (blockIdx.z / cblocks) * 64, c0 = (blockIdx.z - (blockIdx.z / cblocks) * cblocks) * 64;
+  const int Q = a.Qm, nrows = a.N * a.Pm;
+  const int r_begin = split * a.pix_per_split;  // pix_per_split counts OUTPUT ROWS in this kernel
+  const int r_end = r_begin + a.pix_per_split < nrows ? r_begin + a.pix_per_split : nrows;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * a.C * 4u));
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (uint32_t)((uint64_t)a.P * a.Kout * 4u));
+  const int lrow = lane >> 4, pc = lane & 15;
+  const int sc = pc ^ (lrow << 2);  // (row & 3) == lrow for rows 4*ins + lrow
+  auto stage = [&](int orow, int buf) {
+    char* db = smem + buf * STAGE;
+    char* xb = db + TILE_D;
+    const int n = orow / a.Pm, h = orow - n * a.Pm;
+    const int ih = h + rt - 1;
+    const bool row_ok = (unsigned)ih < (unsigned)a.H;
+    // 16 dY rows-of-4 + 16 X rows-of-4 = 32 instructions, 8 per wave
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int ins = wave * 8 + q;
+      if (ins < 16) {
+        const int row = ins * 4 + lrow;  // dY pixel w = row
+        const uint32_t od = row < Q ? (uint32_t)((((int64_t)orow * Q + row) * a.Kout + k0 + sc * 4) * 4) : kOOB;
+        buf_lds16(rd, db + ins * 1024, od);
+      } else {
+        const int xi = ins - 16;
+        const int row = xi * 4 + lrow;  // input pixel iw = row - 1
+        const int iw = row - 1;
+        const uint32_t ox = (row_ok && (unsigned)iw < (unsigned)a.W && row < Q + 2)
+                                ? (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0 + sc * 4) * 4) : kOOB;
+        buf_lds16(rx, xb + xi * 1024, ox);
+      }
+    }
+  };
+  f32x4_t acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  int aoff[4], bcol[3], bsh[3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 16 + fr;  // k within the 64-wide block
+    aoff[i] = fq * ROW + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int cc = wave * 48 + j * 16;  // (s, c) column of this fragment
+    bsh[j] = cc / 64;                   // tap s: the input tile shifted by s rows
+    bcol[j] = (cc & 63) + fr;
+  }
+  const int steps = (Q + 3) / 4;
+  if (r_end > r_begin) {
+    stage(r_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int orow = r_begin; orow < r_end; ++orow) {
+      const int cur = (orow - r_begin) & 1;
+      if (orow + 1 < r_end) stage(orow + 1, cur ^ 1);
+      const char* db = smem + cur * STAGE;
+      const char* xb = db + TILE_D;
+      for (int s4 = 0; s4 < steps; ++s4) {
+        float av[4], bv[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = *(const float*)(db + s4 * 4 * ROW + aoff[i]);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int row = s4 * 4 + fq + bsh[j];
+          bv[j] = *(const float*)(xb + row * ROW + ((((bcol[j] >> 2) ^ ((row & 3) << 2))) << 4) + (bcol[j] & 3) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // lane holds dW[k = k0 + i*16 + 4*fq + r][tap (rt, s), c = c0 + bcol - fr + fr]; ws column = (rt*3 + s)*C + c
+  float* out = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + i * 16 + 4 * fq + r;
+        out[(int64_t)k * a.ldw + (rt * 3 + bsh[j]) * a.C + c0 + bcol[j]] = acc[i][j][r];
+      }
+}
+
+bool wgrad32_halo_supported(const Wgrad32Args& a) {
+  return a.T == 3 && a.U == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 && a.Kout % 64 == 0 &&
+         a.Pm == a.H && a.Qm == a.W && a.Qm <= kHaloMaxQ;
+}
+
 void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
+  if (a.tile == 3) {  // halo kernel (wgrad32_halo_supported): splits over output rows
+    if (!wgrad32_halo_supported(a))
+      pdt_hip_fail("wgrad32: halo kernel needs a 3x3/s1/p1 conv, 64-channel blocks and W <= 62", hipErrorInvalidValue,
+                   __FILE__, __LINE__);
+    PDT_COUNT("wgrad32_halo");
+    dim3 grid(a.splits, 3, (a.Kout / 64) * (a.C / 64)), block(256);
+    hipLaunchKernelGGL(wgrad32_halo_kernel, grid, block, 0, s, a);
+    return;
+  }
   if (a.tile == 128) {
     PDT_COUNT("wgrad32_wide");
     dim3 grid(a.splits, a.Kout / 128, a.T * a.U * (a.C / 128)), block(512);

@@ -139,6 +139,8 @@ class ResNetExecutor32(ResNetExecutor):
         return 128 if n % 128 == 0 else 64
 
     _WIDE = os.environ.get("PDT_FP32_TILE", "wide") == "wide"
+    # 64-channel GEMMs (layer1, the stem): rows per tile (128: 4 waves of 64x32; 256: 4 waves of 64x64; 512: 8 waves)
+    _BM64 = int(os.environ.get("PDT_FP32_BM64", "128"))
 
     def _tile32(self, n: int, m: int):
         """(BM, BN) of the fp32 implicit GEMM: 8-wave 256-row tiles (256x256 / 256x128, twice / 1.3x the FLOP per
@@ -149,6 +151,8 @@ class ResNetExecutor32(ResNetExecutor):
                 return 256, 256
             if n % 128 == 0:
                 return 256, 128
+            if n == 64 and self._BM64 in (256, 512):
+                return self._BM64, 64
         return 128, self._bn_tile(n)
 
     def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool):
@@ -166,20 +170,34 @@ class ResNetExecutor32(ResNetExecutor):
         self.C.conv32_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases,
                             *self._tile32(c.cin, N * P * Q))
 
+    _HALO = os.environ.get("PDT_FP32_HALO", "1") == "1"
+
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
                accumulate=False):
         ldw = R * S * C
         npix = N * P * Q
-        # 128 x 128 / 8-wave tiles when both channel counts allow (twice the FLOP per staged byte, fp32.hip)
-        tile = 128 if (self._WIDE and C % 128 == 0 and cout % 128 == 0) else 64
+        # 3x3 / s1 / p1 over 64-channel blocks with wide rows (layer1): the halo kernel, all three taps of a kernel
+        # row per block (48 FLOP per staged byte); else 128 x 128 / 8-wave tiles when both channel counts allow
+        # (32 FLOP/B), else 64 x 64 (16 FLOP/B)
+        if (self._HALO and R == 3 and S == 3 and st == 1 and pad == 1 and P == H and Q == W and 28 <= Q <= 62
+                and C == 64 and cout % 64 == 0):
+            tile = 3
+        else:
+            tile = 128 if (self._WIDE and C % 128 == 0 and cout % 128 == 0) else 64
         key = (cout, R, S, C, npix, tile)
         plan = self._plans.get(key)
         if plan is None:
-            per_split = (cout // tile) * R * S * (C // tile)
-            target = self.wgrad_blocks if tile == 64 else self.wgrad_blocks // 2  # 2 wide blocks per CU
-            splits = max(1, min(target // max(per_split, 1), (npix + 63) // 64))
-            pps = ((npix + splits - 1) // splits + 63) // 64 * 64
-            splits = (npix + pps - 1) // pps
+            if tile == 3:  # splits over the N * P output rows; 3 kernel rows x channel blocks per split
+                per_split = 3 * (cout // 64) * (C // 64)
+                splits = max(1, min(1024 // per_split, N * P))
+                pps = (N * P + splits - 1) // splits
+                splits = (N * P + pps - 1) // pps
+            else:
+                per_split = (cout // tile) * R * S * (C // tile)
+                target = self.wgrad_blocks if tile == 64 else self.wgrad_blocks // 2  # 2 wide blocks per CU
+                splits = max(1, min(target // max(per_split, 1), (npix + 63) // 64))
+                pps = ((npix + splits - 1) // splits + 63) // 64 * 64
+                splits = (npix + pps - 1) // pps
             plan = self._plans[key] = (splits, pps)
         splits, pps = plan
         ws = self._buf("ws", splits * cout * ldw, torch.float32)
@@ -225,7 +243,8 @@ class ResNetExecutor32(ResNetExecutor):
             Cn.im2col32(x32[n0:n1], cols, n1 - n0, 3, H, W, st.R, st.S, st.st, st.pad, STEM_K)
             spc = self._buf("stats_chunk", self.n_slots * st.cout * 2, torch.float64) if train else None
             Cn.conv32_fwd(cols, wst, y0[n0 * P0 * Q0 * st.cout:n1 * P0 * Q0 * st.cout], None, spc,
-                          (n1 - n0) * P0 * Q0, 1, 1, STEM_K, st.cout, 1, 1, 1, 1, 1, 0, 128, 64)
+                          (n1 - n0) * P0 * Q0, 1, 1, STEM_K, st.cout, 1, 1, 1, 1, 1, 0,
+                          *self._tile32(st.cout, (n1 - n0) * P0 * Q0))
             if train:
                 sp.add_(spc)  # chunks in a fixed order: deterministic
         if train:

@@ -29,6 +29,7 @@ def _rel(a, b):
 
 
 SHAPES = [  # N, H, Cin, Cout, k, stride
+    (2, 56, 64, 64, 3, 1), (3, 30, 64, 128, 3, 1),  # layer1 geometry (the halo weight-gradient kernel) and a ragged W
     (4, 14, 64, 128, 3, 1), (4, 14, 64, 64, 3, 2), (4, 14, 128, 256, 1, 2), (3, 9, 192, 128, 3, 1),
     (2, 7, 256, 512, 3, 2), (5, 10, 64, 256, 1, 1),
 ]
@@ -37,6 +38,8 @@ SHAPES = [  # N, H, Cin, Cout, k, stride
 def _tiles(n):
     """every (BM, BN) tile the fp32 conv kernel has for a GEMM-N of n: the 4-wave 128-row and 8-wave 256-row ones"""
     out = [(128, 128 if n % 128 == 0 else 64)]
+    if n == 64:
+        out += [(256, 64), (512, 64)]
     if n % 256 == 0:
         out.append((256, 256))
     if n % 128 == 0:
@@ -92,11 +95,14 @@ def test_conv32_fwd_dgrad_wgrad_match_torch(shape):
     npix = N * P * P
     pps = ((npix + 2) // 3 + 63) // 64 * 64
     splits = (npix + pps - 1) // pps
-    for tile in (64, 128) if cin % 128 == 0 and cout % 128 == 0 else (64,):
-        ws = torch.empty(splits * cout * ldw, device=DEV)
-        C.wgrad32(xh, gyh, ws, N, H, H, cin, cout, k, k, P, P, st, pad, ldw, splits, pps, tile)
+    tiles = [64] + ([128] if cin % 128 == 0 and cout % 128 == 0 else []) + (
+        [3] if k == 3 and st == 1 and cin % 64 == 0 and cout % 64 == 0 and H <= 62 else [])
+    for tile in tiles:
+        sp, pp = (splits, pps) if tile != 3 else (3, (N * P + 2) // 3)  # halo kernel: splits over output rows
+        ws = torch.empty(sp * cout * ldw, device=DEV)
+        C.wgrad32(xh, gyh, ws, N, H, H, cin, cout, k, k, P, P, st, pad, ldw, sp, pp, tile)
         dw = torch.empty(cout * ldw, device=DEV)
-        C.wgrad_reduce(ws, splits, cout, ldw, ldw, cout * ldw, dw, ldw, 1.0, False)
+        C.wgrad_reduce(ws, sp, cout, ldw, ldw, cout * ldw, dw, ldw, 1.0, False)
         assert _rel(dw.view(cout, k, k, cin), w.grad.permute(0, 2, 3, 1)) < 1e-5, tile
 
 
