@@ -103,9 +103,11 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
                         "supported, torch otherwise")
     g.add_argument("--precision", default="auto", choices=["auto", "bf16", "fp16", "fp32"],
                    help="compute dtype; auto = fp16 with --use_amp, bf16 otherwise on GPU, fp32 on CPU")
-    g.add_argument("--eval-precision", default="compute", choices=["compute", "fp32"],
-                   help="validation dtype: the training compute dtype, or fp32 on the native fp32 kernels over the "
-                        "fp32 master weights (the reference validates without autocast)")
+    g.add_argument("--eval-precision", default="auto", choices=["auto", "compute", "fp32"],
+                   help="validation dtype: fp32 on the native fp32 kernels over the fp32 master weights (the reference "
+                        "validates without autocast, `distributed_syncBN_amp.py:309-317`, and in fp32 everywhere), or "
+                        "the training compute dtype; auto = fp32 for distributed.py / distributed_syncBN_amp.py, compute "
+                        "for native DataParallel")
     g.add_argument("--synthetic", default=False, type=str2bool, nargs="?", const=True,
                    help="use synthetic ImageNet-shaped data instead of --data")
     g.add_argument("--synthetic-train-size", type=int, default=1281167)

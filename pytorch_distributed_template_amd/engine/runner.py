@@ -247,7 +247,7 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
                              comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)),
                              grad_compress=getattr(args, "grad_compress", "none"),
                              comm_transport=getattr(args, "comm_transport", "auto"),
-                             eval_fp32=getattr(args, "eval_precision", "compute") == "fp32", **kw)
+                             eval_fp32=getattr(args, "eval_precision", "auto") in ("fp32", "auto"), **kw)
     from .torch_trainer import TorchTrainer
     # CPU ranks: --comm native routes buckets / buffer broadcasts / metrics through the C++ communicator and bucketer
     # over the host shared-memory transport (on GPUs the torch engine keeps c10d, whose RCCL it already set up)
