@@ -933,6 +933,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_pre_supported", &conv_fwd_pre_supported);
   m.def("bn_slot_sum", &bn_slot_sum);
   m.def("stat_slots", &stat_slots);
+  m.def("conv_l1_set_pp", &pdt::conv_l1_set_pp, py::arg("mode"),
+        "layer1 kernel choice: 1 = 8-wave ping-pong, 0 = 4-wave, -1 = PDT_CONV_L1_PP (default); returns the previous");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_finalize_slots", &bn_finalize_slots);
   m.def("bn_bwd_finalize_slots", &bn_bwd_finalize_slots);

@@ -17,6 +17,7 @@
 //     registers across all of a block's tiles.
 // Backward-data is the same convolution of dY with the transposed, 180-degree-rotated weights
 // ([C][3][3][K] with taps reversed): ``flip`` reads tap 8 - t of the derived dgrad weights.
+#include <cstdlib>
 #include <type_traits>
 
 #include "../common.h"
@@ -354,6 +355,386 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 8-wave "ping-pong" variant of the kernel above (the default; PDT_CONV_L1_PP=0 selects the 4-wave one).
+//
+// The 4-wave kernel runs one wave per SIMD, so everything that is not an MFMA -- the epilogue (16-bit
+// conversion, statistics, 14-16 scattered stores per lane), the fused producer-BN transform of the halo
+// (PRE), the barrier at every tile -- leaves the matrix pipe idle, and its 14 pixel groups split 4/4/3/3
+// over the waves (two SIMDs idle a quarter of every tile).  Here two groups of 4 waves (one wave of each
+// group per SIMD) work on alternate tiles of the block one phase apart:
+//     phase A: group 0 computes tile 2i        | group 1: epilogue of tile 2i-1, DMA (+ PRE transform) of 2i+1
+//     phase B: group 0: epilogue 2i, DMA 2i+2   | group 1 computes tile 2i+1
+// so on every SIMD one wave's MFMAs run while its partner does the memory / VALU work of the other tile.
+// LDS: the resident weights (72 KB, shared) + ONE halo buffer per group (2 x 43.5 KB) = the same 160 KB.
+// A group's buffer is refilled in its memory phase right after its compute phase read it (the phase
+// barrier orders the two), and each wave waits for its own DMA pieces (counted vmcnt) and -- PRE --
+// transforms exactly the halo chunks it DMA'd itself, so no extra barrier is needed before the next
+// compute phase's barrier.  Work split inside a group: 2 (32 output channels) x 2 (7 pixel groups) --
+// balanced, 14 MFMAs per 9 LDS reads per K-step.
+template <int DT, int EPI, bool RES, bool PRE, bool FLIP>
+__global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int NJ = 7;  // pixel groups per wave
+  __shared__ __attribute__((aligned(1024))) char smem[kLds + 1024];
+  char* const wl = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, gw = wave & 3;
+  const int wn = gw & 1, wm = gw >> 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, pch = lane & 7;
+  char* const sbuf = smem + kWB + grp * kStageB;  // this group's halo buffer
+
+  const int TH = (a.H + 3) / 4;
+  const int tiles = a.N * TH;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, lb = blockIdx.x >> 3, per_x = G >> 3;
+  const int t_per = (tiles + 7) >> 3;
+  const int t_begin = xcd * t_per, t_end = min(tiles, t_begin + t_per);
+  const int first = t_begin + lb;
+  const int nk = first < t_end ? (t_end - first + per_x - 1) / per_x : 0;  // this block's tiles (block-uniform)
+
+  const uint32_t img_bytes = (uint32_t)a.N * a.H * kW * 128u;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, img_bytes);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)kWB);
+  const __amdgpu_buffer_rsrc_t ry1 = make_rsrc(EPI >= 2 ? a.bn_y1 : a.x, img_bytes);
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? a.res : a.x, img_bytes);
+  const __amdgpu_buffer_rsrc_t rmask = make_rsrc(EPI == 3 ? (const void*)a.bn_mask : (const void*)a.x, img_bytes / 16u);
+
+  // ---- resident weights: 72 DMA instructions, 9 per wave (all DMA here is asm: explicitly counted) ----
+#pragma unroll
+  for (int m = 0; m < 9; ++m) {
+    const int ii = wave + 8 * m;
+    const int L = ii * 64 + lrow * 8 + pch;
+    const int co = L / 72, p = L - co * 72;
+    buf_lds16_asm(rw, wl + ii * 1024, (uint32_t)(co * 72 + wswz(co, p)) * 16u);
+  }
+  // ---- a group's halo DMA: 44 instructions, 11 per wave, the last one half-masked ----
+  auto stage_tile = [&](int t) {
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    int lr = lrow;
+    asm volatile("" : "+v"(lr));  // per-call row decode: hoisted out of the tile loop it is ~40 live registers
+#pragma unroll
+    for (int m = 0; m < 11; ++m) {
+      const int ii = gw + 4 * m;
+      const int R = ii * 8 + lr;
+      if (R < kXRows) {
+        const int hr = R / kXP, wc = R - (R / kXP) * kXP;
+        const int h = h0 - 1 + hr, w = wc - 1;
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW;
+        buf_lds16_asm(rx, sbuf + ii * 1024,
+                      ok ? (uint32_t)((((n * a.H + h) * kW + w) * 64 + (pch ^ (wc & 7)) * 8) * 2) : kOOB);
+      }
+    }
+    asm volatile("" ::: "memory");  // no later store may be scheduled ahead of the DMA (counted waits below)
+  };
+  // PRE: this lane's halo chunks are row (gw + 4m) * 8 + lrow, physical chunk pch = logical chunk pch ^ (column & 7);
+  // the BN coefficients of each chunk's 8 channels come from the LDS coefficient block (registers are short here)
+  auto transform = [&](int t) {  // after this wave's own DMA of tile t landed
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    const float* cpre = (const float*)(smem + kLds);
+#pragma unroll
+    for (int m = 0; m < 11; ++m) {
+      const int R = (gw + 4 * m) * 8 + lrow;
+      const bool live = R < kXRows;
+      const int Rc = live ? R : 0;
+      const int hr = Rc / kXP, wc = Rc - (Rc / kXP) * kXP;
+      const int h = h0 - 1 + hr, w = wc - 1;
+      const bool ok = live && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW;
+      const float* cp = cpre + (pch ^ (wc & 7)) * 8;
+      float sc[8], sh[8];
+      *(float4*)&sc[0] = *(const float4*)(cp);
+      *(float4*)&sc[4] = *(const float4*)(cp + 4);
+      *(float4*)&sh[0] = *(const float4*)(cp + 64);
+      *(float4*)&sh[4] = *(const float4*)(cp + 68);
+      char* q = sbuf + Rc * 128 + pch * 16;
+      const uint4 v = *(const uint4*)q;
+      if (ok) *(uint4*)q = pre_act8<DT>(v, sc, sh);
+    }
+  };
+
+  // per pixel group: halo row (tap 0,0) of this lane's pixel; groups wm*7 .. wm*7+6 of the tile
+  // Fragment addresses without per-read arithmetic.  This kernel swizzles a halo row by its COLUMN (physical
+  // chunk = logical chunk ^ (column & 7); conflict-free like the row swizzle, tools/lds_sim.py): a tap (tr, tu)
+  // shifts the row by dR = 58 tr + tu but the column only by tu, so baddr[j][tu] -- the LDS byte address of
+  // group j's kk = 0 fragment at column shift tu -- plus the immediate dR * 128 addresses every tap; kk = 1 flips
+  // address bit 6 (its chunk is the kk = 0 chunk ^ 4).  The weight address is one base per kk plus immediates
+  // (cout block i, tap): 23 address registers in all, one VALU op (the xor) per fragment read at kk = 1.
+  uint32_t baddr[NJ][3];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int px = (wm * NJ + j) * 16 + pix_of_lane(fr);
+    const int r = px / kW, w = px - (px / kW) * kW;
+    const int R0 = r * kXP + w;  // halo column of tap (., 0) is w
+#pragma unroll
+    for (int tu = 0; tu < 3; ++tu)
+      baddr[j][tu] = (uint32_t)(kWB + grp * kStageB + R0 * 128 + ((fq ^ ((w + tu) & 7)) << 4));
+  }
+  const uint32_t abase0 = (uint32_t)((wn * 32 + fr) * 1152 + ((fq ^ ((fr >> 1) & 7)) << 4));
+  const uint32_t abase1 = abase0 ^ 64u;
+  auto xor64 = [](uint32_t x) {
+    uint32_t r;
+    asm volatile("v_xor_b32 %0, 64, %1" : "=v"(r) : "v"(x));
+    return r;
+  };
+
+  constexpr int KS = EPI == 0 ? 1 : 2;
+  float sacc[2][4][KS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
+
+  float* const cfl = (float*)(smem + kLds);
+  if constexpr (EPI >= 2) {
+    if (tid < 256) cfl[tid] = a.bn_coef1[tid];  // published by the prologue barrier
+  }
+  if constexpr (PRE) {
+    if (tid < 128) cfl[tid] = a.pre_coef[tid];  // scale[64] | shift[64]
+    __syncthreads();                            // the prologue transform reads them
+  }
+  auto coef = [&](int q, int i) { return *(const float4*)(cfl + q * 64 + wn * 32 + i * 16 + 4 * fq); };
+
+  f32x4_t acc[2][NJ];
+  // epilogue operands of the tile being computed: loaded at the start of its compute phase (latency hidden
+  // under the MFMAs), pinned complete at its end
+  // epilogue operands (residual, BN input, ReLU mask) are loaded at the start of the memory phase, see memphase
+  u32x2v pre_res[RES ? NJ : 1][RES ? 2 : 1], pre_y1[EPI >= 2 ? NJ : 1][EPI >= 2 ? 2 : 1];
+  u32x2v pre_m[EPI == 3 ? NJ : 1];
+  // a tile's 4 x 56 output pixels are one contiguous block: pixel px of tile t is element (t's first pixel + px) * 64
+  const int lpx0 = pix_of_lane(fr) * 64;
+  int lpx = lpx0;  // re-opaqued per use site (see stage_tile)
+  auto obase_of = [&](int t, int j) {
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    return (int64_t)(n * a.H + h0) * (kW * 64) + (lpx + (wm * NJ + j) * 1024);
+  };
+
+  auto compute = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    vec8 af[2][2], bf[2][NJ];
+    auto load = [&](int st, int sl) {
+      const int tap = st >> 1, kk = st & 1;
+      const int tr = tap / 3, tu = tap % 3;
+      const int wtap = FLIP ? 8 - tap : tap;
+      const int dR = tr * kXP + tu;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[sl][i] = *(const vec8*)(smem + (kk ? abase1 : abase0) + i * 16 * 1152 + wtap * 128);
+      // (volatile xor: computed here, not hoisted out of the tile loop as 49 more live registers)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bf[sl][j] = *(const vec8*)(smem + (kk ? xor64(baddr[j][tu]) : baddr[j][tu]) + dR * 128);
+    };
+    __builtin_amdgcn_s_setprio(1);
+    load(0, 0);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      if (st + 1 < 18) load(st + 1, (st + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = E::mfma16x16x32(af[st & 1][i], bf[st & 1][j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // epilogue: lane holds couts wn*32 + i*16 + 4*fq + r of pixel (wm*7 + j)*16 + pix_of_lane(fr); exactly
+  // 2 * NJ = 14 stores per lane (every pixel of a tile is in range: H % 4 == 0)
+  constexpr int kStores = 2 * NJ;
+  auto epilogue = [&](int t) {
+    lpx = lpx0;
+    asm volatile("" : "+v"(lpx));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t ob = obase_of(t, j);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c0 = wn * 32 + i * 16 + 4 * fq;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (RES) {
+          const u32x2v rr = pre_res[j][i];
+          v[0] += E::to_f((uint16_t)(rr[0] & 0xffff));
+          v[1] += E::to_f((uint16_t)(rr[0] >> 16));
+          v[2] += E::to_f((uint16_t)(rr[1] & 0xffff));
+          v[3] += E::to_f((uint16_t)(rr[1] >> 16));
+        }
+        float y1[4];
+        if constexpr (EPI >= 2) {
+          const u32x2v q1 = pre_y1[j][i];
+          y1[0] = E::to_f((uint16_t)(q1[0] & 0xffff)); y1[1] = E::to_f((uint16_t)(q1[0] >> 16));
+          y1[2] = E::to_f((uint16_t)(q1[1] & 0xffff)); y1[3] = E::to_f((uint16_t)(q1[1] >> 16));
+          if constexpr (EPI == 2) {
+            const float4 sc = coef(0, i), sh = coef(1, i);
+            if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
+            if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
+            if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
+            if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
+          } else {
+            const uint32_t mb = c0 < 32 ? pre_m[j][0] >> c0 : pre_m[j][1] >> (c0 - 32);
+            if (!(mb & 1u)) v[0] = 0.f;
+            if (!(mb & 2u)) v[1] = 0.f;
+            if (!(mb & 4u)) v[2] = 0.f;
+            if (!(mb & 8u)) v[3] = 0.f;
+          }
+        }
+        uint16_t o[4];
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2) o[r2] = E::from_f(v[r2]);
+        uint2 packed;
+        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        *(uint2*)(a.y + ob + c0) = packed;
+        if constexpr (EPI == 1) {
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2) {
+            const float q = E::to_f(o[r2]);
+            sacc[i][r2][0] += q;
+            sacc[i][r2][1] += q * q;
+          }
+        } else if constexpr (EPI >= 2) {
+          const float4 mu = coef(2, i), is = coef(3, i);
+          const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2) {
+            const float dz = E::to_f(o[r2]);
+            sacc[i][r2][0] += dz;
+            sacc[i][r2][1] += dz * (y1[r2] - m1[r2]) * i1[r2];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one pixel group at a time: bounded epilogue temporaries
+    }
+  };
+
+  // memory phase of a group: DMA of tile k_dma into its (just read) buffer first, then the epilogue of tile
+  // k_epi under it, then wait for this wave's DMA only (the epilogue's stores are the kStores youngest
+  // vector-memory operations) and, PRE, transform the chunks this wave DMA'd
+  auto memphase = [&](int k_epi, int k_dma) {
+    constexpr bool OPS = RES || EPI >= 2;
+    if constexpr (OPS) {
+      // epilogue operands of tile k_epi: asm buffer loads (uncounted by the compiler) ahead of the DMA, waited for
+      // with the DMA still in flight (vmcnt(11): the 11 DMA pieces are the youngest), pinned by "+v" operands
+      if (k_epi >= 0) {
+        // buffer loads: one 32-bit offset per pixel group (the channel block is an immediate), not 14 pointers
+        const int t = first + k_epi * per_x;
+        const int n = t / TH, h0 = (t - n * TH) * 4;
+        const uint32_t tb = (uint32_t)(n * a.H + h0) * (kW * 64u);  // tile's first element (< 2^31: 4 GB tensors)
+        lpx = lpx0;
+        asm volatile("" : "+v"(lpx));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const uint32_t e = tb + (uint32_t)(lpx + (wm * NJ + j) * 1024);
+          const uint32_t yo = (e + wn * 32 + 4 * fq) * 2u;
+          if constexpr (RES) {
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_res[j][0]) : "v"(yo), "s"(rres));
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_res[j][1]) : "v"(yo), "s"(rres));
+          }
+          if constexpr (EPI >= 2) {
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_y1[j][0]) : "v"(yo), "s"(ry1));
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_y1[j][1]) : "v"(yo), "s"(ry1));
+          }
+          if constexpr (EPI == 3)
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_m[j]) : "v"(e >> 3), "s"(rmask));
+        }
+      }
+    }
+    if (k_dma >= 0) stage_tile(first + k_dma * per_x);
+    if constexpr (OPS) {
+      if (k_epi >= 0) {
+        if (k_dma >= 0)
+          asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (RES) asm volatile("" : "+v"(pre_res[j][0]), "+v"(pre_res[j][1]));
+          if constexpr (EPI >= 2) asm volatile("" : "+v"(pre_y1[j][0]), "+v"(pre_y1[j][1]));
+          if constexpr (EPI == 3) asm volatile("" : "+v"(pre_m[j]));
+        }
+      }
+    }
+    if (k_epi >= 0) epilogue(first + k_epi * per_x);
+    if (k_dma >= 0) {
+      if (k_epi >= 0)
+        __builtin_amdgcn_s_waitcnt((kStores & 0xF) | ((kStores >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (PRE) transform(first + k_dma * per_x);
+    }
+  };
+  auto phase_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: group g stages the block's tile g
+  if (grp < nk) stage_tile(first + grp * per_x);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight pieces and halo pieces
+  if constexpr (PRE) {
+    if (grp < nk) transform(first + grp * per_x);
+  }
+  phase_barrier();
+  // phase p: the group with grp == p & 1 computes tile p; the other one finishes tile p - 1 and stages tile p + 1
+  // (tile 1 was staged by the prologue).  The phase count is block-uniform: every wave passes the same barriers.
+  const int nphase = 2 * ((nk + 1) >> 1) + 1;
+  for (int p = 0; p < nphase; ++p) {
+    if ((p & 1) == grp) {
+      if (p < nk) compute(first + p * per_x);
+    } else {
+      const int ke = p - 1 < nk ? p - 1 : -1;  // p - 1 < 0 -> -1 as well
+      const int kd = p >= 1 && p + 1 < nk ? p + 1 : -1;
+      if (ke >= 0 || kd >= 0) memphase(ke, kd);
+    }
+    if (p + 1 < nphase) phase_barrier();
+  }
+
+  if constexpr (EPI > 0) {
+    // block totals: DPP row scan over the 16 pixel lanes, then the 8 waves through LDS (group 0's halo
+    // buffer is free once every wave passed the barrier below), summed in a fixed order per channel
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* red = (float*)(smem + kWB);  // [8 waves][32 channels][2]
+    if (fr == 15) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lc = i * 16 + 4 * fq + r;
+          red[(wave * 32 + lc) * 2 + 0] = sacc[i][r][0];
+          red[(wave * 32 + lc) * 2 + 1] = sacc[i][r][1];
+        }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int c = tid >> 1, k = tid & 1, cn = c >> 5, lc = c & 31;
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) s += red[((g * 4 + m * 2 + cn) * 32 + lc) * 2 + k];
+      a.srows[(int64_t)blockIdx.x * 128 + tid] = s;
+    }
+  }
+}
+
 bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
   // H % 4 == 0: whole 4-row tiles only (the epilogue has no per-pixel range checks; see conv_l1_kernel)
   if (a.C != 64 || a.Kout != 64 || a.cs != 64 || a.W != kW || a.OW != kW || a.bnb == 3 || a.H % 4 != 0) return false;
@@ -376,6 +757,14 @@ bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
   return false;
 }
 
+static int g_conv_l1_pp = -1;  // -1: PDT_CONV_L1_PP decides; 0 / 1: set by conv_l1_set_pp (tests, A/B)
+
+int conv_l1_set_pp(int mode) {
+  const int old = g_conv_l1_pp;
+  g_conv_l1_pp = mode;
+  return old;
+}
+
 void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s) {
   ConvFwdArgs a = args;
   if (a.nphase == 1) a.w = args.w + args.pwoff[0];
@@ -392,17 +781,33 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     pdt_hip_fail("conv_l1: the fused producer BN (pre_coef) needs a forward conv with statistics, no residual",
                  hipErrorInvalidValue, __FILE__, __LINE__);
   if (a.pre_coef) PDT_COUNT("conv_l1_fwd_fused_bn_relu");
+  // PDT_CONV_L1_PP=0: the 4-wave kernel everywhere (A/B).  The 8-wave ping-pong kernel takes every variant
+  // except the block-output BN-backward epilogue (EPI 3: residual + BN input + ReLU mask operands do not fit
+  // its 256 registers without spilling), which stays on the 4-wave kernel.
+  static const bool pp_env = [] {
+    const char* e = getenv("PDT_CONV_L1_PP");
+    return e && e[0] == '1';  // opt-in until measured on the GPU
+  }();
+  const bool pp_on = g_conv_l1_pp >= 0 ? g_conv_l1_pp != 0 : pp_env;
+  const bool pp = pp_on && (epi == 0 || (epi == 1 && !rs && !flip) || (epi == 2 && !rs));
+  if (pp) PDT_COUNT("conv_l1_pp");
   Scratch part(a.stats ? (size_t)G * 128 * sizeof(float) : 0, s);
   a.srows = part.as<float>();
-#define PDT_L1(DT_, E_, R_) hipLaunchKernelGGL((conv_l1_kernel<DT_, E_, R_>), dim3(G), dim3(256), 0, s, a, flip)
-#define PDT_L1P(DT_) hipLaunchKernelGGL((conv_l1_kernel<DT_, 1, false, true>), dim3(G), dim3(256), 0, s, a, flip)
-#define PDT_L1_DT(DT_)                                                                                 \
-  if (epi == 0 && !rs) PDT_L1(DT_, 0, false);                                                          \
-  else if (epi == 0 && rs) PDT_L1(DT_, 0, true);                                                       \
-  else if (epi == 1 && !rs && a.pre_coef) PDT_L1P(DT_);                                                 \
-  else if (epi == 1 && !rs) PDT_L1(DT_, 1, false);                                                     \
-  else if (epi == 2 && !rs) PDT_L1(DT_, 2, false);                                                     \
-  else if (epi == 3 && rs) PDT_L1(DT_, 3, true);                                                       \
+  const dim3 grid(G);
+#define PDT_L1OLD(DT_, E_, R_, P_) hipLaunchKernelGGL((conv_l1_kernel<DT_, E_, R_, P_>), grid, dim3(256), 0, s, a, flip)
+#define PDT_L1PP(DT_, E_, R_, P_, F_) hipLaunchKernelGGL((conv_l1pp_kernel<DT_, E_, R_, P_, F_>), grid, dim3(512), 0, s, a)
+#define PDT_L1_DT(DT_)                                                                                   \
+  if (pp) {                                                                                              \
+    if (epi == 0 && !rs) { if (flip) PDT_L1PP(DT_, 0, false, false, true); else PDT_L1PP(DT_, 0, false, false, false); } \
+    else if (epi == 0) { if (flip) PDT_L1PP(DT_, 0, true, false, true); else PDT_L1PP(DT_, 0, true, false, false); }    \
+    else if (epi == 1) { if (a.pre_coef) PDT_L1PP(DT_, 1, false, true, false); else PDT_L1PP(DT_, 1, false, false, false); } \
+    else { if (flip) PDT_L1PP(DT_, 2, false, false, true); else PDT_L1PP(DT_, 2, false, false, false); }                \
+  } else if (epi == 0 && !rs) PDT_L1OLD(DT_, 0, false, false);                                            \
+  else if (epi == 0 && rs) PDT_L1OLD(DT_, 0, true, false);                                               \
+  else if (epi == 1 && !rs && a.pre_coef) PDT_L1OLD(DT_, 1, false, true);                                \
+  else if (epi == 1 && !rs) PDT_L1OLD(DT_, 1, false, false);                                             \
+  else if (epi == 2 && !rs) PDT_L1OLD(DT_, 2, false, false);                                             \
+  else if (epi == 3 && rs) PDT_L1OLD(DT_, 3, true, false);                                               \
   else pdt_hip_fail("conv_l1: unsupported epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
   if (dtype == kBF16) {
     PDT_L1_DT(kBF16)
@@ -410,8 +815,8 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     PDT_L1_DT(kF16)
   }
 #undef PDT_L1_DT
-#undef PDT_L1P
-#undef PDT_L1
+#undef PDT_L1PP
+#undef PDT_L1OLD
   if (a.stats) stat_rows_reduce_launch(a.srows, G, 128, a.stats, s);
 }
 

@@ -659,3 +659,55 @@ def test_fused_producer_bn_relu_layer1(dtype):
     assert torch.equal(ws_u, ws_f)
     # not eligible: H % 4 != 0 (partial row tiles go to the generic kernel, which has no fused producer BN)
     assert not C.conv_fwd_pre_supported(N, 10, W)
+
+
+@pytest.mark.parametrize("N,H", [(3, 12), (5, 56), (1, 4)])
+@pytest.mark.parametrize("variant", ["fwd", "fwd_stats", "fwd_pre", "dgrad_res", "dgrad_bn"])
+def test_conv_l1_pingpong_matches_4wave(variant, N, H):
+    """The 8-wave ping-pong layer1 kernel (two wave groups on alternate tiles, column-swizzled halo, counted
+    waits) must write BIT-IDENTICAL outputs to the 4-wave kernel (same MFMA order per accumulator) and the same
+    statistics up to fp32 summation order; block counts 1..many tiles (odd / even tiles per block)."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    torch.manual_seed(31)
+    W = 56
+    x = _rand16(N, H, W, 64)
+    w = _rand16(64, 3, 3, 64, scale=1.0 / 24)
+    coef = torch.cat([torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.5,
+                      torch.randn(64, device=DEV) * 0.1, torch.rand(64, device=DEV) + 0.5]).contiguous()
+    res = _rand16(N, H, W, 64)
+    y1 = _rand16(N, H, W, 64)
+    from pytorch_distributed_template_amd.ops import conv
+
+    def run(pp):
+        old = C.conv_l1_set_pp(pp)
+        try:
+            C.reset_dispatch_counts()
+            y = torch.empty_like(x)
+            st = torch.zeros(C.stat_slots() * 64 * 2, dtype=torch.float64, device=DEV)
+            if variant == "fwd":
+                C.conv_fwd(x, w, y, None, None, N, H, W, 64, 64, 3, 3, H, W, 1, 1, -1, -1, 1, 1, H, W, 1, 1, 0, 0,
+                           256, 64, 64, 0)
+            elif variant == "fwd_stats":
+                C.conv_fwd(x, w, y, None, st, N, H, W, 64, 64, 3, 3, H, W, 1, 1, -1, -1, 1, 1, H, W, 1, 1, 0, 0,
+                           256, 64, 64, 0)
+            elif variant == "fwd_pre":
+                C.conv_fwd_pre(x, w, y, st, coef, N, H, W)
+            elif variant == "dgrad_res":
+                y = conv.conv_dgrad(x, w, H, W, 1, 1, residual=res)
+            else:
+                y = conv.conv_dgrad(x, w, H, W, 1, 1, bnb=(1, y1, coef, None, None, None, st))
+            torch.cuda.synchronize()
+            return y, st, dict(C.dispatch_counts())
+        finally:
+            C.conv_l1_set_pp(old)
+
+    y4, s4, d4 = run(0)
+    y8, s8, d8 = run(1)
+    assert d8.get("conv_l1_pp", 0) >= 1 and d4.get("conv_l1_pp", 0) == 0
+    assert torch.equal(y4, y8)
+    assert torch.allclose(s4.view(-1, 128).sum(0), s8.view(-1, 128).sum(0), rtol=1e-6, atol=1e-6)
+    ref = None
+    if variant.startswith("fwd") and variant != "fwd_pre":
+        ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+        assert _rel(y8, ref) < 1e-2

@@ -4,6 +4,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -35,3 +37,18 @@ def test_timeline_gaps_busy_union_and_gaps(tmp_path):
     gaps = [ln for ln in out if "gap" in ln]
     assert "40.0 us" in gaps[0] and "after conv_fwd_kernel<0>" in gaps[0] and "before sgd_kernel<0>" in gaps[0]
     assert "20.0 us" in gaps[1] and "after sgd_kernel<0>" in gaps[1]  # previous step's last kernel
+
+
+def test_counted_waits_in_layer1_pingpong_kernel():
+    """The 8-wave layer1 kernel counts its asm DMA / operand loads itself (s_waitcnt vmcnt(11) / vmcnt(14)); a spill
+    or a store scheduled into those windows would be a silent race.  Compile it (hipcc -S, gfx950) and check every
+    instantiation's ISA: no scratch instructions, each counted window holds at least its count of younger ops."""
+    import shutil
+    import subprocess
+    import sys
+    if shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not available")
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "check_counted_waits.py")
+    r = subprocess.run([sys.executable, tool], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("ok ") >= 8, r.stdout
