@@ -785,7 +785,7 @@ PDT_DEVICE int l1_swz(int row2d, int col) { return (((col >> 1) & 1) << 1) | ((r
 
 // PRE: x is the raw output of the block's first conv; its BatchNorm + ReLU is applied to each staged X halo in
 // LDS (conv_l1.hip, PRE) -- the activation is never materialised.
-template <int DT, bool PRE = false>
+template <int DT, bool PRE = false, bool kL1Pipe = true>
 __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -890,6 +890,51 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
     }
     const char* sx = smem + buf * kL1Stage;
     const char* sy = sx + kL1XBytes;
+    if constexpr (kL1Pipe) {
+      // software-pipelined: the fragments of the next tap (or of the next column block's first tap) are read
+      // while this tap's 4 MFMAs run -- one wave per SIMD, so nothing else would cover the transposed-read latency
+      // (the straight loop below exposes it on every tap: ~36 % MFMA busy).  Tap t >= 1 of a block reads into
+      // slot t & 1; tap 0 into the carried slot (nb / na), loaded during the previous block's last tap.
+      auto rd_a = [&](int j, vec8 (&dst)[2]) {
+        const int ycol = 8 * j + q;
+        const char* yb = sy + (g * kL1W + ycol) * 128;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dst[i] = frag(yb, g, ycol, kh * 2 + i);
+      };
+      auto rd_b = [&](int j, int tp, vec8 (&dst)[2]) {
+        const int tr = tp / 3, tu = tp - tr * 3;
+        const int xcol = 8 * j + tu + q;
+        const char* xb = sx + ((g + tr) * kL1XP + xcol) * 128;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) dst[c] = frag(xb, g + tr, xcol, chh * 2 + c);
+      };
+      vec8 na[2], nb[2];
+      rd_a(0, na);
+      rd_b(0, 0, nb);
+#pragma unroll 1
+      for (int j = 0; j < kL1W / 8; ++j) {
+        vec8 af[2] = {na[0], na[1]};
+        vec8 bs[3][2] = {{nb[0], nb[1]}, {nb[0], nb[1]}, {nb[0], nb[1]}};  // [2] = tap 0's slot
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const int cur = tp == 0 ? 2 : (tp & 1);
+          if (tp < 8) {
+            rd_b(j, tp + 1, bs[(tp + 1) & 1]);
+          } else if (j + 1 < kL1W / 8) {
+            rd_a(j + 1, na);
+            rd_b(j + 1, 0, nb);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) acc[tp][i][c] = E::mfma16x16x32(af[i], bs[cur][c], acc[tp][i][c]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      buf ^= 1;
+      continue;
+    }
 #pragma unroll 1
     for (int j = 0; j < kL1W / 8; ++j) {
       // A = dY^T (rows k): output row g, columns 8j + q (+4)
@@ -946,17 +991,25 @@ int wgrad3x3_c64_blocks() {
 
 void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s) {
   PDT_COUNT("wgrad3x3_c64");
-  if (a.pre_coef) {
-    PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
-    if (dtype == kBF16)
-      hipLaunchKernelGGL((wgrad3x3_c64_kernel<kBF16, true>), dim3(blocks), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((wgrad3x3_c64_kernel<kF16, true>), dim3(blocks), dim3(256), 0, s, a);
-  } else if (dtype == kBF16) {
-    hipLaunchKernelGGL((wgrad3x3_c64_kernel<kBF16>), dim3(blocks), dim3(256), 0, s, a);
+  // PDT_WGRAD_L1_PIPE=0: the unpipelined tap loop (A/B)
+  static const bool pipe = [] {
+    const char* e = getenv("PDT_WGRAD_L1_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  if (a.pre_coef) PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
+#define PDT_W3(DT_, P_)                                                                         \
+  do {                                                                                          \
+    if (pipe)                                                                                   \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, true>), dim3(blocks), dim3(256), 0, s, a);  \
+    else                                                                                        \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, false>), dim3(blocks), dim3(256), 0, s, a); \
+  } while (0)
+  if (dtype == kBF16) {
+    if (a.pre_coef) PDT_W3(kBF16, true); else PDT_W3(kBF16, false);
   } else {
-    hipLaunchKernelGGL((wgrad3x3_c64_kernel<kF16>), dim3(blocks), dim3(256), 0, s, a);
+    if (a.pre_coef) PDT_W3(kF16, true); else PDT_W3(kF16, false);
   }
+#undef PDT_W3
 }
 
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)
