@@ -192,7 +192,9 @@ class ShmGroup {
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
     while (hdr_->gen.load(std::memory_order_acquire) == g) {
-      if (aborted()) throw std::runtime_error("shm group: a peer aborted the group");
+      // an abort raised AFTER the last rank completed this barrier must not fail it: re-check the generation
+      if (aborted() && hdr_->gen.load(std::memory_order_acquire) == g)
+        throw std::runtime_error("shm group: a peer aborted the group");
       if (++spins > 1024) {
         if (timeout_s_ > 0 && elapsed(t0) > timeout_s_) {
           abort();
