@@ -891,6 +891,34 @@ void colsum32(const Tensor& d, int64_t B, int64_t ld, int64_t ncols, Tensor& out
   pdt::colsum32_launch(pf(d, "d"), B, ld, ncols, pf(out, "out"), (float)scale, cur_stream());
 }
 
+// window-mode fp32 stem (conv32 over the zero-padded NHWC4 image, K = R kernel rows x 32: 8 pixels x 4 channels)
+void stem_pack32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t pad, int64_t Hp,
+                 int64_t Wp) {
+  TORCH_CHECK(C <= 3 && x.numel() >= N * C * H * W && out.numel() == N * Hp * Wp * 4 && Hp >= H + 2 * pad &&
+              Wp >= W + 2 * pad, "stem_pack32: sizes");
+  pdt::stem_pack32_launch(pf(x, "x"), pf(out, "out"), N, C, H, W, pad, Hp, Wp, cur_stream());
+}
+
+void conv32_stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& stats, int64_t N, int64_t Hp, int64_t Wp,
+                     int64_t R, int64_t P, int64_t Q, int64_t stride, int64_t Kout, int64_t bm, int64_t bn) {
+  TORCH_CHECK(xp.numel() == N * Hp * Wp * 4 && w.numel() == Kout * R * 32 && y.numel() == N * P * Q * Kout,
+              "conv32_stem_fwd: size mismatch");
+  TORCH_CHECK((P - 1) * stride + R <= Hp && (Q - 1) * stride + 8 <= Wp && Kout % bn == 0,
+              "conv32_stem_fwd: the padded image must hold every 8-pixel window");
+  TORCH_CHECK(xp.numel() < (int64_t(1) << 30) && N * P * Q < (int64_t(1) << 31), "conv32_stem_fwd: operands too large");
+  pdt::Conv32Args a{};
+  a.x = pf(xp, "xp"); a.w = pf(w, "w"); a.y = pf(y, "y");
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * Kout * 2, "conv32_stem_fwd: stats buffer too small");
+    a.stats = pd(*stats, "stats");
+  }
+  a.N = N; a.H = Hp; a.W = Wp; a.C = 32; a.cs = 4; a.Kout = Kout; a.T = R; a.U = 1; a.Pm = P; a.Qm = Q;
+  a.ist_h = stride; a.ist_w = stride; a.ioff_h = 0; a.ioff_w = 0; a.tstep_h = 1; a.tstep_w = 0;
+  a.OH = P; a.OW = Q; a.ost_h = 1; a.ost_w = 1; a.ooff_h = 0; a.ooff_w = 0;
+  a.M = N * P * Q;
+  pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
+}
+
 void im2col32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
               int64_t stride, int64_t pad, int64_t ldk) {
   const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
@@ -982,5 +1010,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool32_bwd", &avgpool32_bwd);
   m.def("xent32", &xent32);
   m.def("colsum32", &colsum32);
+  m.def("stem_pack32", &stem_pack32);
+  m.def("conv32_stem_fwd", &conv32_stem_fwd);
   m.def("im2col32", &im2col32);
 }

@@ -15,6 +15,8 @@ struct Conv32Args {
   float* srows;
   int srows_pp;
   int N, H, W, C, Kout, T, U;
+  int cs;  // elements per input pixel (0: == C).  4: the stem's "window" mode over a zero-padded NHWC4 image, one
+           // 32-element K-step = 8 consecutive pixels x 4 channels of a kernel row (conv_fwd.hip's window mode)
   int Pm, Qm;
   int ist_h, ist_w, ioff_h, ioff_w, tstep_h, tstep_w;
   int OH, OW, ost_h, ost_w, ooff_h, ooff_w;
@@ -57,6 +59,8 @@ void xent32_launch(const float* logits, int ldl, const float* bias, const int64_
                    float* out_logits, float* dlogits, const float* loss_scale, float grad_div, float* row_loss,
                    float* row_correct, hipStream_t s);
 void colsum32_launch(const float* d, int B, int ld, int ncols, float* out, float scale, hipStream_t s);
+// fp32 NCHW images -> zero-padded NHWC4 [N][Hp][Wp][4] (channel 3 and the border zero): the window-mode stem operand
+void stem_pack32_launch(const float* x, float* out, int N, int C, int H, int W, int pad, int Hp, int Wp, hipStream_t s);
 void im2col32_launch(const float* x, float* out, int N, int C, int H, int W, int R, int S, int stride, int pad, int ldk,
                      hipStream_t s);
 

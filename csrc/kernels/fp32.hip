@@ -91,7 +91,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
   const int TU = a.T * a.U;
   const int ksteps = TU * (a.C / 32);
 
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * a.C * 4u));
+  const int cs = a.cs ? a.cs : a.C;  // element stride between input pixels (window mode: 4)
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * cs * 4u));
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)((uint64_t)a.Kout * TU * a.C * 4u));
   const int lrow = lane >> 3, pchunk = lane & 7;
   int brow_h[B_INSTR], brow_w[B_INSTR];
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
       const int i = (int)fdiv((uint32_t)rem, fd_q), jj = rem - i * a.Qm;
       brow_h[j] = i * a.ist_h + a.ioff_h;
       brow_w[j] = jj * a.ist_w + a.ioff_w;
-      brow_off[j] = (uint32_t)((((int64_t)(nimg * a.H + brow_h[j]) * a.W + brow_w[j]) * a.C + bch * 4) * 4);
+      brow_off[j] = (uint32_t)((((int64_t)(nimg * a.H + brow_h[j]) * a.W + brow_w[j]) * cs + bch * 4) * 4);
     } else {
       brow_h[j] = -(1 << 29);
       brow_w[j] = 0;
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
 #pragma unroll
     for (int j = 0; j < A_INSTR; ++j) buf_lds16(rw, sbase + (wave * A_INSTR + j) * 1024, arow_off[j] + a_delta);
     const int dh = t * a.tstep_h, dw = u * a.tstep_w;
-    const int b_delta = ((dh * a.W + dw) * a.C + c0) * 4;
+    const int b_delta = ((dh * a.W + dw) * cs + c0) * 4;
 #pragma unroll
     for (int j = 0; j < B_INSTR; ++j) {
       const int h = brow_h[j] + dh, w = brow_w[j] + dw;
@@ -1006,6 +1007,31 @@ __global__ __launch_bounds__(256) void colsum32_kernel(const float* __restrict__
 
 void colsum32_launch(const float* d, int B, int ld, int ncols, float* out, float scale, hipStream_t s) {
   hipLaunchKernelGGL(colsum32_kernel, dim3((ncols + 63) / 64), dim3(256), 0, s, d, B, ld, ncols, out, scale);
+}
+
+// fp32 NCHW images -> zero-padded NHWC4: one thread per padded pixel, one 16-byte store
+__global__ __launch_bounds__(256) void stem_pack32_kernel(const float* __restrict__ x, float* __restrict__ out, int C,
+                                                          int H, int W, int pad, int Hp, int Wp, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int wp = (int)(i % Wp);
+  const int64_t t = i / Wp;
+  const int hp = (int)(t % Hp);
+  const int n = (int)(t / Hp);
+  const int h = hp - pad, w = wp - pad;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (c < C) v[c] = x[(((int64_t)n * C + c) * H + h) * W + w];
+  }
+  *(f32x4v*)(out + i * 4) = f32x4v{v[0], v[1], v[2], v[3]};
+}
+
+void stem_pack32_launch(const float* x, float* out, int N, int C, int H, int W, int pad, int Hp, int Wp, hipStream_t s) {
+  const int64_t total = (int64_t)N * Hp * Wp;
+  hipLaunchKernelGGL(stem_pack32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, out, C, H, W, pad,
+                     Hp, Wp, total);
 }
 
 // fp32 NCHW images -> im2col rows [N*OH*OW][ldk], column k = (r*S + s)*C + c (zero beyond R*S*C / outside)

@@ -97,6 +97,19 @@ class ResNetExecutor32(ResNetExecutor):
         self.stem_w_off = off[0]
         derived_maps.append(m.reshape(-1).to(torch.int32))
         off[0] += m.numel()
+        # window-mode stem (PDT_FP32_STEM_WIN=1): [64][R][32] over the zero-padded NHWC4 image, column s * 4 + c of kernel
+        # row r (s = 7 and c = 3 zero) -- no im2col buffer in the forward pass
+        self.stem_win = os.environ.get("PDT_FP32_STEM_WIN", "0") == "1" and s.S <= 7 and s.cin <= 3
+        if self.stem_win:
+            r = torch.arange(s.R).view(1, -1, 1)
+            j = torch.arange(32).view(1, 1, -1)
+            o3 = torch.arange(s.cout).view(-1, 1, 1)
+            sj, cj = j // 4, j % 4
+            mw = torch.where((sj < s.S) & (cj < s.cin), s.slot.offset + ((o3 * s.R + r) * s.S + sj) * s.cin + cj,
+                             torch.full_like(o3 * r * j, -1))
+            self.stem_win_off = off[0]
+            derived_maps.append(mw.reshape(-1).to(torch.int32))
+            off[0] += mw.numel()
         # stem weight gradient: [64][STEM_K] GEMM result -> KRSC slot
         self.stem_gidx = (torch.arange(s.cout).view(-1, 1) * STEM_K + torch.arange(kk).view(1, -1)).reshape(-1).to(
             torch.int32).to(self.device)
@@ -237,7 +250,16 @@ class ResNetExecutor32(ResNetExecutor):
         if train:
             sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64)
             sp.zero_()
-        for n0 in range(0, N, ch):
+        if self.stem_win:
+            Hp = max(H + 2 * st.pad, (P0 - 1) * st.st + st.R)
+            Wp = max(W + 2 * st.pad, (Q0 - 1) * st.st + 8)
+            xp = self._buf("stem_in", N * Hp * Wp * 4, torch.float32)
+            Cn.stem_pack32(x32, xp, N, 3, H, W, st.pad, Hp, Wp)
+            wwin = self.derived[self.stem_win_off:self.stem_win_off + st.cout * st.R * 32]
+            Cn.conv32_stem_fwd(xp, wwin, y0, sp, N, Hp, Wp, st.R, P0, Q0, st.st, st.cout,
+                               *self._tile32(st.cout, N * P0 * Q0))
+            ch = N + 1  # no im2col chunks
+        for n0 in range(0, N if not self.stem_win else 0, ch):
             n1 = min(N, n0 + ch)
             cols = self._buf("stem_cols", (n1 - n0) * P0 * Q0 * STEM_K, torch.float32)
             Cn.im2col32(x32[n0:n1], cols, n1 - n0, 3, H, W, st.R, st.S, st.st, st.pad, STEM_K)

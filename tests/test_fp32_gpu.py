@@ -220,3 +220,51 @@ def test_fp32_syncbn_native_comm_world1_equals_plain_bn():
         torch.cuda.synchronize()
         out.append(tr.flat.data.clone())
     assert _rel(out[0], out[1]) < 1e-5
+
+
+@pytest.mark.parametrize("tile", [(128, 64), (256, 64)])
+def test_conv32_stem_window_mode_matches_torch(tile):
+    """fp32 stem in window mode (conv32 over the zero-padded NHWC4 image: K = 7 kernel rows x (8 pixels x 4 channels),
+    no im2col buffer) vs torch's fp32 conv2d, with the BN statistics epilogue."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    torch.manual_seed(3)
+    N, H, W = 3, 64, 48
+    x = torch.randn(N, 3, H, W, device=DEV)
+    w = torch.randn(64, 3, 7, 7, device=DEV) / 147 ** 0.5
+    P, Q = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = max(H + 6, (P - 1) * 2 + 7), max(W + 6, (Q - 1) * 2 + 8)
+    xp = torch.empty(N * Hp * Wp * 4, device=DEV)
+    C.stem_pack32(x, xp, N, 3, H, W, 3, Hp, Wp)
+    ww = torch.zeros(64, 7, 8, 4, device=DEV)
+    ww[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    y = torch.empty(N * P * Q * 64, device=DEV)
+    st = torch.zeros(C.stat_slots() * 64 * 2, dtype=torch.float64, device=DEV)
+    C.conv32_stem_fwd(xp, ww.reshape(-1).contiguous(), y, st, N, Hp, Wp, 7, P, Q, 2, 64, *tile)
+    ref = F.conv2d(x, w, stride=2, padding=3).permute(0, 2, 3, 1)
+    assert _rel(y.view(N, P, Q, 64), ref) < 1e-5
+    s = st.view(-1, 64, 2).sum(0)
+    yf = y.view(-1, 64).double()
+    assert torch.allclose(s[:, 0], yf.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_fp32_executor_window_stem_matches_im2col_stem(monkeypatch):
+    """PDT_FP32_STEM_WIN=1 (window-mode stem forward) trains like the im2col stem: same loss / gradients to fp32
+    rounding of a different summation order."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    torch.manual_seed(0)
+    model = registry.create("resnet18")
+    x = torch.randn(4, 3, 64, 64, device=DEV)
+    t = torch.randint(0, 1000, (4,), device=DEV)
+    outs = []
+    for win in ("0", "1"):
+        monkeypatch.setenv("PDT_FP32_STEM_WIN", win)
+        tr = NativeTrainer(copy.deepcopy(model), torch.device(DEV), dtype=torch.float32, lr=0.0)
+        assert tr.executor.stem_win == (win == "1")
+        logits, met = tr.train_step(x, t)
+        torch.cuda.synchronize()
+        outs.append((logits.float().clone(), tr.flat.grad.clone()))
+    assert _rel(outs[1][0], outs[0][0]) < 1e-5
+    assert _rel(outs[1][1], outs[0][1]) < 1e-4
