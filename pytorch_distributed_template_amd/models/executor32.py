@@ -97,9 +97,9 @@ class ResNetExecutor32(ResNetExecutor):
         self.stem_w_off = off[0]
         derived_maps.append(m.reshape(-1).to(torch.int32))
         off[0] += m.numel()
-        # window-mode stem (PDT_FP32_STEM_WIN=1): [64][R][32] over the zero-padded NHWC4 image, column s * 4 + c of kernel
+        # window-mode stem (default; PDT_FP32_STEM_WIN=0: the im2col GEMM): [64][R][32] over the zero-padded NHWC4 image, column s * 4 + c of kernel
         # row r (s = 7 and c = 3 zero) -- no im2col buffer in the forward pass
-        self.stem_win = os.environ.get("PDT_FP32_STEM_WIN", "0") == "1" and s.S <= 7 and s.cin <= 3
+        self.stem_win = os.environ.get("PDT_FP32_STEM_WIN", "1") == "1" and s.S <= 7 and s.cin <= 3
         if self.stem_win:
             r = torch.arange(s.R).view(1, -1, 1)
             j = torch.arange(32).view(1, 1, -1)

