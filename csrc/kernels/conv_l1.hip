@@ -356,7 +356,8 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// 8-wave "ping-pong" variant of the kernel above (the default; PDT_CONV_L1_PP=0 selects the 4-wave one).
+// 8-wave "ping-pong" variant of the kernel above (the default; PDT_CONV_L1_PP=0 selects the 4-wave one):
+// ResNet-18 bs1200 bf16 layer1 forward / backward-data 3.2 -> 2.5 ms of kernel time, 21.34 -> 21.04 ms/step (same box).
 //
 // The 4-wave kernel runs one wave per SIMD, so everything that is not an MFMA -- the epilogue (16-bit
 // conversion, statistics, 14-16 scattered stores per lane), the fused producer-BN transform of the halo
@@ -786,7 +787,7 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
   // its 256 registers without spilling), which stays on the 4-wave kernel.
   static const bool pp_env = [] {
     const char* e = getenv("PDT_CONV_L1_PP");
-    return e && e[0] == '1';  // opt-in until measured on the GPU
+    return !(e && e[0] == '0');
   }();
   const bool pp_on = g_conv_l1_pp >= 0 ? g_conv_l1_pp != 0 : pp_env;
   const bool pp = pp_on && (epi == 0 || (epi == 1 && !rs && !flip) || (epi == 2 && !rs));
