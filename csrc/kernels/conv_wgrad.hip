@@ -991,10 +991,11 @@ int wgrad3x3_c64_blocks() {
 
 void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s) {
   PDT_COUNT("wgrad3x3_c64");
-  // PDT_WGRAD_L1_PIPE=0: the unpipelined tap loop (A/B)
+  // PDT_WGRAD_L1_PIPE=1: the software-pipelined tap loop.  Off by default: in isolation it ran 682 vs 758 TF/s
+  // (tools/conv_bench.py) and the whole step measured 20.97 / 20.82 vs 21.03 / 21.00 ms with it (same box)
   static const bool pipe = [] {
     const char* e = getenv("PDT_WGRAD_L1_PIPE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (a.pre_coef) PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
 #define PDT_W3(DT_, P_)                                                                         \

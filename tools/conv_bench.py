@@ -82,6 +82,7 @@ def main():
     ap.add_argument("--skip-stem", action="store_true")
     ap.add_argument("--shapes", default="", help="comma-separated indices into SHAPES (default: all)")
     ap.add_argument("--r50", action="store_true", help="ResNet-50 1x1 shapes (SHAPES_R50), forward with statistics")
+    ap.add_argument("--stats", action="store_true", help="forward tiles with the BN statistics epilogue (as in training)")
     a = ap.parse_args()
     C = native.C
     dev = "cuda"
@@ -105,7 +106,7 @@ def main():
         for (bm, bn, bk) in FWD_TILES:
             if co % bn:
                 continue
-            sp = torch.zeros(C.stat_slots() * co * 2, dtype=torch.float64, device=dev) if a.r50 else None
+            sp = torch.zeros(C.stat_slots() * co * 2, dtype=torch.float64, device=dev) if (a.r50 or a.stats) else None
 
             def f(bm=bm, bn=bn, bk=bk, sp=sp):
                 C.conv_fwd(x, w, y, None, sp, N, H, H, ci, co, k, k, P, P, st, st, -pad, -pad, 1, 1, P, P, 1, 1,
