@@ -919,6 +919,25 @@ void conv32_stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& s
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
 }
 
+// fp32 stem weight gradient in window-pair mode over the zero-padded NHWC4 image (no im2col): "tap" t = kernel rows
+// (2t, 2t+1), 64 columns = 8 pixels x 4 channels of each; ws[split][Kout][npairs * 64]
+void wgrad32_stem(const Tensor& xp, const Tensor& dy, Tensor& ws, int64_t N, int64_t Hp, int64_t Wp, int64_t npairs,
+                  int64_t Kout, int64_t P, int64_t Q, int64_t stride, int64_t splits, int64_t pix_per_split) {
+  TORCH_CHECK(xp.numel() == N * Hp * Wp * 4 && dy.numel() == N * P * Q * Kout && Kout % 64 == 0, "wgrad32_stem: sizes");
+  TORCH_CHECK((P - 1) * stride + 2 * npairs <= Hp && (Q - 1) * stride + 8 <= Wp, "wgrad32_stem: padded image too small");
+  TORCH_CHECK(ws.numel() >= splits * Kout * npairs * 64 && pix_per_split % 64 == 0 && splits * pix_per_split >= N * P * Q,
+              "wgrad32_stem: bad workspace / split plan");
+  TORCH_CHECK(xp.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30), "wgrad32_stem: operands too large");
+  pdt::Wgrad32Args a{};
+  a.tile = 64;
+  a.x = pf(xp, "xp"); a.dy = pf(dy, "dy"); a.ws = pf(ws, "ws");
+  a.N = N; a.H = Hp; a.W = Wp; a.C = 64; a.Kout = Kout; a.T = npairs; a.U = 1; a.Pm = P; a.Qm = Q;
+  a.stride = stride; a.pad = 0; a.ldw = npairs * 64; a.splits = splits; a.pix_per_split = pix_per_split;
+  a.P = N * P * Q;
+  a.cs = 4; a.pair_skip = Wp * 4; a.tstep = 2;
+  pdt::wgrad32_launch(a, cur_stream());
+}
+
 void im2col32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
               int64_t stride, int64_t pad, int64_t ldk) {
   const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
@@ -1012,5 +1031,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum32", &colsum32);
   m.def("stem_pack32", &stem_pack32);
   m.def("conv32_stem_fwd", &conv32_stem_fwd);
+  m.def("wgrad32_stem", &wgrad32_stem);
   m.def("im2col32", &im2col32);
 }

@@ -314,11 +314,13 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(Wgrad32Args a) {
   const int t = tap / a.U, u = tap - t * a.U;
   const int64_t p_begin = (int64_t)split * a.pix_per_split;
   const int64_t p_end = p_begin + a.pix_per_split < a.P ? p_begin + a.pix_per_split : a.P;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * a.C * 4u));
+  const int cs = a.cs ? a.cs : a.C;  // elements per input pixel (window-pair mode: 4)
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * cs * 4u));
   const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (uint32_t)((uint64_t)a.P * a.Kout * 4u));
   // DMA lane geometry: one wave-instruction = 4 rows x 16 chunks of 16 B; source chunk = LDS chunk ^ (row & 3) << 2
   const int lrow = lane >> 4, pc = lane & 15;
   const int sc = pc ^ (lrow << 2);
+  const int pskip = sc >= 8 ? a.pair_skip : 0;
   const int PQ = a.Pm * a.Qm;
   auto stage = [&](int64_t p0, int buf) {
     char* dyb = smem + buf * 2 * TILE;
@@ -334,9 +336,9 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(Wgrad32Args a) {
         const int n = (int)(p / PQ);
         const int rem = (int)(p - (int64_t)n * PQ);
         const int i = rem / a.Qm, j = rem - (rem / a.Qm) * a.Qm;
-        const int ih = i * a.stride - a.pad + t, iw = j * a.stride - a.pad + u;
+        const int ih = i * a.stride - a.pad + t * a.tstep, iw = j * a.stride - a.pad + u;
         if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-          ox = (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0 + sc * 4) * 4);
+          ox = (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * cs + c0 + sc * 4 + pskip) * 4);
       }
       buf_lds16(rd, dyb + ins * 1024, od);
       buf_lds16(rx, xb + ins * 1024, ox);

@@ -110,6 +110,12 @@ class ResNetExecutor32(ResNetExecutor):
             self.stem_win_off = off[0]
             derived_maps.append(mw.reshape(-1).to(torch.int32))
             off[0] += mw.numel()
+            # its weight gradient comes out as [64][kernel-row pair t][row 2t: 8 px x 4 ch | row 2t+1: same] (wgrad32_stem)
+            self.stem_pairs = (s.R + 1) // 2
+            kk_, rr, ss, cc = torch.meshgrid(torch.arange(s.cout), torch.arange(s.R), torch.arange(s.S),
+                                             torch.arange(s.cin), indexing="ij")
+            self.stem_gidx_win = (kk_ * (self.stem_pairs * 64) + (rr // 2) * 64 + (rr % 2) * 32 + ss * 4 + cc).reshape(
+                -1).to(torch.int32).to(self.device)
         # stem weight gradient: [64][STEM_K] GEMM result -> KRSC slot
         self.stem_gidx = (torch.arange(s.cout).view(-1, 1) * STEM_K + torch.arange(kk).view(1, -1)).reshape(-1).to(
             torch.int32).to(self.device)
@@ -251,10 +257,11 @@ class ResNetExecutor32(ResNetExecutor):
             sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64)
             sp.zero_()
         if self.stem_win:
-            Hp = max(H + 2 * st.pad, (P0 - 1) * st.st + st.R)
+            Hp = max(H + 2 * st.pad, (P0 - 1) * st.st + 2 * ((st.R + 1) // 2))  # + the pair-mode row R (weight 0)
             Wp = max(W + 2 * st.pad, (Q0 - 1) * st.st + 8)
             xp = self._buf("stem_in", N * Hp * Wp * 4, torch.float32)
             Cn.stem_pack32(x32, xp, N, 3, H, W, st.pad, Hp, Wp)
+            self._stem_xp = (xp, Hp, Wp)
             wwin = self.derived[self.stem_win_off:self.stem_win_off + st.cout * st.R * 32]
             Cn.conv32_stem_fwd(xp, wwin, y0, sp, N, Hp, Wp, st.R, P0, Q0, st.st, st.cout,
                                *self._tile32(st.cout, N * P0 * Q0))
@@ -279,6 +286,8 @@ class ResNetExecutor32(ResNetExecutor):
         Cn.bn_relu_maxpool32(y0, self.stem_bn.coef, x, idx, N, P0, Q0, st.cout)
         saved = {"N": N, "H": H, "W": W, "x32": x32, "y0": y0, "P0": P0, "Q0": Q0, "idx": idx, "x0": x, "H1": H1,
                  "W1": W1}
+        if self.stem_win:
+            saved["xp"], saved["Hp"], saved["Wp"] = self._stem_xp
         Hc, Wc, Cc = H1, W1, st.cout
         recs = []
         for bi, b in enumerate(self.blocks):
@@ -417,6 +426,25 @@ class ResNetExecutor32(ResNetExecutor):
         self.bn_reduce(sbn, dz0, None, saved["y0"], N * P0 * Q0)
         dy0 = dz0  # in place: each element read then written by the same thread
         Cn.bn_bwd_apply32(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
+        if self.stem_win:  # window-pair weight gradient straight from the padded NHWC4 image (no im2col)
+            npix = N * P0 * Q0
+            key = ("stem_win", npix)
+            plan = self._plans.get(key)
+            if plan is None:
+                per_split = (st.cout // 64) * self.stem_pairs
+                splits = max(1, min(self.wgrad_blocks // per_split, (npix + 63) // 64))
+                pps = ((npix + splits - 1) // splits + 63) // 64 * 64
+                plan = self._plans[key] = ((npix + pps - 1) // pps, pps)
+            splits, pps = plan
+            ldw = self.stem_pairs * 64
+            ws = self._buf("ws", splits * st.cout * ldw, torch.float32)
+            Cn.wgrad32_stem(saved["xp"], dy0, ws, N, saved["Hp"], saved["Wp"], self.stem_pairs, st.cout, P0, Q0, st.st,
+                            splits, pps)
+            tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
+            Cn.wgrad_reduce(ws, splits, st.cout, ldw, ldw, st.cout * ldw, tmp, ldw, 1.0, False)
+            Cn.gather32(tmp, self.stem_gidx_win, self._g(st.slot))
+            self.grad_ready(st.pid)
+            return
         tmp = self._buf("stem_dw", st.cout * STEM_K, torch.float32)
         ch = self._stem_chunk(N)
         for i, n0 in enumerate(range(0, N, ch)):

@@ -273,3 +273,27 @@ def test_fp32_executor_window_stem_matches_im2col_stem(monkeypatch):
     # batch 4): bounded, not bitwise
     assert _rel(outs[1][1], outs[0][1]) < 1e-4
     assert _rel(outs[1][2], outs[0][2]) < 5e-2
+
+
+def test_wgrad32_stem_window_pair_matches_torch():
+    """fp32 stem weight gradient in window-pair mode (tap = kernel-row pair over the padded NHWC4 image) vs
+    torch.nn.grad.conv2d_weight in fp32."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    torch.manual_seed(4)
+    N, H, W = 3, 40, 36
+    x = torch.randn(N, 3, H, W, device=DEV)
+    P, Q = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = max(H + 6, (P - 1) * 2 + 8), max(W + 6, (Q - 1) * 2 + 8)
+    xp = torch.empty(N * Hp * Wp * 4, device=DEV)
+    C.stem_pack32(x, xp, N, 3, H, W, 3, Hp, Wp)
+    dy = torch.randn(N, P, Q, 64, device=DEV)
+    npix = N * P * Q
+    splits, pps = 7, ((npix + 6) // 7 + 63) // 64 * 64
+    splits = (npix + pps - 1) // pps
+    ws = torch.empty(splits * 64 * 256, device=DEV)
+    C.wgrad32_stem(xp, dy.contiguous(), ws, N, Hp, Wp, 4, 64, P, Q, 2, splits, pps)
+    dw = ws.view(splits, 64, 4, 2, 8, 4).sum(0)  # [k][pair][row in pair][pixel s][channel]
+    dw = dw.reshape(64, 8, 8, 4)[:, :7, :7, :3].permute(0, 3, 1, 2)  # rows 0..7 -> 7 kernel rows
+    ref = torch.nn.grad.conv2d_weight(x, (64, 3, 7, 7), dy.permute(0, 3, 1, 2), stride=2, padding=3)
+    assert _rel(dw, ref) < 1e-5

@@ -1,4 +1,8 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1
-timeout -k 10 300 python tools/conv_bench.py --skip-stem --shapes 1,2,3 --stats --reps 5 > gpurun_out/cb_stats.log 2>&1 || exit $?
-grep shape gpurun_out/cb_stats.log | cut -c1-400
-REPS=2 bash tools/gpu_bench_ab.sh "PDT_WGRAD_STREAM=0 PDT_WGRAD_L1_PIPE=1" "PDT_WGRAD_STREAM=0 PDT_WGRAD_L1_PIPE=0" "PDT_WGRAD_L1_PIPE=1" "PDT_WGRAD_L1_PIPE=0"
+timeout -k 10 300 python bench.py --arch resnet50 --dtype fp16 --steps 10 --warmup 3 > gpurun_out/b50.log 2>&1 || exit $?; grep -o '"ms_per_step": [0-9.]*' gpurun_out/b50.log
+timeout -k 10 300 python tools/conv_bench.py --skip-stem --r50 --reps 5 > gpurun_out/cb_r50.log 2>&1 || exit $?
+grep shape gpurun_out/cb_r50.log | cut -c1-330
+cd /tmp && export TMPDIR=/tmp
+PDT_WGRAD_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof50" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --arch resnet50 --dtype fp16 --steps 4 --warmup 2 > "$GRAFT_REPO_ROOT/gpurun_out/prof50.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof32" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --dtype fp32 --steps 3 --warmup 1 > "$GRAFT_REPO_ROOT/gpurun_out/prof32.log" 2>&1 || exit $?
+echo DONE
