@@ -934,7 +934,7 @@ void wgrad32_stem(const Tensor& xp, const Tensor& dy, Tensor& ws, int64_t N, int
   a.N = N; a.H = Hp; a.W = Wp; a.C = 64; a.Kout = Kout; a.T = npairs; a.U = 1; a.Pm = P; a.Qm = Q;
   a.stride = stride; a.pad = 0; a.ldw = npairs * 64; a.splits = splits; a.pix_per_split = pix_per_split;
   a.P = N * P * Q;
-  a.cs = 4; a.pair_skip = Wp * 4; a.tstep = 2;
+  a.cs = 4; a.pair_skip = Wp * 4 - 32; a.tstep = 2;  // chunks 8..15 = the NEXT row's first 32 elements
   pdt::wgrad32_launch(a, cur_stream());
 }
 

@@ -40,7 +40,8 @@ struct Wgrad32Args {
   int tile = 64;  // 64: 64x64 output tile, 4 waves | 128: 128x128, 8 waves (C, Kout % 128 == 0)
   // window-pair mode (the fp32 stem's weight gradient over the zero-padded NHWC4 image; 64x64 tile only): cs = 4
   // elements per pixel, a "tap" t is the kernel-row pair (2t, 2t+1) = input row offset t * tstep, and its 64 columns
-  // are 8 pixels x 4 channels of row 2t (chunks 0..7) then of row 2t+1 (chunks 8..15: + pair_skip elements)
+  // are 8 pixels x 4 channels of row 2t (chunks 0..7) then of row 2t+1 (chunks 8..15 read element sc * 4 + pair_skip:
+  // pair_skip = one padded row - 32)
   int cs = 0, pair_skip = 0, tstep = 1;
 };
 void wgrad32_launch(const Wgrad32Args& a, hipStream_t s);

@@ -266,12 +266,14 @@ def test_fp32_executor_window_stem_matches_im2col_stem(monkeypatch):
         logits, met = tr.train_step(x, t)
         torch.cuda.synchronize()
         ex = tr.executor
-        outs.append((logits.float().clone(), ex._g(ex.fc_slot).clone(), tr.flat.grad.clone()))
+        outs.append((logits.float().clone(), ex._g(ex.fc_slot).clone(), tr.flat.grad.clone(),
+                     ex._g(ex.stem.slot).clone()))
     assert _rel(outs[1][0], outs[0][0]) < 1e-5
     # the fc gradient sees the forward only through features and logits; the whole-network gradient also goes
     # through max-pool argmaxes and ReLU masks that a last-bit difference of the stem output can flip (random init,
     # batch 4): bounded, not bitwise
     assert _rel(outs[1][1], outs[0][1]) < 1e-4
+    assert _rel(outs[1][3], outs[0][3]) < 5e-2, (outs[1][3][:8], outs[0][3][:8])
     assert _rel(outs[1][2], outs[0][2]) < 5e-2
 
 
