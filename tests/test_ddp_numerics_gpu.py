@@ -153,7 +153,9 @@ def test_native_syncbn_equals_full_batch(tmp_path, steps, comm):
            if e_sync[k] > max(1.5 * e_floor[k], 0.02) or
            (e_nosync[k] > 0.05 and e_floor[k] < 0.5 * e_nosync[k] and e_sync[k] > 0.75 * e_nosync[k])]
     assert not bad, bad[:8]
-    assert e_sync["fc.weight"] < 0.02 and e_sync["fc.bias"] < 1e-3
+    # the fc layer sees the chaos only through its input features: a tight bound, widened by its own measured floor
+    assert e_sync["fc.weight"] < max(0.02, 2 * e_floor["fc.weight"]), (e_sync["fc.weight"], e_floor["fc.weight"])
+    assert e_sync["fc.bias"] < max(1e-3, 2 * e_floor["fc.bias"]), (e_sync["fc.bias"], e_floor["fc.bias"])
     fb = tr.buffers.fdata.cpu()
     assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-3  # running mean / var (unbiased, global count)
     assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
