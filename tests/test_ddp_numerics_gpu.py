@@ -157,7 +157,10 @@ def test_native_syncbn_equals_full_batch(tmp_path, steps, comm):
     assert e_sync["fc.weight"] < max(0.02, 2 * e_floor["fc.weight"]), (e_sync["fc.weight"], e_floor["fc.weight"])
     assert e_sync["fc.bias"] < max(1e-3, 2 * e_floor["fc.bias"]), (e_sync["fc.bias"], e_floor["fc.bias"])
     fb = tr.buffers.fdata.cpu()
-    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-3  # running mean / var (unbiased, global count)
+    # running mean / var (unbiased, global count): after step 1 they see the chaotic update, so bound by the floor too
+    fb_floor = ((floor_tr.buffers.fdata.cpu() - fb).norm() / fb.norm()).item()
+    fb_err = ((res["fbuf"] - fb).norm() / fb.norm()).item()
+    assert fb_err < max(1e-3, 2 * fb_floor), (fb_err, fb_floor)
     assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
     assert torch.allclose(res["met"], torch.stack(mets).cpu(), rtol=2e-3, atol=2e-3)
 
