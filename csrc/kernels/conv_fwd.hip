@@ -114,12 +114,46 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
   constexpr int BM_T = WAVES_M * WM;
   constexpr int SPITCH = BN * 2 + 16;  // staged row pitch (+16 B: consecutive rows rotate by 4 banks)
   constexpr int STG_OFF = 16384;       // behind the statistics scratch and the BN coefficients
-  constexpr bool CAN_STAGE = SMEM >= STG_OFF + BM_T * SPITCH;
+  // the whole tile staged at once, or -- when only one wave row-group's WM x BN slice fits (the 256 x 256 ping-pong
+  // tile: 128 KB of LDS) -- one pass per wave row-group: its waves stage, then every wave writes those rows back
+  constexpr bool FULL = SMEM >= STG_OFF + BM_T * SPITCH;
+  constexpr bool PERGRP = !FULL && WAVES_M > 1 && EPI != 2 && SMEM >= STG_OFF + WM * SPITCH;  // (EPI 2: spills)
+  constexpr bool CAN_STAGE = FULL || PERGRP;
   static_assert(!CAN_STAGE || RED_BYTES + 6 * BN * 4 <= STG_OFF, "epilogue LDS regions overlap");
   const bool stage = CAN_STAGE && a.stage_out;
   char* stg = smem + STG_OFF;
+  const int srow0 = FULL ? wm * WM : 0;  // this wave's first row in the staging buffer
   constexpr bool RC = RES == 2;
   const bool res_on = !RC || (int)blockIdx.y == a.res_phase;  // compact: this block's phase owns the residual
+  // write the staged rows of wave row-group g (PERGRP) or of the whole tile (FULL) back: 16 B per lane, whole
+  // BN-channel rows per pixel
+  auto copy_rows = [&](int g) {
+    constexpr int CPR = BN / 8;
+    constexpr int SROWS = FULL ? BM_T : WM;
+    for (int q = tid; q < SROWS * CPR; q += NW_ * 64) {
+      const int row = q / CPR, ch = q - row * CPR;
+      const int64_t m = m0 + (FULL ? 0 : g * WM) + row;
+      if (m < a.M) {
+        const int mm = (int)m;
+        const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
+        const int rem = mm - nimg * PQ;
+        const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
+        const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
+        const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout + n0 + ch * 8;
+        *(uint4*)(a.y + ob) = *(const uint4*)(stg + row * SPITCH + ch * 16);
+      }
+    }
+  };
+  // PERGRP: row-group g stages its slice while the groups before it are written back (each wave runs its own
+  // fragment loop once, and every wave passes 2 x WAVES_M barriers)
+  if constexpr (PERGRP) {
+    if (stage)
+      for (int g = 0; g < wm; ++g) {
+        __syncthreads();
+        copy_rows(g);
+        __syncthreads();
+      }
+  }
 #pragma unroll
   for (int jc = 0; jc < FM; jc += JC) {
     int64_t obase[JC];
@@ -206,7 +240,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
         packed.x = (uint32_t)ov[0] | ((uint32_t)ov[1] << 16);
         packed.y = (uint32_t)ov[2] | ((uint32_t)ov[3] << 16);
         if (CAN_STAGE && stage)
-          *(uint2*)(stg + (wm * WM + j * 16 + fr) * SPITCH + (wn * WN + i * 16 + 4 * fq) * 2) = packed;
+          *(uint2*)(stg + (srow0 + j * 16 + fr) * SPITCH + (wn * WN + i * 16 + 4 * fq) * 2) = packed;
         else
           *(uint2*)(a.y + o) = packed;
         if constexpr (EPI == 1) {
@@ -237,21 +271,16 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
   }
 
   if constexpr (CAN_STAGE) {
-    if (stage) {  // write the staged tile back: 16 B per lane, whole BN-channel rows per pixel
-      __syncthreads();
-      constexpr int CPR = BN / 8;
-      for (int q = tid; q < BM_T * CPR; q += NW_ * 64) {
-        const int row = q / CPR, ch = q - row * CPR;
-        const int64_t m = m0 + row;
-        if (m < a.M) {
-          const int mm = (int)m;
-          const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
-          const int rem = mm - nimg * PQ;
-          const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
-          const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
-          const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout + n0 + ch * 8;
-          *(uint4*)(a.y + ob) = *(const uint4*)(stg + row * SPITCH + ch * 16);
+    if (stage) {
+      if constexpr (PERGRP) {
+        for (int g = wm; g < WAVES_M; ++g) {
+          __syncthreads();
+          copy_rows(g);
+          __syncthreads();
         }
+      } else {
+        __syncthreads();
+        copy_rows(0);
       }
     }
   }
@@ -548,7 +577,7 @@ PDT_DEVICE void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <int DT, int BM, int BN, int EPI, int RES>
+template <int DT, int BM, int BN, int EPI, int RES, bool PP_STAGE = (EPI != 2)>  // (EPI 2 + staging spills)
 __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
   if (args.nphase > 0) {  // multi-phase launch (strided backward-data): this block's phase geometry
@@ -752,11 +781,20 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
     __builtin_amdgcn_s_barrier();
   }
 
-  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW, PP_STAGE ? 2 * BUF : 0>(a, acc, m0, n0, tile_m, wn, wm, tid,
+                                                                                  lane, smem);
 }
 
 template <int DT, int BM, int BN>
-static void launch_pp(const ConvFwdArgs& a, hipStream_t s) {
+static void launch_pp(const ConvFwdArgs& args, hipStream_t s) {
+  // PDT_PP_STAGE=0: the ping-pong kernel stores straight from the accumulators (A/B); default: LDS-staged row stores,
+  // one wave row-group at a time (conv_epilogue PERGRP)
+  static const bool pp_stage = [] {
+    const char* e = getenv("PDT_PP_STAGE");
+    return !(e && e[0] == '0');
+  }();
+  ConvFwdArgs a = args;
+  if (!pp_stage) a.stage_out = 0;
   int gx = a.m_tiles * a.n_tiles;
   if (a.nphase > 0) {
     gx = 0;
