@@ -148,7 +148,7 @@ def main():
                 C.conv_wgrad_3x3c64(x, dy, ws, N, H, H)
                 C.wgrad_reduce(ws, blocks, 64, 576, 576, 64 * 576, outw, 576, 1.0, False)
             row["wgrad_l1"] = round(flops / timeit(l1, a.reps) / 1e9, 1)
-        for tb in (256, 512, 1024, 2048):
+        for tb in (256, 512, 1024, 2048, 4096, 8192):
             row[f"wgrad_{tb}"] = round(flops / timeit(lambda tb=tb: conv.conv_wgrad(x, dy, k, k, st, pad, tb), a.reps) / 1e9, 1)
         print(json.dumps(row), flush=True)
         res.append(row)

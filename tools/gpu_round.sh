@@ -91,6 +91,20 @@ for stage in "$@"; do
         > gpurun_out/rehearse4.log 2>&1; rc=$?
       grep metric gpurun_out/rehearse4.log
       [ $rc -eq 0 ] || { tail -30 gpurun_out/rehearse4.log; echo "rehearse4 failed rc=$rc"; exit $rc; } ;;
+    prof50)
+      cd /tmp && export TMPDIR=/tmp
+      PDT_WGRAD_STREAM=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof50" -o run -- \
+        python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --arch resnet50 --dtype fp16 --steps 4 --warmup 2 > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof50.log" 2>&1; rc=$?
+      cd "${GRAFT_REPO_ROOT:-/root/repo}"
+      [ $rc -eq 0 ] || { echo "prof50 failed rc=$rc"; exit $rc; } ;;
+    r50sweep)
+      timeout -k 10 600 python tools/conv_bench.py --skip-stem --r50 --reps 5 > gpurun_out/cb_r50.log 2>&1; rc=$?
+      grep shape gpurun_out/cb_r50.log | cut -c1-200
+      [ $rc -eq 0 ] || { echo "r50 sweep failed rc=$rc"; exit $rc; } ;;
+    fp32win)
+      timeout -k 10 300 python -u -m pytest tests/test_fp32_gpu.py -x -q -k "window" --timeout 120 --timeout-method thread > gpurun_out/t_fp32win.log 2>&1; rc=$?
+      tail -3 gpurun_out/t_fp32win.log
+      ok_rc $rc || { echo "pytest crashed rc=$rc"; exit $rc; } ;;
     bench50)
       timeout -k 10 600 python bench.py --arch resnet50 --dtype fp16 --steps 10 --warmup 3 > gpurun_out/bench50.log 2>&1; rc=$?
       grep metric gpurun_out/bench50.log
