@@ -12,6 +12,13 @@ struct Conv32Args {
   float* y;
   const float* res;
   double* stats;  // optional [kStatSlots][Kout][2] (sum, sumsq); filled through per-block rows (srows)
+  // bnb != 0 (backward-data only): the consumer BatchNorm's backward reduce fused into the epilogue -- the output is
+  // dz = dx * (bn_mref > 0) (bn_mref: the post-ReLU activation) and stats receives (sum dz, sum dz * xhat) with
+  // xhat = (bn_y1 - mean) * invstd, coef = [scale | shift | mean | invstd] x Kout
+  int bnb = 0;
+  const float* bn_mref = nullptr;
+  const float* bn_y1 = nullptr;
+  const float* bn_coef = nullptr;
   float* srows;
   int srows_pp;
   int N, H, W, C, Kout, T, U;

@@ -207,6 +207,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
       const int n = n0 + wn * WN + i * 16 + 4 * fq;
       f32x4v v = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if constexpr (RES) v += *(const f32x4v*)(a.res + ob + n);
+      if constexpr (EPI == 2) {  // fused BN-backward reduce of the consumer BN (see Conv32Args::bnb)
+        const f32x4v m = *(const f32x4v*)(a.bn_mref + ob + n);
+        const f32x4v x1 = (*(const f32x4v*)(a.bn_y1 + ob + n) - *(const f32x4v*)(a.bn_coef + 2 * a.Kout + n)) *
+                          *(const f32x4v*)(a.bn_coef + 3 * a.Kout + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = m[r] > 0.f ? v[r] : 0.f;
+          sacc[i][r][0] += v[r];
+          sacc[i][r][1] += v[r] * x1[r];
+        }
+      }
       *(f32x4v*)(a.y + ob + n) = v;
       if constexpr (EPI == 1) {
 #pragma unroll
@@ -217,7 +228,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
       }
     }
   }
-  if constexpr (EPI == 1) {
+  if constexpr (EPI != 0) {
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -278,10 +289,15 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
   Scratch part(a.stats ? (size_t)srows * a.Kout * 2 * sizeof(float) : 0, s);
   a.srows = part.as<float>();
   const bool st = a.stats != nullptr, rs = a.res != nullptr;
+  if (a.bnb && (!st || rs || a.nphase == 0))
+    pdt_hip_fail("conv32: the fused BN-backward epilogue needs a backward-data launch with stats and no residual",
+                 hipErrorInvalidValue, __FILE__, __LINE__);
+  if (a.bnb) PDT_COUNT("conv32_dgrad_bn_reduce_epilogue");
 #define PDT_C32(BM_, BN_, WM_, WN_)                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                          \
     dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(64 * WM_ * WN_);                                   \
-    if (st && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, true>), grid, block, 0, s, a); \
+    if (a.bnb) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 2, false>), grid, block, 0, s, a);  \
+    else if (st && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, true>), grid, block, 0, s, a); \
     else if (st) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, false>), grid, block, 0, s, a); \
     else if (rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, true>), grid, block, 0, s, a);  \
     else hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, false>), grid, block, 0, s, a);         \

@@ -181,13 +181,17 @@ class ResNetExecutor32(ResNetExecutor):
                           *self._tile32(c.cout, N * P * Q))
         return P, Q, sp
 
-    def _dgrad(self, c: _Conv, dy, N, H, W, P, Q, dx, res=None):
+    def _dgrad(self, c: _Conv, dy, N, H, W, P, Q, dx, res=None, bnb=None):
+        """``bnb = (mref, y1, coef, slots)``: the consumer BatchNorm's backward reduce fused into the epilogue (dx then
+        holds dz = dx * (mref > 0) and the slots receive sum dz, sum dz * xhat -- no separate bn_bwd_reduce32 pass)."""
         # every sub-pixel phase of the stride in one launch; a phase without taps (odd phases of a 1x1/2 conv)
         # runs zero K-steps and writes zeros (+ the residual)
         phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
                   if H - ph > 0 and W - pw > 0]
         self.C.conv32_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases,
-                            *self._tile32(c.cin, N * P * Q))
+                            *self._tile32(c.cin, N * P * Q), *(bnb or ()))
+
+    _FUSE_BN = os.environ.get("PDT_FP32_FUSE_BN", "1") == "1"
 
     _HALO = os.environ.get("PDT_FP32_HALO", "1") == "1"
 
@@ -408,11 +412,18 @@ class ResNetExecutor32(ResNetExecutor):
                 self.grad_ready(c.pid)
                 if ci > 0:
                     da = self._buf("da", N * h * w * c.cin, torch.float32)
-                    self._dgrad(c, dy, N, h, w, P, Q, da)
                     bnp, yp, ap = bns[ci - 1], rec["ys"][ci - 1], rec["as"][ci - 1]
-                    self.bn_reduce(bnp, da, ap, yp, N * h * w)
+                    if self._FUSE_BN:  # dgrad epilogue writes dz and reduces the inner BN's backward sums
+                        slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
+                        self._dgrad(c, dy, N, h, w, P, Q, da, bnb=(ap, yp, bnp.coef, slots))
+                        self._bn_bwd_finish(slots, N * h * w, bnp)
+                        mref = None
+                    else:
+                        self._dgrad(c, dy, N, h, w, P, Q, da)
+                        self.bn_reduce(bnp, da, ap, yp, N * h * w)
+                        mref = ap
                     dyp = self._buf(("dy", (len(convs) - ci) % 2 + 1), yp.numel(), torch.float32)
-                    Cn.bn_bwd_apply32(da, ap, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
+                    Cn.bn_bwd_apply32(da, mref, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
                     dy = dyp
                 else:
                     self._dgrad(c, dy, N, h, w, P, Q, gnext, res=res)

@@ -299,3 +299,28 @@ def test_wgrad32_stem_window_pair_matches_torch():
     dw = dw.reshape(64, 8, 8, 4)[:, :7, :7, :3].permute(0, 3, 1, 2)  # rows 0..7 -> 7 kernel rows
     ref = torch.nn.grad.conv2d_weight(x, (64, 3, 7, 7), dy.permute(0, 3, 1, 2), stride=2, padding=3)
     assert _rel(dw, ref) < 1e-5
+
+
+def test_fp32_fused_bn_backward_reduce_matches_separate_pass(monkeypatch):
+    """The inner BatchNorms' backward reduce fused into the fp32 backward-data epilogue (conv32 EPI 2) gives the
+    gradients of the separate bn_bwd_reduce32 pass to fp32 summation-order rounding, and really runs."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    from pytorch_distributed_template_amd.models.executor32 import ResNetExecutor32
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(1)
+    model = registry.create("resnet18")
+    x = torch.randn(4, 3, 64, 64, device=DEV)
+    t = torch.randint(0, 1000, (4,), device=DEV)
+    outs = []
+    for fuse in (False, True):
+        monkeypatch.setattr(ResNetExecutor32, "_FUSE_BN", fuse)
+        tr = NativeTrainer(copy.deepcopy(model), torch.device(DEV), dtype=torch.float32, lr=0.0)
+        native.C.reset_dispatch_counts()
+        logits, met = tr.train_step(x, t)
+        torch.cuda.synchronize()
+        n_fused = dict(native.C.dispatch_counts()).get("conv32_dgrad_bn_reduce_epilogue", 0)
+        assert (n_fused > 0) == fuse
+        outs.append((logits.float().clone(), tr.flat.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])  # the forward is untouched
+    assert _rel(outs[1][1], outs[0][1]) < 1e-3
