@@ -757,7 +757,8 @@ void conv32_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, co
 void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
                   int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride,
                   const std::vector<std::vector<int64_t>>& phases, int64_t bm, int64_t bn, const OptT& bn_mref = {},
-                  const OptT& bn_y1 = {}, const OptT& bn_coef = {}, const OptT& stats = {}) {
+                  const OptT& bn_y1 = {}, const OptT& bn_coef = {}, const OptT& stats = {}, const OptT& bn_y2 = {},
+                  const OptT& bn_coef2 = {}) {
   TORCH_CHECK(dy.numel() == N * P * Q * K && dx.numel() == N * H * W * C, "conv32_dgrad: size mismatch");
   TORCH_CHECK(K % 32 == 0 && C % bn == 0, "conv32_dgrad: K % 32 / C % bn must be 0");
   TORCH_CHECK(dy.numel() < (int64_t(1) << 30) && wt.numel() < (int64_t(1) << 30), "conv32_dgrad: operands too large");
@@ -769,13 +770,19 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
     a.res = pf(*res, "res");
   }
   if (bn_mref.has_value()) {  // fused BN-backward reduce (Conv32Args::bnb)
-    TORCH_CHECK(bn_y1.has_value() && bn_coef.has_value() && stats.has_value() && !res.has_value(),
-                "conv32_dgrad: the fused BN-backward reduce needs mref, y1, coef and stats, and no residual");
+    TORCH_CHECK(bn_y1.has_value() && bn_coef.has_value() && stats.has_value(),
+                "conv32_dgrad: the fused BN-backward reduce needs mref, y1, coef and stats");
+    const int64_t KO = bn_y2.has_value() ? 4 : 2;
     TORCH_CHECK(bn_mref->numel() == dx.numel() && bn_y1->numel() == dx.numel() && bn_coef->numel() >= 4 * C &&
-                stats->numel() >= pdt::kStatSlots * C * 2, "conv32_dgrad: fused BN-backward operand sizes");
+                stats->numel() >= pdt::kStatSlots * C * KO, "conv32_dgrad: fused BN-backward operand sizes");
     a.bnb = 1;
     a.bn_mref = pf(*bn_mref, "bn_mref"); a.bn_y1 = pf(*bn_y1, "bn_y1"); a.bn_coef = pf(*bn_coef, "bn_coef");
     a.stats = pd(*stats, "stats");
+    if (bn_y2.has_value()) {
+      TORCH_CHECK(bn_coef2.has_value() && bn_y2->numel() == dx.numel() && bn_coef2->numel() >= 4 * C,
+                  "conv32_dgrad: second BN branch operands");
+      a.bn_y2 = pf(*bn_y2, "bn_y2"); a.bn_coef2 = pf(*bn_coef2, "bn_coef2");
+    }
   }
   a.N = N; a.H = P; a.W = Q; a.C = K; a.Kout = C;
   a.ist_h = 1; a.ist_w = 1; a.tstep_h = -1; a.tstep_w = -1;
@@ -1030,7 +1037,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv32_dgrad", &conv32_dgrad, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("res"), py::arg("N"),
         py::arg("P"), py::arg("Q"), py::arg("K"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("stride"),
         py::arg("phases"), py::arg("bm"), py::arg("bn"), py::arg("bn_mref") = py::none(), py::arg("bn_y1") = py::none(),
-        py::arg("bn_coef") = py::none(), py::arg("stats") = py::none());
+        py::arg("bn_coef") = py::none(), py::arg("stats") = py::none(), py::arg("bn_y2") = py::none(),
+        py::arg("bn_coef2") = py::none());
   m.def("wgrad32", &wgrad32);
   m.def("bn_apply32", &bn_apply32);
   m.def("bn_bwd_reduce32_blocks", &bn_bwd_reduce32_blocks);

@@ -19,6 +19,10 @@ struct Conv32Args {
   const float* bn_mref = nullptr;
   const float* bn_y1 = nullptr;
   const float* bn_coef = nullptr;
+  // a second BN branch sharing dz (a downsample block's output: the main-branch and the downsample BN); stats then
+  // receive 4 quantities per channel: (sum dz, sum dz * xhat1, sum dz, sum dz * xhat2)
+  const float* bn_y2 = nullptr;
+  const float* bn_coef2 = nullptr;
   float* srows;
   int srows_pp;
   int N, H, W, C, Kout, T, U;

@@ -36,9 +36,10 @@ static int ew_blocks(int64_t n) {
 template <int EPI, int BN_>
 PDT_DEVICE void zero_stat_row32(const Conv32Args& a) {
   if constexpr (EPI != 0) {
+    constexpr int KO = EPI == 3 ? 4 : 2;
     const int tm = (int)blockIdx.x / a.n_tiles, tn = (int)blockIdx.x - tm * a.n_tiles;
-    float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * 2 + (int64_t)tn * BN_ * 2;
-    for (int i = threadIdx.x; i < BN_ * 2; i += blockDim.x) dst[i] = 0.f;
+    float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * KO + (int64_t)tn * BN_ * KO;
+    for (int i = threadIdx.x; i < BN_ * KO; i += blockDim.x) dst[i] = 0.f;
   }
 }
 
@@ -187,11 +188,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
   }
 
   // ---- epilogue: lane holds output channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
-  float sacc[FN][4][2];
+  // EPI 1: forward statistics | 2: fused BN-backward reduce, one branch | 3: two branches (Conv32Args::bnb)
+  constexpr int KS = EPI == 3 ? 3 : 2;  // accumulated quantities per channel
+  float sacc[FN][4][KS];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { sacc[i][r][0] = 0.f; sacc[i][r][1] = 0.f; }
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
     const int64_t m = m0 + wm * WM + j * 16 + fr;
@@ -207,7 +212,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
       const int n = n0 + wn * WN + i * 16 + 4 * fq;
       f32x4v v = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if constexpr (RES) v += *(const f32x4v*)(a.res + ob + n);
-      if constexpr (EPI == 2) {  // fused BN-backward reduce of the consumer BN (see Conv32Args::bnb)
+      if constexpr (EPI >= 2) {  // fused BN-backward reduce of the consumer BN (see Conv32Args::bnb)
         const f32x4v m = *(const f32x4v*)(a.bn_mref + ob + n);
         const f32x4v x1 = (*(const f32x4v*)(a.bn_y1 + ob + n) - *(const f32x4v*)(a.bn_coef + 2 * a.Kout + n)) *
                           *(const f32x4v*)(a.bn_coef + 3 * a.Kout + n);
@@ -216,6 +221,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
           v[r] = m[r] > 0.f ? v[r] : 0.f;
           sacc[i][r][0] += v[r];
           sacc[i][r][1] += v[r] * x1[r];
+        }
+        if constexpr (EPI == 3) {
+          const f32x4v x2 = (*(const f32x4v*)(a.bn_y2 + ob + n) - *(const f32x4v*)(a.bn_coef2 + 2 * a.Kout + n)) *
+                            *(const f32x4v*)(a.bn_coef2 + 3 * a.Kout + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sacc[i][r][2] += v[r] * x2[r];
         }
       }
       *(f32x4v*)(a.y + ob + n) = v;
@@ -232,29 +243,31 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sacc[i][r][0] = row16_sum(sacc[i][r][0]);
-        sacc[i][r][1] = row16_sum(sacc[i][r][1]);
-      }
-    float* red = (float*)smem;  // [WAVES_M][BN][2] (the LDS ring is free: every wave passed the last barrier)
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
+    float* red = (float*)smem;  // [WAVES_M][BN][KS] (the LDS ring is free: every wave passed the last barrier)
     if (fr == 15) {
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int nl = wn * WN + i * 16 + 4 * fq + r;
-          red[(wm * BN + nl) * 2 + 0] = sacc[i][r][0];
-          red[(wm * BN + nl) * 2 + 1] = sacc[i][r][1];
+#pragma unroll
+          for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
         }
     }
     __syncthreads();
-    for (int idx = tid; idx < BN * 2; idx += 64 * NW) {
-      const int nl = idx >> 1, k = idx & 1;
+    // stored quantities per channel: KO = 2, or 4 for two branches (sum dz stored twice: the finalize's layout)
+    constexpr int KO = EPI == 3 ? 4 : 2;
+    for (int idx = tid; idx < BN * KO; idx += 64 * NW) {
+      const int nl = idx / KO, ko = idx - nl * KO;
+      const int k = EPI == 3 ? (ko == 2 ? 0 : (ko == 3 ? 2 : ko)) : ko;
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < WAVES_M; ++w) t += red[(w * BN + nl) * 2 + k];
+      for (int w = 0; w < WAVES_M; ++w) t += red[(w * BN + nl) * KS + k];
       const int64_t row = (a.nphase > 0 ? (int64_t)blockIdx.y * a.srows_pp : 0) + tile_m;
-      a.srows[(row * a.Kout + n0 + nl) * 2 + k] = t;
+      a.srows[(row * a.Kout + n0 + nl) * KO + ko] = t;
     }
   }
 }
@@ -286,22 +299,27 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
   }
   if (gx == 0 || a.n_tiles == 0) return;
   PDT_COUNT(a.nphase > 0 ? "conv32_dgrad" : "conv32_fwd");
-  Scratch part(a.stats ? (size_t)srows * a.Kout * 2 * sizeof(float) : 0, s);
+  const int KO = a.bnb && a.bn_y2 ? 4 : 2;
+  Scratch part(a.stats ? (size_t)srows * a.Kout * KO * sizeof(float) : 0, s);
   a.srows = part.as<float>();
   const bool st = a.stats != nullptr, rs = a.res != nullptr;
-  if (a.bnb && (!st || rs || a.nphase == 0))
-    pdt_hip_fail("conv32: the fused BN-backward epilogue needs a backward-data launch with stats and no residual",
-                 hipErrorInvalidValue, __FILE__, __LINE__);
+  if (a.bnb && (!st || a.nphase == 0))
+    pdt_hip_fail("conv32: the fused BN-backward epilogue needs a backward-data launch with stats", hipErrorInvalidValue,
+                 __FILE__, __LINE__);
   if (a.bnb) PDT_COUNT("conv32_dgrad_bn_reduce_epilogue");
+  const int two = a.bn_y2 != nullptr;
 #define PDT_C32(BM_, BN_, WM_, WN_)                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                          \
     dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(64 * WM_ * WN_);                                   \
-    if (a.bnb) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 2, false>), grid, block, 0, s, a);  \
+    if (a.bnb && two && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 3, true>), grid, block, 0, s, a); \
+    else if (a.bnb && two) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 3, false>), grid, block, 0, s, a); \
+    else if (a.bnb && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 2, true>), grid, block, 0, s, a);   \
+    else if (a.bnb) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 2, false>), grid, block, 0, s, a);  \
     else if (st && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, true>), grid, block, 0, s, a); \
     else if (st) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, false>), grid, block, 0, s, a); \
     else if (rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, true>), grid, block, 0, s, a);  \
     else hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, false>), grid, block, 0, s, a);         \
-    if (st) stat_rows_reduce_launch(a.srows, srows, a.Kout * 2, a.stats, s);                               \
+    if (st) stat_rows_reduce_launch(a.srows, srows, a.Kout * KO, a.stats, s);                              \
     return;                                                                                              \
   }
   PDT_C32(128, 128, 2, 2)

@@ -375,6 +375,7 @@ class ResNetExecutor32(ResNetExecutor):
         g = self._buf("g_a", N * Hc * Wc * Cc, torch.float32)
         Cn.avgpool32_bwd(dfeat, g, N, Hc * Wc, Cc, self.feat)
         gsel = 0
+        g_fused = None  # this block's output-BN backward sums, reduced by the previous backward-data epilogue
         for bi in range(len(self.blocks) - 1, -1, -1):
             b, rec = self.blocks[bi], saved["blocks"][bi]
             convs, bns = b["convs"], b["bns"]
@@ -383,13 +384,18 @@ class ResNetExecutor32(ResNetExecutor):
             ds = b["ds_conv"] is not None
             dsbn = b["ds_bn"] if ds else None
             # block output: dz = g * relu'(out); BN backward of the last BN (+ the downsample BN sharing dz)
-            self.bn_reduce(bns[-1], g, rec["out"], rec["ys"][-1], N * h_last * w_last, dsbn,
-                           rec["yd"] if ds else None)
+            if g_fused is not None:  # g already holds dz
+                self._bn_bwd_finish(g_fused, N * h_last * w_last, bns[-1], dsbn)
+                mref = None
+            else:
+                self.bn_reduce(bns[-1], g, rec["out"], rec["ys"][-1], N * h_last * w_last, dsbn,
+                               rec["yd"] if ds else None)
+                mref = rec["out"]
             dy = self._buf(("dy", 0), rec["ys"][-1].numel(), torch.float32)
             gnext = self._buf("g_b" if gsel == 0 else "g_a", N * Hin * Win * Cin, torch.float32)
             if ds:
                 dyd = self._buf("dyd", rec["yd"].numel(), torch.float32)
-                Cn.bn_bwd_apply32(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy, rec["yd"], dsbn.bcoef, dyd, None,
+                Cn.bn_bwd_apply32(g, mref, rec["ys"][-1], bns[-1].bcoef, dy, rec["yd"], dsbn.bcoef, dyd, None,
                                   convs[-1].cout)
                 dc = b["ds_conv"]
                 P, Q = dc.out_hw(Hin, Win)
@@ -398,6 +404,9 @@ class ResNetExecutor32(ResNetExecutor):
                 self.grad_ready(dc.pid)
                 self._dgrad(dc, dyd, N, Hin, Win, P, Q, gnext)
                 res = gnext
+            elif mref is None:  # g is dz already: it is the identity branch's gradient too
+                Cn.bn_bwd_apply32(g, None, rec["ys"][-1], bns[-1].bcoef, dy, None, None, None, None, convs[-1].cout)
+                res = g
             else:
                 dz = self._buf("dz_id", g.numel(), torch.float32)
                 Cn.bn_bwd_apply32(g, rec["out"], rec["ys"][-1], bns[-1].bcoef, dy, None, None, None, dz,
@@ -425,8 +434,20 @@ class ResNetExecutor32(ResNetExecutor):
                     dyp = self._buf(("dy", (len(convs) - ci) % 2 + 1), yp.numel(), torch.float32)
                     Cn.bn_bwd_apply32(da, mref, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
                     dy = dyp
+                elif self._FUSE_BN and bi > 0:
+                    # gnext is the previous block's output gradient: reduce that block's output-BN backward sums
+                    # (ReLU mask from its output, one or two BN branches) in this dgrad's epilogue
+                    pb, prec = self.blocks[bi - 1], saved["blocks"][bi - 1]
+                    pds = pb["ds_conv"] is not None
+                    K = 4 if pds else 2
+                    slots = self._buf(("bnslots", c.cin, K), self.n_slots * c.cin * K, torch.float64)
+                    bnb = (prec["out"], prec["ys"][-1], pb["bns"][-1].coef, slots) + (
+                        (prec["yd"], pb["ds_bn"].coef) if pds else ())
+                    self._dgrad(c, dy, N, h, w, P, Q, gnext, res=res, bnb=bnb)
+                    g_fused = slots
                 else:
                     self._dgrad(c, dy, N, h, w, P, Q, gnext, res=res)
+                    g_fused = None
             g = gnext
             gsel ^= 1
         # stem: max-pool backward + ReLU mask (from the BN input) -> BN backward -> im2col weight gradient
