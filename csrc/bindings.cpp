@@ -999,6 +999,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stat_slots", &stat_slots);
   m.def("conv_l1_set_pp", &pdt::conv_l1_set_pp, py::arg("mode"),
         "layer1 kernel choice: 1 = 8-wave ping-pong, 0 = 4-wave, -1 = PDT_CONV_L1_PP (default); returns the previous");
+  m.def("conv32_set_halo", &pdt::conv32_set_halo, py::arg("on"),
+        "fp32 3x3/s1 64-channel convolutions: 1 = halo kernel (default unless PDT_FP32_CONV_HALO=0), 0 = per-tap "
+        "restaging kernel; returns the previous setting");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_finalize_slots", &bn_finalize_slots);
   m.def("bn_bwd_finalize_slots", &bn_bwd_finalize_slots);

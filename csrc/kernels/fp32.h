@@ -40,6 +40,9 @@ struct Conv32Args {
   uint32_t ppq_mul[4], ppq_shift[4], pq1_mul[4], pq1_shift[4];
 };
 void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s);
+// 3x3 / stride-1 same-grid convolutions on 64-channel output tiles: the halo kernel (default) or conv32_kernel (0); returns the
+// previous setting
+int conv32_set_halo(int on);
 
 // fp32 weight gradient: ws[split][Kout][ldw], column tap*C + c, split-K over pixels (sum with wgrad_reduce).
 struct Wgrad32Args {

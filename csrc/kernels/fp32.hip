@@ -16,6 +16,8 @@
 //     four different bank groups (ds_read_b32, conflict free).
 //   * BN apply / backward reduce / backward apply, stem BN+ReLU+max-pool and its backward, average pool,
 //     softmax cross-entropy + accuracy, bias column sums, stem im2col: float4-vectorised NHWC kernels.
+#include <cstdlib>
+
 #include "../common.h"
 #include "conv_fwd.h"
 #include "fp32.h"
@@ -40,6 +42,101 @@ PDT_DEVICE void zero_stat_row32(const Conv32Args& a) {
     const int tm = (int)blockIdx.x / a.n_tiles, tn = (int)blockIdx.x - tm * a.n_tiles;
     float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * KO + (int64_t)tn * BN_ * KO;
     for (int i = threadIdx.x; i < BN_ * KO; i += blockDim.x) dst[i] = 0.f;
+  }
+}
+
+// Shared epilogue of the fp32 implicit-GEMM kernels (conv32_kernel, conv32_halo_kernel): acc[i][j] holds
+// output channels n0 + wn*WN + i*16 + 4*(lane>>4) + r of pixel m0 + wm*WM + j*16 + (lane&15).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool RES>
+PDT_DEVICE void conv32_epilogue(const Conv32Args& a, f32x4_t (&acc)[BN / WAVES_N / 16][BM / WAVES_M / 16],
+                                int64_t m0, int n0, int tile_m, int wn, int wm, int tid, int lane, char* smem) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WN = BN / WAVES_N, WM = BM / WAVES_M;
+  constexpr int FN = WN / 16, FM = WM / 16;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int PQ = a.Pm * a.Qm;
+  const FastDiv fd_pq{a.pq_mul, a.pq_shift}, fd_q{a.q_mul, a.q_shift};
+  // EPI 1: forward statistics | 2: fused BN-backward reduce, one branch | 3: two branches (Conv32Args::bnb)
+  constexpr int KS = EPI == 3 ? 3 : 2;  // accumulated quantities per channel
+  float sacc[FN][4][KS];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int64_t m = m0 + wm * WM + j * 16 + fr;
+    if (m >= a.M) continue;
+    const int mm = (int)m;
+    const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
+    const int rem = mm - nimg * PQ;
+    const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
+    const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
+    const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * WN + i * 16 + 4 * fq;
+      f32x4v v = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if constexpr (RES) v += *(const f32x4v*)(a.res + ob + n);
+      if constexpr (EPI >= 2) {  // fused BN-backward reduce of the consumer BN (see Conv32Args::bnb)
+        const f32x4v m = *(const f32x4v*)(a.bn_mref + ob + n);
+        const f32x4v x1 = (*(const f32x4v*)(a.bn_y1 + ob + n) - *(const f32x4v*)(a.bn_coef + 2 * a.Kout + n)) *
+                          *(const f32x4v*)(a.bn_coef + 3 * a.Kout + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = m[r] > 0.f ? v[r] : 0.f;
+          sacc[i][r][0] += v[r];
+          sacc[i][r][1] += v[r] * x1[r];
+        }
+        if constexpr (EPI == 3) {
+          const f32x4v x2 = (*(const f32x4v*)(a.bn_y2 + ob + n) - *(const f32x4v*)(a.bn_coef2 + 2 * a.Kout + n)) *
+                            *(const f32x4v*)(a.bn_coef2 + 3 * a.Kout + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sacc[i][r][2] += v[r] * x2[r];
+        }
+      }
+      *(f32x4v*)(a.y + ob + n) = v;
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sacc[i][r][0] += v[r];
+          sacc[i][r][1] += v[r] * v[r];
+        }
+      }
+    }
+  }
+  if constexpr (EPI != 0) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
+    float* red = (float*)smem;  // [WAVES_M][BN][KS] (the LDS ring is free: every wave passed the last barrier)
+    if (fr == 15) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * WN + i * 16 + 4 * fq + r;
+#pragma unroll
+          for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
+        }
+    }
+    __syncthreads();
+    // stored quantities per channel: KO = 2, or 4 for two branches (sum dz stored twice: the finalize's layout)
+    constexpr int KO = EPI == 3 ? 4 : 2;
+    for (int idx = tid; idx < BN * KO; idx += 64 * NW) {
+      const int nl = idx / KO, ko = idx - nl * KO;
+      const int k = EPI == 3 ? (ko == 2 ? 0 : (ko == 3 ? 2 : ko)) : ko;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w) t += red[(w * BN + nl) * KS + k];
+      const int64_t row = (a.nphase > 0 ? (int64_t)blockIdx.y * a.srows_pp : 0) + tile_m;
+      a.srows[(row * a.Kout + n0 + nl) * KO + ko] = t;
+    }
   }
 }
 
@@ -187,92 +284,197 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
     }
   }
 
-  // ---- epilogue: lane holds output channels n = n0 + wn*WN + i*16 + 4*fq + r of pixel m ----
-  // EPI 1: forward statistics | 2: fused BN-backward reduce, one branch | 3: two branches (Conv32Args::bnb)
-  constexpr int KS = EPI == 3 ? 3 : 2;  // accumulated quantities per channel
-  float sacc[FN][4][KS];
+  conv32_epilogue<BM, BN, WAVES_M, WAVES_N, EPI, RES>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+}
+
+// ----------------------------------------------------------------------------------------- conv32 halo
+// 3x3 / stride-1 convolutions whose output grid is the input grid (ResNet layer1, 64 -> 64 channels: forward and
+// backward-data; per-tap input offsets dh, dw in {-1, 0, 1}).  conv32_kernel re-stages the activation tile for every
+// one of the 9 taps (21 FLOP per staged byte at 128 x 64, the L2 -> LDS stream bounds it); here a block stages, per
+// 32-channel chunk, the input rows its 256 output pixels span plus one halo row above and below -- each (W + 2) LDS
+// rows of 128 B with a zero column on either side, source-swizzled like the GEMM tiles -- ONCE, and runs all 9 taps
+// off it: a tap is a per-lane LDS row offset dh * (W + 2) + dw.  A pixel whose tap row leaves its own image (a
+// block's rows may span two images) reads a zero LDS row instead.  Per K-step only the 8 KB weight tap tile is
+// staged (2-deep ring): ~70 FLOP per staged byte.  8 waves (4 x 2 of 64 x 32), 74 KB LDS: two blocks per CU.
+// K order: chunk-major (chunk, tap), so the fp32 sums differ from conv32_kernel's (tap, chunk) order in rounding.
+constexpr int kHalo32Rows = 464;  // LDS rows of one halo chunk: ((W + 254) / W + 3) * (W + 2) <= 464 (W = 56: 8 x 58)
+
+template <int EPI, bool RES>
+__global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
+  Conv32Args a = args;
+  if (args.nphase > 0) {  // single-phase (stride-1) backward-data launch: the phase's weights and tap offsets
+    a.ioff_h = args.pioff_h[0]; a.ioff_w = args.pioff_w[0];
+    a.w = args.w + args.pwoff[0];
+  }
+  constexpr int BM = 256, BN = 64, WAVES_M = 4, WAVES_N = 2, NW = WAVES_M * WAVES_N;
+  constexpr int WN = BN / WAVES_N, WM = BM / WAVES_M, FN = WN / 16, FM = WM / 16;
+  constexpr int ROWB = 128;                          // 32 fp32 channels per LDS row
+  constexpr int A_BYTES = BN * ROWB;                 // one weight tap tile (8 KB), 1 DMA instruction per wave
+  constexpr int OFF_H = 2 * A_BYTES;                 // the halo chunk
+  constexpr int OFF_Z = OFF_H + kHalo32Rows * ROWB;  // one zero row
+  constexpr int NHI = kHalo32Rows / 8;               // halo DMA instructions (8 rows each)
+  constexpr int HI = (NHI + NW - 1) / NW;            // ... per wave
+  static_assert(A_BYTES == NW * 1024, "one weight DMA instruction per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[OFF_Z + ROWB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WAVES_N, wm = wave / WAVES_N;
+  const int nwg = a.m_tiles * a.n_tiles;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile_m = bid / a.n_tiles, tile_n = bid % a.n_tiles;
+  const int64_t m0 = (int64_t)tile_m * BM;
+  const int n0 = tile_n * BN;
+  const int Wd = a.W, W2 = a.W + 2, C = a.C;
+  const FastDiv fd_pq{a.pq_mul, a.pq_shift}, fd_q{a.q_mul, a.q_shift};  // Pm * Qm == H * W, Qm == W
+  const int mlast = (int)(m0 + BM < a.M ? m0 + BM : a.M) - 1;
+  const int gA = (int)fdiv((uint32_t)m0, fd_q);  // first output row, rows of all images stacked
+  const int gB = (int)fdiv((uint32_t)mlast, fd_q);
+  const int hrows = (gB - gA + 3) * W2;           // LDS rows in use (host: <= kHalo32Rows)
+  const int NG = a.N * a.H;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * C * 4u));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)((uint64_t)a.Kout * 9 * C * 4u));
+  const int lrow = lane >> 3, pchunk = lane & 7;
+
+  // halo DMA sources: LDS row hr = (halo row) * W2 + column + 1; rows outside the tensor, the zero columns and
+  // the unused tail read zeros (kOOB)
+  uint32_t hoff[HI];
 #pragma unroll
-  for (int i = 0; i < FN; ++i)
+  for (int k = 0; k < HI; ++k) {
+    const int hr = (wave * HI + k) * 8 + lrow;
+    const int hrow = hr / W2, col = hr - hrow * W2 - 1;
+    const int g = gA - 1 + hrow;
+    const bool ok = hr < hrows && g >= 0 && g < NG && col >= 0 && col < Wd;
+    hoff[k] = ok ? (uint32_t)(((g * Wd + col) * C + (pchunk ^ ((hr >> 1) & 7)) * 4) * 4) : kOOB;
+  }
+  const int arow = wave * 8 + lrow;
+  const uint32_t aoff = (uint32_t)(((n0 + arow) * 9 * C + (pchunk ^ ((arow >> 1) & 7)) * 4) * 4);
+  auto stage_halo = [&](int kc) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
+    for (int k = 0; k < HI; ++k) {
+      const int ii = wave * HI + k;  // wave-uniform
+      if (ii < NHI && ii * 8 < hrows)
+        buf_lds16_asm(rx, smem + OFF_H + ii * 1024, hoff[k] == kOOB ? kOOB : hoff[k] + (uint32_t)kc * 128u);
+    }
+  };
+  auto stage_w = [&](int kc, int tap, int buf) {
+    buf_lds16_asm(rw, smem + buf * A_BYTES + wave * 1024, aoff + (uint32_t)((tap * C + kc * 32) * 4));
+  };
+
+  // per-lane output pixel geometry: halo base row and the pixel's row within its image
+  const int fr = lane & 15, fq = lane >> 4;
+  int hb[FM], hin[FM];
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
     const int64_t m = m0 + wm * WM + j * 16 + fr;
-    if (m >= a.M) continue;
-    const int mm = (int)m;
-    const int nimg = (int)fdiv((uint32_t)mm, fd_pq);
-    const int rem = mm - nimg * PQ;
-    const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
-    const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
-    const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
-#pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int n = n0 + wn * WN + i * 16 + 4 * fq;
-      f32x4v v = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if constexpr (RES) v += *(const f32x4v*)(a.res + ob + n);
-      if constexpr (EPI >= 2) {  // fused BN-backward reduce of the consumer BN (see Conv32Args::bnb)
-        const f32x4v m = *(const f32x4v*)(a.bn_mref + ob + n);
-        const f32x4v x1 = (*(const f32x4v*)(a.bn_y1 + ob + n) - *(const f32x4v*)(a.bn_coef + 2 * a.Kout + n)) *
-                          *(const f32x4v*)(a.bn_coef + 3 * a.Kout + n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = m[r] > 0.f ? v[r] : 0.f;
-          sacc[i][r][0] += v[r];
-          sacc[i][r][1] += v[r] * x1[r];
-        }
-        if constexpr (EPI == 3) {
-          const f32x4v x2 = (*(const f32x4v*)(a.bn_y2 + ob + n) - *(const f32x4v*)(a.bn_coef2 + 2 * a.Kout + n)) *
-                            *(const f32x4v*)(a.bn_coef2 + 3 * a.Kout + n);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sacc[i][r][2] += v[r] * x2[r];
-        }
-      }
-      *(f32x4v*)(a.y + ob + n) = v;
-      if constexpr (EPI == 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          sacc[i][r][0] += v[r];
-          sacc[i][r][1] += v[r] * v[r];
-        }
-      }
+    if (m < a.M) {
+      const int g = (int)fdiv((uint32_t)m, fd_q);
+      const int nimg = (int)fdiv((uint32_t)m, fd_pq);
+      hb[j] = (g - gA + 1) * W2 + ((int)m - g * Wd) + 1;
+      hin[j] = g - nimg * a.H;
+    } else {  // past the end: any in-range LDS row (the result is not stored)
+      hb[j] = W2 + 1;
+      hin[j] = 0;
     }
   }
-  if constexpr (EPI != 0) {
+  int a_off[FN];
 #pragma unroll
-    for (int i = 0; i < FN; ++i)
+  for (int i = 0; i < FN; ++i) a_off[i] = (wn * WN + i * 16 + fr) * ROWB;
+  const int sw = (fr >> 1) & 7;
+
+  f32x4_t acc[FN][FM];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int k = 0; k < KS; ++k) sacc[i][r][k] = row16_sum(sacc[i][r][k]);
-    float* red = (float*)smem;  // [WAVES_M][BN][KS] (the LDS ring is free: every wave passed the last barrier)
-    if (fr == 15) {
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf, int tap) {
+    const int t = tap / 3, u = tap - 3 * t;
+    const int dh = a.ioff_h + t * a.tstep_h, dw = a.ioff_w + u * a.tstep_w;
+    const int delta = dh * W2 + dw;
+    int bo[FM], bsw[FM];
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int nl = wn * WN + i * 16 + 4 * fq + r;
-#pragma unroll
-          for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
-        }
+    for (int j = 0; j < FM; ++j) {
+      const int hr = hb[j] + delta;
+      const bool ok = (unsigned)(hin[j] + dh) < (unsigned)a.H;
+      bo[j] = ok ? OFF_H + hr * ROWB : OFF_Z;
+      bsw[j] = ok ? (hr >> 1) & 7 : 0;
     }
+    const char* sa = smem + buf * A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f32x4v af[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) af[i] = *(const f32x4v*)(sa + a_off[i] + (((kk * 4 + fq) ^ sw) << 4));
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfr[j] = *(const f32x4v*)(smem + bo[j] + (((kk * 4 + fq) ^ bsw[j]) << 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i][j] = mfma4(af[i][e], bfr[j][e], acc[i][j]);
+    }
+  };
+
+  const int nchunks = C / 32;
+  if (tid < 8) *(f32x4v*)(smem + OFF_Z + tid * 16) = f32x4v{0.f, 0.f, 0.f, 0.f};
+  stage_halo(0);
+  stage_w(0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int kc = 0, tap = 0;
+  for (int ks = 0; ks < 9 * nchunks; ++ks) {
+    const int nkc = tap == 8 ? kc + 1 : kc, ntap = tap == 8 ? 0 : tap + 1;
+    const bool more = nkc < nchunks;
+    if (more) stage_w(nkc, ntap, (ks + 1) & 1);  // the other ring slot: its last reader passed the last barrier
+    compute(ks & 1, tap);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // stored quantities per channel: KO = 2, or 4 for two branches (sum dz stored twice: the finalize's layout)
-    constexpr int KO = EPI == 3 ? 4 : 2;
-    for (int idx = tid; idx < BN * KO; idx += 64 * NW) {
-      const int nl = idx / KO, ko = idx - nl * KO;
-      const int k = EPI == 3 ? (ko == 2 ? 0 : (ko == 3 ? 2 : ko)) : ko;
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WAVES_M; ++w) t += red[(w * BN + nl) * KS + k];
-      const int64_t row = (a.nphase > 0 ? (int64_t)blockIdx.y * a.srows_pp : 0) + tile_m;
-      a.srows[(row * a.Kout + n0 + nl) * KO + ko] = t;
+    if (more && nkc != kc) {  // next chunk: restage the halo once every wave is past its last read of it
+      stage_halo(nkc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
+    kc = nkc;
+    tap = ntap;
   }
+  conv32_epilogue<BM, BN, WAVES_M, WAVES_N, EPI, RES>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
+}
+
+// conv32_halo_kernel's geometry contract (see above); PDT_FP32_CONV_HALO=0 / conv32_set_halo(0): the tap-restaging
+// conv32_kernel for A/B
+static bool g_conv32_halo = [] {
+  const char* e = getenv("PDT_FP32_CONV_HALO");
+  return !(e && e[0] == '0');
+}();
+int conv32_set_halo(int on) {
+  const int prev = g_conv32_halo ? 1 : 0;
+  g_conv32_halo = on != 0;
+  return prev;
+}
+
+static bool conv32_halo_ok(const Conv32Args& a, int bn) {
+  if (!g_conv32_halo || bn != 64 || a.nphase > 1 || a.Kout % 64 != 0 || a.C % 32 != 0) return false;
+  if (a.cs != 0 && a.cs != a.C) return false;
+  const bool ph = a.nphase == 1;
+  const int T = ph ? a.pT[0] : a.T, U = ph ? a.pU[0] : a.U;
+  const int ioh = ph ? a.pioff_h[0] : a.ioff_h, iow = ph ? a.pioff_w[0] : a.ioff_w;
+  const int Pm = ph ? a.pPm[0] : a.Pm, Qm = ph ? a.pQm[0] : a.Qm;
+  if (T != 3 || U != 3 || a.ist_h != 1 || a.ist_w != 1 || Pm != a.H || Qm != a.W) return false;
+  if (a.ost_h != 1 || a.ost_w != 1 || a.OH != a.H || a.OW != a.W) return false;
+  if (ph ? (a.pooff_h[0] != 0 || a.pooff_w[0] != 0) : (a.ooff_h != 0 || a.ooff_w != 0)) return false;
+  for (int t = 0; t < 3; ++t) {
+    const int dh = ioh + t * a.tstep_h, dw = iow + t * a.tstep_w;
+    if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return false;
+  }
+  if (a.W < 1 || ((a.W + 254) / a.W + 3) * (a.W + 2) > kHalo32Rows) return false;
+  return (int64_t)a.N * a.H * a.W * a.C < (int64_t(1) << 29);
 }
 
 void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
+  const bool halo = conv32_halo_ok(a, bn);
+  if (halo) bm = 256;
   a.m_tiles = (int)((a.M + bm - 1) / bm);
   a.n_tiles = a.Kout / bn;
   {
@@ -308,6 +510,20 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
                  __FILE__, __LINE__);
   if (a.bnb) PDT_COUNT("conv32_dgrad_bn_reduce_epilogue");
   const int two = a.bn_y2 != nullptr;
+  if (halo) {
+    PDT_COUNT("conv32_halo");
+    dim3 grid(gx, 1), block(512);
+    if (a.bnb && two && rs) hipLaunchKernelGGL((conv32_halo_kernel<3, true>), grid, block, 0, s, a);
+    else if (a.bnb && two) hipLaunchKernelGGL((conv32_halo_kernel<3, false>), grid, block, 0, s, a);
+    else if (a.bnb && rs) hipLaunchKernelGGL((conv32_halo_kernel<2, true>), grid, block, 0, s, a);
+    else if (a.bnb) hipLaunchKernelGGL((conv32_halo_kernel<2, false>), grid, block, 0, s, a);
+    else if (st && rs) hipLaunchKernelGGL((conv32_halo_kernel<1, true>), grid, block, 0, s, a);
+    else if (st) hipLaunchKernelGGL((conv32_halo_kernel<1, false>), grid, block, 0, s, a);
+    else if (rs) hipLaunchKernelGGL((conv32_halo_kernel<0, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv32_halo_kernel<0, false>), grid, block, 0, s, a);
+    if (st) stat_rows_reduce_launch(a.srows, srows, a.Kout * KO, a.stats, s);
+    return;
+  }
 #define PDT_C32(BM_, BN_, WM_, WN_)                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                          \
     dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(64 * WM_ * WN_);                                   \

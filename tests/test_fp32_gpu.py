@@ -324,3 +324,54 @@ def test_fp32_fused_bn_backward_reduce_matches_separate_pass(monkeypatch):
         outs.append((logits.float().clone(), tr.flat.grad.clone()))
     assert torch.equal(outs[0][0], outs[1][0])  # the forward is untouched
     assert _rel(outs[1][1], outs[0][1]) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,W,cin,cout", [(2, 56, 56, 64, 64), (5, 10, 10, 64, 64), (3, 7, 9, 128, 128)])
+def test_conv32_halo_kernel_matches_restaging_kernel_and_torch(N, H, W, cin, cout):
+    """The fp32 3x3/s1 halo kernel (all 9 taps off one staged halo per 32-channel chunk; tiles spanning several
+    images, ragged widths, 2 output-channel tiles) vs torch fp32 and vs the per-tap restaging conv32_kernel:
+    forward + residual + BN statistics, and stride-1 backward-data."""
+    from pytorch_distributed_template_amd.ops import native
+    from pytorch_distributed_template_amd.ops.conv import dgrad_phases, dgrad_weight_index
+    C = native.C
+    torch.manual_seed(3)
+    x = torch.randn(N, cin, H, W, device=DEV, requires_grad=True)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5).requires_grad_()
+    res = torch.randn(N, cout, H, W, device=DEV)
+    y = F.conv2d(x, w, padding=1)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xh, wk = x.detach().permute(0, 2, 3, 1).contiguous(), w.detach().permute(0, 2, 3, 1).contiguous()
+    resh, gyh = res.permute(0, 2, 3, 1).contiguous(), gy.permute(0, 2, 3, 1).contiguous()
+    ref = (y.detach() + res).permute(0, 2, 3, 1)
+    wflat = wk.reshape(-1)
+    pieces, phases, off = [], [], 0
+    for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(3, 3, 1, 1):
+        idx = dgrad_weight_index(cout, cin, 3, 3, rs, ss).to(DEV)
+        pieces.append(wflat[idx])
+        phases.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, off])
+        off += idx.numel()
+    wt = torch.cat(pieces)
+    got = {}
+    prev = C.conv32_set_halo(1)
+    try:
+        for halo in (1, 0):
+            C.conv32_set_halo(halo)
+            C.reset_dispatch_counts()
+            out = torch.empty(N, H, W, cout, device=DEV)
+            sp = torch.zeros(C.stat_slots() * cout * 2, dtype=torch.float64, device=DEV)
+            C.conv32_fwd(xh, wflat, out, resh, sp, N, H, W, cin, cout, 3, 3, H, W, 1, 1, 128, 64)
+            dx = torch.empty(N, H, W, cin, device=DEV)
+            C.conv32_dgrad(gyh, wt, dx, None, N, H, W, cout, cin, H, W, 1, phases, 128, 64)
+            torch.cuda.synchronize()
+            n = dict(C.dispatch_counts()).get("conv32_halo", 0)
+            assert n == (2 if halo else 0), n
+            assert _rel(out, ref) < 1e-5, halo
+            s = sp.view(C.stat_slots(), cout, 2).sum(0)
+            assert _rel(s[:, 0], ref.reshape(-1, cout).double().sum(0)) < 1e-6
+            assert _rel(s[:, 1], (ref.reshape(-1, cout).double() ** 2).sum(0)) < 1e-6
+            assert _rel(dx, x.grad.permute(0, 2, 3, 1)) < 1e-5, halo
+            got[halo] = (out, dx)
+    finally:
+        C.conv32_set_halo(prev)
+    assert _rel(got[1][0], got[0][0]) < 1e-6 and _rel(got[1][1], got[0][1]) < 1e-6
