@@ -868,6 +868,31 @@ void bn_relu_maxpool32(const Tensor& y, const Tensor& coef, Tensor& out, Tensor&
                                 cur_stream());
 }
 
+// the stem's backward tail without the dz tensor: fused max-pool backward + ReLU mask + BN-backward reduce / apply
+void stem_pool_bwd_reduce32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& slots,
+                            int64_t blocks, int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dp.numel() == N * OH * OW * C && y.numel() == N * H * W * C && idx.numel() == dp.numel() && C % 4 == 0 &&
+                  C / 4 <= 256 && 256 % (C / 4) == 0 && coef.numel() >= 4 * C && slots.numel() >= pdt::kStatSlots * C * 2 &&
+                  N * H * W < (int64_t(1) << 31),
+              "stem_pool_bwd_reduce32: bad sizes");
+  check_dev(idx, "idx");
+  pdt::stem_pool_bwd_reduce32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"),
+                                     pd(slots, "slots"), (int)blocks, N, H, W, C, cur_stream());
+}
+
+void stem_pool_bwd_apply32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, const Tensor& b,
+                           Tensor& dy, int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dp.numel() == N * OH * OW * C && y.numel() == N * H * W * C && dy.numel() == y.numel() &&
+                  idx.numel() == dp.numel() && C % 4 == 0 && coef.numel() >= 4 * C && b.numel() >= 3 * C &&
+                  N * H * W < (int64_t(1) << 31),
+              "stem_pool_bwd_apply32: bad sizes");
+  check_dev(idx, "idx");
+  pdt::stem_pool_bwd_apply32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"), pf(b, "b"),
+                                    pf(dy, "dy"), N, H, W, C, cur_stream());
+}
+
 void maxpool_bwd_relu32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& dz, int64_t N,
                         int64_t H, int64_t W, int64_t C) {
   const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
@@ -1049,6 +1074,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply32", &bn_bwd_apply32);
   m.def("bn_relu_maxpool32", &bn_relu_maxpool32);
   m.def("maxpool_bwd_relu32", &maxpool_bwd_relu32);
+  m.def("stem_pool_bwd_reduce32", &stem_pool_bwd_reduce32);
+  m.def("stem_pool_bwd_apply32", &stem_pool_bwd_apply32);
   m.def("avgpool32_fwd", &avgpool32_fwd);
   m.def("avgpool32_bwd", &avgpool32_bwd);
   m.def("xent32", &xent32);

@@ -70,6 +70,12 @@ void bn_bwd_apply32_launch(const float* g, const float* mref, const float* y1, c
                            const float* y2, const float* b2, float* dy2, float* dz, int64_t n, int C, hipStream_t s);
 void bn_relu_maxpool32_launch(const float* y, const float* coef, float* out, uint8_t* idx, int N, int H, int W, int C,
                               hipStream_t s);
+// the stem's backward tail with dz recomputed instead of stored (max-pool backward x ReLU mask): BN-backward reduce
+// into fp64 slots, and the apply dy = A*dz + B*y + C
+void stem_pool_bwd_reduce32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, double* slots,
+                                   int blocks, int N, int H, int W, int C, hipStream_t s);
+void stem_pool_bwd_apply32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, const float* b,
+                                  float* dy, int N, int H, int W, int C, hipStream_t s);
 void maxpool_bwd_relu32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, float* dz, int N,
                                int H, int W, int C, hipStream_t s);
 void avgpool32_fwd_launch(const float* x, float* feat, int N, int HW, int C, int ldf, hipStream_t s);

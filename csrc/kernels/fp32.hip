@@ -1158,6 +1158,121 @@ void maxpool_bwd_relu32_launch(const float* dp, const uint8_t* idx, const float*
                      y, coef, dz, N, H, W, C, OH, OW);
 }
 
+// The stem's backward tail without the dz tensor (N x H x W x C fp32, 3.85 GB at ResNet-18 bs1200): dz = max-pool
+// backward (gather over the <= 4 pooling windows covering a pixel, argmax routing) x ReLU mask (BN output > 0) is
+// recomputed from the pooled gradient, the argmax bytes and y0 by both the BN-backward reduce and the apply, instead
+// of maxpool_bwd_relu32 writing it and bn_bwd_reduce32 / bn_bwd_apply32 reading it back: ~28 -> ~14 GB of traffic.
+// The gather and the float operations are maxpool_bwd_relu32's, and the reduce's thread / row / block structure is
+// bn_bwd_reduce32's (NV = 1): the results equal the three separate passes' up to the compiler's fma contraction.
+PDT_DEVICE f32x4v stem_pool_dz32(const float* __restrict__ dp, const uint8_t* __restrict__ idx, const f32x4v yy,
+                                 const float* __restrict__ coef, int n, int h, int w, int c0, int C, int OH, int OW) {
+  f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+  for (int oh = h / 2; oh <= (h + 1) / 2; ++oh) {
+    const int kh = h - (oh * 2 - 1);
+    if (oh >= OH || kh < 0 || kh > 2) continue;
+    for (int ow = w / 2; ow <= (w + 1) / 2; ++ow) {
+      const int kw = w - (ow * 2 - 1);
+      if (ow >= OW || kw < 0 || kw > 2) continue;
+      const uint8_t pos = (uint8_t)(kh * 3 + kw);
+      const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+      const uint32_t ib = *(const uint32_t*)(idx + o);
+      const f32x4v gv = *(const f32x4v*)(dp + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((uint8_t)(ib >> (8 * e)) == pos) acc[e] += gv[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (!(yy[e] * coef[c0 + e] + coef[C + c0 + e] > 0.f)) acc[e] = 0.f;
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void stem_pool_bwd_reduce32_kernel(const float* __restrict__ dp,
+                                                                     const uint8_t* __restrict__ idx,
+                                                                     const float* __restrict__ y,
+                                                                     const float* __restrict__ coef,
+                                                                     float* __restrict__ srows, int N, int H, int W,
+                                                                     int C, int OH, int OW) {
+  const int lanes_c = C / 4, rpi = 256 / lanes_c;
+  const int cl = threadIdx.x % lanes_c, rl = threadIdx.x / lanes_c;
+  const int64_t rows = (int64_t)N * H * W;
+  const int c0 = cl * 4;
+  float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rl < rpi) {
+    const f32x4v mean = *(const f32x4v*)(coef + 2 * C + c0), istd = *(const f32x4v*)(coef + 3 * C + c0);
+    for (int64_t r = (int64_t)blockIdx.x * rpi + rl; r < rows; r += (int64_t)gridDim.x * rpi) {
+      const int pix = (int)r;
+      const int w = pix % W, nh = pix / W;
+      const int h = nh % H, n = nh / H;
+      const f32x4v yy = *(const f32x4v*)(y + r * C + c0);
+      const f32x4v dz = stem_pool_dz32(dp, idx, yy, coef, n, h, w, c0, C, OH, OW);
+      const f32x4v x1 = (yy - mean) * istd;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s0[e] += dz[e];
+        s1[e] += dz[e] * x1[e];
+      }
+    }
+  }
+  extern __shared__ float red[];  // [rpi][C][2]
+  if (rl < rpi) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[((int64_t)rl * C + c0 + e) * 2 + 0] = s0[e];
+      red[((int64_t)rl * C + c0 + e) * 2 + 1] = s1[e];
+    }
+  }
+  __syncthreads();
+  float* dst = srows + (int64_t)blockIdx.x * C * 2;
+  for (int i = threadIdx.x; i < C * 2; i += 256) {
+    float tt = 0.f;
+    for (int q = 0; q < rpi; ++q) tt += red[(int64_t)q * C * 2 + i];
+    dst[i] = tt;
+  }
+}
+
+void stem_pool_bwd_reduce32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, double* slots,
+                                   int blocks, int N, int H, int W, int C, hipStream_t s) {
+  if (C % 4 != 0 || C / 4 > 256 || 256 % (C / 4) != 0)
+    pdt_hip_fail("stem_pool_bwd_reduce32: C / 4 must divide 256", hipErrorInvalidValue, __FILE__, __LINE__);
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  PDT_COUNT("stem_pool_bwd_fused32");
+  const int rpi = 256 / (C / 4);
+  Scratch part((size_t)blocks * C * 2 * sizeof(float), s);
+  float* srows = part.as<float>();
+  hipLaunchKernelGGL(stem_pool_bwd_reduce32_kernel, dim3(blocks), dim3(256), (size_t)rpi * C * 2 * sizeof(float), s, dp,
+                     idx, y, coef, srows, N, H, W, C, OH, OW);
+  stat_rows_reduce_launch(srows, blocks, C * 2, slots, s);
+}
+
+// dy = A*dz + B*y + C with dz recomputed (stem_pool_dz32): bn_bwd_apply32<false, 1, false> over maxpool_bwd_relu32's dz
+__global__ __launch_bounds__(256) void stem_pool_bwd_apply32_kernel(const float* __restrict__ dp,
+                                                                    const uint8_t* __restrict__ idx,
+                                                                    const float* __restrict__ y,
+                                                                    const float* __restrict__ coef,
+                                                                    const float* __restrict__ b, float* __restrict__ dy,
+                                                                    int N, int H, int W, int C, int OH, int OW) {
+  const int cv = C / 4;
+  const int64_t total = (int64_t)N * H * W * cv;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
+    const int pix = (int)(v / cv);
+    const int c0 = (int)(v - (int64_t)pix * cv) * 4;
+    const int w = pix % W, nh = pix / W;
+    const int h = nh % H, n = nh / H;
+    const f32x4v yy = ((const f32x4v*)y)[v];
+    const f32x4v dz = stem_pool_dz32(dp, idx, yy, coef, n, h, w, c0, C, OH, OW);
+    ((f32x4v*)dy)[v] = *(const f32x4v*)(b + c0) * dz + *(const f32x4v*)(b + C + c0) * yy + *(const f32x4v*)(b + 2 * C + c0);
+  }
+}
+
+void stem_pool_bwd_apply32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, const float* b,
+                                  float* dy, int N, int H, int W, int C, hipStream_t s) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(stem_pool_bwd_apply32_kernel, dim3(ew_blocks((int64_t)N * H * W * (C / 4))), dim3(256), 0, s, dp,
+                     idx, y, coef, b, dy, N, H, W, C, OH, OW);
+}
+
 // global average pool [N][HW][C] -> feat [N][ldf] (columns >= C are left alone) and its backward
 __global__ __launch_bounds__(256) void avgpool32_fwd_kernel(const float* __restrict__ x, float* __restrict__ feat, int N,
                                                             int HW, int C, int ldf) {

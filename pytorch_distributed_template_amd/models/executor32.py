@@ -194,6 +194,9 @@ class ResNetExecutor32(ResNetExecutor):
     _FUSE_BN = os.environ.get("PDT_FP32_FUSE_BN", "1") == "1"
 
     _HALO = os.environ.get("PDT_FP32_HALO", "1") == "1"
+    # stem backward tail: max-pool backward + ReLU mask recomputed inside the BN-backward reduce and apply (no dz
+    # tensor); PDT_FP32_STEM_FUSE=0: maxpool_bwd_relu32 + bn_bwd_reduce32 + bn_bwd_apply32 over a stored dz
+    _FUSE_STEM = os.environ.get("PDT_FP32_STEM_FUSE", "1") == "1"
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
                accumulate=False):
@@ -454,10 +457,19 @@ class ResNetExecutor32(ResNetExecutor):
         st, sbn = self.stem, self.stem_bn
         P0, Q0, H, W = saved["P0"], saved["Q0"], saved["H"], saved["W"]
         dz0 = self._buf("dz0", saved["y0"].numel(), torch.float32)
-        Cn.maxpool_bwd_relu32(g, saved["idx"], saved["y0"], sbn.coef, dz0, N, P0, Q0, st.cout)
-        self.bn_reduce(sbn, dz0, None, saved["y0"], N * P0 * Q0)
-        dy0 = dz0  # in place: each element read then written by the same thread
-        Cn.bn_bwd_apply32(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
+        if self._FUSE_STEM:  # dz recomputed by the reduce and the apply: never stored
+            rows = N * P0 * Q0
+            slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
+            Cn.stem_pool_bwd_reduce32(g, saved["idx"], saved["y0"], sbn.coef, slots,
+                                      Cn.bn_bwd_reduce32_blocks(rows, st.cout), N, P0, Q0, st.cout)
+            self._bn_bwd_finish(slots, rows, sbn, None)
+            dy0 = dz0
+            Cn.stem_pool_bwd_apply32(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
+        else:
+            Cn.maxpool_bwd_relu32(g, saved["idx"], saved["y0"], sbn.coef, dz0, N, P0, Q0, st.cout)
+            self.bn_reduce(sbn, dz0, None, saved["y0"], N * P0 * Q0)
+            dy0 = dz0  # in place: each element read then written by the same thread
+            Cn.bn_bwd_apply32(dz0, None, saved["y0"], sbn.bcoef, dy0, None, None, None, None, st.cout)
         if self.stem_win:  # window-pair weight gradient straight from the padded NHWC4 image (no im2col)
             npix = N * P0 * Q0
             key = ("stem_win", npix)

@@ -375,3 +375,27 @@ def test_conv32_halo_kernel_matches_restaging_kernel_and_torch(N, H, W, cin, cou
     finally:
         C.conv32_set_halo(prev)
     assert _rel(got[1][0], got[0][0]) < 1e-6 and _rel(got[1][1], got[0][1]) < 1e-6
+
+
+def test_fp32_fused_stem_tail_matches_the_separate_passes(monkeypatch):
+    """The stem's backward tail with dz recomputed inside the BN-backward reduce and apply (no stored dz) gives the
+    gradients of maxpool_bwd_relu32 + bn_bwd_reduce32 + bn_bwd_apply32 to fp32 rounding (the same operations; the
+    compiler's fma contraction may differ between the kernels), and really runs."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    from pytorch_distributed_template_amd.models.executor32 import ResNetExecutor32
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(2)
+    model = registry.create("resnet18")
+    x = torch.randn(3, 3, 80, 72, device=DEV)
+    t = torch.randint(0, 1000, (3,), device=DEV)
+    outs = []
+    for fuse in (False, True):
+        monkeypatch.setattr(ResNetExecutor32, "_FUSE_STEM", fuse)
+        tr = NativeTrainer(copy.deepcopy(model), torch.device(DEV), dtype=torch.float32, lr=0.0)
+        native.C.reset_dispatch_counts()
+        logits, met = tr.train_step(x, t)
+        torch.cuda.synchronize()
+        assert (dict(native.C.dispatch_counts()).get("stem_pool_bwd_fused32", 0) > 0) == fuse
+        outs.append(tr.flat.grad.clone())
+    assert _rel(outs[1], outs[0]) < 1e-5
