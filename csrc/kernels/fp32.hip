@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce32_kernel(const float
                                                                      const float* __restrict__ y,
                                                                      const float* __restrict__ coef,
                                                                      float* __restrict__ srows, int N, int H, int W,
-                                                                     int C, int OH, int OW) {
+                                                                     int C, int OH, int OW, FastDiv fw, FastDiv fh) {
   const int lanes_c = C / 4, rpi = 256 / lanes_c;
   const int cl = threadIdx.x % lanes_c, rl = threadIdx.x / lanes_c;
   const int64_t rows = (int64_t)N * H * W;
@@ -1203,8 +1203,8 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce32_kernel(const float
     const f32x4v mean = *(const f32x4v*)(coef + 2 * C + c0), istd = *(const f32x4v*)(coef + 3 * C + c0);
     for (int64_t r = (int64_t)blockIdx.x * rpi + rl; r < rows; r += (int64_t)gridDim.x * rpi) {
       const int pix = (int)r;
-      const int w = pix % W, nh = pix / W;
-      const int h = nh % H, n = nh / H;
+      const int nh = (int)fdiv((uint32_t)pix, fw), w = pix - nh * W;
+      const int n = (int)fdiv((uint32_t)nh, fh), h = nh - n * H;
       const f32x4v yy = *(const f32x4v*)(y + r * C + c0);
       const f32x4v dz = stem_pool_dz32(dp, idx, yy, coef, n, h, w, c0, C, OH, OW);
       const f32x4v x1 = (yy - mean) * istd;
@@ -1242,7 +1242,7 @@ void stem_pool_bwd_reduce32_launch(const float* dp, const uint8_t* idx, const fl
   Scratch part((size_t)blocks * C * 2 * sizeof(float), s);
   float* srows = part.as<float>();
   hipLaunchKernelGGL(stem_pool_bwd_reduce32_kernel, dim3(blocks), dim3(256), (size_t)rpi * C * 2 * sizeof(float), s, dp,
-                     idx, y, coef, srows, N, H, W, C, OH, OW);
+                     idx, y, coef, srows, N, H, W, C, OH, OW, make_fastdiv((uint32_t)W), make_fastdiv((uint32_t)H));
   stat_rows_reduce_launch(srows, blocks, C * 2, slots, s);
 }
 
@@ -1252,14 +1252,16 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_apply32_kernel(const float*
                                                                     const float* __restrict__ y,
                                                                     const float* __restrict__ coef,
                                                                     const float* __restrict__ b, float* __restrict__ dy,
-                                                                    int N, int H, int W, int C, int OH, int OW) {
-  const int cv = C / 4;
+                                                                    int N, int H, int W, int C, int OH, int OW, FastDiv fw,
+                                                                    FastDiv fh) {
+  const int cv = C / 4;  // a power of two (host-checked)
+  const int cshift = __builtin_ctz(cv);
   const int64_t total = (int64_t)N * H * W * cv;
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
-    const int pix = (int)(v / cv);
-    const int c0 = (int)(v - (int64_t)pix * cv) * 4;
-    const int w = pix % W, nh = pix / W;
-    const int h = nh % H, n = nh / H;
+    const int pix = (int)(v >> cshift);
+    const int c0 = (int)(v - ((int64_t)pix << cshift)) * 4;
+    const int nh = (int)fdiv((uint32_t)pix, fw), w = pix - nh * W;
+    const int n = (int)fdiv((uint32_t)nh, fh), h = nh - n * H;
     const f32x4v yy = ((const f32x4v*)y)[v];
     const f32x4v dz = stem_pool_dz32(dp, idx, yy, coef, n, h, w, c0, C, OH, OW);
     ((f32x4v*)dy)[v] = *(const f32x4v*)(b + c0) * dz + *(const f32x4v*)(b + C + c0) * yy + *(const f32x4v*)(b + 2 * C + c0);
@@ -1269,8 +1271,10 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_apply32_kernel(const float*
 void stem_pool_bwd_apply32_launch(const float* dp, const uint8_t* idx, const float* y, const float* coef, const float* b,
                                   float* dy, int N, int H, int W, int C, hipStream_t s) {
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  if (C % 4 != 0 || ((C / 4) & (C / 4 - 1)) != 0)
+    pdt_hip_fail("stem_pool_bwd_apply32: C / 4 must be a power of two", hipErrorInvalidValue, __FILE__, __LINE__);
   hipLaunchKernelGGL(stem_pool_bwd_apply32_kernel, dim3(ew_blocks((int64_t)N * H * W * (C / 4))), dim3(256), 0, s, dp,
-                     idx, y, coef, b, dy, N, H, W, C, OH, OW);
+                     idx, y, coef, b, dy, N, H, W, C, OH, OW, make_fastdiv((uint32_t)W), make_fastdiv((uint32_t)H));
 }
 
 // global average pool [N][HW][C] -> feat [N][ldf] (columns >= C are left alone) and its backward

@@ -460,8 +460,9 @@ class ResNetExecutor32(ResNetExecutor):
         if self._FUSE_STEM:  # dz recomputed by the reduce and the apply: never stored
             rows = N * P0 * Q0
             slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
-            Cn.stem_pool_bwd_reduce32(g, saved["idx"], saved["y0"], sbn.coef, slots,
-                                      Cn.bn_bwd_reduce32_blocks(rows, st.cout), N, P0, Q0, st.cout)
+            # 4x the blocks of a plain reduce: the per-pixel window gather is latency-bound, not a stream
+            blocks = max(1, min(4096, rows // 256))
+            Cn.stem_pool_bwd_reduce32(g, saved["idx"], saved["y0"], sbn.coef, slots, blocks, N, P0, Q0, st.cout)
             self._bn_bwd_finish(slots, rows, sbn, None)
             dy0 = dz0
             Cn.stem_pool_bwd_apply32(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
