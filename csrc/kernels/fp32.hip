@@ -901,8 +901,11 @@ template <int RESMODE, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply32_kernel(const float* __restrict__ y, const float* __restrict__ coef,
                                                          const float* __restrict__ res, const float* __restrict__ rcoef,
                                                          float* __restrict__ out, int64_t n4, int C) {
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
-    const int c = (int)((v * 4) % C);
+  // channel of float4 v, stepped with the grid stride (one 64-bit modulo per thread, not per element)
+  const int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x, vs = (int64_t)gridDim.x * 256;
+  const int cstep = (int)((vs * 4) % C);
+  int c = (int)((v0 * 4) % C);
+  for (int64_t v = v0; v < n4; v += vs, c = c + cstep >= C ? c + cstep - C : c + cstep) {
     f32x4v val = ((const f32x4v*)y)[v] * *(const f32x4v*)(coef + c) + *(const f32x4v*)(coef + C + c);
     if constexpr (RESMODE == 1) val += ((const f32x4v*)res)[v];
     if constexpr (RESMODE == 2)
@@ -1037,8 +1040,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply32_kernel(const float* __rest
                                                              float* __restrict__ dy1, const float* __restrict__ y2,
                                                              const float* __restrict__ b2, float* __restrict__ dy2,
                                                              float* __restrict__ dz_out, int64_t n4, int C) {
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
-    const int c = (int)((v * 4) % C);
+  const int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x, vs = (int64_t)gridDim.x * 256;
+  const int cstep = (int)((vs * 4) % C);
+  int c = (int)((v0 * 4) % C);
+  for (int64_t v = v0; v < n4; v += vs, c = c + cstep >= C ? c + cstep - C : c + cstep) {
     f32x4v dz = ((const f32x4v*)g)[v];
     if constexpr (MASK) {
       const f32x4v m = ((const f32x4v*)mref)[v];
