@@ -964,7 +964,8 @@ void conv32_stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& s
 // fp32 stem weight gradient in window-pair mode over the zero-padded NHWC4 image (no im2col): "tap" t = kernel rows
 // (2t, 2t+1), 64 columns = 8 pixels x 4 channels of each; ws[split][Kout][npairs * 64]
 void wgrad32_stem(const Tensor& xp, const Tensor& dy, Tensor& ws, int64_t N, int64_t Hp, int64_t Wp, int64_t npairs,
-                  int64_t Kout, int64_t P, int64_t Q, int64_t stride, int64_t splits, int64_t pix_per_split) {
+                  int64_t Kout, int64_t P, int64_t Q, int64_t stride, int64_t splits, int64_t pix_per_split,
+                  int64_t all_pairs = 0) {
   TORCH_CHECK(xp.numel() == N * Hp * Wp * 4 && dy.numel() == N * P * Q * Kout && Kout % 64 == 0, "wgrad32_stem: sizes");
   TORCH_CHECK((P - 1) * stride + 2 * npairs <= Hp && (Q - 1) * stride + 8 <= Wp, "wgrad32_stem: padded image too small");
   TORCH_CHECK(ws.numel() >= splits * Kout * npairs * 64 && pix_per_split % 64 == 0 && splits * pix_per_split >= N * P * Q,
@@ -977,6 +978,10 @@ void wgrad32_stem(const Tensor& xp, const Tensor& dy, Tensor& ws, int64_t N, int
   a.stride = stride; a.pad = 0; a.ldw = npairs * 64; a.splits = splits; a.pix_per_split = pix_per_split;
   a.P = N * P * Q;
   a.cs = 4; a.pair_skip = Wp * 4 - 32; a.tstep = 2;  // chunks 8..15 = the NEXT row's first 32 elements
+  if (all_pairs) {  // wgrad32_stem4_kernel: one block per split covers every pair (needs 4 pairs)
+    TORCH_CHECK(npairs == 4, "wgrad32_stem: all_pairs needs 4 kernel-row pairs");
+    a.tile = 4;
+  }
   pdt::wgrad32_launch(a, cur_stream());
 }
 
@@ -1082,6 +1087,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum32", &colsum32);
   m.def("stem_pack32", &stem_pack32);
   m.def("conv32_stem_fwd", &conv32_stem_fwd);
-  m.def("wgrad32_stem", &wgrad32_stem);
+  m.def("wgrad32_stem", &wgrad32_stem, py::arg("xp"), py::arg("dy"), py::arg("ws"), py::arg("N"), py::arg("Hp"),
+        py::arg("Wp"), py::arg("npairs"), py::arg("Kout"), py::arg("P"), py::arg("Q"), py::arg("stride"),
+        py::arg("splits"), py::arg("pix_per_split"), py::arg("all_pairs") = 0);
   m.def("im2col32", &im2col32);
 }

@@ -653,6 +653,114 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(Wgrad32Args a) {
       }
 }
 
+// Window-pair stem weight gradient with ALL kernel-row pairs per block (the fp32 twin of the 16-bit
+// wgrad_stem_kernel): wgrad32_kernel runs one block per (pair, split) and so stages every dY tile once per pair
+// (4x) at 16 FLOP per staged byte.  Here a block stages one 32-pixel dY tile plus the 4 pair-windows of X (8 KB
+// each, 40 KB per stage, 2-deep ring: 80 KB, two blocks per CU) and 8 waves own (pair = wave / 2) x (32 window
+// columns) x all 64 output channels: 26 FLOP per staged byte.  Same LDS element layout and window addressing as
+// wgrad32_kernel (Wgrad32Args window-pair fields).
+__global__ __launch_bounds__(512) void wgrad32_stem4_kernel(Wgrad32Args a) {
+  constexpr int PIX = 32;             // pixels per staged chunk
+  constexpr int TILE = PIX * 64 * 4;  // 8 KiB per operand tile ([pixel][64] fp32, 256 B rows)
+  constexpr int NT = 5;               // dY + 4 pair windows
+  constexpr int STAGE = NT * TILE;
+  constexpr int INS = NT * TILE / 1024 / 8;  // DMA wave-instructions per wave per stage (5)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 1, wc = wave & 1;  // pair, 32-column half
+  const int split = blockIdx.x, k0 = blockIdx.y * 64;
+  const int64_t p_begin = (int64_t)split * a.pix_per_split;
+  const int64_t p_end = p_begin + a.pix_per_split < a.P ? p_begin + a.pix_per_split : a.P;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)((uint64_t)a.N * a.H * a.W * 4u * 4u));
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (uint32_t)((uint64_t)a.P * a.Kout * 4u));
+  const int lrow = lane >> 4, pc = lane & 15;
+  const int sc = pc ^ (lrow << 2);
+  const int pskip = sc >= 8 ? a.pair_skip : 0;
+  const int PQ = a.Pm * a.Qm;
+  auto stage = [&](int64_t p0, int buf) {
+    char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int q = 0; q < INS; ++q) {
+      const int ins = wave * INS + q;  // 0..39: tile ins / 8, rows (ins % 8) * 4 + lrow
+      const int tile = ins >> 3;
+      const int row = (ins & 7) * 4 + lrow;
+      const int64_t p = p0 + row;
+      uint32_t off = kOOB;
+      if (p < p_end) {
+        if (tile == 0) {
+          off = (uint32_t)((p * a.Kout + k0 + sc * 4) * 4);
+        } else {
+          const int n = (int)(p / PQ);
+          const int rem = (int)(p - (int64_t)n * PQ);
+          const int i = rem / a.Qm, j = rem - (rem / a.Qm) * a.Qm;
+          const int ih = i * a.stride + (tile - 1) * a.tstep, iw = j * a.stride;
+          if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+            off = (uint32_t)(((((int64_t)n * a.H + ih) * a.W + iw) * 4 + sc * 4 + pskip) * 4);
+        }
+      }
+      buf_lds16_asm(tile == 0 ? rd : rx, sb + ins * 1024, off);
+    }
+  };
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  // element (row, col) of a tile: row*256 + (((col >> 2) ^ ((row & 3) << 2)) << 4) + (col & 3)*4; the rows read
+  // together are 4s + fq, so (row & 3) == fq
+  int aoff[4], boff[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 16 + fr;
+    aoff[i] = fq * 256 + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wc * 32 + j * 16 + fr;
+    boff[j] = (1 + wt) * TILE + fq * 256 + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
+  }
+  const int nchunks = p_end > p_begin ? (int)((p_end - p_begin + PIX - 1) / PIX) : 0;
+  if (nchunks > 0) {
+    stage(p_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const int cur = ch & 1;
+      if (ch + 1 < nchunks) stage(p_begin + (int64_t)(ch + 1) * PIX, cur ^ 1);
+      const char* base = smem + cur * STAGE;
+#pragma unroll 4
+      for (int s4 = 0; s4 < PIX / 4; ++s4) {
+        const char* sb = base + s4 * 4 * 256;
+        float av[4], bv[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = *(const float*)(sb + aoff[i]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = *(const float*)(sb + boff[j]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // lane holds dW[k = k0 + i*16 + 4*fq + r][pair wt, c = wc*32 + j*16 + fr]
+  float* out = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + i * 16 + 4 * fq + r;
+        const int c = wc * 32 + j * 16 + fr;
+        out[(int64_t)k * a.ldw + wt * 64 + c] = acc[i][j][r];
+      }
+}
+
 // Wide variant: 128 (Kout) x 128 (C) output tile of one tap, 8 waves as 2 (k) x 4 (c), each 64 x 32 (4 x 2 MFMA
 // tiles), 32-pixel chunks (dY and X tiles 16 KB each, 512-byte rows, 2-deep LDS-DMA ring: 64 KB, two blocks per
 // CU).  32 FLOP per staged byte against the 64 x 64 kernel's 16: the 64 x 64 tile needs ~10 TB/s of L2 traffic at
@@ -882,6 +990,16 @@ void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
     PDT_COUNT("wgrad32_halo");
     dim3 grid(a.splits, 3, (a.Kout / 64) * (a.C / 64)), block(256);
     hipLaunchKernelGGL(wgrad32_halo_kernel, grid, block, 0, s, a);
+    return;
+  }
+  if (a.tile == 4) {  // window-pair stem, all 4 pairs per block
+    if (a.cs != 4 || a.T != 4 || a.U != 1 || a.C != 64 || a.Kout % 64 != 0 || a.ldw != 256 || a.pad != 0 ||
+        a.pix_per_split % 32 != 0)
+      pdt_hip_fail("wgrad32: the 4-pair stem kernel needs the window-pair geometry (cs 4, 4 pairs, C 64)",
+                   hipErrorInvalidValue, __FILE__, __LINE__);
+    PDT_COUNT("wgrad32_stem4");
+    dim3 grid(a.splits, a.Kout / 64), block(512);
+    hipLaunchKernelGGL(wgrad32_stem4_kernel, grid, block, 0, s, a);
     return;
   }
   if (a.tile == 128) {

@@ -197,6 +197,8 @@ class ResNetExecutor32(ResNetExecutor):
     # stem backward tail: max-pool backward + ReLU mask recomputed inside the BN-backward reduce and apply (no dz
     # tensor); PDT_FP32_STEM_FUSE=0: maxpool_bwd_relu32 + bn_bwd_reduce32 + bn_bwd_apply32 over a stored dz
     _FUSE_STEM = os.environ.get("PDT_FP32_STEM_FUSE", "1") == "1"
+    # stem weight gradient: every kernel-row pair per block (dY staged once, not once per pair); 0: one block per pair
+    _STEM4 = os.environ.get("PDT_FP32_STEM4", "1") == "1"
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
                accumulate=False):
@@ -484,7 +486,7 @@ class ResNetExecutor32(ResNetExecutor):
             ldw = self.stem_pairs * 64
             ws = self._buf("ws", splits * st.cout * ldw, torch.float32)
             Cn.wgrad32_stem(saved["xp"], dy0, ws, N, saved["Hp"], saved["Wp"], self.stem_pairs, st.cout, P0, Q0, st.st,
-                            splits, pps)
+                            splits, pps, 1 if (self._STEM4 and self.stem_pairs == 4) else 0)
             tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
             Cn.wgrad_reduce(ws, splits, st.cout, ldw, ldw, st.cout * ldw, tmp, ldw, 1.0, False)
             Cn.gather32(tmp, self.stem_gidx_win, self._g(st.slot))

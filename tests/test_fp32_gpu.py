@@ -277,9 +277,11 @@ def test_fp32_executor_window_stem_matches_im2col_stem(monkeypatch):
     assert _rel(outs[1][2], outs[0][2]) < 5e-2
 
 
-def test_wgrad32_stem_window_pair_matches_torch():
+@pytest.mark.parametrize("all_pairs", [0, 1])
+def test_wgrad32_stem_window_pair_matches_torch(all_pairs):
     """fp32 stem weight gradient in window-pair mode (tap = kernel-row pair over the padded NHWC4 image) vs
-    torch.nn.grad.conv2d_weight in fp32."""
+    torch.nn.grad.conv2d_weight in fp32: one block per pair (wgrad32_kernel) and all 4 pairs per block
+    (wgrad32_stem4_kernel)."""
     from pytorch_distributed_template_amd.ops import native
     C = native.C
     torch.manual_seed(4)
@@ -294,7 +296,9 @@ def test_wgrad32_stem_window_pair_matches_torch():
     splits, pps = 7, ((npix + 6) // 7 + 63) // 64 * 64
     splits = (npix + pps - 1) // pps
     ws = torch.empty(splits * 64 * 256, device=DEV)
-    C.wgrad32_stem(xp, dy.contiguous(), ws, N, Hp, Wp, 4, 64, P, Q, 2, splits, pps)
+    C.reset_dispatch_counts()
+    C.wgrad32_stem(xp, dy.contiguous(), ws, N, Hp, Wp, 4, 64, P, Q, 2, splits, pps, all_pairs)
+    assert dict(C.dispatch_counts()).get("wgrad32_stem4", 0) == all_pairs
     dw = ws.view(splits, 64, 4, 2, 8, 4).sum(0)  # [k][pair][row in pair][pixel s][channel]
     dw = dw.reshape(64, 8, 8, 4)[:, :7, :7, :3].permute(0, 3, 1, 2)  # rows 0..7 -> 7 kernel rows
     ref = torch.nn.grad.conv2d_weight(x, (64, 3, 7, 7), dy.permute(0, 3, 1, 2), stride=2, padding=3)
