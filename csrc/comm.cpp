@@ -286,7 +286,15 @@ class Communicator {
     TORCH_CHECK(device >= 0, "rccl: a device is required");
     make_streams();
     transport_ = std::make_unique<RcclTransport>(id, world, rank);
-    if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });
+    if (timeout_s_ > 0) {
+      live_watchdogs().fetch_add(1);
+      watchdog_ = std::thread([this] { watch(); });
+    }
+  }
+  // live watchdog threads in this process (teardown checks: tests/test_end_to_end_cpu.py)
+  static std::atomic<int>& live_watchdogs() {
+    static std::atomic<int> n{0};
+    return n;
   }
   // Host shared-memory group (``device`` < 0: host tensors only; >= 0: device tensors staged through the host)
   Communicator(std::unique_ptr<Transport> t, int world, int rank, int device, double timeout_s)
@@ -323,7 +331,7 @@ class Communicator {
   // Not while the caller's stream is being captured into a HIP graph: the collective is then a graph node
   // (replayed later, possibly many times) and an event recorded now would never complete as a real event.
   // Synchronous transports have nothing in flight to watch.
-  void track(const char* what, hipStream_t on = nullptr) {
+  void track(const std::string& what, hipStream_t on = nullptr) {
     if (timeout_s_ <= 0 || device_ < 0 || transport().synchronous()) return;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(at::hip::getCurrentHIPStream().stream(), &cap) == hipSuccess &&
@@ -345,8 +353,7 @@ class Communicator {
   // compute stream, completing when the replayed step (and its collectives) did.
   void track_compute(const std::string& what) {
     if (device_ < 0) return;
-    replay_what_ = what;
-    track(replay_what_.c_str(), at::hip::getCurrentHIPStream().stream());
+    track(what, at::hip::getCurrentHIPStream().stream());
   }
   // Test hook: a pending "collective" that never completes, enqueued ``age_s`` seconds ago.
   void inject_stall(double age_s) {
@@ -440,7 +447,7 @@ class Communicator {
   struct Pending {
     hipEvent_t ev;  // nullptr: injected stall (never completes)
     std::chrono::steady_clock::time_point t;
-    const char* what;
+    std::string what;  // by value: the watchdog reads it, the caller's string may change or die
   };
 
   void make_streams() {
@@ -460,7 +467,10 @@ class Communicator {
       stop_ = true;
     }
     cv_.notify_all();
-    if (watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();
+    if (watchdog_.get_id() != std::this_thread::get_id()) {
+      watchdog_.join();
+      live_watchdogs().fetch_sub(1);
+    }
   }
 
   [[noreturn]] void fail(const std::string& why) {
@@ -528,7 +538,6 @@ class Communicator {
   std::deque<Pending> pending_;
   std::vector<hipEvent_t> free_evs_;
   std::thread watchdog_;
-  std::string replay_what_;
 };
 
 std::shared_ptr<Communicator> make_host_communicator(const std::string& name, int world, int rank, int device,
@@ -652,7 +661,8 @@ void register_comm(py::module& m) {
       .def("wait", &Communicator::wait)
       .def("async_error", &Communicator::async_error)
       .def("abort", &Communicator::abort)
-      .def("destroy", &Communicator::destroy);
+      .def("destroy", &Communicator::destroy)
+      .def_static("live_watchdogs", []() { return Communicator::live_watchdogs().load(); });
   py::class_<Bucketer>(m, "Bucketer")
       .def(py::init<std::shared_ptr<Communicator>, Tensor, std::vector<int64_t>, std::vector<int64_t>,
                     std::vector<int64_t>, int64_t>(),

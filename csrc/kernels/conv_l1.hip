@@ -505,8 +505,12 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
   // epilogue operands of the tile being computed: loaded at the start of its compute phase (latency hidden
   // under the MFMAs), pinned complete at its end
   // epilogue operands (residual, BN input, ReLU mask) are loaded at the start of the memory phase, see memphase
-  u32x2v pre_res[RES ? NJ : 1][RES ? 2 : 1], pre_y1[EPI >= 2 ? NJ : 1][EPI >= 2 ? 2 : 1];
-  u32x2v pre_m[EPI == 3 ? NJ : 1];
+  // EPI 3 (block-output BN-backward: residual + BN input + ReLU mask, 5 operand loads per pixel group) holds the
+  // operands of at most NJO = 4 groups at once: all 7 would spill (~70 registers beside the accumulators), so its
+  // epilogue runs in two halves (groups 0-3, then 4-6), each with its own operand loads (see memphase)
+  constexpr int NJO = EPI == 3 ? 4 : NJ;
+  u32x2v pre_res[RES ? NJO : 1][RES ? 2 : 1], pre_y1[EPI >= 2 ? NJO : 1][EPI >= 2 ? 2 : 1];
+  u32x2v pre_m[EPI == 3 ? NJO : 1];
   // a tile's 4 x 56 output pixels are one contiguous block: pixel px of tile t is element (t's first pixel + px) * 64
   const int lpx0 = pix_of_lane(fr) * 64;
   int lpx = lpx0;  // re-opaqued per use site (see stage_tile)
@@ -552,18 +556,25 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
   // epilogue: lane holds couts wn*32 + i*16 + 4*fq + r of pixel (wm*7 + j)*16 + pix_of_lane(fr); exactly
   // 2 * NJ = 14 stores per lane (every pixel of a tile is in range: H % 4 == 0)
   constexpr int kStores = 2 * NJ;
-  auto epilogue = [&](int t) {
+  // HOLD: the packed outputs go to held[j - J0][i] instead of memory (stored later by store_held)
+  uint2 held[NJO][2];
+  auto epilogue = [&](int t, auto J0c, auto J1c, auto HOLDc) {  // pixel groups [J0, J1); operands in pre_*[j - J0]
+    constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
+    constexpr bool HOLD = decltype(HOLDc)::value;
+    (void)held;
+    (void)pre_m; (void)pre_res; (void)pre_y1;
     lpx = lpx0;
     asm volatile("" : "+v"(lpx));
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = J0; j < J1; ++j) {
+      const int jo = j - J0;
       const int64_t ob = obase_of(t, j);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int c0 = wn * 32 + i * 16 + 4 * fq;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if constexpr (RES) {
-          const u32x2v rr = pre_res[j][i];
+          const u32x2v rr = pre_res[jo][i];
           v[0] += E::to_f((uint16_t)(rr[0] & 0xffff));
           v[1] += E::to_f((uint16_t)(rr[0] >> 16));
           v[2] += E::to_f((uint16_t)(rr[1] & 0xffff));
@@ -571,7 +582,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
         }
         float y1[4];
         if constexpr (EPI >= 2) {
-          const u32x2v q1 = pre_y1[j][i];
+          const u32x2v q1 = pre_y1[jo][i];
           y1[0] = E::to_f((uint16_t)(q1[0] & 0xffff)); y1[1] = E::to_f((uint16_t)(q1[0] >> 16));
           y1[2] = E::to_f((uint16_t)(q1[1] & 0xffff)); y1[3] = E::to_f((uint16_t)(q1[1] >> 16));
           if constexpr (EPI == 2) {
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint32_t mb = c0 < 32 ? pre_m[j][0] >> c0 : pre_m[j][1] >> (c0 - 32);
+            const uint32_t mb = c0 < 32 ? pre_m[jo][0] >> c0 : pre_m[jo][1] >> (c0 - 32);
             if (!(mb & 1u)) v[0] = 0.f;
             if (!(mb & 2u)) v[1] = 0.f;
             if (!(mb & 4u)) v[2] = 0.f;
@@ -594,7 +605,10 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
         uint2 packed;
         packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
         packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-        *(uint2*)(a.y + ob + c0) = packed;
+        if constexpr (HOLD)
+          held[jo][i] = packed;
+        else
+          *(uint2*)(a.y + ob + c0) = packed;
         if constexpr (EPI == 1) {
 #pragma unroll
           for (int r2 = 0; r2 < 4; ++r2) {
@@ -617,60 +631,101 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     }
   };
 
+  auto store_held = [&](int t, auto J0c, auto J1c) {
+    constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
+    lpx = lpx0;
+    asm volatile("" : "+v"(lpx));
+#pragma unroll
+    for (int j = J0; j < J1; ++j) {
+      const int64_t ob = obase_of(t, j);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) *(uint2*)(a.y + ob + wn * 32 + i * 16 + 4 * fq) = held[j - J0][i];
+    }
+  };
+
   // memory phase of a group: DMA of tile k_dma into its (just read) buffer first, then the epilogue of tile
   // k_epi under it, then wait for this wave's DMA only (the epilogue's stores are the kStores youngest
-  // vector-memory operations) and, PRE, transform the chunks this wave DMA'd
+  // vector-memory operations) and, PRE, transform the chunks this wave DMA'd.
+  // Epilogue operands of tile k_epi: asm buffer loads (uncounted by the compiler), waited for with counted vmcnt and
+  // pinned by "+v" operands; one 32-bit offset per pixel group (the channel block is an immediate), not 14 pointers.
+  auto load_ops = [&](int t, auto J0c, auto J1c) {
+    constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
+    (void)pre_m; (void)rmask; (void)pre_res; (void)rres; (void)pre_y1; (void)ry1;  // (generic lambda: capture them)
+    const int n = t / TH, h0 = (t - n * TH) * 4;
+    const uint32_t tb = (uint32_t)(n * a.H + h0) * (kW * 64u);  // tile's first element (< 2^31: 4 GB tensors)
+    lpx = lpx0;
+    asm volatile("" : "+v"(lpx));
+#pragma unroll
+    for (int j = J0; j < J1; ++j) {
+      const int jo = j - J0;
+      const uint32_t e = tb + (uint32_t)(lpx + (wm * NJ + j) * 1024);
+      const uint32_t yo = (e + wn * 32 + 4 * fq) * 2u;
+      if constexpr (RES) {
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_res[jo][0]) : "v"(yo), "s"(rres));
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_res[jo][1]) : "v"(yo), "s"(rres));
+      }
+      if constexpr (EPI >= 2) {
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_y1[jo][0]) : "v"(yo), "s"(ry1));
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_y1[jo][1]) : "v"(yo), "s"(ry1));
+      }
+      if constexpr (EPI == 3)
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_m[jo]) : "v"(e >> 3), "s"(rmask));
+    }
+  };
+  auto pin_ops = [&](auto NOc) {  // after the covering wait: no use of the operands may be scheduled ahead of it
+    constexpr int NO = decltype(NOc)::value;
+    (void)pre_m; (void)pre_res; (void)pre_y1;
+#pragma unroll
+    for (int jo = 0; jo < NO; ++jo) {
+      if constexpr (RES) asm volatile("" : "+v"(pre_res[jo][0]), "+v"(pre_res[jo][1]));
+      if constexpr (EPI >= 2) asm volatile("" : "+v"(pre_y1[jo][0]), "+v"(pre_y1[jo][1]));
+      if constexpr (EPI == 3) asm volatile("" : "+v"(pre_m[jo]));
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using IH = std::integral_constant<int, NJO>;
+  using IN = std::integral_constant<int, NJ>;
   auto memphase = [&](int k_epi, int k_dma) {
     constexpr bool OPS = RES || EPI >= 2;
+    const int te = first + k_epi * per_x;
     if constexpr (OPS) {
-      // epilogue operands of tile k_epi: asm buffer loads (uncounted by the compiler) ahead of the DMA, waited for
-      // with the DMA still in flight (vmcnt(11): the 11 DMA pieces are the youngest), pinned by "+v" operands
-      if (k_epi >= 0) {
-        // buffer loads: one 32-bit offset per pixel group (the channel block is an immediate), not 14 pointers
-        const int t = first + k_epi * per_x;
-        const int n = t / TH, h0 = (t - n * TH) * 4;
-        const uint32_t tb = (uint32_t)(n * a.H + h0) * (kW * 64u);  // tile's first element (< 2^31: 4 GB tensors)
-        lpx = lpx0;
-        asm volatile("" : "+v"(lpx));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const uint32_t e = tb + (uint32_t)(lpx + (wm * NJ + j) * 1024);
-          const uint32_t yo = (e + wn * 32 + 4 * fq) * 2u;
-          if constexpr (RES) {
-            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_res[j][0]) : "v"(yo), "s"(rres));
-            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_res[j][1]) : "v"(yo), "s"(rres));
-          }
-          if constexpr (EPI >= 2) {
-            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_y1[j][0]) : "v"(yo), "s"(ry1));
-            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_y1[j][1]) : "v"(yo), "s"(ry1));
-          }
-          if constexpr (EPI == 3)
-            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_m[j]) : "v"(e >> 3), "s"(rmask));
-        }
-      }
+      if (k_epi >= 0) load_ops(te, I0{}, IH{});  // ahead of the DMA: waited for with the DMA still in flight
     }
     if (k_dma >= 0) stage_tile(first + k_dma * per_x);
     if constexpr (OPS) {
       if (k_epi >= 0) {
         if (k_dma >= 0)
-          asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(11)" ::: "memory");  // the 11 DMA pieces are the youngest
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          if constexpr (RES) asm volatile("" : "+v"(pre_res[j][0]), "+v"(pre_res[j][1]));
-          if constexpr (EPI >= 2) asm volatile("" : "+v"(pre_y1[j][0]), "+v"(pre_y1[j][1]));
-          if constexpr (EPI == 3) asm volatile("" : "+v"(pre_m[j]));
-        }
+        pin_ops(IH{});
       }
     }
-    if (k_epi >= 0) epilogue(first + k_epi * per_x);
-    if (k_dma >= 0) {
-      if (k_epi >= 0)
-        __builtin_amdgcn_s_waitcnt((kStores & 0xF) | ((kStores >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (PRE) transform(first + k_dma * per_x);
+    if constexpr (NJO < NJ) {
+      // EPI 3, two halves: groups 0-3 computed into registers (held, not stored yet), the operands of groups 4-6
+      // loaded into the freed operand registers, THEN the first half's 8 stores: the second half's loads are older
+      // than those stores, so vmcnt(8) waits for the loads (and the DMA) without draining the stores
+      if (k_epi >= 0) {
+        epilogue(te, I0{}, IH{}, std::true_type{});
+        load_ops(te, IH{}, IN{});
+        __builtin_amdgcn_sched_barrier(0);
+        store_held(te, I0{}, IH{});
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        pin_ops(std::integral_constant<int, NJ - NJO>{});
+        epilogue(te, IH{}, IN{}, std::false_type{});
+      }
+      if (k_dma >= 0 && k_epi < 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (PRE never combines with EPI 3)
+    } else {
+      if (k_epi >= 0) epilogue(te, I0{}, IN{}, std::false_type{});
+      if (k_dma >= 0) {
+        if (k_epi >= 0)
+          __builtin_amdgcn_s_waitcnt((kStores & 0xF) | ((kStores >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (PRE) transform(first + k_dma * per_x);
+      }
     }
   };
   auto phase_barrier = [&]() {
@@ -790,7 +845,7 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     return !(e && e[0] == '0');
   }();
   const bool pp_on = g_conv_l1_pp >= 0 ? g_conv_l1_pp != 0 : pp_env;
-  const bool pp = pp_on && (epi == 0 || (epi == 1 && !rs && !flip) || (epi == 2 && !rs));
+  const bool pp = pp_on && (epi == 0 || (epi == 1 && !rs && !flip) || (epi == 2 && !rs) || (epi == 3 && rs));
   if (pp) PDT_COUNT("conv_l1_pp");
   Scratch part(a.stats ? (size_t)G * 128 * sizeof(float) : 0, s);
   a.srows = part.as<float>();
@@ -802,7 +857,8 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     if (epi == 0 && !rs) { if (flip) PDT_L1PP(DT_, 0, false, false, true); else PDT_L1PP(DT_, 0, false, false, false); } \
     else if (epi == 0) { if (flip) PDT_L1PP(DT_, 0, true, false, true); else PDT_L1PP(DT_, 0, true, false, false); }    \
     else if (epi == 1) { if (a.pre_coef) PDT_L1PP(DT_, 1, false, true, false); else PDT_L1PP(DT_, 1, false, false, false); } \
-    else { if (flip) PDT_L1PP(DT_, 2, false, false, true); else PDT_L1PP(DT_, 2, false, false, false); }                \
+    else if (epi == 2) { if (flip) PDT_L1PP(DT_, 2, false, false, true); else PDT_L1PP(DT_, 2, false, false, false); } \
+    else { if (flip) PDT_L1PP(DT_, 3, true, false, true); else PDT_L1PP(DT_, 3, true, false, false); }                  \
   } else if (epi == 0 && !rs) PDT_L1OLD(DT_, 0, false, false);                                            \
   else if (epi == 0 && rs) PDT_L1OLD(DT_, 0, true, false);                                               \
   else if (epi == 1 && !rs && a.pre_coef) PDT_L1OLD(DT_, 1, false, true);                                \

@@ -65,15 +65,16 @@ class NativeTrainer:
         self._comm_events = [] if time_comm else None
         # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full SyncBN path
         # with identity all-reduces), else over torch.distributed at world > 1.
-        # Native: the statistics get a communicator of their OWN (PDT_SYNCBN_COMM=own, default) and are all-reduced
+        # Native, PDT_SYNCBN_COMM=own: the statistics get a communicator of their OWN and are all-reduced
         # inline on the compute stream, forward and backward.  They are tiny and latency-bound and sit on the critical
         # path (dgrad -> BN sums -> all-reduce -> finalize -> apply -> next dgrad), so they must never queue behind a
         # 25 MiB gradient bucket on the bucket communicator's stream; RCCL orders collectives per communicator, so
         # two communicators issued in the same host order on every rank keep both sequences consistent.
-        # PDT_SYNCBN_COMM=shared: one communicator (forward inline, backward on the comm stream behind the buckets).
+        # PDT_SYNCBN_COMM=shared (the default until a >= 2-GPU run has validated two concurrent RCCL communicators,
+        # tests/test_multigpu.py): one communicator (forward inline, backward on the comm stream behind the buckets).
         nsync = sync_bn and self.ncomm is not None
         self.ncomm_bn = None
-        if nsync and os.environ.get("PDT_SYNCBN_COMM", "own") == "own":
+        if nsync and os.environ.get("PDT_SYNCBN_COMM", "shared") == "own":
             from ..parallel.comm import NativeComm
             self.ncomm_bn = NativeComm(self.device, process_group, timeout_s=comm_timeout_s, transport=comm_transport)
         sync_kw = dict(syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed and not nsync)
@@ -128,11 +129,24 @@ class NativeTrainer:
             self.flat.refresh_shadow()
 
     def close(self) -> None:
-        """Collective teardown of the native communicators (every rank, same point)."""
+        """Collective teardown of the native communicators (every rank, same point: runner._finish after its barrier,
+        bench.py after the timed steps): ncclCommDestroy, watchdog threads joined.  Idempotent."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         for c in (self.ncomm_bn, self.ncomm):
             if c is not None:
                 c.destroy()
         self.ncomm_bn = None
+        self.ncomm = None
+
+    def abort(self) -> None:
+        """Failure path (an exception left the epoch loop): abort the communicators -- pending RCCL work is cancelled
+        and the watchdog stops -- so this rank can exit instead of hanging in a collective; not collective."""
+        for c in (self.ncomm_bn, self.ncomm):
+            if c is not None:
+                c.abort()
+        self.ncomm_bn = None
+        self.ncomm = None
 
     def on_state_loaded(self) -> None:
         """After ``model.load_state_dict`` (resume): re-derive the 16-bit shadow and the kernel weight layouts."""

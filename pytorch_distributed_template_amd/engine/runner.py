@@ -251,7 +251,9 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
     from .torch_trainer import TorchTrainer
     # CPU ranks: --comm native routes buckets / buffer broadcasts / metrics through the C++ communicator and bucketer
     # over the host shared-memory transport (on GPUs the torch engine keeps c10d, whose RCCL it already set up)
-    tcomm = getattr(args, "comm", "native") if device.type == "cpu" else "torch"
+    # (single node only: the host transport is one shared-memory segment; multi-node CPU runs keep c10d / gloo)
+    from ..parallel.comm import single_node
+    tcomm = getattr(args, "comm", "native") if device.type == "cpu" and single_node(world) else "torch"
     return TorchTrainer(model, device, dtype=dtype, comm=tcomm, comm_timeout_s=float(getattr(args, "dist_timeout", 0.0)),
                         **kw, **torch_kw)
 
@@ -352,9 +354,25 @@ def main(mode: str, argv: Optional[list] = None) -> int:
         best_acc1_index = int(ck.get("best_acc1_index", 0))
         ddp_print("=> resumed from {} (epoch {})".format(args.resume, start_epoch), logger, rank)
 
+    try:
+        rc = _run_epochs(args, trainer, optimizer, lr_scheduler, train_loader, val_loader, train_sampler, val_sampler,
+                         start_epoch, best_acc1, best_acc1_index, mode, logger, writer, rank, device)
+    except BaseException:
+        # no collective teardown is possible once a rank left the epoch loop abnormally: abort the native
+        # communicators (pending RCCL work is cancelled, the watchdog stops) so this rank exits instead of hanging in
+        # a collective its peers will never join; the launcher then ends the group
+        abort = getattr(trainer, "abort", None)
+        if abort is not None:
+            abort()
+        raise
+    _finish(writer, logger, distributed, trainer)
+    return rc
+
+
+def _run_epochs(args, trainer, optimizer, lr_scheduler, train_loader, val_loader, train_sampler, val_sampler,
+                start_epoch, best_acc1, best_acc1_index, mode, logger, writer, rank, device) -> int:
     if args.evaluate:
         validate(val_loader, trainer, -1, args, logger, writer, rank, device)
-        _finish(writer, logger, distributed)
         return 0
 
     total_start = time.time()
@@ -389,14 +407,25 @@ def main(mode: str, argv: Optional[list] = None) -> int:
                             is_best, args.outpath)
     total_end = time.time()
     ddp_print("||==> total_time_cost={:.4f}s".format(total_end - total_start), logger, rank)
-    _finish(writer, logger, distributed)
     return 0
 
 
-def _finish(writer, logger, distributed: bool) -> None:
+def _finish(writer, logger, distributed: bool, trainer=None) -> None:
+    """Reference teardown (`distributed_syncBN_amp.py:236-237`: writer close) + collective teardown: every rank passes
+    the barrier, then destroys its native communicators (ncclCommDestroy, watchdog stopped) at the same point, then
+    the process group."""
     if writer is not None:
         writer.close()
     close_logger(logger)
     if distributed and dist.is_initialized():
         dist.barrier()
+    close = getattr(trainer, "close", None)
+    if close is not None:
+        close()
+        if os.environ.get("PDT_COMM_TRACE") == "1" and getattr(trainer, "ncomm", 1) is None:
+            from ..parallel.comm import live_watchdogs
+            sys.stderr.write(f"[pdt comm] rank {dist.get_rank() if dist.is_initialized() else 0}: trainer closed, "
+                             f"live watchdogs {live_watchdogs()}\n")
+            sys.stderr.flush()
+    if distributed and dist.is_initialized():
         dist.destroy_process_group()

@@ -72,6 +72,18 @@ class TorchTrainer:
     def on_state_loaded(self) -> None:
         """Parameters are views of the flat buffer, so ``load_state_dict`` already updated them."""
 
+    def close(self) -> None:
+        """Collective teardown of the native communicator (--comm native on CPU ranks); idempotent."""
+        if self.ncomm is not None:
+            self.ncomm.destroy()
+            self.ncomm = None
+
+    def abort(self) -> None:
+        """Failure path: abort the native communicator (not collective)."""
+        if self.ncomm is not None:
+            self.ncomm.abort()
+            self.ncomm = None
+
     def _autocast(self):
         if self.dtype == torch.float32:
             return contextlib.nullcontext()

@@ -143,6 +143,10 @@ class ResNetExecutor:
         # layer2 2-branch 766 -> 508 us), after which fusing at every resolution measured equal or faster than
         # the separate reduce (A/B 21.76 -> 21.71 ms/step), so it is the default everywhere.
         self.fuse_block_bn_maxhw = int(os.environ.get("PDT_FUSE_BLOCK_BN_MAXHW", "1000000"))
+        # BatchNorm finalize fused into the statistics reduction of the op producing the statistics (one launch per BN
+        # layer and direction fewer: csrc/kernels/bn.hip stat_rows_fin_kernel; PDT_FUSE_FIN=0: separate finalize).
+        # Not with SyncBN (its all-reduce sits between the reduction and the finalize).
+        self.fuse_fin = os.environ.get("PDT_FUSE_FIN", "1") == "1" and hasattr(self.C, "stat_fin_arm_fwd")
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -331,11 +335,15 @@ class ResNetExecutor:
                 self.C.wgrad_3x3c64_supported(64, 64, 3, 3, W, 1, 1))
 
     def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None,
-                 pre=None, stats_tag=None):
+                 pre=None, stats_tag=None, fin: Optional[_BN] = None):
+        """``fin``: the BatchNorm consuming y -- its training finalize runs as part of this op (fused into the
+        statistics reduction where possible, else as the separate finalize launch right after)."""
         if pre is not None:  # x is the producer conv's raw output; pre = its BN coefficients (layer1 only)
             key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
             sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
+            armed = self._arm_fwd(fin, sp, N * H * W)
             self.C.conv_fwd_pre(x, self._w(c), y, sp, pre, N, H, W)
+            self._fin_fwd(fin, sp, N * H * W, armed)
             return H, W, sp, N * H * W
         cin = cin or c.cin
         R = R or c.R
@@ -359,8 +367,36 @@ class ResNetExecutor:
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
                             -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
         bm, bn = self._tile(("fwd", N, H, W, cin, c.cout, R, S, st, stats), c.cout, bk, launch, kdim=cin * R * S)
+        armed = self._arm_fwd(fin, sp, M) if stats else False
         launch(bm, bn)
+        if stats:
+            self._fin_fwd(fin, sp, M, armed)
         return P, Q, sp, M
+
+    def _arm_fwd(self, bn: Optional[_BN], sp, count: int) -> bool:
+        if bn is None or not self.fuse_fin or self.syncbn:
+            return False
+        self.C.stat_fin_arm_fwd(sp, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
+                                bn.mod.running_mean, bn.mod.running_var, bn.coef, bn.sums, True)
+        return True
+
+    def _fin_fwd(self, bn: Optional[_BN], sp, count: int, armed: bool) -> None:
+        if bn is None:
+            return
+        if armed and self.C.stat_fin_take():
+            return
+        self.bn_train_finalize(bn, sp, 0, count)
+
+    def _arm_bwd(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None) -> bool:
+        if not self.fuse_fin or self.syncbn:
+            return False
+        self.C.stat_fin_arm_bwd(slots, 4 if bn2 is not None else 2, float(count), bn1.coef, self._p(bn1.gslot),
+                                self._g(bn1.gslot), self._g(bn1.bslot), bn1.bcoef,
+                                bn2.coef if bn2 is not None else None, self._p(bn2.gslot) if bn2 is not None else None,
+                                self._g(bn2.gslot) if bn2 is not None else None,
+                                self._g(bn2.bslot) if bn2 is not None else None,
+                                bn2.bcoef if bn2 is not None else None, 1.0)
+        return True
 
     # per-shape tile choice: the static table (ops.conv.conv_tile), or -- with autotune on, the analogue of
     # the reference's cudnn.benchmark=True (`distributed.py:104`) -- the fastest candidate timed once per shape
@@ -423,7 +459,7 @@ class ResNetExecutor:
                             bn.eps, bn.coef)
 
     def conv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, res=None, wgrad_x=None, wgrad_geom=None, bnb=None,
-                 res_phase: int = -1, compact: bool = False, pre=None):
+                 res_phase: int = -1, compact: bool = False, pre=None, fin=None):
         """Weight gradient into the flat grad buffer (+ notify), then data gradient into ``dx``.
 
         ``bnb`` = (mode, y1, coef1, y2, coef2, out_mask, slots): fuse the consuming BatchNorm's backward
@@ -462,6 +498,11 @@ class ResNetExecutor:
                                      bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
         key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
         bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
+        if fin is not None and bnb is not None:  # fin = (count, bn1, bn2): the fused reduce's BN-backward finalize
+            armed = self._arm_bwd(bnb[6], fin[0], fin[1], fin[2])
+            launch(bm, bn)
+            self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2], armed)
+            return
         launch(bm, bn)
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
@@ -498,13 +539,21 @@ class ResNetExecutor:
         blocks = self.C.bn_bwd_reduce_blocks(rows, C)
         K = 4 if bn2 is not None else 2
         slots = self._buf(("bnslots", C, K), self.n_slots * C * K, torch.float64)
+        armed = self._arm_bwd(slots, count, bn1, bn2)
         self.C.bn_bwd_reduce(g, out_mask, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows, C)
-        self._bn_bwd_finish(slots, count, bn1, bn2)
+        self._bn_bwd_finish(slots, count, bn1, bn2, armed)
 
-    def _bn_bwd_finish(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None):
-        """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients."""
+    def _bn_bwd_finish(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None, armed: bool = False):
+        """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients.  ``armed``: the producing op's
+        statistics reduction was armed to finalize itself (_arm_bwd); if it did, only the readiness is left."""
         C = bn1.C
         K = 4 if bn2 is not None else 2
+        if armed and self.C.stat_fin_take():
+            for b in (bn1, bn2):
+                if b is not None:
+                    self.grad_ready(b.gslot.index)
+                    self.grad_ready(b.bslot.index)
+            return
         if not self.syncbn:  # slot sum + finalize of both branches in one launch
             self.C.bn_bwd_finalize_slots(
                 slots, K, float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot), self._g(bn1.bslot),
@@ -557,15 +606,15 @@ class ResNetExecutor:
         y0 = self._buf("y0", N * P0 * Q0 * st.cout)
         wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * st.R * 32]
         sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64) if train else None
+        armed = self._arm_fwd(self.stem_bn, sp, N * P0 * Q0) if train else False
         if self.stem_kernel and Cn.stem_fwd_supported(Hp, Wp, P0, Q0):
             Cn.stem_fwd(xp, wst, y0, sp, N, Hp, Wp, P0, Q0, self.stem_blocks_per_cu)
         else:  # generic implicit GEMM in window mode (one 32-wide K step per kernel row)
             bm, bn = self.stem_tile
             Cn.conv_fwd(xp, wst, y0, None, sp, N, Hp, Wp, 32, st.cout, st.R, 1, P0, Q0, st.st, st.st, 0, 0, 1, 0,
                         P0, Q0, 1, 1, 0, 0, bm, bn, 32, 4)
-        tiles = N * P0 * Q0
         if train:
-            self.bn_train_finalize(self.stem_bn, sp, tiles, N * P0 * Q0)
+            self._fin_fwd(self.stem_bn, sp, N * P0 * Q0, armed)
         else:
             self.bn_eval(self.stem_bn)
         H1, W1 = (P0 - 1) // 2 + 1, (Q0 - 1) // 2 + 1
@@ -587,12 +636,11 @@ class ResNetExecutor:
                 # its all-reduce (bn_train_finalize_pair); its partial rows get their own buffer meanwhile
                 defer = train and self.syncbn and ci == nconv - 1 and b["ds_conv"] is not None
                 _, _, sp, tiles = self.conv_fwd(c, cur, N, h, w, y, train, pre=pre,
-                                                stats_tag="deferred" if defer else None)
+                                                stats_tag="deferred" if defer else None,
+                                                fin=bn if train and not defer else None)
                 if defer:
                     deferred = (bn, sp, N * P * Q)
-                elif train:
-                    self.bn_train_finalize(bn, sp, tiles, N * P * Q)
-                else:
+                elif not train:
                     self.bn_eval(bn)
                 rec["ys"].append(y)
                 rec["hw"].append((h, w, P, Q))
@@ -618,12 +666,11 @@ class ResNetExecutor:
             if b["ds_conv"] is not None:
                 dc, dbn = b["ds_conv"], b["ds_bn"]
                 yd = self._buf(("yd", bi), N * h * w * dc.cout)
-                _, _, sp, tiles = self.conv_fwd(dc, x, N, Hc, Wc, yd, train)
+                _, _, sp, tiles = self.conv_fwd(dc, x, N, Hc, Wc, yd, train,
+                                                fin=dbn if train and not self.syncbn else None)
                 if train and self.syncbn:
                     self.bn_train_finalize_pair(deferred[0], deferred[1], deferred[2], dbn, sp, N * h * w)
-                elif train:
-                    self.bn_train_finalize(dbn, sp, tiles, N * h * w)
-                else:
+                elif not train:
                     self.bn_eval(dbn)
                 Cn.bn_apply(rec["ys"][-1], bnl.coef, yd, dbn.coef, out, cl.cout, 2, True, om)
                 rec["yd"] = yd
@@ -703,8 +750,7 @@ class ResNetExecutor:
             # block-output reduction: BN of the last conv (+ downsample BN) share dz = g * relu'(out)
             ds = b["ds_conv"] is not None
             dsbn = b["ds_bn"] if ds else None
-            if g_fused is not None:  # g already holds dz; sums are in the slots
-                self._bn_bwd_finish(g_fused, cnt, bns[-1], dsbn)
+            if g_fused is not None:  # g already holds dz; its BN-backward sums were finalized with that dgrad
                 mask_src = None
             else:
                 self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["omask"], cnt, dsbn, rec["yd"] if ds else None)
@@ -760,8 +806,7 @@ class ResNetExecutor:
                     yp = rec["ys"][ci - 1]
                     slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, da, bnb=(1, yp, bnp.coef, None, None, None, slots),
-                                  pre=xpre)
-                    self._bn_bwd_finish(slots, N * h * w, bnp)
+                                  pre=xpre, fin=(N * h * w, bnp, None))
                     dname = "dy_c" if dname == "dy_a" else "dy_a"
                     dyp = self._buf(bk_(dname), yp.numel())
                     Cn.bn_bwd_apply(da, None, yp, bnp.bcoef, dyp, None, None, None, None, c.cin)
@@ -775,7 +820,9 @@ class ResNetExecutor:
                     slots = self._buf(("bnslots", c.cin, K), self.n_slots * c.cin * K, torch.float64)
                     bnb = (3 if pds else 2, prec["ys"][-1], pb["bns"][-1].coef, prec["yd"] if pds else None,
                            pb["ds_bn"].coef if pds else None, prec["omask"], slots)
-                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, bnb=bnb, res_phase=res_phase)
+                    # (that block's BN-backward finalize runs with this launch: conv_bwd fin)
+                    self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, bnb=bnb, res_phase=res_phase,
+                                  fin=(N * h * w, pb["bns"][-1], pb["ds_bn"] if pds else None))
                     g_fused = slots
                 else:
                     self.conv_bwd(c, xin, N, h, w, dy, P, Q, gnext, res=res, res_phase=res_phase)
@@ -788,8 +835,9 @@ class ResNetExecutor:
         P0, Q0 = saved["P0"], saved["Q0"]
         slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
         # BN-backward sums from the pooled output alone (ReLU mask = out > 0, BN input recovered from out)
+        armed = self._arm_bwd(slots, N * P0 * Q0, sbn)
         Cn.stem_pool_bwd_reduce_out(g, saved["x0"], sbn.coef, slots, N, P0, Q0, st.cout)
-        self._bn_bwd_finish(slots, N * P0 * Q0, sbn)
+        self._bn_bwd_finish(slots, N * P0 * Q0, sbn, None, armed)
         ldw = self.stem_pairs * 64
         if self._stem_fused_ok(Q0):
             # the stem weight gradient computes its dY tiles itself (max-pool backward + ReLU + BN-backward

@@ -45,7 +45,9 @@ class FlatParams:
     """Flattened trainable parameters of ``model`` (in ``model.named_parameters()`` order)."""
 
     def __init__(self, model: nn.Module, device: torch.device, shadow_dtype: Optional[torch.dtype] = None,
-                 align: int = 64):
+                 align: int = 64, guards: bool = True):
+        """``guards=False``: no validation canaries in the gradient gaps (DataParallel replicas, whose whole gradient
+        buffers are reduce-added into GPU 0's: the canaries would be summed into its guard bands)."""
         self.device = torch.device(device)
         self.slots: List[ParamSlot] = []
         self.params: List[nn.Parameter] = []
@@ -78,7 +80,7 @@ class FlatParams:
         # parameters that receive weight decay: all of them, like the reference (SURVEY §2.2 --wd)
         self.refresh_shadow()
         # (single process only: a multi-rank run all-reduces whole bucket ranges, canaries included)
-        if guard and self.device.type == "cuda" and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        if guards and guard and self.device.type == "cuda" and int(os.environ.get("WORLD_SIZE", "1")) == 1:
             self._install_guards(validate)
 
     def _install_guards(self, validate) -> None:

@@ -35,6 +35,11 @@ def _gpus_shared(world: int) -> bool:
     return torch.cuda.is_available() and local > torch.cuda.device_count()
 
 
+def single_node(world: int) -> bool:
+    """Every rank on this node (the host shared-memory transport maps ONE segment: it cannot span nodes)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", world)) >= world
+
+
 class NativeComm:
     """A process-group-like wrapper over :class:`_C.Communicator`."""
 
@@ -67,6 +72,11 @@ class NativeComm:
             transport = "host" if self.device.type != "cuda" or _gpus_shared(self.world) else "rccl"
         if transport not in ("rccl", "host"):
             raise ValueError(f"comm transport must be auto, rccl or host, got {transport!r}")
+        if transport == "host" and self.world > 1 and not single_node(self.world):
+            # fail fast: the other nodes would retry shm_open on a segment that exists only on node 0 until the timeout
+            raise ValueError(f"the host shared-memory comm transport needs every rank on one node (WORLD_SIZE="
+                             f"{self.world}, LOCAL_WORLD_SIZE={os.environ.get('LOCAL_WORLD_SIZE')}); use --comm torch "
+                             "(c10d / gloo) or one rank per GPU (rccl) across nodes")
         if transport == "rccl" and self.device.type != "cuda":
             raise ValueError("the rccl transport needs GPU tensors; use transport='host' on the CPU")
         self.transport = transport
@@ -136,10 +146,25 @@ class NativeComm:
 
     def abort(self) -> None:
         self.comm.abort()
+        _trace(f"rank {self.rank}/{self.world}: {self.transport} communicator aborted")
 
     def destroy(self) -> None:
         """Collective teardown (every rank, same point): stop the watchdog, ncclCommDestroy."""
         self.comm.destroy()
+        _trace(f"rank {self.rank}/{self.world}: {self.transport} communicator destroyed")
+
+
+def live_watchdogs() -> int:
+    """Native communicator watchdog threads still running in this process (0 after a clean teardown)."""
+    return int(native.C.Communicator.live_watchdogs())
+
+
+def _trace(msg: str) -> None:
+    """PDT_COMM_TRACE=1: communicator lifecycle events on stderr (teardown tests)."""
+    if os.environ.get("PDT_COMM_TRACE") == "1":
+        import sys
+        sys.stderr.write(f"[pdt comm] {msg}\n")
+        sys.stderr.flush()
 
 
 class NativeBucketer:

@@ -85,7 +85,7 @@ class NativeDataParallelTrainer:
         self.executors = []
         for m, d in zip(replicas, self.devices):
             with torch.cuda.device(d):
-                f = FlatParams(m, d, dtype if dtype != torch.float32 else None)
+                f = FlatParams(m, d, dtype if dtype != torch.float32 else None, guards=len(self.devices) == 1)
                 b = FlatBuffers(m, d)
                 self.flats.append(f)
                 self.buffers.append(b)

@@ -32,7 +32,7 @@ def main():
     sync_bn = os.environ.get("PDT_TEST_SYNCBN", "0") == "1"
     # ranks start from different weights: the constructor broadcast must equalise them
     model = make_model(seed=0 if rank == 0 else rank + 100)
-    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}[os.environ.get("PDT_TEST_DTYPE", "bf16")]
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[os.environ.get("PDT_TEST_DTYPE", "bf16")]
     tr = NativeTrainer(model, dev, dtype=dtype, sync_bn=sync_bn, bucket_cap_mb=4, comm=comm,
                        comm_timeout_s=300.0)
     local = None

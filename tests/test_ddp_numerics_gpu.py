@@ -47,10 +47,10 @@ def _run_ranks(tmp_path, nproc=2, **env):
     return torch.load(out, weights_only=True)
 
 
-def _single(steps_fn):
+def _single(steps_fn, dtype=torch.bfloat16):
     from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
     model = make_model(seed=0)
-    tr = NativeTrainer(model, "cuda:0", dtype=torch.bfloat16)
+    tr = NativeTrainer(model, "cuda:0", dtype=dtype)
     before = tr.flat.data.clone()
     steps_fn(tr)
     torch.cuda.synchronize()
@@ -122,13 +122,53 @@ def _update_errors(tr, before, a, b):
     return out
 
 
-@pytest.mark.parametrize("steps,comm", [(1, "torch"), (2, "torch"), (2, "native")])
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_native_syncbn_fp32_equals_full_batch(tmp_path, nproc):
+    """SyncBN correctness without 16-bit chaos: in fp32 (the reference's `distributed.py` precision, exact-fp32
+    MFMA kernels) SyncBN DDP over ``nproc`` ranks x B (the native communicator: ranks share cuda:0, host transport)
+    must equal ONE process running the full batch nproc x B with plain BN after one step -- every parameter's
+    update within 1e-4 relative, running mean / var within 1e-5, num_batches_tracked exact.  A count, eps,
+    variance-bias or gradient-scale error in the native SyncBN path is orders of magnitude larger
+    (`distributed_syncBN_amp.py:142-147`; upstream semantics SURVEY §3.5)."""
+    res = _run_ranks(tmp_path, nproc=nproc, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=1, PDT_TEST_COMM="native",
+                     PDT_TEST_DTYPE="fp32")
+    assert res["transport"] == "host"
+    check_syncbn_fp32_full_batch(res, nproc)
+
+
+def check_syncbn_fp32_full_batch(res, nproc):
+    """The fp32 SyncBN contract (see test_native_syncbn_fp32_equals_full_batch) for rank 0's saved state ``res``
+    after one step at world ``nproc``; also used by the >= 2-GPU tests (tests/test_multigpu.py)."""
+    X, T = make_batch(nproc * B, HW)
+    x, t = X.cuda(), T.cuda()
+    box = {}
+
+    def run(tr):
+        _, m = tr.train_step(x, t)
+        box["met"] = m.clone()
+
+    tr, before = _single(run, dtype=torch.float32)
+    before, full = before.cpu(), tr.flat.data.cpu()
+    e = _update_errors(tr, before, res["data"], full)
+    bad = [(k, v) for k, v in e.items() if v > 1e-4]
+    assert not bad, sorted(bad, key=lambda kv: -kv[1])[:8]
+    fb = tr.buffers.fdata.cpu()
+    rs_err = ((res["fbuf"] - fb).abs() / fb.abs().clamp_min(1e-6)).max().item()
+    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-5 and rs_err < 1e-4, rs_err
+    assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
+    assert torch.allclose(res["met"][0], box["met"].cpu(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("steps,comm", [(1, "torch"), (1, "native"), (2, "torch"), (2, "native")])
 def test_native_syncbn_equals_full_batch(tmp_path, steps, comm):
     """A random-init ResNet's gradient is chaotic in 16-bit arithmetic: nudging the INPUT by one part in 1e6
     already moves the parameter updates by 10-60 % (the "floor", measured here).  SyncBN(2 x B/2) must
     agree with the full batch within that floor, and far better than plain DDP(2 x B/2), whose per-rank
     BN statistics genuinely differ; a scale error on any tensor (e.g. gamma/beta gradients world x) is
-    >= 100 % and fails.  Running statistics, num_batches_tracked and the loss must match closely."""
+    >= 100 % and fails.  Running statistics, num_batches_tracked and the loss must match closely.
+    One step: the original strict bounds (better than DDP everywhere, fc within 2e-2 / 1e-3, running statistics
+    within 1e-3); two steps: bounds relative to the measured floor (the second step sees the chaotic first update).
+    The chaos-free check of the same path is test_native_syncbn_fp32_equals_full_batch."""
     res = _run_ranks(tmp_path, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=steps, PDT_TEST_COMM=comm)
     nosync = _run_ranks(tmp_path, PDT_TEST_SYNCBN=0, PDT_TEST_STEPS=steps, PDT_TEST_COMM=comm)["data"]
     X, T = make_batch(2 * B, HW)
@@ -149,18 +189,23 @@ def test_native_syncbn_equals_full_batch(tmp_path, steps, comm):
     e_floor = _update_errors(tr, before, floor_tr.flat.data.cpu(), full)
     # "better than plain DDP" is only testable where the input-noise floor is well below the DDP error: a parameter
     # whose floor is itself ~ the DDP error (e.g. 0.54 vs 0.58) is noise-dominated, and only the floor bound applies
+    strict = steps == 1
     bad = [(k, round(e_sync[k], 4), round(e_floor[k], 4), round(e_nosync[k], 4)) for k in e_sync
            if e_sync[k] > max(1.5 * e_floor[k], 0.02) or
-           (e_nosync[k] > 0.05 and e_floor[k] < 0.5 * e_nosync[k] and e_sync[k] > 0.75 * e_nosync[k])]
+           (e_nosync[k] > 0.05 and (strict or e_floor[k] < 0.5 * e_nosync[k]) and e_sync[k] > 0.75 * e_nosync[k])]
     assert not bad, bad[:8]
-    # the fc layer sees the chaos only through its input features: a tight bound, widened by its own measured floor
-    assert e_sync["fc.weight"] < max(0.02, 2 * e_floor["fc.weight"]), (e_sync["fc.weight"], e_floor["fc.weight"])
-    assert e_sync["fc.bias"] < max(1e-3, 2 * e_floor["fc.bias"]), (e_sync["fc.bias"], e_floor["fc.bias"])
     fb = tr.buffers.fdata.cpu()
-    # running mean / var (unbiased, global count): after step 1 they see the chaotic update, so bound by the floor too
-    fb_floor = ((floor_tr.buffers.fdata.cpu() - fb).norm() / fb.norm()).item()
     fb_err = ((res["fbuf"] - fb).norm() / fb.norm()).item()
-    assert fb_err < max(1e-3, 2 * fb_floor), (fb_err, fb_floor)
+    if strict:
+        assert e_sync["fc.weight"] < 0.02 and e_sync["fc.bias"] < 1e-3, (e_sync["fc.weight"], e_sync["fc.bias"])
+        assert fb_err < 1e-3, fb_err  # running mean / var (unbiased, global count)
+    else:
+        # the fc layer sees the chaos only through its input features: its own measured floor widens the bound
+        assert e_sync["fc.weight"] < max(0.02, 2 * e_floor["fc.weight"]), (e_sync["fc.weight"], e_floor["fc.weight"])
+        assert e_sync["fc.bias"] < max(1e-3, 2 * e_floor["fc.bias"]), (e_sync["fc.bias"], e_floor["fc.bias"])
+        # running statistics after step 1 see the chaotic update: bounded by the floor too
+        fb_floor = ((floor_tr.buffers.fdata.cpu() - fb).norm() / fb.norm()).item()
+        assert fb_err < max(1e-3, 2 * fb_floor), (fb_err, fb_floor)
     assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
     assert torch.allclose(res["met"], torch.stack(mets).cpu(), rtol=2e-3, atol=2e-3)
 

@@ -172,3 +172,42 @@ def test_fault_injection_tears_down_group(tmp_path, mode, port):
     assert f"[fault injection] rank 1: {mode} at epoch 0 iteration 1" in log
     assert "terminating the group" in log, log[-3000:]
     assert time.time() - t0 < 240
+
+
+def test_entry_script_tears_down_native_comm(tmp_path):
+    """Communicator lifecycle on the entry-script path (reference teardown `distributed_syncBN_amp.py:236-237`):
+    distributed.py at world 2 on the CPU runs its gradient buckets / buffer broadcasts / metrics through the native
+    C++ communicator (host shared-memory transport, --comm native); at the end every rank passes the barrier, then
+    destroys its communicator collectively (runner._finish -> trainer.close()), with no watchdog thread left, and
+    the job exits 0."""
+    out = str(tmp_path / "output_teardown")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="1", PDT_COMM_TRACE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc_per_node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29631", "distributed.py", "--outpath", out, "-b", "8", "--comm", "native",
+           "--dist-timeout", "120"] + COMMON
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = r.stdout + r.stderr
+    assert r.returncode == 0, log[-3000:]
+    for rk in (0, 1):
+        assert f"[pdt comm] rank {rk}/2: host communicator destroyed" in log, log[-3000:]
+        assert f"[pdt comm] rank {rk}: trainer closed, live watchdogs 0" in log, log[-3000:]
+    assert "communicator aborted" not in log
+
+
+def test_entry_script_aborts_native_comm_on_failure(tmp_path):
+    """Failure path: rank 1 stops making progress (PDT_FAULT_INJECT hang); rank 0's next native collective times
+    out (--dist-timeout), the exception leaves the epoch loop and runner aborts rank 0's communicator (not a
+    collective teardown) before the job ends non-zero -- without hanging."""
+    import time
+    out = str(tmp_path / "output_abort")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="1", PDT_COMM_TRACE="1", PDT_FAULT_INJECT="1:1:hang")
+    cmd = [sys.executable, "-m", "pytorch_distributed_template_amd.launch", "--nproc_per_node=2",
+           "--master_addr=127.0.0.1", "--master_port=29632", "--grace_s=2", "distributed.py", "--outpath", out,
+           "-b", "8", "--comm", "native", "--dist-timeout", "15"] + COMMON
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    log = r.stdout + r.stderr
+    assert r.returncode != 0, log[-3000:]
+    assert "[fault injection] rank 1: hang at epoch 0 iteration 1" in log
+    assert "[pdt comm] rank 0/2: host communicator aborted" in log, log[-3000:]
+    assert time.time() - t0 < 240

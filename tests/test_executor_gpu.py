@@ -151,21 +151,26 @@ def test_train_step_matches_reference_224(arch, N):
     assert not bad, bad[:5]
 
 
-def _grads_after_step(side: bool, delay_side: int = 0, delay_main: int = 0, arch="resnet18", N=16, steps=1):
+def _grads_after_step(side: bool, delay_side: int = 0, delay_main: int = 0, arch="resnet18", N=16, steps=1,
+                      env=None, dtype=torch.bfloat16):
     """Run ``steps`` train steps (+ SGD + derived-layout refresh) and return (grad, data, buffers) copies.
     ``delay_side`` / ``delay_main`` spin-kernel cycles are injected ahead of every side-stream weight
-    gradient / after it on the compute stream, to shake out missing cross-stream dependencies."""
+    gradient / after it on the compute stream, to shake out missing cross-stream dependencies.  ``env``: extra
+    PDT_* settings read when the executor is built."""
     import os
     from pytorch_distributed_template_amd.optim.sgd import FusedSGD
-    old = os.environ.get("PDT_WGRAD_STREAM")
-    os.environ["PDT_WGRAD_STREAM"] = "1" if side else "0"
+    env = dict(env or {})
+    env["PDT_WGRAD_STREAM"] = "1" if side else "0"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        model, ref, flat, ex, x, t = _setup(arch, N=N, HW=224, dtype=torch.bfloat16)
+        model, ref, flat, ex, x, t = _setup(arch, N=N, HW=224, dtype=dtype)
     finally:
-        if old is None:
-            os.environ.pop("PDT_WGRAD_STREAM")
-        else:
-            os.environ["PDT_WGRAD_STREAM"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     del ref
     if delay_side or delay_main:
         orig = ex._side_wgrad
@@ -200,6 +205,27 @@ def test_side_stream_bitwise_equals_single_stream(delay_side, delay_main):
     g1, d1, b1, _ = _grads_after_step(True, delay_side, delay_main, steps=2)
     bad = [(s.name, int((g0[s.offset:s.offset + s.numel] != g1[s.offset:s.offset + s.numel]).sum()))
            for s in slots if not torch.equal(g0[s.offset:s.offset + s.numel], g1[s.offset:s.offset + s.numel])]
+    assert not bad, bad[:10]
+    assert torch.equal(d0, d1)
+    assert torch.equal(b0, b1)
+
+
+@pytest.mark.parametrize("arch,dtype", [("resnet18", torch.bfloat16), ("resnet50", torch.float16)])
+def test_fused_bn_finalize_bitwise(arch, dtype):
+    """The BatchNorm finalize fused into the statistics reduction (the last block of the reduction finalizes,
+    csrc/kernels/bn.hip stat_rows_fin_kernel) must give BIT-identical gradients, weights and running statistics to
+    the separate finalize launches (PDT_FUSE_FIN=0), over two steps, and must actually run for every BN layer."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    g0, d0, b0, slots = _grads_after_step(True, arch=arch, N=8, steps=2, env={"PDT_FUSE_FIN": "0"}, dtype=dtype)
+    C.reset_dispatch_counts()
+    g1, d1, b1, _ = _grads_after_step(True, arch=arch, N=8, steps=2, env={"PDT_FUSE_FIN": "1"}, dtype=dtype)
+    n_bn = sum(1 for s in slots if s.name.endswith(".weight") and ("bn" in s.name or "downsample.1" in s.name))
+    n_ds = sum(1 for s in slots if s.name.endswith("downsample.1.weight"))
+    fused = dict(C.dispatch_counts()).get("stat_rows_fused_finalize", 0)
+    # per step: every BN forward; backward every BN, a downsample block's two output BNs sharing one finalize
+    assert fused == 2 * (2 * n_bn - n_ds), (fused, n_bn, n_ds)
+    bad = [s.name for s in slots if not torch.equal(g0[s.offset:s.offset + s.numel], g1[s.offset:s.offset + s.numel])]
     assert not bad, bad[:10]
     assert torch.equal(d0, d1)
     assert torch.equal(b0, b1)

@@ -662,7 +662,7 @@ def test_fused_producer_bn_relu_layer1(dtype):
 
 
 @pytest.mark.parametrize("N,H", [(3, 12), (5, 56), (1, 4)])
-@pytest.mark.parametrize("variant", ["fwd", "fwd_stats", "fwd_pre", "dgrad_res", "dgrad_bn"])
+@pytest.mark.parametrize("variant", ["fwd", "fwd_stats", "fwd_pre", "dgrad_res", "dgrad_bn", "dgrad_bn_out"])
 def test_conv_l1_pingpong_matches_4wave(variant, N, H):
     """The 8-wave ping-pong layer1 kernel (two wave groups on alternate tiles, column-swizzled halo, counted
     waits) must write BIT-IDENTICAL outputs to the 4-wave kernel (same MFMA order per accumulator) and the same
@@ -678,6 +678,7 @@ def test_conv_l1_pingpong_matches_4wave(variant, N, H):
     res = _rand16(N, H, W, 64)
     y1 = _rand16(N, H, W, 64)
     from pytorch_distributed_template_amd.ops import conv
+    omask = conv.pack_relu_mask(_rand16(N, H, W, 64))
 
     def run(pp):
         old = C.conv_l1_set_pp(pp)
@@ -695,6 +696,9 @@ def test_conv_l1_pingpong_matches_4wave(variant, N, H):
                 C.conv_fwd_pre(x, w, y, st, coef, N, H, W)
             elif variant == "dgrad_res":
                 y = conv.conv_dgrad(x, w, H, W, 1, 1, residual=res)
+            elif variant == "dgrad_bn_out":
+                # block-output BN-backward reduce (residual + ReLU bitmask + BN input): EPI 3, epilogue in two halves
+                y = conv.conv_dgrad(x, w, H, W, 1, 1, residual=res, bnb=(2, y1, coef, None, None, omask, st))
             else:
                 y = conv.conv_dgrad(x, w, H, W, 1, 1, bnb=(1, y1, coef, None, None, None, st))
             torch.cuda.synchronize()
