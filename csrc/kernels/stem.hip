@@ -114,17 +114,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int g = 0; g < kGroups; ++g) acc[i][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     const char* sb = smem + buf * kStage + 2 * wave * row_bytes + (fr + fq) * 16;
+    // kernel row r+1's fragments are read while row r's 28 MFMAs run (explicit register double buffer pinned by
+    // scheduling barriers: read right before their MFMAs, each row's 11 LDS reads were exposed -- PMC: 63 % of the
+    // wave cycles issue-stalled, 28 % MFMA busy)
+    vec8 af[2][4], bf[2][kGroups];
+    auto load = [&](int r, int sl) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[sl][i] = *(const vec8*)(wl + (i * 16 + fr) * kWPitch + (r * 4 + fq) * 16);
+#pragma unroll
+      for (int g = 0; g < kGroups; ++g) bf[sl][g] = *(const vec8*)(sb + r * row_bytes + g * 256);
+    };
+    load(0, 0);
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-      vec8 af[4], bf[kGroups];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *(const vec8*)(wl + (i * 16 + fr) * kWPitch + (r * 4 + fq) * 16);
-#pragma unroll
-      for (int g = 0; g < kGroups; ++g) bf[g] = *(const vec8*)(sb + r * row_bytes + g * 256);
+      if (r + 1 < kRows) load(r + 1, (r + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int g = 0; g < kGroups; ++g) acc[i][g] = E::mfma16x16x32(af[i], bf[g], acc[i][g]);
+        for (int g = 0; g < kGroups; ++g) acc[i][g] = E::mfma16x16x32(af[r & 1][i], bf[r & 1][g], acc[i][g]);
+      __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- epilogue: lane holds couts i*16 + 4*fq + r of pixel (oh, g*16 + fr) ----
