@@ -483,44 +483,6 @@ void bn_bwd_finalize_slots(const Tensor& slots, int64_t K, double count, const T
                                     cur_stream());
 }
 
-// Fused finalize (csrc/kernels/conv_fwd.h StatFin): arm on this host thread right before the op producing the
-// statistics into `slots`; its reduction launch then finalizes too.  stat_fin_take() reports whether it did (and
-// disarms): if not, launch bn_finalize_slots / bn_bwd_finalize_slots as before.
-void stat_fin_arm_fwd(const Tensor& slots, double count, const Tensor& gamma, const Tensor& beta, double eps,
-                      double momentum, Tensor& rm, Tensor& rv, Tensor& coef, Tensor& sums, bool update_running) {
-  const int64_t C = gamma.numel();
-  TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * 2 && coef.numel() >= 4 * C && sums.numel() >= 2 * C &&
-                  beta.numel() == C && rm.numel() == C && rv.numel() == C,
-              "stat_fin_arm_fwd: bad sizes");
-  pdt::StatFin f;
-  f.kind = 1; f.K = 2; f.C = (int)C; f.slots = pd(slots, "slots"); f.count = count;
-  f.gamma = pf(gamma, "gamma"); f.beta = pf(beta, "beta"); f.eps = (float)eps; f.momentum = (float)momentum;
-  f.rm = pf(rm, "running_mean"); f.rv = pf(rv, "running_var"); f.coef = pf(coef, "coef"); f.sums = pd(sums, "sums");
-  f.update_running = update_running ? 1 : 0;
-  pdt::stat_fin_arm(f);
-}
-
-void stat_fin_arm_bwd(const Tensor& slots, int64_t K, double count, const Tensor& coef1, const Tensor& gamma1,
-                      const OptT& dgamma1, const OptT& dbeta1, Tensor& bcoef1, const OptT& coef2, const OptT& gamma2,
-                      const OptT& dgamma2, const OptT& dbeta2, const OptT& bcoef2, double gscale) {
-  const int64_t C = gamma1.numel();
-  TORCH_CHECK((K == 2 || K == 4) && slots.numel() >= pdt::kStatSlots * C * K && bcoef1.numel() >= 3 * C &&
-                  coef1.numel() >= 4 * C,
-              "stat_fin_arm_bwd: bad sizes");
-  TORCH_CHECK(K == 2 || (coef2.has_value() && gamma2.has_value() && bcoef2.has_value() && bcoef2->numel() >= 3 * C &&
-                         coef2->numel() >= 4 * C && gamma2->numel() == C),
-              "stat_fin_arm_bwd: K == 4 needs the second branch");
-  pdt::StatFin f;
-  f.kind = 2; f.K = (int)K; f.C = (int)C; f.slots = pd(slots, "slots"); f.count = count;
-  f.coef1 = pf(coef1, "coef1"); f.gamma1 = pf(gamma1, "gamma1"); f.dgamma1 = pfo(dgamma1, "dgamma1");
-  f.dbeta1 = pfo(dbeta1, "dbeta1"); f.bcoef1 = pf(bcoef1, "bcoef1"); f.coef2 = pfo(coef2, "coef2");
-  f.gamma2 = pfo(gamma2, "gamma2"); f.dgamma2 = pfo(dgamma2, "dgamma2"); f.dbeta2 = pfo(dbeta2, "dbeta2");
-  f.bcoef2 = pfo(bcoef2, "bcoef2"); f.gscale = (float)gscale;
-  pdt::stat_fin_arm(f);
-}
-
-bool stat_fin_take() { return pdt::stat_fin_take(); }
-
 void bn_finalize(const Tensor& sums, double count, const Tensor& gamma, const Tensor& beta, double eps, double momentum,
                  Tensor& rm, Tensor& rv, Tensor& coef, bool update_running) {
   const int64_t C = gamma.numel();
@@ -1072,9 +1034,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "restaging kernel; returns the previous setting");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_finalize_slots", &bn_finalize_slots);
-  m.def("stat_fin_arm_fwd", &stat_fin_arm_fwd);
-  m.def("stat_fin_arm_bwd", &stat_fin_arm_bwd);
-  m.def("stat_fin_take", &stat_fin_take);
   m.def("bn_bwd_finalize_slots", &bn_bwd_finalize_slots);
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_apply", &bn_apply);

@@ -8,9 +8,7 @@
 //                    branches that share dz, e.g. the main and downsample branch of a residual block)
 //                    -> bn_slot_sum -> bn_bwd_finalize (dgamma/dbeta into the grad buffer,
 //                    per-channel coefficients) -> bn_bwd_apply (dy = a*dz + b*y + c per branch).
-#include <atomic>
 #include <cstdlib>
-#include <mutex>
 #include "../common.h"
 #include "bn.h"
 #include "conv_fwd.h"
@@ -50,6 +48,9 @@ __global__ __launch_bounds__(256) void stat_rows_reduce_kernel(const float* __re
     slots[(int64_t)s * CK + col] = ((a + part[0][threadIdx.x]) + part[1][threadIdx.x]) + part[2][threadIdx.x];
 }
 
+void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s) {
+  hipLaunchKernelGGL(stat_rows_reduce_kernel, dim3((CK + 63) / 64, kStatSlots), dim3(256), 0, s, rows, R, CK, slots);
+}
 
 // slots [kStatSlots][C][K] double (the fixed-order row sums of stat_rows_reduce)
 //   -> sums[k*C + c] double  (channel-major per quantity: the SyncBN all-reduce message)
@@ -419,160 +420,6 @@ __device__ inline void bn_bwd_coef(double sdz, double sdzx, double count, float 
   bcoef[c] = A;
   bcoef[C + c] = -A * invstd * mdzx;
   bcoef[2 * C + c] = -A * mdz + A * invstd * mdzx * mean;
-}
-
-// ---- fused finalize: the statistics reduction and the BatchNorm finalize in ONE launch --------------------------
-// The last block (of the kStatSlots slot blocks) to finish a 64-column chunk sums that chunk's slots and finalizes
-// its channels -- bit-identical to stat_rows_reduce + bn_finalize_slots / bn_bwd_finalize_slots (same fixed
-// summation order, same arithmetic), one dependent launch (~4-5 us of a kernel boundary) fewer per BatchNorm.
-// Hand-off without fences (MI355X_MICROARCH, inter-workgroup visibility, "Valid forms"): every block writes its slot
-// values write-through (agent-scope relaxed atomic stores = `sc1` stores), waits vmcnt(0), passes a workgroup
-// barrier, then one lane adds to the chunk's counter (agent scope); the block whose add returns kStatSlots - 1 reads
-// all slots of the chunk with `sc1` loads (L2-served, never a stale L1 line) and resets the counter.  (A release /
-// acquire fence pair instead costs ~2 us per block: measured 12-22 us per launch vs ~5 + 5 us for two launches.)
-static thread_local StatFin g_fin;
-static thread_local bool g_fin_armed = false, g_fin_taken = false;
-
-void stat_fin_arm(const StatFin& f) {
-  g_fin = f;
-  g_fin_armed = true;
-  g_fin_taken = false;
-}
-
-bool stat_fin_take() {
-  const bool t = g_fin_taken;
-  g_fin_armed = false;
-  g_fin_taken = false;
-  return t;
-}
-
-// per-device counter rings: a launch takes the next 256-counter region (zero on entry, zero again on exit)
-static unsigned* fin_counters(int* ring) {
-  constexpr int kRings = 64, kPer = 256;
-  static unsigned* bufs[64] = {};
-  static std::atomic<unsigned> next{0};
-  int dev = 0;
-  PDT_HIP_CHECK(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) pdt_hip_fail("stat_fin: device index", hipErrorInvalidValue, __FILE__, __LINE__);
-  static std::mutex mu;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (!bufs[dev]) {
-      PDT_HIP_CHECK(hipMalloc(&bufs[dev], sizeof(unsigned) * kRings * kPer));
-      PDT_HIP_CHECK(hipMemset(bufs[dev], 0, sizeof(unsigned) * kRings * kPer));
-      PDT_HIP_CHECK(hipDeviceSynchronize());
-    }
-  }
-  *ring = (int)(next.fetch_add(1) % kRings);
-  return bufs[dev] + (size_t)*ring * kPer;
-}
-
-template <int KIND, int K>  // KIND 1: forward BN finalize (K = 2); 2: BN-backward finalize (K = 2 or 4)
-__global__ __launch_bounds__(256) void stat_rows_fin_kernel(const float* __restrict__ rows, int R, int CK,
-                                                            double* __restrict__ slots, StatFin f,
-                                                            unsigned* __restrict__ counter) {
-  __shared__ double part[3][64];
-  __shared__ double tot[64];
-  __shared__ int last;
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63), lane4 = threadIdx.x >> 6;
-  {  // this block's slot: exactly stat_rows_reduce_kernel
-    const int s = blockIdx.y;
-    const int lo = (int)((int64_t)s * R / kStatSlots), hi = (int)((int64_t)(s + 1) * R / kStatSlots);
-    double a = 0.0;
-    if (col < CK) {
-      const float* p = rows + col;
-      int r = lo + lane4;
-      double b = 0.0, c = 0.0, d = 0.0;
-      for (; r + 12 < hi; r += 16) {
-        a += (double)p[(int64_t)r * CK];
-        b += (double)p[(int64_t)(r + 4) * CK];
-        c += (double)p[(int64_t)(r + 8) * CK];
-        d += (double)p[(int64_t)(r + 12) * CK];
-      }
-      for (; r < hi; r += 4) a += (double)p[(int64_t)r * CK];
-      a = (a + b) + (c + d);
-    }
-    if (lane4 > 0) part[lane4 - 1][threadIdx.x & 63] = a;
-    __syncthreads();
-    if (lane4 == 0 && col < CK) {
-      const double v = ((a + part[0][threadIdx.x]) + part[1][threadIdx.x]) + part[2][threadIdx.x];
-      __hip_atomic_store((unsigned long long*)(slots + (int64_t)s * CK + col), __builtin_bit_cast(unsigned long long, v),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(counter + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned)(kStatSlots - 1);
-    if (last) __hip_atomic_exchange(counter + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last) return;
-  // slot totals of the chunk's 64 columns in slot_sum_block's order: quarter q sums slots q*16 .. q*16+15, then
-  // ((q0 + q1) + q2) + q3
-  double sq = 0.0;
-  if (col < CK) {
-#pragma unroll
-    for (int g = 0; g < 16; ++g)
-      sq += __builtin_bit_cast(double, __hip_atomic_load((unsigned long long*)(slots + (int64_t)(lane4 * 16 + g) * CK + col),
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  }
-  __syncthreads();  // (part is reused)
-  if (lane4 > 0) part[lane4 - 1][threadIdx.x & 63] = sq;
-  __syncthreads();
-  if (lane4 == 0) tot[threadIdx.x] = ((sq + part[0][threadIdx.x]) + part[1][threadIdx.x]) + part[2][threadIdx.x];
-  __syncthreads();
-  const int C = CK / K;
-  const int c = blockIdx.x * (64 / K) + (int)threadIdx.x;
-  if ((int)threadIdx.x >= 64 / K || c >= C) return;
-  const double* sv = tot + threadIdx.x * K;
-  if constexpr (KIND == 1) {
-    const double s0 = sv[0], s1 = sv[1], count = f.count;
-    f.sums[c] = s0;
-    f.sums[C + c] = s1;
-    const double mean = s0 / count;
-    double var = s1 / count - mean * mean;
-    if (var < 0) var = 0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-    const float sc = f.gamma[c] * invstd;
-    f.coef[c] = sc;
-    f.coef[C + c] = f.beta[c] - (float)mean * sc;
-    f.coef[2 * C + c] = (float)mean;
-    f.coef[3 * C + c] = invstd;
-    if (f.update_running) {
-      const double unbiased = count > 1 ? var * count / (count - 1) : var;
-      f.rm[c] = (1.f - f.momentum) * f.rm[c] + f.momentum * (float)mean;
-      f.rv[c] = (1.f - f.momentum) * f.rv[c] + f.momentum * (float)unbiased;
-    }
-  } else {
-    bn_bwd_coef(sv[0], sv[1], f.count, f.coef1[2 * C + c], f.coef1[3 * C + c], f.gamma1[c], f.dgamma1, f.dbeta1,
-                f.gscale, f.bcoef1, C, c);
-    if constexpr (K == 4)
-      bn_bwd_coef(sv[2], sv[3], f.count, f.coef2[2 * C + c], f.coef2[3 * C + c], f.gamma2[c], f.dgamma2, f.dbeta2,
-                  f.gscale, f.bcoef2, C, c);
-  }
-}
-
-void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s) {
-  if (g_fin_armed && g_fin.slots == slots && CK == g_fin.C * g_fin.K && !g_fin_taken) {
-    int ring = 0;
-    unsigned* ctr = fin_counters(&ring);
-    const dim3 grid((CK + 63) / 64, kStatSlots);
-    if (grid.x > 256) pdt_hip_fail("stat_fin: too many column chunks", hipErrorInvalidValue, __FILE__, __LINE__);
-    if (g_fin.kind == 1 && g_fin.K == 2)
-      hipLaunchKernelGGL((stat_rows_fin_kernel<1, 2>), grid, dim3(256), 0, s, rows, R, CK, slots, g_fin, ctr);
-    else if (g_fin.kind == 2 && g_fin.K == 2)
-      hipLaunchKernelGGL((stat_rows_fin_kernel<2, 2>), grid, dim3(256), 0, s, rows, R, CK, slots, g_fin, ctr);
-    else if (g_fin.kind == 2 && g_fin.K == 4)
-      hipLaunchKernelGGL((stat_rows_fin_kernel<2, 4>), grid, dim3(256), 0, s, rows, R, CK, slots, g_fin, ctr);
-    else
-      pdt_hip_fail("stat_fin: unsupported finalize", hipErrorInvalidValue, __FILE__, __LINE__);
-    PDT_COUNT("stat_rows_fused_finalize");
-    g_fin_taken = true;
-    return;
-  }
-  hipLaunchKernelGGL(stat_rows_reduce_kernel, dim3((CK + 63) / 64, kStatSlots), dim3(256), 0, s, rows, R, CK, slots);
 }
 
 template <int K>

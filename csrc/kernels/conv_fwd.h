@@ -15,39 +15,6 @@ constexpr int kStatSlots = 64;  // slot copies of per-channel statistics accumul
 // is written, so the slots need no zeroing.
 void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s);
 
-// Fused BatchNorm finalize of a statistics reduction (csrc/kernels/bn.hip).  Armed on the host thread right before
-// the op that produces the statistics; the next stat_rows_reduce_launch into ``slots`` (with CK == C * K) then
-// also finalizes -- forward (kind 1: coef, sums, running stats) or backward (kind 2: bcoef / dgamma / dbeta of one
-// or two branches) -- exactly as bn_finalize_slots / bn_bwd_finalize_slots would.  stat_fin_take() disarms and
-// tells whether it happened (if not, the caller launches the separate finalize).
-struct StatFin {
-  int kind = 0, K = 2, C = 0;
-  const double* slots = nullptr;
-  double count = 1.0;
-  // kind 1
-  const float* gamma = nullptr;
-  const float* beta = nullptr;
-  float eps = 0.f, momentum = 0.f;
-  float* rm = nullptr;
-  float* rv = nullptr;
-  float* coef = nullptr;
-  double* sums = nullptr;
-  int update_running = 0;
-  // kind 2
-  const float* coef1 = nullptr;
-  const float* gamma1 = nullptr;
-  float* dgamma1 = nullptr;
-  float* dbeta1 = nullptr;
-  float* bcoef1 = nullptr;
-  const float* coef2 = nullptr;
-  const float* gamma2 = nullptr;
-  float* dgamma2 = nullptr;
-  float* dbeta2 = nullptr;
-  float* bcoef2 = nullptr;
-  float gscale = 1.f;
-};
-void stat_fin_arm(const StatFin& f);
-bool stat_fin_take();
 
 // Generalised implicit-GEMM convolution (see conv_fwd.hip for the geometry contract).
 struct ConvFwdArgs {

@@ -143,10 +143,6 @@ class ResNetExecutor:
         # layer2 2-branch 766 -> 508 us), after which fusing at every resolution measured equal or faster than
         # the separate reduce (A/B 21.76 -> 21.71 ms/step), so it is the default everywhere.
         self.fuse_block_bn_maxhw = int(os.environ.get("PDT_FUSE_BLOCK_BN_MAXHW", "1000000"))
-        # BatchNorm finalize fused into the statistics reduction of the op producing the statistics (one launch per BN
-        # layer and direction fewer: csrc/kernels/bn.hip stat_rows_fin_kernel; PDT_FUSE_FIN=0: separate finalize).
-        # Not with SyncBN (its all-reduce sits between the reduction and the finalize).
-        self.fuse_fin = os.environ.get("PDT_FUSE_FIN", "1") == "1" and hasattr(self.C, "stat_fin_arm_fwd")
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -336,14 +332,13 @@ class ResNetExecutor:
 
     def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None,
                  pre=None, stats_tag=None, fin: Optional[_BN] = None):
-        """``fin``: the BatchNorm consuming y -- its training finalize runs as part of this op (fused into the
-        statistics reduction where possible, else as the separate finalize launch right after)."""
+        """``fin``: the BatchNorm consuming y -- its training finalize is launched right behind the conv."""
         if pre is not None:  # x is the producer conv's raw output; pre = its BN coefficients (layer1 only)
             key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
             sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
-            armed = self._arm_fwd(fin, sp, N * H * W)
             self.C.conv_fwd_pre(x, self._w(c), y, sp, pre, N, H, W)
-            self._fin_fwd(fin, sp, N * H * W, armed)
+            if fin is not None:
+                self.bn_train_finalize(fin, sp, 0, N * H * W)
             return H, W, sp, N * H * W
         cin = cin or c.cin
         R = R or c.R
@@ -367,36 +362,10 @@ class ResNetExecutor:
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
                             -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
         bm, bn = self._tile(("fwd", N, H, W, cin, c.cout, R, S, st, stats), c.cout, bk, launch, kdim=cin * R * S)
-        armed = self._arm_fwd(fin, sp, M) if stats else False
         launch(bm, bn)
-        if stats:
-            self._fin_fwd(fin, sp, M, armed)
+        if stats and fin is not None:
+            self.bn_train_finalize(fin, sp, 0, M)
         return P, Q, sp, M
-
-    def _arm_fwd(self, bn: Optional[_BN], sp, count: int) -> bool:
-        if bn is None or not self.fuse_fin or self.syncbn:
-            return False
-        self.C.stat_fin_arm_fwd(sp, float(count), self._p(bn.gslot), self._p(bn.bslot), bn.eps, bn.momentum,
-                                bn.mod.running_mean, bn.mod.running_var, bn.coef, bn.sums, True)
-        return True
-
-    def _fin_fwd(self, bn: Optional[_BN], sp, count: int, armed: bool) -> None:
-        if bn is None:
-            return
-        if armed and self.C.stat_fin_take():
-            return
-        self.bn_train_finalize(bn, sp, 0, count)
-
-    def _arm_bwd(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None) -> bool:
-        if not self.fuse_fin or self.syncbn:
-            return False
-        self.C.stat_fin_arm_bwd(slots, 4 if bn2 is not None else 2, float(count), bn1.coef, self._p(bn1.gslot),
-                                self._g(bn1.gslot), self._g(bn1.bslot), bn1.bcoef,
-                                bn2.coef if bn2 is not None else None, self._p(bn2.gslot) if bn2 is not None else None,
-                                self._g(bn2.gslot) if bn2 is not None else None,
-                                self._g(bn2.bslot) if bn2 is not None else None,
-                                bn2.bcoef if bn2 is not None else None, 1.0)
-        return True
 
     # per-shape tile choice: the static table (ops.conv.conv_tile), or -- with autotune on, the analogue of
     # the reference's cudnn.benchmark=True (`distributed.py:104`) -- the fastest candidate timed once per shape
@@ -498,12 +467,9 @@ class ResNetExecutor:
                                      bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
         key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
         bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
-        if fin is not None and bnb is not None:  # fin = (count, bn1, bn2): the fused reduce's BN-backward finalize
-            armed = self._arm_bwd(bnb[6], fin[0], fin[1], fin[2])
-            launch(bm, bn)
-            self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2], armed)
-            return
         launch(bm, bn)
+        if fin is not None and bnb is not None:  # fin = (count, bn1, bn2): the fused reduce's BN-backward finalize
+            self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2])
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None, cs=0,
                win=False, dil=1, pre=None):
@@ -539,21 +505,13 @@ class ResNetExecutor:
         blocks = self.C.bn_bwd_reduce_blocks(rows, C)
         K = 4 if bn2 is not None else 2
         slots = self._buf(("bnslots", C, K), self.n_slots * C * K, torch.float64)
-        armed = self._arm_bwd(slots, count, bn1, bn2)
         self.C.bn_bwd_reduce(g, out_mask, y1, bn1.coef, y2, bn2.coef if bn2 is not None else None, slots, blocks, rows, C)
-        self._bn_bwd_finish(slots, count, bn1, bn2, armed)
+        self._bn_bwd_finish(slots, count, bn1, bn2)
 
-    def _bn_bwd_finish(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None, armed: bool = False):
-        """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients.  ``armed``: the producing op's
-        statistics reduction was armed to finalize itself (_arm_bwd); if it did, only the readiness is left."""
+    def _bn_bwd_finish(self, slots, count: int, bn1: _BN, bn2: Optional[_BN] = None):
+        """Slot sums (+ SyncBN all-reduce) -> dgamma/dbeta and the apply coefficients."""
         C = bn1.C
         K = 4 if bn2 is not None else 2
-        if armed and self.C.stat_fin_take():
-            for b in (bn1, bn2):
-                if b is not None:
-                    self.grad_ready(b.gslot.index)
-                    self.grad_ready(b.bslot.index)
-            return
         if not self.syncbn:  # slot sum + finalize of both branches in one launch
             self.C.bn_bwd_finalize_slots(
                 slots, K, float(count), bn1.coef, self._p(bn1.gslot), self._g(bn1.gslot), self._g(bn1.bslot),
@@ -606,7 +564,6 @@ class ResNetExecutor:
         y0 = self._buf("y0", N * P0 * Q0 * st.cout)
         wst = self.derived[self.stem_w_off:self.stem_w_off + st.cout * st.R * 32]
         sp = self._buf(("stats", st.cout), self.n_slots * st.cout * 2, torch.float64) if train else None
-        armed = self._arm_fwd(self.stem_bn, sp, N * P0 * Q0) if train else False
         if self.stem_kernel and Cn.stem_fwd_supported(Hp, Wp, P0, Q0):
             Cn.stem_fwd(xp, wst, y0, sp, N, Hp, Wp, P0, Q0, self.stem_blocks_per_cu)
         else:  # generic implicit GEMM in window mode (one 32-wide K step per kernel row)
@@ -614,7 +571,7 @@ class ResNetExecutor:
             Cn.conv_fwd(xp, wst, y0, None, sp, N, Hp, Wp, 32, st.cout, st.R, 1, P0, Q0, st.st, st.st, 0, 0, 1, 0,
                         P0, Q0, 1, 1, 0, 0, bm, bn, 32, 4)
         if train:
-            self._fin_fwd(self.stem_bn, sp, N * P0 * Q0, armed)
+            self.bn_train_finalize(self.stem_bn, sp, 0, N * P0 * Q0)
         else:
             self.bn_eval(self.stem_bn)
         H1, W1 = (P0 - 1) // 2 + 1, (Q0 - 1) // 2 + 1
@@ -835,9 +792,8 @@ class ResNetExecutor:
         P0, Q0 = saved["P0"], saved["Q0"]
         slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
         # BN-backward sums from the pooled output alone (ReLU mask = out > 0, BN input recovered from out)
-        armed = self._arm_bwd(slots, N * P0 * Q0, sbn)
         Cn.stem_pool_bwd_reduce_out(g, saved["x0"], sbn.coef, slots, N, P0, Q0, st.cout)
-        self._bn_bwd_finish(slots, N * P0 * Q0, sbn, None, armed)
+        self._bn_bwd_finish(slots, N * P0 * Q0, sbn)
         ldw = self.stem_pairs * 64
         if self._stem_fused_ok(Q0):
             # the stem weight gradient computes its dY tiles itself (max-pool backward + ReLU + BN-backward

@@ -50,7 +50,6 @@ class ResNetExecutor32(ResNetExecutor):
         self.dtype = torch.float32
         self._user_grad_ready = grad_ready or (lambda pid: None)
         self.side = None  # one stream: every kernel here is MFMA- or bandwidth-bound on its own
-        self.fuse_fin = False  # (the fused statistics finalize is wired for the 16-bit kernels only)
         self._on_side = False
         self._pending_reads = {}
         self.syncbn_group = syncbn_group
