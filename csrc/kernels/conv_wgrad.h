@@ -32,7 +32,8 @@ struct ConvWgradArgs {
   const float* pre_coef = nullptr;
 };
 
-int wgrad_tile(int C, int Kout, int win);  // 256 (ping-pong), 128 or 64
+int wgrad_tile(int C, int Kout, int win);  // 256 (ping-pong), 128 (C == 64: two-tap pairs) or 64
+int wgrad_ctiles(const ConvWgradArgs& a);  // (tap, c) tiles of the dW column axis for a.tile
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks);
 void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s);
 // 3x3/s1/p1 C = Kout = 64, W = 56 specialisation: all 9 taps per block, persistent over 4-row tiles;

@@ -462,9 +462,21 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
 // 128 (c) x 128 (k) tile variant for layers with C, Kout multiples of 128: 4 waves in a 2x2 grid over
 // the output tile, each wave owning 64x64 for ALL 64 pixels of a K-step (32 MFMAs per K-step per wave,
 // 4x the MFMA work per loaded pixel row of the 64x64 variant).  64 KiB of LDS -> 2 blocks per CU.
+//
+// PAIR (C == 64, Kout % 128 == 0: ResNet layer2's first 3x3/2 conv and its 1x1/2 downsample): the 128-wide
+// c side of the tile is TWO TAPS of 64 channels -- X row chunk ch < 8 is gathered through tap 2*nt, chunk
+// ch >= 8 through tap 2*nt + 1 -- so the 64-channel layers run at the 128x128 tile's MFMA work per staged
+// byte instead of the 64x64 kernel's.  With C == 64 the two taps' columns tap*64 + c are contiguous in
+// dW, so the epilogue is unchanged; an odd tap count leaves the last tile's second half dead (zero-filled
+// DMA, its two waves skip the MFMAs and the store).
 PDT_DEVICE int tr_swz16(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
 
-template <int DT>
+int wgrad_ctiles(const ConvWgradArgs& a) {
+  if (a.tile == 128 && a.C == 64) return (a.T * a.U + 1) / 2;
+  return a.T * a.U * (a.C / a.tile);
+}
+
+template <int DT, bool PAIR>
 __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -479,8 +491,9 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wave & 1, wk = wave >> 1;
 
-  const int c_tiles = a.C / 128;
-  const int n_tiles = a.T * a.U * c_tiles;
+  const int taps = a.T * a.U;
+  const int c_tiles = PAIR ? 1 : a.C / 128;
+  const int n_tiles = PAIR ? (taps + 1) / 2 : taps * c_tiles;
   const int k_tiles = a.Kout / 128;
   const int nwg = k_tiles * n_tiles * a.splits;
   const int bid = xcd_remap(blockIdx.x, nwg);
@@ -488,16 +501,24 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   const int split = bid / (k_tiles * n_tiles);
   const int kt = tile % k_tiles;
   const int nt = tile / k_tiles;
-  const int tap = nt / c_tiles;
-  const int c0 = (nt - tap * c_tiles) * 128;
+  const int tap = PAIR ? 2 * nt : nt / c_tiles;  // PAIR: the first of the two taps
+  const int c0 = PAIR ? 0 : (nt - tap * c_tiles) * 128;
   const int k0 = kt * 128;
-  const int t = tap / a.U, u = tap - (tap / a.U) * a.U;
 
   const int pix_begin = split * a.pix_per_split;
   const int pix_end = min(a.P, pix_begin + a.pix_per_split);
   const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
 
-  const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
+  // tap offsets of the two column halves (equal unless PAIR)
+  int th2[2], tw2[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int tp = PAIR ? min(tap + h, taps - 1) : tap;
+    const int t = tp / a.U, u = tp - (tp / a.U) * a.U;
+    th2[h] = t * a.dil_h - a.pad_h;
+    tw2[h] = u * a.dil_w - a.pad_w;
+  }
+  const bool half1_live = !PAIR || tap + 1 < taps;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
 
@@ -512,7 +533,13 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
       const int row = (wave * 4 + j) * 4 + lrow;  // 0..63
       const int lch = pch ^ tr_swz16(row);
       uint32_t xo, yo;
-      wgrad_rows<false>(a, pbase + row, th, tw, c0, lch, k0, xo, yo);
+      if constexpr (PAIR) {
+        const int h = lch >> 3;  // column half -> tap; channel (lch & 7) * 8 of that tap
+        wgrad_rows<false>(a, pbase + row, th2[h], tw2[h], -h * 64, lch, k0, xo, yo);
+        if (h && !half1_live) xo = kOOB;
+      } else {
+        wgrad_rows<false>(a, pbase + row, th2[0], tw2[0], c0, lch, k0, xo, yo);
+      }
       buf_lds16_asm(rx, sb + (wave * 4 + j) * 1024, xo);
       buf_lds16_asm(ry, sb + XB + (wave * 4 + j) * 1024, yo);
     }
@@ -560,15 +587,18 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
               (lds_s16x4*)(sb + XB + r1 * ROWB + (((kc >> 3) ^ sw1) << 4) + (kc & 7) * 2));
           bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
+        if (wc == 0 || half1_live) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+            for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   }
+  if (wc == 1 && !half1_live) return;
   // acc[i][j]: rows c = wc*64 + 16i + 4*(lane>>4) + r, col k = wk*64 + 16j + (lane&15)
   float* dst = a.ws + ((int64_t)split * a.Kout + k0) * a.ldw + tap * a.C + c0;
 #pragma unroll
@@ -1075,13 +1105,19 @@ int wgrad_tile(int C, int Kout, int win) {
     const char* e = getenv("PDT_WGRAD_PP");
     return !(e && e[0] == '0');
   }();
+  // PDT_WGRAD_PAIR=0 keeps C == 64 layers on the 64x64 kernel (A/B sweeps)
+  static const bool pair_on = [] {
+    const char* e = getenv("PDT_WGRAD_PAIR");
+    return !(e && e[0] == '0');
+  }();
   if (!win && pp_on && C % 256 == 0 && Kout % 256 == 0) return 256;
+  if (!win && pair_on && C == 64 && Kout % 128 == 0) return 128;  // two-tap pair tile
   return (!win && C % 128 == 0 && Kout % 128 == 0) ? 128 : 64;
 }
 
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
   a.tile = wgrad_tile(a.C, a.Kout, a.win);
-  const int tiles = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile);
+  const int tiles = (a.Kout / a.tile) * wgrad_ctiles(a);
   int splits = (target_blocks + tiles - 1) / tiles;
   if (a.tile == 256) {
     // one 8-wave block per CU: aim at whole rounds of the CU count (a 2.1-round grid runs 3 rounds)
@@ -1107,7 +1143,7 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
 
 void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   ConvWgradArgs a = args;
-  const int nwg = (a.Kout / a.tile) * a.T * a.U * (a.C / a.tile) * a.splits;
+  const int nwg = (a.Kout / a.tile) * wgrad_ctiles(a) * a.splits;
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
   a.div_pq_mul = dpq.mul; a.div_pq_shift = dpq.shift; a.div_q_mul = dq.mul; a.div_q_shift = dq.shift;
@@ -1117,12 +1153,18 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kBF16>), dim3(nwg), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
+  } else if (a.tile == 128 && a.C == 64) {
+    PDT_COUNT("conv_wgrad_128_pair");
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16, true>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kF16, true>), dim3(nwg), dim3(256), 0, s, a);
   } else if (a.tile == 128) {
     PDT_COUNT("conv_wgrad_128");
     if (dtype == kBF16)
-      hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16>), dim3(nwg), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16, false>), dim3(nwg), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_wgrad128_kernel<kF16>), dim3(nwg), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kF16, false>), dim3(nwg), dim3(256), 0, s, a);
   } else if (a.win && a.T == 4 && a.U == 1 && a.C == 64 && a.Kout == 64 && a.ldw >= 256) {
     // ResNet stem (4 kernel-row pairs): one block per split covers all pairs
     if (a.f_y != nullptr)

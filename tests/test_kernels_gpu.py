@@ -79,6 +79,26 @@ def test_conv_wgrad(case):
     assert _rel(dw, ref) < 2e-3
 
 
+@pytest.mark.parametrize("case", [(2, 15, 13, 64, 256, 3, 2, 1), (4, 14, 14, 64, 128, 3, 1, 1),
+                                  (3, 14, 14, 64, 128, 1, 2, 0), (2, 9, 9, 64, 384, 1, 1, 0)])
+@pytest.mark.parametrize("target", [64, 2048])
+def test_conv_wgrad_two_tap_pair_tile(case, target):
+    """C == 64, Kout % 128 == 0 runs the 128x128 wgrad kernel with its c side split over two taps (an odd tap count
+    leaves the last tile's second half dead): every tap's dW against torch fp32, few and many splits."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    N, H, W, C, K, R, st, pad = case
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    assert native.C.conv_wgrad_plan(K, R, R, C, N * P * Q, target, False)[2] == 128
+    torch.manual_seed(12)
+    x = _rand16(N, H, W, C)
+    dy = _rand16(N, P, Q, K)
+    dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=target)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
+                                      stride=st, padding=pad).permute(0, 2, 3, 1)
+    for t in range(R * R):  # per tap: a dead or misplaced half shows up as one tap's block
+        assert _rel(dw.reshape(K, R * R, C)[:, t], ref.reshape(K, R * R, C)[:, t]) < 2e-3, t
+
+
 def test_conv_wgrad_many_splits():
     from pytorch_distributed_template_amd.ops import conv
     torch.manual_seed(3)
