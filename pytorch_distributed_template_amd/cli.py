@@ -106,8 +106,8 @@ def build_parser(mode: str) -> argparse.ArgumentParser:
     g.add_argument("--eval-precision", default="auto", choices=["auto", "compute", "fp32"],
                    help="validation dtype: fp32 on the native fp32 kernels over the fp32 master weights (the reference "
                         "validates without autocast, `distributed_syncBN_amp.py:309-317`, and in fp32 everywhere), or "
-                        "the training compute dtype; auto = fp32 for distributed.py / distributed_syncBN_amp.py, compute "
-                        "for native DataParallel")
+                        "the training compute dtype; auto = fp32 (every entry script, native DataParallel included: "
+                        "`dataparallel.py:243-262` validates the fp32 model)")
     g.add_argument("--synthetic", default=False, type=str2bool, nargs="?", const=True,
                    help="use synthetic ImageNet-shaped data instead of --data")
     g.add_argument("--synthetic-train-size", type=int, default=1281167)

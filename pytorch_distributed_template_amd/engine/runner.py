@@ -229,7 +229,9 @@ def build_trainer(mode: str, model, args, device, dtype, engine: str, world: int
             ids = list(range(torch.cuda.device_count()))
             if os.environ.get("PDT_DP_DEVICES"):  # rehearsal: e.g. "0,0" = two replicas sharing GPU 0
                 ids = [int(v) for v in os.environ["PDT_DP_DEVICES"].split(",")]
-            return NativeDataParallelTrainer(model, ids, dtype=dtype, use_amp=use_amp, **common)
+            return NativeDataParallelTrainer(model, ids, dtype=dtype, use_amp=use_amp,
+                                             eval_fp32=getattr(args, "eval_precision", "auto") in ("fp32", "auto"),
+                                             **common)
         from .torch_trainer import TorchTrainer
         # nn.DataParallel semantics on the torch engine too: the node-total batch is scattered over every
         # visible GPU (`dataparallel.py:119`), not run on cuda:0 alone

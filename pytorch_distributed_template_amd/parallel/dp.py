@@ -70,7 +70,7 @@ class _LocalGroup:
 class NativeDataParallelTrainer:
     def __init__(self, model, device_ids: List[int], dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, use_amp: bool = False,
-                 graph: Optional[bool] = None):
+                 graph: Optional[bool] = None, eval_fp32: bool = False):
         self.device_ids = list(device_ids)
         distinct = len(set(self.device_ids))
         # per-replica HIP graphs (see module doc); two eager warm-up steps settle buffers and tile choices
@@ -96,6 +96,18 @@ class NativeDataParallelTrainer:
                     self.executors.append(ResNetExecutor(m, f, d, dtype))
         self.model = model
         self.flat = self.flats[0]
+        # eval_fp32: validation of the fp32 model like the reference's DataParallel (`dataparallel.py:243-262`, no
+        # autocast anywhere): each replica evaluates its shard on the fp32 kernels over the fp32 master weights, which
+        # are broadcast from GPU 0 to the replicas once per weight version (16-bit training replicates only the 16-bit
+        # shadow and the master-read parameters)
+        self._eval32 = None
+        self._eval32_at = -1
+        if eval_fp32 and dtype != torch.float32:
+            from ..models.executor32 import ResNetExecutor32
+            self._eval32 = []
+            for m, f, d in zip(replicas, self.flats, self.devices):
+                with torch.cuda.device(d):
+                    self._eval32.append(ResNetExecutor32(m, f, d))
         self.optimizer = FusedSGD(self.flat, lr, momentum, weight_decay)
         self.optimizer.post_step_hooks.append(self.executors[0].update_derived)
         self.scaler = DeviceGradScaler(self.devices[0], enabled=use_amp and dtype == torch.float16)
@@ -121,6 +133,7 @@ class NativeDataParallelTrainer:
     def on_state_loaded(self) -> None:
         """After ``model.load_state_dict`` (resume): GPU 0's shadow and derived layouts, then every replica's full
         compute state (shadow, master-read parameters, BN buffers, derived layouts)."""
+        self._eval32_at = -1
         with torch.cuda.device(self.devices[0]):
             self.flat.refresh_shadow()
             self.executors[0].update_derived()
@@ -227,13 +240,29 @@ class NativeDataParallelTrainer:
         logits = torch.cat([o.to(self.devices[0]) for o in outs])
         return logits, torch.stack(mets).sum(0)
 
+    def _replicate_fp32(self) -> None:
+        """fp32 validation: the fp32 master on every replica + each replica's fp32 derived layouts, once per weight
+        version (optimizer step or state load)."""
+        if self._eval32_at == self.optimizer.step_count:
+            return
+        if len(self.devices) > 1:
+            self.group.broadcast([f.data for f in self.flats], 0)
+        for i, ex in enumerate(self._eval32):
+            with torch.cuda.device(self.devices[i]):
+                ex.update_derived()
+        self._eval32_at = self.optimizer.step_count
+
     @torch.no_grad()
     def eval_step(self, images, target):
         B = images.size(0)
         self._replicate()
+        executors = self.executors
+        if self._eval32 is not None:
+            self._replicate_fp32()
+            executors = self._eval32
         xs, ts = self._scatter(images, target)
         outs, mets = [], []
-        for i, (ex, x, t) in enumerate(zip(self.executors, xs, ts)):
+        for i, (ex, x, t) in enumerate(zip(executors, xs, ts)):
             if x.shape[0] == 0:
                 continue
             with torch.cuda.device(self.devices[i]):

@@ -95,3 +95,36 @@ def test_dp_runner_sharded_synthetic(tmp_path, monkeypatch):
     assert rc == 0
     log = (tmp_path / "o_resnet18" / "experiment.log").read_text()
     assert "||==> Val epoch" in log
+
+
+@pytest.mark.parametrize("device_ids", [[0], [0, 0]])
+def test_dp_fp32_eval_equals_executor32(device_ids):
+    """dataparallel.py validates the fp32 model (reference `dataparallel.py:243-262`: no autocast anywhere), so native
+    DataParallel with eval_fp32 (--eval-precision auto) evaluates each shard on the fp32 kernels over the fp32 master
+    after bf16 training steps: its logits equal ResNetExecutor32.eval_step on the same master weights and running
+    statistics, shard by shard, bit for bit (one replica, and two replicas sharing cuda:0)."""
+    from pytorch_distributed_template_amd.data.loader import shard_bounds
+    from pytorch_distributed_template_amd.models.executor32 import ResNetExecutor32
+    from pytorch_distributed_template_amd.optim.flat import FlatBuffers, FlatParams
+    from pytorch_distributed_template_amd.parallel.dp import NativeDataParallelTrainer
+    X, T = make_batch(B, HW)
+    x, t = X.cuda(), T.cuda()
+    dp = NativeDataParallelTrainer(make_model(seed=0), device_ids, dtype=torch.bfloat16, eval_fp32=True)
+    for _ in range(2):
+        dp.train_step(x, t)
+    logits, met = dp.eval_step(x, t)
+    logits2, _ = dp.eval_step(x, t)  # same weight version: no re-replication, same result
+    ref_model = make_model(seed=1)
+    ref_model.load_state_dict({k: v.detach().clone() for k, v in dp.model.state_dict().items()})
+    flat = FlatParams(ref_model, "cuda:0", None)
+    FlatBuffers(ref_model, "cuda:0")
+    ex = ResNetExecutor32(ref_model, flat, "cuda:0")
+    ref = torch.cat([ex.eval_step(x[lo:hi], t[lo:hi])[0] for lo, hi in shard_bounds(B, len(device_ids))])
+    torch.cuda.synchronize()
+    assert torch.equal(logits, ref)
+    assert torch.equal(logits2, ref)
+    # the bf16 evaluation differs (it is not what the reference validates)
+    dp16 = NativeDataParallelTrainer(make_model(seed=0), device_ids, dtype=torch.bfloat16)
+    for _ in range(2):
+        dp16.train_step(x, t)
+    assert not torch.equal(dp16.eval_step(x, t)[0], ref)
