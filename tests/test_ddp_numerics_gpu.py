@@ -127,7 +127,8 @@ def test_native_syncbn_fp32_equals_full_batch(tmp_path, nproc):
     """SyncBN correctness without 16-bit chaos: in fp32 (the reference's `distributed.py` precision, exact-fp32
     MFMA kernels) SyncBN DDP over ``nproc`` ranks x B (the native communicator: ranks share cuda:0, host transport)
     must equal ONE process running the full batch nproc x B with plain BN after one step -- every parameter's
-    update within 1e-4 relative, running mean / var within 1e-5, num_batches_tracked exact.  A count, eps,
+    update within max(1e-4, 3 x the reorder floor: the same full-batch step with the ranks' slices rotated),
+    running mean / var within 1e-5, num_batches_tracked exact, loss / accuracy within 1e-5.  A count, eps,
     variance-bias or gradient-scale error in the native SyncBN path is orders of magnitude larger
     (`distributed_syncBN_amp.py:142-147`; upstream semantics SURVEY §3.5)."""
     res = _run_ranks(tmp_path, nproc=nproc, PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=1, PDT_TEST_COMM="native",
@@ -140,21 +141,31 @@ def check_syncbn_fp32_full_batch(res, nproc):
     """The fp32 SyncBN contract (see test_native_syncbn_fp32_equals_full_batch) for rank 0's saved state ``res``
     after one step at world ``nproc``; also used by the >= 2-GPU tests (tests/test_multigpu.py)."""
     X, T = make_batch(nproc * B, HW)
-    x, t = X.cuda(), T.cuda()
     box = {}
 
-    def run(tr):
-        _, m = tr.train_step(x, t)
-        box["met"] = m.clone()
+    def run_on(x, t, key):
+        def run(tr):
+            _, m = tr.train_step(x.cuda(), t.cuda())
+            box[key] = m.clone()
+        return run
 
-    tr, before = _single(run, dtype=torch.float32)
+    tr, before = _single(run_on(X, T, "met"), dtype=torch.float32)
     before, full = before.cpu(), tr.flat.data.cpu()
+    # reorder floor: the same full batch with the ranks' slices rotated -- mathematically the identical step, so its
+    # difference is pure fp32 summation order, amplified through the random-init network's backward chain (a ReLU
+    # flip of a near-zero pre-activation moves whole blocks' gradients, test_fp32_gpu.py); a SyncBN count, eps,
+    # variance-bias or gradient-scale error is far above it
+    tr2, _ = _single(run_on(torch.roll(X, B, 0), torch.roll(T, B, 0), "met2"), dtype=torch.float32)
+    floor = _update_errors(tr, before, tr2.flat.data.cpu(), full)
     e = _update_errors(tr, before, res["data"], full)
-    bad = [(k, v) for k, v in e.items() if v > 1e-4]
-    assert not bad, sorted(bad, key=lambda kv: -kv[1])[:8]
+    fmax = max(floor.values())
+    bad = [(k, v, floor[k]) for k, v in e.items() if v > max(1e-4, 3 * fmax)]
+    assert not bad, (fmax, sorted(bad, key=lambda kv: -kv[1])[:8])
+    assert torch.allclose(box["met2"], box["met"], rtol=1e-5, atol=1e-6)
     fb = tr.buffers.fdata.cpu()
-    rs_err = ((res["fbuf"] - fb).abs() / fb.abs().clamp_min(1e-6)).max().item()
-    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-5 and rs_err < 1e-4, rs_err
+    # every running mean / var element within 1e-5 relative (plus 1e-7 absolute for means that are ~0)
+    rs_err = ((res["fbuf"] - fb).abs() - 1e-5 * fb.abs()).max().item()
+    assert ((res["fbuf"] - fb).norm() / fb.norm()).item() < 1e-5 and rs_err < 1e-7, rs_err
     assert torch.equal(res["ibuf"], tr.buffers.idata.cpu())  # num_batches_tracked
     assert torch.allclose(res["met"][0], box["met"].cpu(), rtol=1e-5, atol=1e-6)
 

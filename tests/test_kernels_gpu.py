@@ -485,6 +485,22 @@ def test_conv_tile_configs(tile):
     assert _rel(dx, refx) < 1e-2
 
 
+@pytest.mark.parametrize("geom", [(3, 17, 224, 3, 0), (2, 9, 24, 3, 2), (2, 7, 20, 3, 1), (1, 5, 18, 3, 2)])
+def test_stem_pack_matches_torch(geom):
+    """fp32 NCHW -> zero-padded bf16 NHWC4 (row-tiled kernel for W % 4 == 0 and even Wp, per-pixel kernel otherwise)
+    equals torch's pad + permute + cast exactly, padding and channel 3 zero."""
+    from pytorch_distributed_template_amd.ops import native
+    N, H, W, pad, ex = geom
+    Hp, Wp = H + 2 * pad, W + 2 * pad + ex
+    torch.manual_seed(13)
+    x = torch.randn(N, 3, H, W, device=DEV)
+    out = torch.full((N * Hp * Wp * 4,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    native.C.stem_pack(x, out, N, 3, H, W, pad, Hp, Wp)
+    ref = torch.zeros(N, Hp, Wp, 4, device=DEV)
+    ref[:, pad:pad + H, pad:pad + W, :3] = x.permute(0, 2, 3, 1)
+    assert torch.equal(out.view(N, Hp, Wp, 4), ref.to(torch.bfloat16))
+
+
 def test_stem_pack_u8_fused_normalize():
     """uint8 pixels normalised inside the stem packing == host-style Normalize then packing."""
     from pytorch_distributed_template_amd.data.transforms import IMAGENET_MEAN, IMAGENET_STD, normalize_on_device
