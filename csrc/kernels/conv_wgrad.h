@@ -16,7 +16,7 @@ struct ConvWgradArgs {
   int cs;              // elements per pixel of x (== C except in window mode)
   int win;             // stem window mode (see conv_wgrad.hip)
   int splits, pix_per_split;  // filled by conv_wgrad_plan
-  int tile;                   // 64, 128 or 256 (filled by conv_wgrad_plan)
+  int tile;                   // 64, 128, 256 or kWgradWide (filled by conv_wgrad_plan)
   uint32_t div_pq_mul, div_pq_shift, div_q_mul, div_q_shift;  // FastDiv of Pm*Qm and Qm (launcher)
   // stem only (f_y != nullptr): dY computed in-kernel from the 3x3/2 max-pool backward + ReLU + BN backward
   // (dy unused).  f_y: conv output [P][64]; f_dp / f_idx: pooled gradient and argmax [N][f_OH][f_OW][64];
@@ -32,6 +32,7 @@ struct ConvWgradArgs {
   const float* pre_coef = nullptr;
 };
 
+constexpr int kWgradWide = 2;  // ConvWgradArgs::tile code of the 256 (c: two 128-wide column blocks) x 128 (k) kernel
 int wgrad_tile(int C, int Kout, int win);  // 256 (ping-pong), 128 (C == 64: two-tap pairs) or 64
 int wgrad_ctiles(const ConvWgradArgs& a);  // (tap, c) tiles of the dW column axis for a.tile
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks);

@@ -472,9 +472,12 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
 PDT_DEVICE int tr_swz16(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
 
 int wgrad_ctiles(const ConvWgradArgs& a) {
+  if (a.tile == kWgradWide) return (a.T * a.U * (a.C / 128) + 1) / 2;
   if (a.tile == 128 && a.C == 64) return (a.T * a.U + 1) / 2;
   return a.T * a.U * (a.C / a.tile);
 }
+
+int wgrad_ktile(const ConvWgradArgs& a) { return a.tile == kWgradWide ? 128 : a.tile; }
 
 template <int DT, bool PAIR>
 __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
@@ -611,6 +614,176 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
     }
 }
 
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their maxima)
+template <int N>
+PDT_DEVICE void wg_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// ------------------------------------------------------------------------------------------------
+// "Wide" 256 (c) x 128 (k) tile for C % 128 == 0, Kout % 128 == 0 layers below the ping-pong kernel's 256 x 256
+// (ResNet-18 layer2's 3x3 128->128 convs, layer3.0's 128->256 ones; ResNet-50 stage 2).  The dW column axis
+// (tap * C + c) is cut into 128-wide column blocks -- one tap's channel range each, contiguous in dW -- and a tile
+// is TWO consecutive column blocks (two taps when C == 128; an odd count leaves the last tile's second half dead).
+// 8 waves as 4 (c) x 2 (k), each owning 64 x 64 over all 64 pixels of a K-step: 85 FLOP per staged byte against
+// the 128 x 128 tile's 64.  One workgroup per CU with a 3-deep ring of 48 KB stages: the DMA of K-step s+2 is
+// issued while K-step s computes, and each K-step waits only for its own stage (counted vmcnt(kWideDma): the 6
+// DMA instructions per wave of the stage behind it stay in flight) -- the 128 x 128 kernel drains its single
+// prefetch (vmcnt(0)) every K-step and is latency-bound at ~30 % MFMA busy.
+constexpr int kWideDma = 6;  // DMA instructions per wave per stage: 4 X (2 sub-tiles x 16 / 8 waves) + 2 dY
+
+template <int DT>
+__global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 64;          // pixels per K-step
+  constexpr int ROWB = 256;        // 128 channels * 2 B
+  constexpr int SUB = BKP * ROWB;  // 16 KiB: one column block's X image, or the dY image
+  constexpr int STAGE = 3 * SUB;   // X block 0 | X block 1 | dY
+  constexpr int NST = 3;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave & 3, wk = wave >> 2;
+
+  const int taps = a.T * a.U;
+  const int cblocks = taps * (a.C / 128);  // 128-wide column blocks of dW
+  const int n_tiles = (cblocks + 1) / 2;
+  const int k_tiles = a.Kout / 128;
+  const int nwg = k_tiles * n_tiles * a.splits;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tile = bid % (k_tiles * n_tiles);
+  const int split = bid / (k_tiles * n_tiles);
+  const int kt = tile % k_tiles;
+  const int nt = tile / k_tiles;
+  const int k0 = kt * 128;
+
+  const int pix_begin = split * a.pix_per_split;
+  const int pix_end = min(a.P, pix_begin + a.pix_per_split);
+  const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
+
+  // the two column blocks: tap offsets and channel base
+  int th2[2], tw2[2], cb0[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int cb = min(2 * nt + h, cblocks - 1);
+    const int tp = cb * 128 / a.C;
+    const int t = tp / a.U, u = tp - (tp / a.U) * a.U;
+    th2[h] = t * a.dil_h - a.pad_h;
+    tw2[h] = u * a.dil_w - a.pad_w;
+    cb0[h] = cb * 128 - tp * a.C;
+  }
+  const bool half1_live = 2 * nt + 1 < cblocks;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
+
+  // DMA lane geometry: 4 rows x 16 chunks per 1 KiB instruction
+  const int lrow = lane >> 4, pch = lane & 15;
+
+  auto stage_load = [&](int step, int buf) {
+    const int pbase = pix_begin + step * BKP;
+    char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // X: instruction i = wave * 4 + j of 32 (sub-tile i >> 4)
+      const int i = wave * 4 + j;
+      const int h = i >> 4;
+      const int row = (i & 15) * 4 + lrow;  // 0..63
+      const int lch = pch ^ tr_swz16(row);
+      uint32_t xo, yo;
+      wgrad_rows<false>(a, pbase + row, th2[h], tw2[h], cb0[h], lch, k0, xo, yo);
+      if (h && !half1_live) xo = kOOB;
+      buf_lds16_asm(rx, sb + h * SUB + (i & 15) * 1024, xo);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // dY: instruction i = wave * 2 + j of 16
+      const int i = wave * 2 + j;
+      const int row = i * 4 + lrow;
+      const int lch = pch ^ tr_swz16(row);
+      uint32_t xo, yo;
+      wgrad_rows<false>(a, pbase + row, th2[0], tw2[0], cb0[0], lch, k0, xo, yo);
+      buf_lds16_asm(ry, sb + 2 * SUB + i * 1024, yo);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+  const int xsub = wc >> 1;  // this wave's X sub-tile (column block)
+  const bool live = xsub == 0 || half1_live;
+  int ccol[4], kcol[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    ccol[f] = (wc & 1) * 64 + f * 16 + 4 * p4;
+    kcol[f] = wk * 64 + f * 16 + 4 * p4;
+  }
+
+  if (nsteps > 0) {
+    stage_load(0, 0);
+    if (nsteps > 1) stage_load(1, 1);
+    for (int s = 0; s < nsteps; ++s) {
+      // stage s landed: the younger stage s+1 (kWideDma per wave) may stay in flight
+      if (s + 1 < nsteps)
+        wg_vm_wait<kWideDma>();
+      else
+        wg_vm_wait<0>();
+      // every wave's DMA of stage s landed; every wave's MFMAs (hence its fragment reads) of stage s-1 done, so
+      // the ring slot of stage s-1 may be refilled.  A plain s_barrier: __syncthreads' release fence would also
+      // drain the stage still in flight (vmcnt(0)).
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 2 < nsteps) stage_load(s + 2, (s + 2) % NST);
+      const char* sb = smem + (s % NST) * STAGE;
+      const char* sx = sb + xsub * SUB;
+      const char* sy = sb + 2 * SUB;
+      if (live) {
+#pragma unroll
+        for (int kk = 0; kk < BKP / 32; ++kk) {
+          const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+          const int sw0 = tr_swz16(r0), sw1 = tr_swz16(r1);
+          vec8 af[4], bfr[4];
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            const int cc = ccol[f], kc = kcol[f];
+            s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)(sx + r0 * ROWB + (((cc >> 3) ^ sw0) << 4) + (cc & 7) * 2));
+            s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)(sx + r1 * ROWB + (((cc >> 3) ^ sw1) << 4) + (cc & 7) * 2));
+            af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)(sy + r0 * ROWB + (((kc >> 3) ^ sw0) << 4) + (kc & 7) * 2));
+            hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)(sy + r1 * ROWB + (((kc >> 3) ^ sw1) << 4) + (kc & 7) * 2));
+            bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        }
+      }
+    }
+  }
+  if (!live) return;
+  // acc[i][j]: rows c = (wc & 1)*64 + 16i + 4*(lane>>4) + r of column block 2nt + xsub, col k = wk*64 + 16j + (lane&15)
+  float* dst = a.ws + ((int64_t)split * a.Kout + k0) * a.ldw + (2 * nt + xsub) * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = wk * 64 + 16 * j + (lane & 15);
+      const int c = (wc & 1) * 64 + 16 * i + 4 * (lane >> 4);
+      *(f32x4_t*)(dst + (int64_t)k * a.ldw + c) = acc[i][j];
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // 256 (c) x 256 (k) ping-pong weight-gradient kernel for layers with C, Kout multiples of 256 (ResNet
 // layer3/4, ResNet-50 stages 2-4): the schedule of conv_pp_kernel (conv_fwd.hip) on the wgrad GEMM.
@@ -624,11 +797,6 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
 // and issues the next K-step's X0, Y0, Y1, X1 DMA with the counted-vmcnt discipline of conv_pp_kernel.
 // The DMA goes through buf_lds16_asm (common.h): with the builtin form the compiler drains the whole
 // DMA pipeline (vmcnt(0)) before every transposed read.
-template <int N>
-PDT_DEVICE void wg_vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
 
 template <int DT>
 __global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
@@ -1110,16 +1278,22 @@ int wgrad_tile(int C, int Kout, int win) {
     const char* e = getenv("PDT_WGRAD_PAIR");
     return !(e && e[0] == '0');
   }();
+  // PDT_WGRAD_WIDE=0 keeps C % 128 == 0 layers below 256 x 256 on the 128 x 128 kernel (A/B sweeps)
+  static const bool wide_on = [] {
+    const char* e = getenv("PDT_WGRAD_WIDE");
+    return !(e && e[0] == '0');
+  }();
   if (!win && pp_on && C % 256 == 0 && Kout % 256 == 0) return 256;
+  if (!win && wide_on && C % 128 == 0 && Kout % 128 == 0) return kWgradWide;
   if (!win && pair_on && C == 64 && Kout % 128 == 0) return 128;  // two-tap pair tile
   return (!win && C % 128 == 0 && Kout % 128 == 0) ? 128 : 64;
 }
 
 void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
   a.tile = wgrad_tile(a.C, a.Kout, a.win);
-  const int tiles = (a.Kout / a.tile) * wgrad_ctiles(a);
+  const int tiles = (a.Kout / wgrad_ktile(a)) * wgrad_ctiles(a);
   int splits = (target_blocks + tiles - 1) / tiles;
-  if (a.tile == 256) {
+  if (a.tile == 256 || a.tile == kWgradWide) {
     // one 8-wave block per CU: aim at whole rounds of the CU count (a 2.1-round grid runs 3 rounds)
     static const int cus = [] {
       int dev = 0, n = 0;
@@ -1143,7 +1317,7 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
 
 void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   ConvWgradArgs a = args;
-  const int nwg = (a.Kout / a.tile) * wgrad_ctiles(a) * a.splits;
+  const int nwg = (a.Kout / wgrad_ktile(a)) * wgrad_ctiles(a) * a.splits;
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
   a.div_pq_mul = dpq.mul; a.div_pq_shift = dpq.shift; a.div_q_mul = dq.mul; a.div_q_shift = dq.shift;
@@ -1153,6 +1327,12 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kBF16>), dim3(nwg), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
+  } else if (a.tile == kWgradWide) {
+    PDT_COUNT("conv_wgrad_wide");
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16>), dim3(nwg), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
   } else if (a.tile == 128 && a.C == 64) {
     PDT_COUNT("conv_wgrad_128_pair");
     if (dtype == kBF16)

@@ -99,6 +99,29 @@ def test_conv_wgrad_two_tap_pair_tile(case, target):
         assert _rel(dw.reshape(K, R * R, C)[:, t], ref.reshape(K, R * R, C)[:, t]) < 2e-3, t
 
 
+@pytest.mark.parametrize("case", [(2, 14, 14, 128, 128, 3, 1, 1), (2, 15, 13, 128, 256, 3, 2, 1),
+                                  (3, 9, 9, 256, 128, 1, 1, 0), (2, 10, 10, 128, 128, 1, 2, 0),
+                                  (1, 7, 7, 384, 128, 3, 1, 1)])
+@pytest.mark.parametrize("target", [64, 2048])
+def test_conv_wgrad_wide_tile(case, target):
+    """C % 128 == 0 and Kout % 128 == 0 below 256 x 256: the wide 256 (two 128-wide column blocks of dW) x 128 kernel
+    with its 3-deep counted-wait DMA ring.  Every column block against torch fp32 (an odd block count leaves the last
+    tile's second half dead), few and many splits (a split of one K-step drains the ring at once)."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    N, H, W, C, K, R, st, pad = case
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    assert native.C.conv_wgrad_plan(K, R, R, C, N * P * Q, target, False)[2] == 2  # kWgradWide
+    torch.manual_seed(14)
+    x = _rand16(N, H, W, C)
+    dy = _rand16(N, P, Q, K)
+    dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=target)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
+                                      stride=st, padding=pad).permute(0, 2, 3, 1)
+    nb = R * R * C // 128
+    for b in range(nb):
+        assert _rel(dw.reshape(K, nb, 128)[:, b], ref.reshape(K, nb, 128)[:, b]) < 2e-3, b
+
+
 def test_conv_wgrad_many_splits():
     from pytorch_distributed_template_amd.ops import conv
     torch.manual_seed(3)

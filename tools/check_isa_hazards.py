@@ -40,9 +40,10 @@ WINDOWS = {
     "conv_l1_kernel": {16: "dma", 12: "dma"},
     "stem_fwd_kernel": {24: "dma"},
     "wgrad_stem_kernel": {10: "dma", 8: "load"},
+    "conv_wgrad_wide_kernel": {6: ("dma", 6)},  # the stage behind: its 6 DMAs stay in flight
 }
 COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "conv_pp_kernel",
-            "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel")
+            "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel")
 
 
 def hip_flags():
@@ -186,18 +187,22 @@ def check_windows(ins, labels, wins):
         if b is not None and b[1] in labels and labels[b[1]] <= j:
             latches.setdefault(labels[b[1]], set()).add(j)
 
-    def walk(j, cnt, what, depth):
+    def walk(j, cnt, what, depth, skip=0):
+        """``skip``: the youngest ``skip`` matching operations are the group the wait leaves in flight (ring
+        pipelines); the window is measured from the one before them."""
         best = None
         while j >= 0:
             u = ins[j]
             if (what == "dma" and is_dma(u)) or (what == "load" and is_vm(u) and "load" in u.split()[0]
                                                  and not u.endswith(" lds")):
-                return cnt if best is None else max(best, cnt)
+                if skip == 0:
+                    return cnt if best is None else max(best, cnt)
+                skip -= 1
             if is_vm(u):
                 cnt += 1
             if j in latches and depth < 4:
                 for l in latches[j]:
-                    r = walk(l, cnt, what, depth + 1)
+                    r = walk(l, cnt, what, depth + 1, skip)
                     if r is not None:
                         best = r if best is None else max(best, r)
             j -= 1
@@ -208,8 +213,8 @@ def check_windows(ins, labels, wins):
         n = vm_wait(t)
         if n is None or n == 0 or n not in wins:
             continue
-        what = wins[n]
-        cnt = walk(i - 1, 0, what, 0)
+        what, skip = wins[n] if isinstance(wins[n], tuple) else (wins[n], 0)
+        cnt = walk(i - 1, 0, what, 0, skip)
         if cnt is None:
             probs.append(f"vmcnt({n}) at instruction {i}: no {what} found before it")
             continue
