@@ -985,6 +985,33 @@ void wgrad32_stem(const Tensor& xp, const Tensor& dy, Tensor& ws, int64_t N, int
   pdt::wgrad32_launch(a, cur_stream());
 }
 
+// wgrad32_stem (4 pairs, all per block) with dY computed in the kernel from the stem's max-pool backward, ReLU mask and
+// BN-backward apply (dp / idx: pooled gradient and argmax, y0: conv output, coef: forward scale | shift, bcoef: A | B |
+// C): stem_pool_bwd_apply32 + wgrad32_stem without the dY tensor
+void wgrad32_stem_fused(const Tensor& xp, const Tensor& dp, const Tensor& idx, const Tensor& y0, const Tensor& coef,
+                        const Tensor& bcoef, Tensor& ws, int64_t N, int64_t Hp, int64_t Wp, int64_t P, int64_t Q,
+                        int64_t stride, int64_t splits, int64_t pix_per_split) {
+  const int64_t OH = (P - 1) / 2 + 1, OW = (Q - 1) / 2 + 1;  // 3x3/2 pad-1 max-pool output
+  TORCH_CHECK(xp.numel() == N * Hp * Wp * 4 && y0.numel() == N * P * Q * 64 && dp.numel() == N * OH * OW * 64 &&
+                  idx.numel() == dp.numel() && idx.scalar_type() == at::kByte && coef.numel() >= 128 &&
+                  bcoef.numel() >= 192, "wgrad32_stem_fused: sizes");
+  TORCH_CHECK((P - 1) * stride + 8 <= Hp && (Q - 1) * stride + 8 <= Wp, "wgrad32_stem_fused: padded image too small");
+  TORCH_CHECK(ws.numel() >= splits * 64 * 256 && pix_per_split % 64 == 0 && splits * pix_per_split >= N * P * Q,
+              "wgrad32_stem_fused: bad workspace / split plan");
+  TORCH_CHECK(xp.numel() < (int64_t(1) << 30) && y0.numel() < (int64_t(1) << 31), "wgrad32_stem_fused: operands too large");
+  check_dev(idx, "idx");
+  pdt::Wgrad32Args a{};
+  a.tile = 4;
+  a.x = pf(xp, "xp"); a.dy = nullptr; a.ws = pf(ws, "ws");
+  a.N = N; a.H = Hp; a.W = Wp; a.C = 64; a.Kout = 64; a.T = 4; a.U = 1; a.Pm = P; a.Qm = Q;
+  a.stride = stride; a.pad = 0; a.ldw = 256; a.splits = splits; a.pix_per_split = pix_per_split;
+  a.P = N * P * Q;
+  a.cs = 4; a.pair_skip = Wp * 4 - 32; a.tstep = 2;
+  a.f_dp = pf(dp, "dp"); a.f_idx = idx.data_ptr<uint8_t>(); a.f_y = pf(y0, "y0"); a.f_coef = pf(coef, "coef");
+  a.f_bcoef = pf(bcoef, "bcoef"); a.f_OH = (int)OH; a.f_OW = (int)OW;
+  pdt::wgrad32_launch(a, cur_stream());
+}
+
 void im2col32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
               int64_t stride, int64_t pad, int64_t ldk) {
   const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
@@ -1087,6 +1114,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum32", &colsum32);
   m.def("stem_pack32", &stem_pack32);
   m.def("conv32_stem_fwd", &conv32_stem_fwd);
+  m.def("wgrad32_stem_fused", &wgrad32_stem_fused);
   m.def("wgrad32_stem", &wgrad32_stem, py::arg("xp"), py::arg("dy"), py::arg("ws"), py::arg("N"), py::arg("Hp"),
         py::arg("Wp"), py::arg("npairs"), py::arg("Kout"), py::arg("P"), py::arg("Q"), py::arg("stride"),
         py::arg("splits"), py::arg("pix_per_split"), py::arg("all_pairs") = 0);

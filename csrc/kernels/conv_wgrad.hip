@@ -479,6 +479,15 @@ int wgrad_ctiles(const ConvWgradArgs& a) {
 
 int wgrad_ktile(const ConvWgradArgs& a) { return a.tile == kWgradWide ? 128 : a.tile; }
 
+// pixels per K-step of the wide kernel (PDT_WGRAD_WIDE_BKP=32: two workgroups per CU)
+static int wide_bkp() {
+  static const int bkp = [] {
+    const char* e = getenv("PDT_WGRAD_WIDE_BKP");
+    return e && atoi(e) == 32 ? 32 : 64;
+  }();
+  return bkp;
+}
+
 template <int DT, bool PAIR>
 __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
@@ -631,15 +640,19 @@ PDT_DEVICE void wg_vm_wait() {
 // issued while K-step s computes, and each K-step waits only for its own stage (counted vmcnt(kWideDma): the 6
 // DMA instructions per wave of the stage behind it stay in flight) -- the 128 x 128 kernel drains its single
 // prefetch (vmcnt(0)) every K-step and is latency-bound at ~30 % MFMA busy.
-constexpr int kWideDma = 6;  // DMA instructions per wave per stage: 4 X (2 sub-tiles x 16 / 8 waves) + 2 dY
+// BKP = 32 (PDT_WGRAD_WIDE_BKP=32): 24 KB stages, two workgroups per CU (4 waves per SIMD, <= 128 VGPRs).
+// DMA instructions per wave per stage: X 2 sub-tiles x BKP/4 rows-of-4 over 8 waves, dY BKP/4 over 8 waves.
+template <int BKP>
+constexpr int wide_dma() { return 2 * (BKP / 4) / 8 + (BKP / 4) / 8; }
 
-template <int DT>
-__global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
+template <int DT, int BKP>
+__global__ __launch_bounds__(512, BKP == 32 ? 2 : 1) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
-  constexpr int BKP = 64;          // pixels per K-step
+  constexpr int kWideDma = wide_dma<BKP>();
+  constexpr int XI = BKP / 4 / 8;  // DMA instructions per wave per sub-tile image (X: 2 sub-tiles, dY: 1)
   constexpr int ROWB = 256;        // 128 channels * 2 B
-  constexpr int SUB = BKP * ROWB;  // 16 KiB: one column block's X image, or the dY image
+  constexpr int SUB = BKP * ROWB;  // one column block's X image, or the dY image
   constexpr int STAGE = 3 * SUB;   // X block 0 | X block 1 | dY
   constexpr int NST = 3;
   __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
@@ -686,20 +699,21 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
   auto stage_load = [&](int step, int buf) {
     const int pbase = pix_begin + step * BKP;
     char* sb = smem + buf * STAGE;
+    constexpr int RI = BKP / 4;  // DMA instructions (4 rows each) per sub-tile image
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // X: instruction i = wave * 4 + j of 32 (sub-tile i >> 4)
-      const int i = wave * 4 + j;
-      const int h = i >> 4;
-      const int row = (i & 15) * 4 + lrow;  // 0..63
+    for (int j = 0; j < 2 * XI; ++j) {  // X: instruction i = wave * 2XI + j of 2RI (sub-tile i / RI)
+      const int i = wave * 2 * XI + j;
+      const int h = i / RI;
+      const int row = (i % RI) * 4 + lrow;  // 0..BKP-1
       const int lch = pch ^ tr_swz16(row);
       uint32_t xo, yo;
       wgrad_rows<false>(a, pbase + row, th2[h], tw2[h], cb0[h], lch, k0, xo, yo);
       if (h && !half1_live) xo = kOOB;
-      buf_lds16_asm(rx, sb + h * SUB + (i & 15) * 1024, xo);
+      buf_lds16_asm(rx, sb + h * SUB + (i % RI) * 1024, xo);
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {  // dY: instruction i = wave * 2 + j of 16
-      const int i = wave * 2 + j;
+    for (int j = 0; j < XI; ++j) {  // dY: instruction i = wave * XI + j of RI
+      const int i = wave * XI + j;
       const int row = i * 4 + lrow;
       const int lch = pch ^ tr_swz16(row);
       uint32_t xo, yo;
@@ -1304,7 +1318,8 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
     // one full round: each block then streams ~130 K-steps (ResNet-18 layer3/4), amortising its prologue
     // and its 256 KB fp32 partial; measured faster than two rounds (tools/conv_bench.py wgrad_256 column)
     (void)target_blocks;
-    splits = cus / tiles > 0 ? cus / tiles : 1;
+    const int per_cu = (a.tile == kWgradWide && wide_bkp() == 32) ? 2 : 1;
+    splits = per_cu * cus / tiles > 0 ? per_cu * cus / tiles : 1;
   }
   const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
@@ -1330,9 +1345,16 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   } else if (a.tile == kWgradWide) {
     PDT_COUNT("conv_wgrad_wide");
     if (dtype == kBF16)
-      hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16>), dim3(nwg), dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
+    if (wide_bkp() == 32) {
+      if (dtype == kBF16)
+        hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16, 32>), dim3(nwg), dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16, 32>), dim3(nwg), dim3(512), 0, s, a);
+    } else if (dtype == kBF16) {
+      hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16, 64>), dim3(nwg), dim3(512), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16, 64>), dim3(nwg), dim3(512), 0, s, a);
+    }
   } else if (a.tile == 128 && a.C == 64) {
     PDT_COUNT("conv_wgrad_128_pair");
     if (dtype == kBF16)

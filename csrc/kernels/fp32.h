@@ -57,6 +57,16 @@ struct Wgrad32Args {
   // are 8 pixels x 4 channels of row 2t (chunks 0..7) then of row 2t+1 (chunks 8..15 read element sc * 4 + pair_skip:
   // pair_skip = one padded row - 32)
   int cs = 0, pair_skip = 0, tstep = 1;
+  // 4-pair stem kernel only (f_y != nullptr): dY is not read but computed per staged chunk from the max-pool backward,
+  // the ReLU mask and the BN-backward apply (the math of stem_pool_bwd_apply32): f_dp / f_idx pooled gradient and
+  // argmax [N][f_OH][f_OW][64], f_y the conv output [P][64], f_coef the forward BN coefficients (scale | shift),
+  // f_bcoef the backward apply's A | B | C (64 each)
+  const float* f_dp = nullptr;
+  const uint8_t* f_idx = nullptr;
+  const float* f_y = nullptr;
+  const float* f_coef = nullptr;
+  const float* f_bcoef = nullptr;
+  int f_OH = 0, f_OW = 0;
 };
 void wgrad32_launch(const Wgrad32Args& a, hipStream_t s);
 

@@ -653,12 +653,62 @@ __global__ __launch_bounds__(256) void wgrad32_kernel(Wgrad32Args a) {
       }
 }
 
+// dY of the fp32 stem backward for 4 channels of one conv-output pixel, in two halves so the loads can be issued
+// ahead of the MFMAs that hide them: stem_dy32_load gathers the conv output and the (up to 4) pooling windows that
+// can select the pixel; stem_dy32_finish applies the max-pool backward, the ReLU mask and dy = A*dz + B*y + C --
+// the float operations and their order are stem_pool_dz32's + stem_pool_bwd_apply32's (windows in (oh, ow)
+// ascending order, invalid ones skipped), so the result is the separate apply pass's.
+struct StemDy32In {
+  f32x4v yy, gv[4];
+  uint32_t ib[4];
+  int pos[4];  // kernel tap (kh * 3 + kw) of the pixel in window wi, -1: no such window
+};
+PDT_DEVICE void stem_dy32_load(const Wgrad32Args& a, int64_t p, int c0, StemDy32In& in) {
+  const int PQ = a.Pm * a.Qm;
+  const int n = (int)(p / PQ);
+  const int rem = (int)(p - (int64_t)n * PQ);
+  const int h = rem / a.Qm, w = rem - (rem / a.Qm) * a.Qm;
+  in.yy = *(const f32x4v*)(a.f_y + p * 64 + c0);
+  const int oh0 = h >> 1, oh1 = (h + 1) >> 1, ow0 = w >> 1, ow1 = (w + 1) >> 1;
+#pragma unroll
+  for (int wi = 0; wi < 4; ++wi) {
+    const int oh = wi >> 1 ? oh1 : oh0, ow = wi & 1 ? ow1 : ow0;
+    const int kh = h - (oh * 2 - 1), kw = w - (ow * 2 - 1);
+    const bool ok = (!(wi >> 1) || oh1 != oh0) && (!(wi & 1) || ow1 != ow0) && oh < a.f_OH && ow < a.f_OW &&
+                    kh >= 0 && kh <= 2 && kw >= 0 && kw <= 2;
+    in.pos[wi] = ok ? kh * 3 + kw : -1;
+    const int64_t o = (((int64_t)n * a.f_OH + (ok ? oh : oh0)) * a.f_OW + (ok ? ow : ow0)) * 64 + c0;
+    in.ib[wi] = *(const uint32_t*)(a.f_idx + o);
+    in.gv[wi] = *(const f32x4v*)(a.f_dp + o);
+  }
+}
+PDT_DEVICE f32x4v stem_dy32_finish(const Wgrad32Args& a, const StemDy32In& in, int c0) {
+  f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int wi = 0; wi < 4; ++wi) {
+    if (in.pos[wi] < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if ((int)((in.ib[wi] >> (8 * e)) & 0xffu) == in.pos[wi]) acc[e] += in.gv[wi][e];
+  }
+  const f32x4v yy = in.yy;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (!(yy[e] * a.f_coef[c0 + e] + a.f_coef[64 + c0 + e] > 0.f)) acc[e] = 0.f;
+  const float* b = a.f_bcoef;
+  return *(const f32x4v*)(b + c0) * acc + *(const f32x4v*)(b + 64 + c0) * yy + *(const f32x4v*)(b + 128 + c0);
+}
+
 // Window-pair stem weight gradient with ALL kernel-row pairs per block (the fp32 twin of the 16-bit
 // wgrad_stem_kernel): wgrad32_kernel runs one block per (pair, split) and so stages every dY tile once per pair
 // (4x) at 16 FLOP per staged byte.  Here a block stages one 32-pixel dY tile plus the 4 pair-windows of X (8 KB
 // each, 40 KB per stage, 2-deep ring: 80 KB, two blocks per CU) and 8 waves own (pair = wave / 2) x (32 window
 // columns) x all 64 output channels: 26 FLOP per staged byte.  Same LDS element layout and window addressing as
 // wgrad32_kernel (Wgrad32Args window-pair fields).
+// FUSE (Wgrad32Args::f_y): the dY tile of every chunk is computed in the kernel (stem_dy32_*) instead of DMA'd --
+// the separate apply pass and its 3.85 GB fp32 dY write + re-read (ResNet-18, B = 1200) disappear.  A thread owns 4
+// channels of one pixel row; the next chunk's gathers are issued before this chunk's MFMAs and finished after them.
+template <bool FUSE>
 __global__ __launch_bounds__(512) void wgrad32_stem4_kernel(Wgrad32Args a) {
   constexpr int PIX = 32;             // pixels per staged chunk
   constexpr int TILE = PIX * 64 * 4;  // 8 KiB per operand tile ([pixel][64] fp32, 256 B rows)
@@ -684,6 +734,7 @@ __global__ __launch_bounds__(512) void wgrad32_stem4_kernel(Wgrad32Args a) {
     for (int q = 0; q < INS; ++q) {
       const int ins = wave * INS + q;  // 0..39: tile ins / 8, rows (ins % 8) * 4 + lrow
       const int tile = ins >> 3;
+      if (FUSE && tile == 0) continue;  // dY computed by dy_store
       const int row = (ins & 7) * 4 + lrow;
       const int64_t p = p0 + row;
       uint32_t off = kOOB;
@@ -721,14 +772,34 @@ __global__ __launch_bounds__(512) void wgrad32_stem4_kernel(Wgrad32Args a) {
     const int col = wc * 32 + j * 16 + fr;
     boff[j] = (1 + wt) * TILE + fq * 256 + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
   }
+  // FUSE: this thread's dY element group -- pixel row dr of the chunk, channels dc .. dc+3 (of the block's k0 slab)
+  const int dr = tid >> 4, dc = k0 + (tid & 15) * 4;
+  StemDy32In din;
+  auto dy_load = [&](int64_t p0) {
+    const int64_t p = p0 + dr;
+    stem_dy32_load(a, p < p_end ? p : p_begin, dc, din);
+  };
+  auto dy_store = [&](int64_t p0, int buf) {
+    const f32x4v v = p0 + dr < p_end ? stem_dy32_finish(a, din, dc) : f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int chunk = tid & 15;
+    *(f32x4v*)(smem + buf * STAGE + dr * 256 + ((chunk ^ ((dr & 3) << 2)) << 4)) = v;
+  };
   const int nchunks = p_end > p_begin ? (int)((p_end - p_begin + PIX - 1) / PIX) : 0;
   if (nchunks > 0) {
     stage(p_begin, 0);
+    if constexpr (FUSE) {
+      dy_load(p_begin);
+      dy_store(p_begin, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int ch = 0; ch < nchunks; ++ch) {
       const int cur = ch & 1;
-      if (ch + 1 < nchunks) stage(p_begin + (int64_t)(ch + 1) * PIX, cur ^ 1);
+      const int64_t pn = p_begin + (int64_t)(ch + 1) * PIX;
+      if (ch + 1 < nchunks) {
+        stage(pn, cur ^ 1);
+        if constexpr (FUSE) dy_load(pn);
+      }
       const char* base = smem + cur * STAGE;
 #pragma unroll 4
       for (int s4 = 0; s4 < PIX / 4; ++s4) {
@@ -742,6 +813,9 @@ __global__ __launch_bounds__(512) void wgrad32_stem4_kernel(Wgrad32Args a) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      }
+      if constexpr (FUSE) {
+        if (ch + 1 < nchunks) dy_store(pn, cur ^ 1);  // slot cur ^ 1 was last read in chunk ch - 1
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -997,9 +1071,16 @@ void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
         a.pix_per_split % 32 != 0)
       pdt_hip_fail("wgrad32: the 4-pair stem kernel needs the window-pair geometry (cs 4, 4 pairs, C 64)",
                    hipErrorInvalidValue, __FILE__, __LINE__);
-    PDT_COUNT("wgrad32_stem4");
     dim3 grid(a.splits, a.Kout / 64), block(512);
-    hipLaunchKernelGGL(wgrad32_stem4_kernel, grid, block, 0, s, a);
+    if (a.f_y != nullptr) {
+      if (a.Kout != 64)
+        pdt_hip_fail("wgrad32: the fused stem kernel needs Kout == 64", hipErrorInvalidValue, __FILE__, __LINE__);
+      PDT_COUNT("wgrad32_stem4_fused");
+      hipLaunchKernelGGL(wgrad32_stem4_kernel<true>, grid, block, 0, s, a);
+    } else {
+      PDT_COUNT("wgrad32_stem4");
+      hipLaunchKernelGGL(wgrad32_stem4_kernel<false>, grid, block, 0, s, a);
+    }
     return;
   }
   if (a.tile == 128) {

@@ -199,6 +199,9 @@ class ResNetExecutor32(ResNetExecutor):
     _FUSE_STEM = os.environ.get("PDT_FP32_STEM_FUSE", "1") == "1"
     # stem weight gradient: every kernel-row pair per block (dY staged once, not once per pair); 0: one block per pair
     _STEM4 = os.environ.get("PDT_FP32_STEM4", "1") == "1"
+    # ... and its dY computed inside that kernel from the pooled gradient, argmax, conv output and BN coefficients (the
+    # apply pass and the fp32 dY tensor disappear); PDT_FP32_STEM_WG_FUSE=0: stem_pool_bwd_apply32 + the plain kernel
+    _STEM_WG_FUSE = os.environ.get("PDT_FP32_STEM_WG_FUSE", "1") == "1"
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
                accumulate=False):
@@ -458,7 +461,7 @@ class ResNetExecutor32(ResNetExecutor):
         # stem: max-pool backward + ReLU mask (from the BN input) -> BN backward -> im2col weight gradient
         st, sbn = self.stem, self.stem_bn
         P0, Q0, H, W = saved["P0"], saved["Q0"], saved["H"], saved["W"]
-        dz0 = self._buf("dz0", saved["y0"].numel(), torch.float32)
+        dz0 = None
         if self._FUSE_STEM:  # dz recomputed by the reduce and the apply: never stored
             rows = N * P0 * Q0
             slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
@@ -466,9 +469,14 @@ class ResNetExecutor32(ResNetExecutor):
             blocks = max(1, min(4096, rows // 256))
             Cn.stem_pool_bwd_reduce32(g, saved["idx"], saved["y0"], sbn.coef, slots, blocks, N, P0, Q0, st.cout)
             self._bn_bwd_finish(slots, rows, sbn, None)
-            dy0 = dz0
-            Cn.stem_pool_bwd_apply32(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
+            wg_fused = (self.stem_win and self._STEM4 and self._STEM_WG_FUSE and self.stem_pairs == 4
+                        and st.cout == 64)
+            if not wg_fused:  # (fused: no 3.85 GB dY buffer at ResNet-18 B = 1200)
+                dy0 = dz0 = self._buf("dz0", saved["y0"].numel(), torch.float32)
+                Cn.stem_pool_bwd_apply32(g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, dy0, N, P0, Q0, st.cout)
         else:
+            wg_fused = False
+            dz0 = self._buf("dz0", saved["y0"].numel(), torch.float32)
             Cn.maxpool_bwd_relu32(g, saved["idx"], saved["y0"], sbn.coef, dz0, N, P0, Q0, st.cout)
             self.bn_reduce(sbn, dz0, None, saved["y0"], N * P0 * Q0)
             dy0 = dz0  # in place: each element read then written by the same thread
@@ -485,8 +493,12 @@ class ResNetExecutor32(ResNetExecutor):
             splits, pps = plan
             ldw = self.stem_pairs * 64
             ws = self._buf("ws", splits * st.cout * ldw, torch.float32)
-            Cn.wgrad32_stem(saved["xp"], dy0, ws, N, saved["Hp"], saved["Wp"], self.stem_pairs, st.cout, P0, Q0, st.st,
-                            splits, pps, 1 if (self._STEM4 and self.stem_pairs == 4) else 0)
+            if wg_fused:
+                Cn.wgrad32_stem_fused(saved["xp"], g, saved["idx"], saved["y0"], sbn.coef, sbn.bcoef, ws, N,
+                                      saved["Hp"], saved["Wp"], P0, Q0, st.st, splits, pps)
+            else:
+                Cn.wgrad32_stem(saved["xp"], dy0, ws, N, saved["Hp"], saved["Wp"], self.stem_pairs, st.cout, P0, Q0,
+                                st.st, splits, pps, 1 if (self._STEM4 and self.stem_pairs == 4) else 0)
             tmp = self._buf("stem_dw", st.cout * ldw, torch.float32)
             Cn.wgrad_reduce(ws, splits, st.cout, ldw, ldw, st.cout * ldw, tmp, ldw, 1.0, False)
             Cn.gather32(tmp, self.stem_gidx_win, self._g(st.slot))

@@ -403,3 +403,41 @@ def test_fp32_fused_stem_tail_matches_the_separate_passes(monkeypatch):
         assert (dict(native.C.dispatch_counts()).get("stem_pool_bwd_fused32", 0) > 0) == fuse
         outs.append(tr.flat.grad.clone())
     assert _rel(outs[1], outs[0]) < 1e-5
+
+
+def test_wgrad32_stem_fused_dy_matches_apply_then_wgrad():
+    """The 4-pair fp32 stem weight gradient with dY computed in the kernel (max-pool backward from the pooled gradient
+    and argmax, ReLU mask, BN-backward apply) equals stem_pool_bwd_apply32 followed by the plain 4-pair kernel: same
+    float operations in the same order -- random argmax codes included (border windows whose code points outside the
+    image select nothing in both), an odd pooled width, and a split whose last chunk is partial."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    torch.manual_seed(6)
+    N, H, W = 2, 42, 38
+    x = torch.randn(N, 3, H, W, device=DEV)
+    P, Q = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    OH, OW = (P - 1) // 2 + 1, (Q - 1) // 2 + 1
+    Hp, Wp = max(H + 6, (P - 1) * 2 + 8), max(W + 6, (Q - 1) * 2 + 8)
+    xp = torch.empty(N * Hp * Wp * 4, device=DEV)
+    C.stem_pack32(x, xp, N, 3, H, W, 3, Hp, Wp)
+    y0 = torch.randn(N * P * Q * 64, device=DEV)
+    dp = torch.randn(N * OH * OW * 64, device=DEV)
+    idx = torch.randint(0, 9, (N * OH * OW * 64,), device=DEV, dtype=torch.uint8)
+    coef = torch.cat([torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.3,  # scale | shift
+                      torch.randn(64, device=DEV), torch.rand(64, device=DEV) + 0.5])  # mean | invstd
+    bcoef = torch.randn(192, device=DEV)
+    npix = N * P * Q
+    pps = ((npix + 4) // 5 + 63) // 64 * 64
+    splits = (npix + pps - 1) // pps
+    assert npix % 32 != 0 or splits * pps > npix
+    dy = torch.empty(npix * 64, device=DEV)
+    C.stem_pool_bwd_apply32(dp, idx, y0, coef, bcoef, dy, N, P, Q, 64)
+    ws_ref = torch.zeros(splits * 64 * 256, device=DEV)
+    C.wgrad32_stem(xp, dy, ws_ref, N, Hp, Wp, 4, 64, P, Q, 2, splits, pps, 1)
+    ws = torch.zeros(splits * 64 * 256, device=DEV)
+    C.reset_dispatch_counts()
+    C.wgrad32_stem_fused(xp, dp, idx, y0, coef, bcoef, ws, N, Hp, Wp, P, Q, 2, splits, pps)
+    torch.cuda.synchronize()
+    assert dict(C.dispatch_counts()).get("wgrad32_stem4_fused", 0) == 1
+    assert _rel(ws, ws_ref) < 1e-6, _rel(ws, ws_ref)
+    print("bit-identical:", torch.equal(ws, ws_ref))
