@@ -1344,7 +1344,6 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
   } else if (a.tile == kWgradWide) {
     PDT_COUNT("conv_wgrad_wide");
-    if (dtype == kBF16)
     if (wide_bkp() == 32) {
       if (dtype == kBF16)
         hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16, 32>), dim3(nwg), dim3(512), 0, s, a);
@@ -1396,6 +1395,7 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
     else
       hipLaunchKernelGGL((conv_wgrad_kernel<kF16, false>), dim3(nwg), dim3(256), 0, s, a);
   }
+  PDT_HIP_CHECK(hipGetLastError());  // a refused launch (e.g. LDS / register limits) must not leave ws stale
 }
 
 void wgrad_reduce_launch(const float* ws, int splits, int rows, int cols, int ldw, int64_t split_stride,

@@ -31,6 +31,8 @@ from ..ops import native
 from ..ops.conv import conv_tile as _conv_tile, dgrad_phases, dgrad_weight_index
 from .resnet import BasicBlock, Bottleneck, ResNet
 
+_BUF_POISON = os.environ.get("PDT_BUF_POISON", "0") == "1"
+
 class _Conv:
     """Static description of one convolution and its derived (dgrad) weight layouts."""
 
@@ -265,6 +267,8 @@ class ResNetExecutor:
                 t = full[:numel]
             else:
                 t = torch.empty(numel, dtype=dtype, device=self.device)
+                if _BUF_POISON:  # PDT_BUF_POISON=1: NaN / 0xFF so a buffer read before any kernel wrote it shows
+                    t.fill_(float("nan") if t.is_floating_point() else -1)
             self._bufs[k] = t
         if self._pending_reads:  # the caller is about to overwrite it: wait for side-stream readers
             ev = self._pending_reads.pop(t.data_ptr(), None)

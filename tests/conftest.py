@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# every executor work buffer starts as NaN / 0xFF (models/executor.py _buf): a kernel that silently does not run (e.g. a
+# refused launch or a dtype branch that skips it) shows up as NaN instead of as a stale buffer's plausible values
+os.environ.setdefault("PDT_BUF_POISON", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

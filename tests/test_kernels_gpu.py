@@ -66,13 +66,14 @@ def test_conv_dgrad(case):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_wgrad(case):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_wgrad(case, dtype):
     from pytorch_distributed_template_amd.ops import conv
     N, H, W, C, K, R, st, pad = case
     torch.manual_seed(2)
     P, Q = conv.out_hw(H, W, R, R, st, pad)
-    x = _rand16(N, H, W, C)
-    dy = _rand16(N, P, Q, K)
+    x = _rand16(N, H, W, C, dtype=dtype)
+    dy = _rand16(N, P, Q, K, dtype=dtype)
     dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=64)
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
                                       stride=st, padding=pad).permute(0, 2, 3, 1)
@@ -82,7 +83,8 @@ def test_conv_wgrad(case):
 @pytest.mark.parametrize("case", [(2, 15, 13, 64, 256, 3, 2, 1), (4, 14, 14, 64, 128, 3, 1, 1),
                                   (3, 14, 14, 64, 128, 1, 2, 0), (2, 9, 9, 64, 384, 1, 1, 0)])
 @pytest.mark.parametrize("target", [64, 2048])
-def test_conv_wgrad_two_tap_pair_tile(case, target):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_wgrad_two_tap_pair_tile(case, target, dtype):
     """C == 64, Kout % 128 == 0 runs the 128x128 wgrad kernel with its c side split over two taps (an odd tap count
     leaves the last tile's second half dead): every tap's dW against torch fp32, few and many splits."""
     from pytorch_distributed_template_amd.ops import conv, native
@@ -90,8 +92,8 @@ def test_conv_wgrad_two_tap_pair_tile(case, target):
     P, Q = conv.out_hw(H, W, R, R, st, pad)
     assert native.C.conv_wgrad_plan(K, R, R, C, N * P * Q, target, False)[2] == 128
     torch.manual_seed(12)
-    x = _rand16(N, H, W, C)
-    dy = _rand16(N, P, Q, K)
+    x = _rand16(N, H, W, C, dtype=dtype)
+    dy = _rand16(N, P, Q, K, dtype=dtype)
     dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=target)
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
                                       stride=st, padding=pad).permute(0, 2, 3, 1)
@@ -103,7 +105,8 @@ def test_conv_wgrad_two_tap_pair_tile(case, target):
                                   (3, 9, 9, 256, 128, 1, 1, 0), (2, 10, 10, 128, 128, 1, 2, 0),
                                   (1, 7, 7, 384, 128, 3, 1, 1)])
 @pytest.mark.parametrize("target", [64, 2048])
-def test_conv_wgrad_wide_tile(case, target):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_wgrad_wide_tile(case, target, dtype):
     """C % 128 == 0 and Kout % 128 == 0 below 256 x 256: the wide 256 (two 128-wide column blocks of dW) x 128 kernel
     with its 3-deep counted-wait DMA ring.  Every column block against torch fp32 (an odd block count leaves the last
     tile's second half dead), few and many splits (a split of one K-step drains the ring at once)."""
@@ -112,8 +115,8 @@ def test_conv_wgrad_wide_tile(case, target):
     P, Q = conv.out_hw(H, W, R, R, st, pad)
     assert native.C.conv_wgrad_plan(K, R, R, C, N * P * Q, target, False)[2] == 2  # kWgradWide
     torch.manual_seed(14)
-    x = _rand16(N, H, W, C)
-    dy = _rand16(N, P, Q, K)
+    x = _rand16(N, H, W, C, dtype=dtype)
+    dy = _rand16(N, P, Q, K, dtype=dtype)
     dw = conv.conv_wgrad(x, dy, R, R, st, pad, target_blocks=target)
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dy.float().permute(0, 3, 1, 2),
                                       stride=st, padding=pad).permute(0, 2, 3, 1)
