@@ -728,9 +728,27 @@ void scatter32(const Tensor& src, const Tensor& idx, Tensor& dst) {
 const float* pfc(const OptT& t, const char* name) { return t.has_value() ? pf(*t, name) : nullptr; }
 
 // forward conv over fp32 NHWC / KRSC (same geometry arguments as conv_fwd; stats -> fp64 slots)
+void conv32_fwd_impl(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N,
+                     int64_t H, int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm,
+                     int64_t stride, int64_t pad, int64_t bm, int64_t bn, const OptT& pre);
+
 void conv32_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N, int64_t H,
                 int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride,
                 int64_t pad, int64_t bm, int64_t bn) {
+  conv32_fwd_impl(x, w, y, res, stats, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, bm, bn, {});
+}
+
+// conv32_fwd over the RAW output of the producer conv: its BatchNorm + ReLU (pre = coef [scale | shift | ...] x C) is
+// applied to the activation fragments in the kernel (relu(bn(x)) is never written)
+void conv32_fwd_pre(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t N, int64_t H, int64_t W,
+                    int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad,
+                    int64_t bm, int64_t bn, const Tensor& pre) {
+  conv32_fwd_impl(x, w, y, {}, stats, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, bm, bn, pre);
+}
+
+void conv32_fwd_impl(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N,
+                     int64_t H, int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm,
+                     int64_t stride, int64_t pad, int64_t bm, int64_t bn, const OptT& pre) {
   TORCH_CHECK(x.numel() == N * H * W * C && w.numel() == Kout * T * U * C && y.numel() == N * Pm * Qm * Kout,
               "conv32_fwd: size mismatch");
   TORCH_CHECK(C % 32 == 0 && Kout % bn == 0, "conv32_fwd: C % 32 / Kout % bn must be 0");
@@ -750,6 +768,10 @@ void conv32_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, co
   a.ist_h = stride; a.ist_w = stride; a.ioff_h = -pad; a.ioff_w = -pad; a.tstep_h = 1; a.tstep_w = 1;
   a.OH = Pm; a.OW = Qm; a.ost_h = 1; a.ost_w = 1; a.ooff_h = 0; a.ooff_w = 0;
   a.M = N * Pm * Qm;
+  if (pre.has_value()) {
+    TORCH_CHECK(pre->numel() >= 2 * C, "conv32_fwd_pre: pre needs scale and shift for every input channel");
+    a.pre_coef = pf(*pre, "pre");
+  }
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
 }
 
@@ -769,14 +791,17 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
     TORCH_CHECK(res->numel() == dx.numel(), "conv32_dgrad: residual size");
     a.res = pf(*res, "res");
   }
-  if (bn_mref.has_value()) {  // fused BN-backward reduce (Conv32Args::bnb)
-    TORCH_CHECK(bn_y1.has_value() && bn_coef.has_value() && stats.has_value(),
-                "conv32_dgrad: the fused BN-backward reduce needs mref, y1, coef and stats");
+  if (bn_y1.has_value()) {  // fused BN-backward reduce (Conv32Args::bnb); no mref: ReLU mask from y1 * scale + shift
+    TORCH_CHECK(bn_coef.has_value() && stats.has_value(),
+                "conv32_dgrad: the fused BN-backward reduce needs y1, coef and stats");
     const int64_t KO = bn_y2.has_value() ? 4 : 2;
-    TORCH_CHECK(bn_mref->numel() == dx.numel() && bn_y1->numel() == dx.numel() && bn_coef->numel() >= 4 * C &&
-                stats->numel() >= pdt::kStatSlots * C * KO, "conv32_dgrad: fused BN-backward operand sizes");
+    TORCH_CHECK((!bn_mref.has_value() || bn_mref->numel() == dx.numel()) && bn_y1->numel() == dx.numel() &&
+                bn_coef->numel() >= 4 * C && stats->numel() >= pdt::kStatSlots * C * KO,
+                "conv32_dgrad: fused BN-backward operand sizes");
     a.bnb = 1;
-    a.bn_mref = pf(*bn_mref, "bn_mref"); a.bn_y1 = pf(*bn_y1, "bn_y1"); a.bn_coef = pf(*bn_coef, "bn_coef");
+    TORCH_CHECK(bn_mref.has_value() || !bn_y2.has_value(), "conv32_dgrad: two BN branches need the mask reference");
+    a.bn_mref = bn_mref.has_value() ? pf(*bn_mref, "bn_mref") : nullptr;
+    a.bn_y1 = pf(*bn_y1, "bn_y1"); a.bn_coef = pf(*bn_coef, "bn_coef");
     a.stats = pd(*stats, "stats");
     if (bn_y2.has_value()) {
       TORCH_CHECK(bn_coef2.has_value() && bn_y2->numel() == dx.numel() && bn_coef2->numel() >= 4 * C,
@@ -805,9 +830,27 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
 }
 
+void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
+                  int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw,
+                  int64_t splits, int64_t pix_per_split, int64_t tile, const OptT& pre);
+
 void wgrad32(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
              int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw, int64_t splits,
              int64_t pix_per_split, int64_t tile) {
+  wgrad32_impl(x, dy, ws, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, ldw, splits, pix_per_split, tile, {});
+}
+
+// wgrad32 with x the producer conv's raw output and its BatchNorm + ReLU (pre = coef) applied in the kernel
+// (tile 128 or 3 only)
+void wgrad32_pre(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
+                 int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw,
+                 int64_t splits, int64_t pix_per_split, int64_t tile, const Tensor& pre) {
+  wgrad32_impl(x, dy, ws, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, ldw, splits, pix_per_split, tile, pre);
+}
+
+void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
+                  int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw,
+                  int64_t splits, int64_t pix_per_split, int64_t tile, const OptT& pre) {
   TORCH_CHECK(tile == 64 || tile == 128 || tile == 3, "wgrad32: tile must be 64, 128 or 3 (3x3 halo kernel)");
   const int64_t cb = tile == 3 ? 64 : tile;
   TORCH_CHECK(C % cb == 0 && Kout % cb == 0, "wgrad32: C and Kout must be multiples of the tile");
@@ -826,6 +869,10 @@ void wgrad32(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H
   a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
   a.stride = stride; a.pad = pad; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
   a.P = N * Pm * Qm;
+  if (pre.has_value()) {
+    TORCH_CHECK(pre->numel() >= 2 * C && (tile == 128 || tile == 3), "wgrad32_pre: coef size / tile (128 or 3)");
+    a.pre_coef = pf(*pre, "pre");
+  }
   pdt::wgrad32_launch(a, cur_stream());
 }
 
@@ -879,6 +926,15 @@ void stem_pool_bwd_reduce32(const Tensor& dp, const Tensor& idx, const Tensor& y
   check_dev(idx, "idx");
   pdt::stem_pool_bwd_reduce32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"),
                                      pd(slots, "slots"), (int)blocks, N, H, W, C, cur_stream());
+}
+
+void stem_pool_bwd_reduce_out32(const Tensor& dp, const Tensor& out, const Tensor& coef, Tensor& slots, int64_t blocks,
+                                int64_t C) {
+  TORCH_CHECK(dp.numel() == out.numel() && dp.numel() % C == 0 && C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0 &&
+                  coef.numel() >= 4 * C && slots.numel() >= pdt::kStatSlots * C * 2 && blocks >= 1,
+              "stem_pool_bwd_reduce_out32: bad sizes");
+  pdt::stem_pool_bwd_reduce_out32_launch(pf(dp, "dp"), pf(out, "out"), pf(coef, "coef"), pd(slots, "slots"),
+                                         (int)blocks, dp.numel() / C, (int)C, cur_stream());
 }
 
 void stem_pool_bwd_apply32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, const Tensor& b,
@@ -1100,6 +1156,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_coef") = py::none(), py::arg("stats") = py::none(), py::arg("bn_y2") = py::none(),
         py::arg("bn_coef2") = py::none());
   m.def("wgrad32", &wgrad32);
+  m.def("wgrad32_pre", &wgrad32_pre);
+  m.def("conv32_fwd_pre", &conv32_fwd_pre);
   m.def("bn_apply32", &bn_apply32);
   m.def("bn_bwd_reduce32_blocks", &bn_bwd_reduce32_blocks);
   m.def("bn_bwd_reduce32", &bn_bwd_reduce32);
@@ -1108,6 +1166,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd_relu32", &maxpool_bwd_relu32);
   m.def("stem_pool_bwd_reduce32", &stem_pool_bwd_reduce32);
   m.def("stem_pool_bwd_apply32", &stem_pool_bwd_apply32);
+  m.def("stem_pool_bwd_reduce_out32", &stem_pool_bwd_reduce_out32);
   m.def("avgpool32_fwd", &avgpool32_fwd);
   m.def("avgpool32_bwd", &avgpool32_bwd);
   m.def("xent32", &xent32);

@@ -174,12 +174,34 @@ class ResNetExecutor32(ResNetExecutor):
                 return self._BM64, 64
         return 128, self._bn_tile(n)
 
-    def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool):
+    def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, pre=None):
+        """``pre``: x is the producer conv's raw output and ``pre`` its BN coefficients -- BN + ReLU applied to the
+        activation fragments inside the kernel (``_pre_ok``)."""
         P, Q = c.out_hw(H, W)
         sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
-        self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad,
-                          *self._tile32(c.cout, N * P * Q))
+        if pre is not None:
+            self.C.conv32_fwd_pre(x, self._w32(c), y, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad,
+                                  *self._tile32(c.cout, N * P * Q), pre)
+        else:
+            self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad,
+                              *self._tile32(c.cout, N * P * Q))
         return P, Q, sp
+
+    # PDT_FP32_PRE=1: the inner BatchNorms' BN + ReLU (SURVEY §7.2 P5) applied by their consumer conv's kernels --
+    # forward fragments and the weight gradient's staged input -- instead of a bn_apply32 pass writing relu(bn(y));
+    # the backward's ReLU mask comes from y and the BN coefficients.  Bit-identical to the separate pass, but OFF by
+    # default: measured 126.1 -> 129.7 ms/step (the fused kernels run 14-21 % slower, +4.6 ms, against the 1.2 ms of
+    # bn_apply32 passes removed: the transform sits between the fragment reads and the MFMAs; profiles/r4_fp32_pre.md)
+    _PRE = os.environ.get("PDT_FP32_PRE", "0") == "1"
+
+    def _pre_ok(self, c: _Conv, H: int, W: int) -> bool:
+        """Can conv ``c`` (input H x W) consume its producer's raw output: its weight gradient must run on a kernel with
+        the fused prologue (3x3 halo or 128-wide tile), the backward's BN reduce must be the fused dgrad epilogue
+        (its ReLU mask is recomputed from y), and the input channels fit the kernels' coefficient tables."""
+        if not (self._PRE and self._FUSE_BN) or c.cin > 256:
+            return False
+        P, Q = c.out_hw(H, W)
+        return self._wgrad_tile(c.cout, c.R, c.S, c.cin, H, W, P, Q, c.st, c.pad) in (3, 128)
 
     def _dgrad(self, c: _Conv, dy, N, H, W, P, Q, dx, res=None, bnb=None):
         """``bnb = (mref, y1, coef, slots)``: the consumer BatchNorm's backward reduce fused into the epilogue (dx then
@@ -202,19 +224,24 @@ class ResNetExecutor32(ResNetExecutor):
     # ... and its dY computed inside that kernel from the pooled gradient, argmax, conv output and BN coefficients (the
     # apply pass and the fp32 dY tensor disappear); PDT_FP32_STEM_WG_FUSE=0: stem_pool_bwd_apply32 + the plain kernel
     _STEM_WG_FUSE = os.environ.get("PDT_FP32_STEM_WG_FUSE", "1") == "1"
+    # stem BN-backward sums over the pooled output (mask out > 0, BN input recovered from out) instead of the window
+    # gather over the 112x112 conv output; PDT_FP32_STEM_REDUCE_OUT=0: stem_pool_bwd_reduce32
+    _STEM_REDUCE_OUT = os.environ.get("PDT_FP32_STEM_REDUCE_OUT", "1") == "1"
 
-    def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
-               accumulate=False):
-        ldw = R * S * C
-        npix = N * P * Q
+    def _wgrad_tile(self, cout, R, S, C, H, W, P, Q, st, pad) -> int:
         # 3x3 / s1 / p1 over 64-channel blocks with wide rows (layer1): the halo kernel, all three taps of a kernel
         # row per block (48 FLOP per staged byte); else 128 x 128 / 8-wave tiles when both channel counts allow
         # (32 FLOP/B), else 64 x 64 (16 FLOP/B)
         if (self._HALO and R == 3 and S == 3 and st == 1 and pad == 1 and P == H and Q == W and 28 <= Q <= 62
                 and C == 64 and cout % 64 == 0):
-            tile = 3
-        else:
-            tile = 128 if (self._WIDE and C % 128 == 0 and cout % 128 == 0) else 64
+            return 3
+        return 128 if (self._WIDE and C % 128 == 0 and cout % 128 == 0) else 64
+
+    def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
+               accumulate=False, pre=None):
+        ldw = R * S * C
+        npix = N * P * Q
+        tile = self._wgrad_tile(cout, R, S, C, H, W, P, Q, st, pad)
         key = (cout, R, S, C, npix, tile)
         plan = self._plans.get(key)
         if plan is None:
@@ -232,7 +259,10 @@ class ResNetExecutor32(ResNetExecutor):
             plan = self._plans[key] = (splits, pps)
         splits, pps = plan
         ws = self._buf("ws", splits * cout * ldw, torch.float32)
-        self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile)
+        if pre is not None:
+            self.C.wgrad32_pre(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile, pre)
+        else:
+            self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile)
         self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, accumulate)
 
     def _stem_chunk(self, N: int) -> int:
@@ -304,11 +334,11 @@ class ResNetExecutor32(ResNetExecutor):
         recs = []
         for bi, b in enumerate(self.blocks):
             rec = {"x": x, "H": Hc, "W": Wc, "C": Cc, "ys": [], "as": [], "hw": []}
-            cur, h, w = x, Hc, Wc
+            cur, h, w, pre = x, Hc, Wc, None
             for ci, (c, bn) in enumerate(zip(b["convs"], b["bns"])):
                 P, Q = c.out_hw(h, w)
                 y = self._buf(("y", bi, ci), N * P * Q * c.cout, torch.float32)
-                _, _, sp = self._conv_fwd(c, cur, N, h, w, y, train)
+                _, _, sp = self._conv_fwd(c, cur, N, h, w, y, train, pre=pre)
                 if train:
                     self.bn_train_finalize(bn, sp, 0, N * P * Q)
                 else:
@@ -316,10 +346,14 @@ class ResNetExecutor32(ResNetExecutor):
                 rec["ys"].append(y)
                 rec["hw"].append((h, w, P, Q))
                 if ci < len(b["convs"]) - 1:
-                    a = self._buf(("a", bi, ci), y.numel(), torch.float32)
-                    Cn.bn_apply32(y, bn.coef, None, None, a, c.cout, 0, True)
-                    rec["as"].append(a)
-                    cur = a
+                    if self._pre_ok(b["convs"][ci + 1], P, Q):  # the consumer applies BN + ReLU: no activation
+                        rec["as"].append(None)
+                        cur, pre = y, bn.coef
+                    else:
+                        a = self._buf(("a", bi, ci), y.numel(), torch.float32)
+                        Cn.bn_apply32(y, bn.coef, None, None, a, c.cout, 0, True)
+                        rec["as"].append(a)
+                        cur, pre = a, None
                 h, w = P, Q
             cl, bnl = b["convs"][-1], b["bns"][-1]
             out = self._buf(("out", bi), N * h * w * cl.cout, torch.float32)
@@ -423,14 +457,17 @@ class ResNetExecutor32(ResNetExecutor):
             for ci in range(len(convs) - 1, -1, -1):
                 c = convs[ci]
                 h, w, P, Q = rec["hw"][ci]
-                xin = rec["as"][ci - 1] if ci > 0 else x
+                xin, pre = (rec["as"][ci - 1], None) if ci > 0 else (x, None)
+                if ci > 0 and xin is None:  # fused producer BN + ReLU (forward): x = the raw conv output
+                    xin, pre = rec["ys"][ci - 1], bns[ci - 1].coef
                 self._wgrad(c.cout, xin, dy, N, h, w, c.cin, c.R, c.S, P, Q, c.st, c.pad, self._g(c.slot),
-                            c.R * c.S * c.cin)
+                            c.R * c.S * c.cin, pre=pre)
                 self.grad_ready(c.pid)
                 if ci > 0:
                     da = self._buf("da", N * h * w * c.cin, torch.float32)
                     bnp, yp, ap = bns[ci - 1], rec["ys"][ci - 1], rec["as"][ci - 1]
-                    if self._FUSE_BN:  # dgrad epilogue writes dz and reduces the inner BN's backward sums
+                    if self._FUSE_BN:  # dgrad epilogue writes dz and reduces the inner BN's backward sums (ReLU
+                        # mask from ap, or -- fused producer BN, ap is None -- from yp * scale + shift)
                         slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
                         self._dgrad(c, dy, N, h, w, P, Q, da, bnb=(ap, yp, bnp.coef, slots))
                         self._bn_bwd_finish(slots, N * h * w, bnp)
@@ -465,9 +502,13 @@ class ResNetExecutor32(ResNetExecutor):
         if self._FUSE_STEM:  # dz recomputed by the reduce and the apply: never stored
             rows = N * P0 * Q0
             slots = self._buf(("bnslots", st.cout, 2), self.n_slots * st.cout * 2, torch.float64)
-            # 4x the blocks of a plain reduce: the per-pixel window gather is latency-bound, not a stream
-            blocks = max(1, min(4096, rows // 256))
-            Cn.stem_pool_bwd_reduce32(g, saved["idx"], saved["y0"], sbn.coef, slots, blocks, N, P0, Q0, st.cout)
+            if self._STEM_REDUCE_OUT:
+                prow = saved["x0"].numel() // st.cout
+                Cn.stem_pool_bwd_reduce_out32(g, saved["x0"], sbn.coef, slots, max(1, min(2048, prow // 64)), st.cout)
+            else:
+                # 4x the blocks of a plain reduce: the per-pixel window gather is latency-bound, not a stream
+                blocks = max(1, min(4096, rows // 256))
+                Cn.stem_pool_bwd_reduce32(g, saved["idx"], saved["y0"], sbn.coef, slots, blocks, N, P0, Q0, st.cout)
             self._bn_bwd_finish(slots, rows, sbn, None)
             wg_fused = (self.stem_win and self._STEM4 and self._STEM_WG_FUSE and self.stem_pairs == 4
                         and st.cout == 64)

@@ -400,7 +400,8 @@ def test_fp32_fused_stem_tail_matches_the_separate_passes(monkeypatch):
         native.C.reset_dispatch_counts()
         logits, met = tr.train_step(x, t)
         torch.cuda.synchronize()
-        assert (dict(native.C.dispatch_counts()).get("stem_pool_bwd_fused32", 0) > 0) == fuse
+        cnt = dict(native.C.dispatch_counts())
+        assert (cnt.get("stem_pool_bwd_fused32", 0) + cnt.get("stem_pool_bwd_reduce_out32", 0) > 0) == fuse
         outs.append(tr.flat.grad.clone())
     assert _rel(outs[1], outs[0]) < 1e-5
 
@@ -441,3 +442,59 @@ def test_wgrad32_stem_fused_dy_matches_apply_then_wgrad():
     assert dict(C.dispatch_counts()).get("wgrad32_stem4_fused", 0) == 1
     assert _rel(ws, ws_ref) < 1e-6, _rel(ws, ws_ref)
     print("bit-identical:", torch.equal(ws, ws_ref))
+
+
+def test_stem_pool_bwd_reduce_out32_matches_window_gather():
+    """The stem's BN-backward sums over the POOLED output (mask out > 0, BN input recovered as (out - shift) / scale)
+    equal the window-gather reduce over the 112x112 conv output to fp32 rounding -- negative and zero BN scales
+    included (a zero scale contributes xhat = 0 in both)."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    torch.manual_seed(8)
+    N, H, W, ch = 3, 23, 18, 64
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y0 = torch.randn(N * H * W * ch, device=DEV)
+    sc = torch.rand(ch, device=DEV) + 0.2
+    sc[:8] = -sc[:8]
+    sc[8] = 0.0
+    coef = torch.cat([sc, torch.randn(ch, device=DEV) * 0.5, torch.randn(ch, device=DEV) * 0.1,
+                      torch.rand(ch, device=DEV) + 0.5])
+    out = torch.empty(N * OH * OW * ch, device=DEV)
+    idx = torch.empty(N * OH * OW * ch, device=DEV, dtype=torch.uint8)
+    C.bn_relu_maxpool32(y0, coef, out, idx, N, H, W, ch)
+    dp = torch.randn(N * OH * OW * ch, device=DEV)
+    ref = torch.zeros(64 * ch * 2, device=DEV, dtype=torch.float64)
+    got = torch.zeros_like(ref)
+    C.stem_pool_bwd_reduce32(dp, idx, y0, coef, ref, 7, N, H, W, ch)
+    C.stem_pool_bwd_reduce_out32(dp, out, coef, got, 5, ch)
+    r, g = ref.view(64, ch, 2).sum(0), got.view(64, ch, 2).sum(0)
+    scale = dp.abs().view(-1, ch).sum(0).double()  # sum |dz| bounds both sums' rounding
+    assert ((r - g).abs() <= 1e-5 * scale[:, None] + 1e-9).all(), ((r - g).abs() / scale[:, None]).max()
+
+
+@pytest.mark.parametrize("arch,HW", [("resnet18", 112), ("resnet50", 64)])
+def test_fp32_fused_producer_bn_equals_separate_pass(monkeypatch, arch, HW):
+    """SURVEY P5 in fp32: the inner BatchNorms' BN + ReLU applied by the consumer conv's kernels (forward activation
+    fragments, the weight gradient's staged input; the backward's ReLU mask recomputed from y) gives the logits, loss,
+    every gradient and the running statistics of the separate bn_apply32 pass BIT FOR BIT -- the same fma + max on
+    the same values, summed in the same order -- and really runs (dispatch counts)."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    from pytorch_distributed_template_amd.models.executor32 import ResNetExecutor32
+    from pytorch_distributed_template_amd.ops import native
+    torch.manual_seed(3)
+    model = registry.create(arch)
+    x = torch.randn(4, 3, HW, HW, device=DEV)
+    t = torch.randint(0, 1000, (4,), device=DEV)
+    outs = []
+    for pre in (False, True):
+        monkeypatch.setattr(ResNetExecutor32, "_PRE", pre)
+        tr = NativeTrainer(copy.deepcopy(model), torch.device(DEV), dtype=torch.float32, lr=0.0)
+        native.C.reset_dispatch_counts()
+        logits, met = tr.train_step(x, t)
+        torch.cuda.synchronize()
+        cnt = dict(native.C.dispatch_counts())
+        assert (cnt.get("conv32_fwd_pre", 0) > 0 and cnt.get("wgrad32_pre", 0) > 0) == pre, cnt
+        outs.append((logits.clone(), met.clone(), tr.flat.grad.clone(), tr.buffers.fdata.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b), _rel(b, a)
