@@ -158,6 +158,14 @@ def check_syncbn_fp32_full_batch(res, nproc):
     tr2, _ = _single(run_on(torch.roll(X, B, 0), torch.roll(T, B, 0), "met2"), dtype=torch.float32)
     floor = _update_errors(tr, before, tr2.flat.data.cpu(), full)
     e = _update_errors(tr, before, res["data"], full)
+    # the classifier's update depends on the forward (SyncBN statistics, counts, eps, variance bias) and the loss
+    # gradient only -- no backward ReLU decision that reordering could flip -- so it is held to the plain 1e-4 bound.
+    # (Already the last block's conv2 / bn2 see ~1e-3 at W = 4: one flipped block-output ReLU mask among the 32 x 49
+    # positions per channel of layer4 moves those sums by ~1/1568 -- measured; hence the reorder floor below.)
+    strict = [k for k in e if k.startswith("fc.")]
+    assert len(strict) == 2, strict
+    bad = [(k, e[k]) for k in strict if e[k] > 1e-4]
+    assert not bad, bad
     fmax = max(floor.values())
     bad = [(k, v, floor[k]) for k, v in e.items() if v > max(1e-4, 3 * fmax)]
     assert not bad, (fmax, sorted(bad, key=lambda kv: -kv[1])[:8])
