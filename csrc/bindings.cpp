@@ -91,6 +91,13 @@ using OptT = std::optional<Tensor>;
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// after every kernel launch of a binding: a launch the runtime refused (LDS / register / grid limits) raises here
+// instead of leaving its output buffer stale
+void launched(const char* op) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, op, ": kernel launch failed: ", hipGetErrorString(e));
+}
+
 void check_dev(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, ": expected a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, ": expected a contiguous tensor");
@@ -179,6 +186,7 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   TORCH_CHECK(M < (int64_t(1) << 31), "conv_fwd: N*Pm*Qm must be < 2^31 (32-bit pixel indexing)");
   a.M = M;
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+  launched("conv_fwd_launch");
 }
 
 // ResNet layer1 3x3/s1/p1 64 -> 64 forward over the RAW output z of the block's first conv, with that conv's
@@ -214,6 +222,7 @@ void conv_fwd_pre(const Tensor& z, const Tensor& w, Tensor& y, const Tensor& sta
   a.tstep_w = 1; a.OH = (int)H; a.OW = (int)W; a.ost_h = 1; a.ost_w = 1;
   a.M = N * H * W;
   pdt::conv_fwd_launch(a, dt, 256, 64, 64, cur_stream());
+  launched("conv_fwd_launch");
 }
 
 // ResNet stem forward (7x7/2, 3 -> 64) over the zero-padded NHWC4 image with window-row weights
@@ -241,6 +250,7 @@ void stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& stats, i
   a.N = (int)N; a.Hp = (int)Hp; a.Wp = (int)Wp; a.P = (int)P; a.Q = (int)Q;
   a.blocks_per_cu = (int)std::max<int64_t>(1, blocks_per_cu);
   pdt::stem_fwd_launch(a, dt, cur_stream());
+  launched("stem_fwd_launch");
 }
 
 int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (int)bm); }
@@ -322,6 +332,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     a.stats = pd(*bn_slots, "bn_slots");
   }
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
+  launched("conv_fwd_launch");
 }
 
 void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P, int64_t Q,
@@ -368,6 +379,7 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   a.tile = pdt::wgrad_tile((int)C, (int)Kout, win ? 1 : 0);
   TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad: bad split plan");
   pdt::conv_wgrad_launch(a, dt, cur_stream());
+  launched("conv_wgrad_launch");
 }
 
 // ResNet stem weight gradient with its dY computed in-kernel (max-pool backward + ReLU mask + BN-backward
@@ -407,6 +419,7 @@ void conv_wgrad_stem_fused(const Tensor& x, const Tensor& dp, const Tensor& idx,
   a.f_bcoef = pf(bcoef, "bcoef");
   a.f_OH = (int)OH; a.f_OW = (int)OW;
   pdt::conv_wgrad_launch(a, dt, cur_stream());
+  launched("conv_wgrad_launch");
 }
 
 // ResNet layer1 weight gradient (3x3/s1/p1, C = Kout = 64, W = 56): all 9 taps per block; writes
@@ -436,6 +449,7 @@ int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t
     a.pre_coef = pf(*pre_coef, "pre_coef");
   }
   pdt::wgrad3x3_c64_launch(a, blocks, dt, cur_stream());
+  launched("wgrad3x3_c64_launch");
   return blocks;
 }
 
@@ -445,12 +459,14 @@ void wgrad_reduce(const Tensor& ws, int64_t splits, int64_t rows, int64_t cols, 
   TORCH_CHECK(out.numel() >= (rows - 1) * ldo + cols, "wgrad_reduce: out too small");
   pdt::wgrad_reduce_launch(pf(ws, "ws"), splits, rows, cols, ldw, split_stride, pf(out, "out"), ldo, (float)scale,
                            accumulate, cur_stream());
+  launched("wgrad_reduce_launch");
 }
 
 // -------------------------------------------------------------------------------------------- bn
 void bn_slot_sum(const Tensor& slots, int64_t C, int64_t K, Tensor& sums) {
   TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K && sums.numel() >= C * K, "bn_slot_sum: bad sizes");
   pdt::bn_slot_sum_launch(pd(slots, "slots"), C, K, pd(sums, "sums"), cur_stream());
+  launched("bn_slot_sum_launch");
 }
 
 int64_t stat_slots() { return pdt::kStatSlots; }
@@ -464,6 +480,7 @@ void bn_finalize_slots(const Tensor& slots, double count, const Tensor& gamma, c
   pdt::bn_finalize_slots_launch(pd(slots, "slots"), count, pf(gamma, "gamma"), pf(beta, "beta"), (float)eps,
                                 (float)momentum, pf(rm, "running_mean"), pf(rv, "running_var"), pf(coef, "coef"),
                                 pd(sums, "sums"), (int)C, update_running, cur_stream());
+  launched("bn_finalize_slots_launch");
 }
 
 // slot sum + backward finalize for one (K = 2) or two (K = 4) BN branches, no SyncBN
@@ -481,6 +498,7 @@ void bn_bwd_finalize_slots(const Tensor& slots, int64_t K, double count, const T
                                     pfo(coef2, "coef2"), pfo(gamma2, "gamma2"), pfo(dgamma2, "dgamma2"),
                                     pfo(dbeta2, "dbeta2"), pfo(bcoef2, "bcoef2"), (float)gscale, (int)C,
                                     cur_stream());
+  launched("bn_bwd_finalize_slots_launch");
 }
 
 void bn_finalize(const Tensor& sums, double count, const Tensor& gamma, const Tensor& beta, double eps, double momentum,
@@ -490,12 +508,14 @@ void bn_finalize(const Tensor& sums, double count, const Tensor& gamma, const Te
   pdt::bn_finalize_launch(pd(sums, "sums"), count, pf(gamma, "gamma"), pf(beta, "beta"), (float)eps, (float)momentum,
                           pf(rm, "running_mean"), pf(rv, "running_var"), pf(coef, "coef"), C, update_running,
                           cur_stream());
+  launched("bn_finalize_launch");
 }
 
 void bn_eval_coef(const Tensor& gamma, const Tensor& beta, const Tensor& rm, const Tensor& rv, double eps, Tensor& coef) {
   const int64_t C = gamma.numel();
   pdt::bn_eval_coef_launch(pf(gamma, "gamma"), pf(beta, "beta"), pf(rm, "rm"), pf(rv, "rv"), (float)eps, pf(coef, "coef"),
                            C, cur_stream());
+  launched("bn_eval_coef_launch");
 }
 
 void bn_apply(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& rcoef, Tensor& out, int64_t C,
@@ -507,6 +527,7 @@ void bn_apply(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& 
   TORCH_CHECK(!mask.has_value() || (resmode != 0 && relu), "bn_apply: the ReLU bitmask is built for residual block outputs");
   pdt::bn_apply_launch(dt, p16(y, "y"), pf(coef, "coef"), p16o(res, "res"), pfo(rcoef, "rcoef"), p16(out, "out"),
                        pmask(mask, y.numel(), "mask"), y.numel(), C, (int)resmode, relu, cur_stream());
+  launched("bn_apply_launch");
 }
 
 int64_t bn_bwd_reduce_blocks(int64_t rows, int64_t C) { return pdt::bn_bwd_reduce_blocks(rows, (int)C); }
@@ -519,6 +540,7 @@ void bn_bwd_reduce(const Tensor& g, const OptT& mask, const Tensor& y1, const Te
   TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K, "bn_bwd_reduce: slots too small");
   pdt::bn_bwd_reduce_launch(dt, p16(g, "g"), pmask(mask, g.numel(), "mask"), p16(y1, "y1"), pf(coef1, "coef1"), p16o(y2, "y2"),
                             pfo(coef2, "coef2"), pd(slots, "slots"), (int)blocks, rows, (int)C, cur_stream());
+  launched("bn_bwd_reduce_launch");
 }
 
 void bn_bwd_finalize(const Tensor& sums, double count, const Tensor& coef, const Tensor& gamma, const OptT& dgamma,
@@ -527,6 +549,7 @@ void bn_bwd_finalize(const Tensor& sums, double count, const Tensor& coef, const
   TORCH_CHECK(bcoef.numel() >= 3 * C, "bn_bwd_finalize: bcoef too small");
   pdt::bn_bwd_finalize_launch(pd(sums, "sums"), count, pf(coef, "coef"), pf(gamma, "gamma"), pfo(dgamma, "dgamma"),
                               pfo(dbeta, "dbeta"), (float)gscale, pf(bcoef, "bcoef"), C, cur_stream());
+  launched("bn_bwd_finalize_launch");
 }
 
 void bn_bwd_apply(const Tensor& g, const OptT& mask, const Tensor& y1, const Tensor& b1, Tensor& dy1, const OptT& y2,
@@ -535,6 +558,7 @@ void bn_bwd_apply(const Tensor& g, const OptT& mask, const Tensor& y1, const Ten
   TORCH_CHECK(C % 8 == 0 && g.numel() % C == 0 && dy1.numel() == g.numel(), "bn_bwd_apply: bad sizes");
   pdt::bn_bwd_apply_launch(dt, p16(g, "g"), pmask(mask, g.numel(), "mask"), p16(y1, "y1"), pf(b1, "b1"), p16(dy1, "dy1"),
                            p16o(y2, "y2"), pfo(b2, "b2"), p16m(dy2, "dy2"), p16m(dz, "dz"), g.numel(), C, cur_stream());
+  launched("bn_bwd_apply_launch");
 }
 
 // ------------------------------------------------------------------------------------------ pool
@@ -548,6 +572,7 @@ void bn_relu_maxpool(const Tensor& y, const Tensor& coef, Tensor& out, Tensor& i
   check_dev(idx, "idx");
   pdt::bn_relu_maxpool_launch(dt, p16(y, "y"), pf(coef, "coef"), p16(out, "out"), idx.data_ptr<uint8_t>(), N, H, W, C,
                               cur_stream());
+  launched("bn_relu_maxpool_launch");
 }
 
 void maxpool_bwd_relu(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& dz, int64_t N,
@@ -559,6 +584,7 @@ void maxpool_bwd_relu(const Tensor& dp, const Tensor& idx, const Tensor& y, cons
   check_dev(idx, "idx");
   pdt::maxpool_bwd_relu_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"), p16(dz, "dz"),
                                N, H, W, C, cur_stream());
+  launched("maxpool_bwd_relu_launch");
 }
 
 // Stem backward (max-pool bwd + ReLU mask + BN bwd) without the 112x112 dz tensor: reduce pass ...
@@ -573,6 +599,7 @@ void stem_pool_bwd_reduce(const Tensor& dp, const Tensor& idx, const Tensor& y, 
   check_dev(idx, "idx");
   pdt::stem_pool_bwd_reduce_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"),
                                    pd(slots, "slots"), N, H, W, C, cur_stream());
+  launched("stem_pool_bwd_reduce_launch");
 }
 
 // pass 1 from the pooled output alone (mask = out > 0, BN input recovered from out)
@@ -586,6 +613,7 @@ void stem_pool_bwd_reduce_out(const Tensor& dp, const Tensor& out, const Tensor&
   TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * 2, "stem_pool_bwd_reduce_out: slots too small");
   pdt::stem_pool_bwd_reduce_out_launch(dt, p16(dp, "dp"), p16(out, "out"), pf(coef, "coef"), pd(slots, "slots"), N, H,
                                        W, C, cur_stream());
+  launched("stem_pool_bwd_reduce_out_launch");
 }
 
 // ... and apply pass writing dy = A*dz + B*y + C (bcoef from bn_bwd_finalize)
@@ -601,18 +629,21 @@ void stem_pool_bwd_apply(const Tensor& dp, const Tensor& idx, const Tensor& y, c
   check_dev(idx, "idx");
   pdt::stem_pool_bwd_apply_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"),
                                   pf(bcoef, "bcoef"), p16(dy, "dy"), N, H, W, C, cur_stream());
+  launched("stem_pool_bwd_apply_launch");
 }
 
 void avgpool_fwd(const Tensor& x, Tensor& feat, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
   const int dt = dt16(x, "x");
   TORCH_CHECK(x.numel() == N * HW * C && feat.numel() >= N * ldf && C % 8 == 0, "avgpool_fwd: bad sizes");
   pdt::avgpool_fwd_launch(dt, p16(x, "x"), p16(feat, "feat"), N, HW, C, ldf, cur_stream());
+  launched("avgpool_fwd_launch");
 }
 
 void avgpool_bwd(const Tensor& dfeat, Tensor& g, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
   const int dt = dt16(dfeat, "dfeat");
   TORCH_CHECK(g.numel() == N * HW * C && dfeat.numel() >= N * ldf && C % 8 == 0, "avgpool_bwd: bad sizes");
   pdt::avgpool_bwd_launch(dt, p16(dfeat, "dfeat"), p16(g, "g"), N, HW, C, ldf, cur_stream());
+  launched("avgpool_bwd_launch");
 }
 
 // ------------------------------------------------------------------------------------------ loss
@@ -628,21 +659,25 @@ void xent(const Tensor& logits, int64_t ldl, const OptT& bias, const Tensor& tar
   pdt::xent_launch(dt, p16(logits, "logits"), ldl, pfo(bias, "bias"), target.data_ptr<int64_t>(), B, ncls,
                    pfo(out_logits, "out_logits"), p16m(dlogits, "dlogits"), pfo(loss_scale, "loss_scale"),
                    (float)grad_div, pf(row_loss, "row_loss"), pf(row_correct, "row_correct"), cur_stream());
+  launched("xent_launch");
 }
 
 void metrics(const Tensor& row_loss, const Tensor& row_correct, int64_t B, Tensor& out) {
   pdt::metrics_launch(pf(row_loss, "row_loss"), pf(row_correct, "row_correct"), B, pf(out, "out"), cur_stream());
+  launched("metrics_launch");
 }
 
 void colsum(const Tensor& d, int64_t B, int64_t ld, int64_t ncols, Tensor& out, double scale) {
   const int dt = dt16(d, "d");
   TORCH_CHECK(d.numel() >= B * ld && out.numel() >= ncols, "colsum: bad sizes");
   pdt::colsum_launch(dt, p16(d, "d"), B, ld, ncols, pf(out, "out"), (float)scale, cur_stream());
+  launched("colsum_launch");
 }
 
 // ----------------------------------------------------------------------------------------- optim
 void nonfinite_check(const Tensor& g, Tensor& found) {
   pdt::nonfinite_check_launch(pf(g, "g"), g.numel(), pf(found, "found"), cur_stream());
+  launched("nonfinite_check_launch");
 }
 
 void sgd(Tensor& p, const Tensor& g, Tensor& buf, const OptT& shadow, const OptT& wd_mask, double lr, double momentum,
@@ -658,11 +693,13 @@ void sgd(Tensor& p, const Tensor& g, Tensor& buf, const OptT& shadow, const OptT
   pdt::sgd_launch(dt, pf(p, "p"), pf(g, "g"), pf(buf, "buf"), p16m(shadow, "shadow"), pfo(wd_mask, "wd_mask"), n,
                   (float)lr, (float)momentum, (float)wd, (float)gscale, pfo(loss_scale, "loss_scale"),
                   pfo(found_inf, "found_inf"), first, cur_stream());
+  launched("sgd_launch");
 }
 
 void cast16(const Tensor& p, Tensor& out) {
   TORCH_CHECK(p.numel() == out.numel(), "cast16: size mismatch");
   pdt::cast16_launch(dt16(out, "out"), pf(p, "p"), p16(out, "out"), p.numel(), cur_stream());
+  launched("cast16_launch");
 }
 
 void amp_update(Tensor& scale, Tensor& tracker, Tensor& found_inf, double growth, double backoff, int64_t interval) {
@@ -670,12 +707,14 @@ void amp_update(Tensor& scale, Tensor& tracker, Tensor& found_inf, double growth
   TORCH_CHECK(tracker.scalar_type() == at::kInt, "amp_update: tracker must be int32");
   pdt::amp_update_launch(pf(scale, "scale"), tracker.data_ptr<int>(), pf(found_inf, "found_inf"), (float)growth,
                          (float)backoff, (int)interval, cur_stream());
+  launched("amp_update_launch");
 }
 
 void gather16(const Tensor& src, const Tensor& idx, Tensor& dst) {
   check_dev(idx, "idx");
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == dst.numel(), "gather16: idx must be int32 like dst");
   pdt::gather16_launch(p16(src, "src"), idx.data_ptr<int>(), p16(dst, "dst"), dst.numel(), cur_stream());
+  launched("gather16_launch");
 }
 
 void im2col(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
@@ -685,6 +724,7 @@ void im2col(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64
   TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * OH * OW * ldk && ldk % 8 == 0 && ldk >= R * S * C,
               "im2col: bad sizes");
   pdt::im2col_launch(dt, pf(x, "x"), p16(out, "out"), N, C, H, W, R, S, stride, pad, ldk, cur_stream());
+  launched("im2col_launch");
 }
 
 void stem_pack(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t pad, int64_t Hp,
@@ -692,6 +732,7 @@ void stem_pack(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, in
   TORCH_CHECK(x.numel() == N * C * H * W && out.numel() == N * Hp * Wp * 4 && C <= 4 && Hp >= H + 2 * pad &&
                   Wp >= W + 2 * pad && N * Hp * Wp < (int64_t(1) << 31), "stem_pack: bad sizes");
   pdt::stem_pack_launch(dt16(out, "out"), pf(x, "x"), p16(out, "out"), N, C, H, W, pad, Hp, Wp, cur_stream());
+  launched("stem_pack_launch");
 }
 
 // uint8 NCHW pixels -> normalised, zero-padded NHWC4 16-bit stem input (v = x * scale[c] + shift[c])
@@ -704,17 +745,20 @@ void stem_pack_u8(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H,
               "stem_pack_u8: bad sizes");
   pdt::stem_pack_u8_launch(dt16(out, "out"), x.data_ptr<uint8_t>(), p16(out, "out"), N, C, H, W, pad, Hp, Wp,
                            pf(scale, "scale"), pf(shift, "shift"), cur_stream());
+  launched("stem_pack_u8_launch");
 }
 
 void bw_probe(int64_t mode, const Tensor& x, const Tensor& y, Tensor& out, int64_t blocks) {
   TORCH_CHECK(x.numel() == y.numel() && out.numel() == x.numel() && x.numel() % 8 == 0, "bw_probe: sizes");
   pdt::bw_probe_launch((int)mode, p16(x, "x"), p16(y, "y"), p16(out, "out"), x.numel(), (int)blocks, cur_stream());
+  launched("bw_probe_launch");
 }
 
 void gather32(const Tensor& src, const Tensor& idx, Tensor& dst) {
   check_dev(idx, "idx");
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == dst.numel(), "gather32: idx must be int32 like dst");
   pdt::gather32_launch(pf(src, "src"), idx.data_ptr<int>(), pf(dst, "dst"), dst.numel(), cur_stream());
+  launched("gather32_launch");
 }
 
 // dst[idx[i]] = src[i]; the caller guarantees 0 <= idx < dst.numel() (checked where the index map is built)
@@ -722,6 +766,7 @@ void scatter32(const Tensor& src, const Tensor& idx, Tensor& dst) {
   check_dev(idx, "idx");
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == src.numel(), "scatter32: idx must be int32 like src");
   pdt::scatter32_launch(pf(src, "src"), idx.data_ptr<int>(), pf(dst, "dst"), src.numel(), cur_stream());
+  launched("scatter32_launch");
 }
 
 // ------------------------------------------------------------------------------------------ fp32 path
@@ -773,6 +818,7 @@ void conv32_fwd_impl(const Tensor& x, const Tensor& w, Tensor& y, const OptT& re
     a.pre_coef = pf(*pre, "pre");
   }
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
+  launched("conv32_launch");
 }
 
 // backward-data over fp32 in ONE launch for every sub-pixel phase (phases as in conv_dgrad)
@@ -828,6 +874,7 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
   a.M = maxM;
   a.Pm = a.pPm[0]; a.Qm = a.pQm[0];
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
+  launched("conv32_launch");
 }
 
 void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
@@ -874,6 +921,7 @@ void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int6
     a.pre_coef = pf(*pre, "pre");
   }
   pdt::wgrad32_launch(a, cur_stream());
+  launched("wgrad32_launch");
 }
 
 void bn_apply32(const Tensor& y, const Tensor& coef, const OptT& res, const OptT& rcoef, Tensor& out, int64_t C,
@@ -883,6 +931,7 @@ void bn_apply32(const Tensor& y, const Tensor& coef, const OptT& res, const OptT
   if (resmode == 2) TORCH_CHECK(rcoef.has_value(), "bn_apply32: residual coefficients");
   pdt::bn_apply32_launch(pf(y, "y"), pf(coef, "coef"), pfc(res, "res"), pfc(rcoef, "rcoef"), pf(out, "out"), y.numel(),
                          C, (int)resmode, relu, cur_stream());
+  launched("bn_apply32_launch");
 }
 
 int64_t bn_bwd_reduce32_blocks(int64_t rows, int64_t C) { return pdt::bn_bwd_reduce32_blocks(rows, (int)C); }
@@ -895,6 +944,7 @@ void bn_bwd_reduce32(const Tensor& g, const OptT& mref, const Tensor& y1, const 
   TORCH_CHECK(slots.numel() >= pdt::kStatSlots * C * K, "bn_bwd_reduce32: slots too small");
   pdt::bn_bwd_reduce32_launch(pf(g, "g"), pfc(mref, "mref"), pf(y1, "y1"), pf(coef1, "coef1"), pfc(y2, "y2"),
                               pfc(coef2, "coef2"), pd(slots, "slots"), (int)blocks, rows, (int)C, cur_stream());
+  launched("bn_bwd_reduce32_launch");
 }
 
 void bn_bwd_apply32(const Tensor& g, const OptT& mref, const Tensor& y1, const Tensor& b1, Tensor& dy1, const OptT& y2,
@@ -903,6 +953,7 @@ void bn_bwd_apply32(const Tensor& g, const OptT& mref, const Tensor& y1, const T
   pdt::bn_bwd_apply32_launch(pf(g, "g"), pfc(mref, "mref"), pf(y1, "y1"), pf(b1, "b1"), pf(dy1, "dy1"), pfc(y2, "y2"),
                              pfc(b2, "b2"), dy2.has_value() ? pf(*dy2, "dy2") : nullptr,
                              dz.has_value() ? pf(*dz, "dz") : nullptr, g.numel(), C, cur_stream());
+  launched("bn_bwd_apply32_launch");
 }
 
 void bn_relu_maxpool32(const Tensor& y, const Tensor& coef, Tensor& out, Tensor& idx, int64_t N, int64_t H, int64_t W,
@@ -913,6 +964,7 @@ void bn_relu_maxpool32(const Tensor& y, const Tensor& coef, Tensor& out, Tensor&
   check_dev(idx, "idx");
   pdt::bn_relu_maxpool32_launch(pf(y, "y"), pf(coef, "coef"), pf(out, "out"), idx.data_ptr<uint8_t>(), N, H, W, C,
                                 cur_stream());
+  launched("bn_relu_maxpool32_launch");
 }
 
 // the stem's backward tail without the dz tensor: fused max-pool backward + ReLU mask + BN-backward reduce / apply
@@ -926,6 +978,7 @@ void stem_pool_bwd_reduce32(const Tensor& dp, const Tensor& idx, const Tensor& y
   check_dev(idx, "idx");
   pdt::stem_pool_bwd_reduce32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"),
                                      pd(slots, "slots"), (int)blocks, N, H, W, C, cur_stream());
+  launched("stem_pool_bwd_reduce32_launch");
 }
 
 void stem_pool_bwd_reduce_out32(const Tensor& dp, const Tensor& out, const Tensor& coef, Tensor& slots, int64_t blocks,
@@ -935,6 +988,7 @@ void stem_pool_bwd_reduce_out32(const Tensor& dp, const Tensor& out, const Tenso
               "stem_pool_bwd_reduce_out32: bad sizes");
   pdt::stem_pool_bwd_reduce_out32_launch(pf(dp, "dp"), pf(out, "out"), pf(coef, "coef"), pd(slots, "slots"),
                                          (int)blocks, dp.numel() / C, (int)C, cur_stream());
+  launched("stem_pool_bwd_reduce_out32_launch");
 }
 
 void stem_pool_bwd_apply32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, const Tensor& b,
@@ -947,6 +1001,7 @@ void stem_pool_bwd_apply32(const Tensor& dp, const Tensor& idx, const Tensor& y,
   check_dev(idx, "idx");
   pdt::stem_pool_bwd_apply32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"), pf(b, "b"),
                                     pf(dy, "dy"), N, H, W, C, cur_stream());
+  launched("stem_pool_bwd_apply32_launch");
 }
 
 void maxpool_bwd_relu32(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& dz, int64_t N,
@@ -958,16 +1013,19 @@ void maxpool_bwd_relu32(const Tensor& dp, const Tensor& idx, const Tensor& y, co
   check_dev(idx, "idx");
   pdt::maxpool_bwd_relu32_launch(pf(dp, "dp"), idx.data_ptr<uint8_t>(), pf(y, "y"), pf(coef, "coef"), pf(dz, "dz"), N, H,
                                  W, C, cur_stream());
+  launched("maxpool_bwd_relu32_launch");
 }
 
 void avgpool32_fwd(const Tensor& x, Tensor& feat, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
   TORCH_CHECK(x.numel() == N * HW * C && feat.numel() >= N * ldf, "avgpool32_fwd: bad sizes");
   pdt::avgpool32_fwd_launch(pf(x, "x"), pf(feat, "feat"), N, HW, C, ldf, cur_stream());
+  launched("avgpool32_fwd_launch");
 }
 
 void avgpool32_bwd(const Tensor& dfeat, Tensor& g, int64_t N, int64_t HW, int64_t C, int64_t ldf) {
   TORCH_CHECK(g.numel() == N * HW * C && dfeat.numel() >= N * ldf, "avgpool32_bwd: bad sizes");
   pdt::avgpool32_bwd_launch(pf(dfeat, "dfeat"), pf(g, "g"), N, HW, C, ldf, cur_stream());
+  launched("avgpool32_bwd_launch");
 }
 
 void xent32(const Tensor& logits, int64_t ldl, const OptT& bias, const Tensor& target, int64_t B, int64_t ncls,
@@ -982,11 +1040,13 @@ void xent32(const Tensor& logits, int64_t ldl, const OptT& bias, const Tensor& t
                      out_logits.has_value() ? pf(*out_logits, "out_logits") : nullptr,
                      dlogits.has_value() ? pf(*dlogits, "dlogits") : nullptr, pfc(loss_scale, "loss_scale"),
                      (float)grad_div, pf(row_loss, "row_loss"), pf(row_correct, "row_correct"), cur_stream());
+  launched("xent32_launch");
 }
 
 void colsum32(const Tensor& d, int64_t B, int64_t ld, int64_t ncols, Tensor& out, double scale) {
   TORCH_CHECK(d.numel() >= B * ld && out.numel() >= ncols, "colsum32: bad sizes");
   pdt::colsum32_launch(pf(d, "d"), B, ld, ncols, pf(out, "out"), (float)scale, cur_stream());
+  launched("colsum32_launch");
 }
 
 // window-mode fp32 stem (conv32 over the zero-padded NHWC4 image, K = R kernel rows x 32: 8 pixels x 4 channels)
@@ -995,6 +1055,7 @@ void stem_pack32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, 
   TORCH_CHECK(C <= 3 && x.numel() >= N * C * H * W && out.numel() == N * Hp * Wp * 4 && Hp >= H + 2 * pad &&
               Wp >= W + 2 * pad, "stem_pack32: sizes");
   pdt::stem_pack32_launch(pf(x, "x"), pf(out, "out"), N, C, H, W, pad, Hp, Wp, cur_stream());
+  launched("stem_pack32_launch");
 }
 
 void conv32_stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& stats, int64_t N, int64_t Hp, int64_t Wp,
@@ -1015,6 +1076,7 @@ void conv32_stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& s
   a.OH = P; a.OW = Q; a.ost_h = 1; a.ost_w = 1; a.ooff_h = 0; a.ooff_w = 0;
   a.M = N * P * Q;
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
+  launched("conv32_launch");
 }
 
 // fp32 stem weight gradient in window-pair mode over the zero-padded NHWC4 image (no im2col): "tap" t = kernel rows
@@ -1039,6 +1101,7 @@ void wgrad32_stem(const Tensor& xp, const Tensor& dy, Tensor& ws, int64_t N, int
     a.tile = 4;
   }
   pdt::wgrad32_launch(a, cur_stream());
+  launched("wgrad32_launch");
 }
 
 // wgrad32_stem (4 pairs, all per block) with dY computed in the kernel from the stem's max-pool backward, ReLU mask and
@@ -1066,6 +1129,7 @@ void wgrad32_stem_fused(const Tensor& xp, const Tensor& dp, const Tensor& idx, c
   a.f_dp = pf(dp, "dp"); a.f_idx = idx.data_ptr<uint8_t>(); a.f_y = pf(y0, "y0"); a.f_coef = pf(coef, "coef");
   a.f_bcoef = pf(bcoef, "bcoef"); a.f_OH = (int)OH; a.f_OW = (int)OW;
   pdt::wgrad32_launch(a, cur_stream());
+  launched("wgrad32_launch");
 }
 
 void im2col32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
@@ -1073,6 +1137,7 @@ void im2col32(const Tensor& x, Tensor& out, int64_t N, int64_t C, int64_t H, int
   const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
   TORCH_CHECK(x.numel() >= N * C * H * W && out.numel() == N * OH * OW * ldk && ldk >= R * S * C, "im2col32: sizes");
   pdt::im2col32_launch(pf(x, "x"), pf(out, "out"), N, C, H, W, R, S, stride, pad, ldk, cur_stream());
+  launched("im2col32_launch");
 }
 
 }  // namespace
