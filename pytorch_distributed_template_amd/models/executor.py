@@ -20,6 +20,7 @@ weights and gradients.  Reference call sites mirror
 """
 from __future__ import annotations
 
+import json
 import os
 
 from typing import Callable, Dict, List, Optional, Tuple
@@ -32,6 +33,23 @@ from ..ops.conv import conv_tile as _conv_tile, dgrad_phases, dgrad_weight_index
 from .resnet import BasicBlock, Bottleneck, ResNet
 
 _BUF_POISON = os.environ.get("PDT_BUF_POISON", "0") == "1"
+
+
+def _load_tuned():
+    """Shipped autotune results (the analogue of a cudnn.benchmark cache, `distributed.py:104`): per-shape conv tiles
+    that PDT_AUTOTUNE=1 measured faster than ops.conv.conv_tile on MI355X (models/tuned_tiles_mi355x.json: ResNet-50
+    at B = 1200).  PDT_TUNED_TILES=0 ignores them."""
+    if os.environ.get("PDT_TUNED_TILES", "1") != "1":
+        return {}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_tiles_mi355x.json")
+    try:
+        with open(path) as f:
+            return {tuple(k): tuple(v) for k, v in json.load(f)["tiles"]}
+    except (OSError, ValueError, KeyError):
+        return {}
+
+
+_TUNED = _load_tuned()
 
 class _Conv:
     """Static description of one convolution and its derived (dgrad) weight layouts."""
@@ -379,7 +397,7 @@ class ResNetExecutor:
         hit = self._tiles.get(key)
         if hit is not None:
             return hit
-        choice = _conv_tile(n_dim, kdim if bk == 64 else 0)
+        choice = _TUNED.get(key) or _conv_tile(n_dim, kdim if bk == 64 else 0)
         if self.autotune and bk == 64:
             cands = [(bm, bn) for bm, bn in self._CANDIDATES if n_dim % bn == 0 and
                      (not fused_epilogue or bm * bn in (16384, 32768, 65536))]
