@@ -41,12 +41,17 @@ def _load_tuned():
     at B = 1200).  PDT_TUNED_TILES=0 ignores them."""
     if os.environ.get("PDT_TUNED_TILES", "1") != "1":
         return {}
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_tiles_mi355x.json")
-    try:
-        with open(path) as f:
-            return {tuple(k): tuple(v) for k, v in json.load(f)["tiles"]}
-    except (OSError, ValueError, KeyError):
-        return {}
+    out = {}
+    paths = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_tiles_mi355x.json")]
+    if os.environ.get("PDT_TUNED_EXTRA"):  # more tables (A/B of candidate entries); later files win
+        paths += os.environ["PDT_TUNED_EXTRA"].split(os.pathsep)
+    for path in paths:
+        try:
+            with open(path) as f:
+                out.update({tuple(k): tuple(v) for k, v in json.load(f)["tiles"]})
+        except (OSError, ValueError, KeyError):
+            pass
+    return out
 
 
 _TUNED = _load_tuned()
