@@ -374,7 +374,8 @@ class ResNetExecutor:
         pad = c.pad if pad is None else pad
         P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
         bk = 64 if cin % 64 == 0 else 32
-        if cin * R * S == 64 and c.cout >= 256 and self.bk32_short:
+        tkey = ("fwd", N, H, W, cin, c.cout, R, S, st, stats)
+        if cin * R * S == 64 and c.cout >= 256 and self.bk32_short and tkey not in _TUNED:
             # a single 64-wide K-step: two 32-wide steps on the 3-stage ring overlap load and MFMA
             # (tools/conv_bench.py --r50: ResNet-50 1x1 64->256 with statistics 162 vs 142 TF/s)
             bk = 32
@@ -388,7 +389,7 @@ class ResNetExecutor:
         def launch(bm, bn):
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
                             -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
-        bm, bn = self._tile(("fwd", N, H, W, cin, c.cout, R, S, st, stats), c.cout, bk, launch, kdim=cin * R * S)
+        bm, bn = self._tile(tkey, c.cout, bk, launch, kdim=cin * R * S)
         launch(bm, bn)
         if stats and fin is not None:
             self.bn_train_finalize(fin, sp, 0, M)
