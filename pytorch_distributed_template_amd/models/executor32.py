@@ -21,6 +21,7 @@ tests/test_fp32_gpu.py judges against the fp64 gradients' own sensitivity to an 
 """
 from __future__ import annotations
 
+import json
 import os
 from typing import Callable, List, Optional
 
@@ -174,17 +175,29 @@ class ResNetExecutor32(ResNetExecutor):
                 return self._BM64, 64
         return 128, self._bn_tile(n)
 
+    # shipped per-conv fp32 tiles (models/tuned_tiles32_mi355x.json; PDT_FP32_TUNED=0 ignores them)
+    _TUNED32 = {}
+    if os.environ.get("PDT_FP32_TUNED", "1") == "1":
+        try:
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_tiles32_mi355x.json")) as _f:
+                _TUNED32 = {tuple(k): tuple(v) for k, v in json.load(_f)["tiles"]}
+        except (OSError, ValueError, KeyError):
+            _TUNED32 = {}
+
+    def _tile32c(self, kind: str, c: _Conv, N: int, H: int, n: int, m: int):
+        return self._TUNED32.get((kind, N, H, c.cin, c.cout, c.R, c.st)) or self._tile32(n, m)
+
     def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, pre=None):
         """``pre``: x is the producer conv's raw output and ``pre`` its BN coefficients -- BN + ReLU applied to the
         activation fragments inside the kernel (``_pre_ok``)."""
         P, Q = c.out_hw(H, W)
         sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
+        tile = self._tile32c("fwd", c, N, H, c.cout, N * P * Q)
         if pre is not None:
-            self.C.conv32_fwd_pre(x, self._w32(c), y, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad,
-                                  *self._tile32(c.cout, N * P * Q), pre)
+            self.C.conv32_fwd_pre(x, self._w32(c), y, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, *tile,
+                                  pre)
         else:
-            self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad,
-                              *self._tile32(c.cout, N * P * Q))
+            self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, *tile)
         return P, Q, sp
 
     # PDT_FP32_PRE=1: the inner BatchNorms' BN + ReLU (SURVEY §7.2 P5) applied by their consumer conv's kernels --
@@ -211,7 +224,7 @@ class ResNetExecutor32(ResNetExecutor):
         phases = [[ph, pw, T, U, ioff_h, ioff_w, doff] for (ph, pw, T, U, ioff_h, ioff_w, doff, dn) in c.phases
                   if H - ph > 0 and W - pw > 0]
         self.C.conv32_dgrad(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, c.st, phases,
-                            *self._tile32(c.cin, N * P * Q), *(bnb or ()))
+                            *self._tile32c("dgrad", c, N, H, c.cin, N * P * Q), *(bnb or ()))
 
     _FUSE_BN = os.environ.get("PDT_FP32_FUSE_BN", "1") == "1"
 
