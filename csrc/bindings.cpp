@@ -21,6 +21,7 @@
 
 #include "dtypes.h"
 #include "kernels/bn.h"
+#include "kernels/conv1x1.h"
 #include "kernels/conv_fwd.h"
 #include "kernels/conv_l1.h"
 #include "kernels/conv_wgrad.h"
@@ -339,6 +340,23 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res,
                 int64_t K, int64_t C, int64_t H, int64_t W, int64_t stride, const std::vector<std::vector<int64_t>>& phases,
                 int64_t bm, int64_t bn, int64_t bk) {
   conv_dgrad_impl(dy, wt, dx, res, N, P, Q, K, C, H, W, stride, phases, bm, bn, bk, 0, {}, {}, {}, {}, {}, {}, -1);
+}
+
+// 1x1 / stride-1 conv, 64 -> 256 channels, as the persistent store-overlapped kernel (conv1x1.hip): y[M][256] from
+// x[M][64] and w[256][64], optional BN statistics (fp64 slots) of the rounded outputs
+bool conv1x1_c64_supported(int64_t C, int64_t Kout) { return pdt::conv1x1_c64_supported((int)C, (int)Kout); }
+
+void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M) {
+  const int dt = dt16(x, "x");
+  TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv1x1_c64: mixed dtypes");
+  TORCH_CHECK(x.numel() >= M * 64 && w.numel() == 256 * 64 && y.numel() >= M * 256, "conv1x1_c64: size mismatch");
+  double* st = nullptr;
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * 256 * 2, "conv1x1_c64: stats buffer too small");
+    st = pd(*stats, "stats");
+  }
+  pdt::conv1x1_c64_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), st, M, dt, cur_stream());
+  launched("conv1x1_c64");
 }
 
 std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks,
@@ -1164,6 +1182,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_dgrad_bn", &conv_dgrad_impl);
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
+  m.def("conv1x1_c64_supported", &conv1x1_c64_supported);
+  m.def("conv1x1_c64", &conv1x1_c64);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_wgrad_stem_fused", &conv_wgrad_stem_fused);
   m.def("wgrad_reduce", &wgrad_reduce);

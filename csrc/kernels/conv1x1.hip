@@ -1,0 +1,225 @@
+// 1x1 / stride-1 "expanding" convolution, 64 -> 256 channels (ResNet-50 layer1: each block's conv3 and the
+// downsample), as a persistent, store-overlapped kernel.
+//
+// With K = 64 a 1x1 conv is one MFMA K-step per output tile: the implicit-GEMM kernels spend a block's life in
+// load latency -> a few MFMAs -> an epilogue that writes 2-4x the bytes it read, and the next tile's load waits
+// for the store queue too (vmcnt counts stores): 777 us (512 x 128 ping-pong) against ~350 us for writing the
+// 1.93 GB output at ResNet-50 B = 1200 (profiles/r2c_resnet50_1x1_write_bound.md).  Here:
+//   * the whole weight matrix (256 x 64, 32 KB) stays in registers as MFMA A fragments (8 per wave) after one
+//     LDS-DMA; each wave owns 64 output channels of every tile;
+//   * blocks are persistent (2 per CU) and walk 128-pixel tiles; a tile's 16 KB input is DMA'd into a 2-deep LDS
+//     ring one tile ahead;
+//   * the per-tile wait is COUNTED: the next tile's DMA is issued before this tile's 16 stores, so waiting for it
+//     (s_waitcnt vmcnt(16)) leaves the stores in flight -- the store stream of tile t overlaps tile t+1;
+//   * BN statistics of the rounded outputs accumulate in registers across all of a block's tiles and are reduced
+//     once (16-lane DPP sums) into the block's partial row (deterministic, conv_fwd.h).
+#include <cstdlib>
+
+#include "../common.h"
+#include "conv1x1.h"
+#include "conv_fwd.h"
+
+namespace pdt {
+
+namespace {
+constexpr int kC = 64, kK = 256;
+constexpr int kBM = 128;               // pixels per tile
+constexpr int kRowB = kC * 2;          // 128 B per pixel row / weight row
+constexpr int kTileB = kBM * kRowB;    // 16 KB
+constexpr int kWB = kK * kRowB;        // 32 KB
+constexpr int kStoresPerTile = 16;     // global stores per wave per full tile: 8 pixel x 2 channel-fragment pairs
+static_assert(kStoresPerTile == 16, "the per-tile s_waitcnt vmcnt(16) literal below");
+}  // namespace
+
+template <int DT, bool STATS>
+__global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __restrict__ x,
+                                                             const uint16_t* __restrict__ w,
+                                                             uint16_t* __restrict__ y, float* __restrict__ srows,
+                                                             int64_t M) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  __shared__ __attribute__((aligned(1024))) char smem[kWB + 2 * kTileB];
+  char* const wl = smem;
+  char* const xl = smem + kWB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  const int sw = (fr >> 1) & 7;  // fragment rows start at multiples of 16: row swizzle (row >> 1) & 7 == sw
+  const int tiles = (int)((M + kBM - 1) / kBM);
+  const int G = gridDim.x;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * kRowB));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)kWB);
+
+  // LDS row images: LDS chunk p of row r holds source chunk p ^ ((r >> 1) & 7) (conflict-free ds_read_b128)
+  // resident weights: 32 DMA instructions of 8 rows x 8 chunks, 8 per wave
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ins = wave * 8 + j;
+    const int row = ins * 8 + lrow;
+    buf_lds16_asm(rw, wl + ins * 1024, (uint32_t)(row * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)));
+  }
+  // one tile's input: 16 instructions, 4 per wave; rows past M read zeros (their results are not stored)
+  auto stage_x = [&](int t, int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ins = wave * 4 + j;
+      const int row = ins * 8 + lrow;
+      const int64_t m = (int64_t)t * kBM + row;
+      const uint32_t off = m < M ? (uint32_t)(m * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
+      buf_lds16_asm(rx, xl + buf * kTileB + ins * 1024, off);
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < tiles) stage_x(t, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // this wave's 64 output channels as resident MFMA A fragments: [cout fragment i][K half kk].  Fragment rows are
+  // permuted (wave_ch below) so that fragments 2p and 2p+1 give a lane 8 CONSECUTIVE channels of its pixel: one
+  // 16-byte store per pixel and fragment pair, 64 contiguous bytes per pixel per store instruction.
+  auto wave_ch = [](int i, int row) { return (i >> 1) * 32 + (row >> 2) * 8 + (i & 1) * 4 + (row & 3); };
+  vec8 af[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int wr = wave * 64 + wave_ch(i, fr);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      af[i][kk] = *(const vec8*)(wl + wr * kRowB + (((kk * 4 + fq) ^ ((wr >> 1) & 7)) << 4));
+  }
+
+  float ssum[4][4], ssq[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { ssum[i][r] = 0.f; ssq[i][r] = 0.f; }
+
+  int buf = 0;
+  bool first = true;
+  for (; t < tiles; t += G) {
+    if (!first) {
+      // tile t's DMA was issued before the previous tile's 16 stores (the previous tile was a full one: only a
+      // block's last tile can be the partial M tail); vector-memory ops retire in order, so waiting down to 16
+      // outstanding retires the DMA and leaves the stores in flight.  Raw barrier (no vmcnt(0) drain): every
+      // wave's part of the DMA landed and every wave finished reading the other ring slot.
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    first = false;
+    if (t + G < tiles) stage_x(t + G, buf ^ 1);
+
+    const char* xb = xl + buf * kTileB;
+    const int64_t mt = (int64_t)t * kBM;
+    // two 64-pixel halves (64 accumulators each, no spills): half 1's MFMAs run behind half 0's stores
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4_t acc[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        vec8 bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bf[j] = *(const vec8*)(xb + ((h * 4 + j) * 16 + fr) * kRowB + (((kk * 4 + fq) ^ sw) << 4));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i][kk], bf[j], acc[i][j]);
+      }
+      // epilogue: fragment pair p gives the lane channels wave*64 + p*32 + 8*fq + [0, 8) of pixel
+      // t*128 + (h*4 + j)*16 + fr
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t m = mt + (h * 4 + j) * 16 + fr;
+        uint16_t* yp = y + m * kK + wave * 64 + 8 * fq;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          uint16_t o[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = E::from_f(acc[2 * p + (r >> 2)][j][r & 3]);
+          uint4 pk;
+          pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+          pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+          pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
+          pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+          if (m < M) {
+            *(uint4*)(yp + p * 32) = pk;
+            if constexpr (STATS) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                const float q = E::to_f(o[r]);
+                ssum[2 * p + (r >> 2)][r & 3] += q;
+                ssq[2 * p + (r >> 2)][r & 3] += q * q;
+              }
+            }
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+  if constexpr (STATS) {
+    // reduce over the 16 pixel lanes; lane fr == 15 owns channel wave*64 + wave_ch(i, 4*fq + r) of the block's row
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ssum[i][r] = row16_sum(ssum[i][r]);
+        ssq[i][r] = row16_sum(ssq[i][r]);
+      }
+    if (fr == 15) {
+      float* dst = srows + (int64_t)blockIdx.x * kK * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wave * 64 + wave_ch(i, 4 * fq + r);
+          *(float2*)(dst + c * 2) = make_float2(ssum[i][r], ssq[i][r]);
+        }
+    }
+  }
+}
+
+bool conv1x1_c64_supported(int C, int Kout) {
+  // PDT_CONV1X1=0: the generic implicit-GEMM kernels (A/B)
+  static const bool on = [] {
+    const char* e = getenv("PDT_CONV1X1");
+    return !(e && e[0] == '0');
+  }();
+  return on && C == kC && Kout == kK;
+}
+
+void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
+                        hipStream_t s) {
+  if (M <= 0) return;
+  if (M * kRowB >= (int64_t(1) << 31) || M * kK >= (int64_t(1) << 31))
+    pdt_hip_fail("conv1x1_c64: operands exceed 32-bit offsets", hipErrorInvalidValue, __FILE__, __LINE__);
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  const int tiles = (int)((M + kBM - 1) / kBM);
+  const int G = tiles < 2 * cus ? tiles : 2 * cus;
+  Scratch part(stats ? (size_t)G * kK * 2 * sizeof(float) : 0, s);
+  float* srows = part.as<float>();
+  PDT_COUNT("conv1x1_c64");
+#define PDT_C1(DT_, ST_) hipLaunchKernelGGL((conv1x1_c64_kernel<DT_, ST_>), dim3(G), dim3(256), 0, s, x, w, y, srows, M)
+  if (dtype == kBF16) {
+    if (stats) PDT_C1(kBF16, true); else PDT_C1(kBF16, false);
+  } else {
+    if (stats) PDT_C1(kF16, true); else PDT_C1(kF16, false);
+  }
+#undef PDT_C1
+  if (stats) stat_rows_reduce_launch(srows, G, kK * 2, stats, s);
+}
+
+}  // namespace pdt

@@ -152,6 +152,7 @@ class ResNetExecutor:
         self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
         self.bk32_short = os.environ.get("PDT_BK32_SHORT", "1") == "1"
+        self._c1x1 = hasattr(self.C, "conv1x1_c64")
         # a layer1 block's inner BN + ReLU applied by its consumers (conv2 forward and conv2 weight
         # gradient) to their staged input tiles in LDS; the activation relu(bn(z1)) is never written or re-read
         self.fuse_pre = os.environ.get("PDT_FUSE_PRE", "1") == "1"
@@ -385,6 +386,13 @@ class ResNetExecutor:
             key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
             sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
         wt = self._w(c) if w is None else w
+        if (R == 1 and S == 1 and st == 1 and pad == 0 and cin == 64 and c.cout == 256 and
+                self._c1x1 and self.C.conv1x1_c64_supported(cin, c.cout)):
+            # ResNet-50 layer1's expanding 1x1 convs: the persistent store-overlapped kernel (conv1x1.hip)
+            self.C.conv1x1_c64(x, wt, y, sp, M)
+            if stats and fin is not None:
+                self.bn_train_finalize(fin, sp, 0, M)
+            return P, Q, sp, M
 
         def launch(bm, bn):
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,

@@ -778,3 +778,34 @@ def test_conv_l1_pingpong_matches_4wave(variant, N, H):
     if variant.startswith("fwd") and variant != "fwd_pre":
         ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
         assert _rel(y8, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M", [12544, 12544 + 37, 70000 + 5])
+def test_conv1x1_c64_matches_implicit_gemm(dtype, M):
+    """Persistent 1x1 64->256 conv (conv1x1.hip) vs the implicit-GEMM conv_fwd on the same operands: outputs
+    bit-identical (same MFMA K order), BN statistics equal to fp64 sums of the stored outputs; M tails and the
+    multi-tile-per-block path (M = 70005: 547 tiles > 2 blocks per CU)."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    if not C.conv1x1_c64_supported(64, 256):
+        pytest.skip("PDT_CONV1X1=0")
+    torch.manual_seed(21)
+    x = _rand16(M, 64, dtype=dtype)
+    w = _rand16(256, 64, dtype=dtype, scale=0.125)
+    y_ref = torch.empty(M, 256, dtype=dtype, device=DEV)
+    C.conv_fwd(x, w, y_ref, None, None, 1, 1, M, 64, 256, 1, 1, 1, M, 1, 1, 0, 0, 1, 1, 1, M, 1, 1, 0, 0,
+               128, 128, 64, 0)
+    for stats in (False, True):
+        y = torch.full((M, 256), float("nan"), dtype=dtype, device=DEV)
+        st = torch.zeros(C.stat_slots() * 256 * 2, dtype=torch.float64, device=DEV) if stats else None
+        C.conv1x1_c64(x, w, y, st, M)
+        torch.cuda.synchronize()
+        assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
+        if stats:
+            s = st.view(-1, 256, 2).sum(0)
+            yf = y.double()
+            assert torch.allclose(s[:, 0], yf.sum(0), rtol=1e-6, atol=1e-3)
+            assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
+    ref = x.float() @ w.float().t()
+    assert _rel(y, ref) < 1e-2

@@ -40,10 +40,12 @@ WINDOWS = {
     "conv_l1_kernel": {16: "dma", 12: "dma"},
     "stem_fwd_kernel": {24: "dma"},
     "wgrad_stem_kernel": {10: "dma", 8: "load"},
-    "conv_wgrad_wide_kernel": {6: ("dma", 6), 3: ("dma", 3)},  # the stage behind (6 / 3 DMAs) stays in flight
+    "conv_wgrad_wide_kernel": {6: ("dma", 6), 3: ("dma", 3)},
+    "conv1x1_c64_kernel": {16: "dma"},  # the previous tile's 16 stores stay in flight
 }
 COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "conv_pp_kernel",
-            "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel")
+            "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel",
+            "conv1x1_c64_kernel")
 
 
 def hip_flags():
