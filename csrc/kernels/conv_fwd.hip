@@ -836,15 +836,17 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     if (rs == 1) PDT_K(0, 1); else if (rs == 2) PDT_K(0, 2); else PDT_K(0, 0);
   } else if (epi == 1 && rs != 2) {
     if (rs) PDT_K(1, 1); else PDT_K(1, 0);
-  } else if constexpr ((BK == 64 && STAGES == 2 && (BN == 128 || BN == 64) && BM * BN == 4096 * NW) ||
+  } else if constexpr ((((BK == 64 && STAGES == 2) || (BK == 32 && STAGES == 3)) && (BN == 128 || BN == 64) &&
+                        BM * BN == 4096 * NW) ||
                        (BM == 256 && BN == 256)) {
-    // fused BN-backward epilogues: only on the backward-data tiles (128x128x64, 256x64x64)
+    // fused BN-backward epilogues: only on the backward-data tiles (128x128, 256x64: BK = 64 on the 2-stage ring,
+    // BK = 32 on the 3-stage ring for short sub-pixel-phase reductions)
     if (epi == 2 && !rs) PDT_K(2, 0);
     else if (epi == 3 && rs) { if (rs == 2) PDT_K(3, 2); else PDT_K(3, 1); }
     else if (epi == 4 && rs) { if (rs == 2) PDT_K(4, 2); else PDT_K(4, 1); }
     else pdt_hip_fail("conv_fwd: unsupported BN-backward epilogue variant", hipErrorInvalidValue, __FILE__, __LINE__);
   } else {
-    pdt_hip_fail("conv_fwd: BN-backward epilogue needs a 128x128x64 or 256x64x64 tile", hipErrorInvalidValue,
+    pdt_hip_fail("conv_fwd: BN-backward epilogue needs a 128x128 or 256x64 tile", hipErrorInvalidValue,
                  __FILE__, __LINE__);
   }
 #undef PDT_K

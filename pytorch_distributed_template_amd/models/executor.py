@@ -33,6 +33,9 @@ from ..ops.conv import conv_tile as _conv_tile, dgrad_phases, dgrad_weight_index
 from .resnet import BasicBlock, Bottleneck, ResNet
 
 _BUF_POISON = os.environ.get("PDT_BUF_POISON", "0") == "1"
+# PDT_DGRAD_BK32=s2|all: backward-data convs (stride-2 only | all) on the 3-stage BK=32 ring instead of the
+# 2-stage BK=64 one (A/B knob)
+_DGRAD_BK32 = os.environ.get("PDT_DGRAD_BK32", "0")
 
 
 def _load_tuned():
@@ -487,6 +490,8 @@ class ResNetExecutor:
             return
         bk = 64 if c.cout % 64 == 0 else 32
         dst = c.st
+        if _DGRAD_BK32 == "all" or (_DGRAD_BK32 == "s2" and dst == 2 and not compact):
+            bk = 32  # 3-stage BK=32 ring: two K-steps in flight for the short sub-pixel-phase reductions
         if compact:
             ph0 = c.phases[0]
             assert c.R == 1 and c.S == 1 and c.pad == 0 and tuple(ph0[:6]) == (0, 0, 1, 1, 0, 0), "compact: 1x1 only"
@@ -502,6 +507,8 @@ class ResNetExecutor:
                 self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, dst, phases, bm, bn,
                                      bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
         key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
+        if bk == 32 and c.cout % 64 == 0:
+            key = key + ("bk32",)  # not a tuned-table shape
         bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
         launch(bm, bn)
         if fin is not None and bnb is not None:  # fin = (count, bn1, bn2): the fused reduce's BN-backward finalize

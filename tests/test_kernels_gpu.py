@@ -809,3 +809,34 @@ def test_conv1x1_c64_matches_implicit_gemm(dtype, M):
             assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
     ref = x.float() @ w.float().t()
     assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("bm,bn", [(256, 64), (128, 128)])
+def test_conv_dgrad_fused_bn_bk32_ring_bit_identical(mode, bm, bn):
+    """The fused BN-backward dgrad epilogue on the 3-stage BK=32 ring (PDT_DGRAD_BK32) is bit-identical to the
+    2-stage BK=64 kernel (same MFMA K order, same epilogue): dz and the statistics slots, stride-2 phases with a
+    compact residual on phase 0."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    N, H, W, C, K, R, st, pad = 3, 28, 28, bn if bn == 128 else 64, 128, 3, 2, 1
+    torch.manual_seed(17)
+    P, Q = conv.out_hw(H, W, R, R, st, pad)
+    dy = _rand16(N, P, Q, K)
+    w = _rand16(K, R, R, C, scale=(1.0 / (K * R * R)) ** 0.5)
+    res = _rand16(N, P, Q, C) if mode > 1 else None
+    y1 = _rand16(N, H, W, C)
+    coef1 = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3,
+                       y1.float().view(-1, C).mean(0), torch.rand(C, device=DEV) + 0.5]).contiguous()
+    y2 = _rand16(N, H, W, C) if mode == 3 else None
+    coef2 = coef1.flip(0).contiguous() if mode == 3 else None
+    om = conv.pack_relu_mask(torch.relu(_rand16(N, H, W, C))) if mode > 1 else None
+    K_ = 4 if mode == 3 else 2
+    outs = []
+    for bk in (64, 32):
+        slots = torch.zeros(native.C.stat_slots() * C * K_, dtype=torch.float64, device=DEV)
+        dz = conv.conv_dgrad(dy, w, H, W, st, pad, residual=res, bnb=(mode, y1, coef1, y2, coef2, om, slots),
+                             tile=(bm, bn, bk), res_phase=0 if res is not None else -1)
+        outs.append((dz, slots))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+    assert torch.equal(outs[0][1], outs[1][1])
