@@ -332,6 +332,18 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     a.bn_mask = pmask(bn_mask, dx.numel(), "bn_mask");
     a.stats = pd(*bn_slots, "bn_slots");
   }
+  if (bnb == 2 && res_phase < 0 && stride == 1 && phases.size() == 1 && K == 64 && C == 256 && H == P && W == Q &&
+      pdt::conv1x1_c64_supported(K, C)) {
+    const auto& f = phases[0];
+    if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
+      // 1x1 256 -> 64 conv's backward-data with the block-output BN-backward epilogue: persistent kernel (conv1x1.hip);
+      // its [256][64] weights start at the phase's offset (bounds checked with the phases above)
+      pdt::conv1x1_c64_bnb_launch(a.x, a.w + f[6], a.y, a.res, a.bn_y1, a.bn_coef1, a.bn_mask, a.stats, N * P * Q, dt,
+                                  cur_stream());
+      launched("conv1x1_c64_bnb");
+      return;
+    }
+  }
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
   launched("conv_fwd_launch");
 }
@@ -1184,6 +1196,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv1x1_c64_supported", &conv1x1_c64_supported);
   m.def("conv1x1_c64", &conv1x1_c64);
+  m.def("conv1x1_c64_mode", [](int64_t set) { return (int64_t)pdt::conv1x1_c64_mode((int)set); });
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_wgrad_stem_fused", &conv_wgrad_stem_fused);
   m.def("wgrad_reduce", &wgrad_reduce);

@@ -8,6 +8,12 @@ namespace pdt {
 // downsample): y[m][k] = sum_c x[m][c] * w[k][c] over M pixels, optional BN statistics of the rounded outputs into
 // fp64 slots (conv_fwd.h).  See conv1x1.hip.
 bool conv1x1_c64_supported(int C, int Kout);
+int conv1x1_c64_mode(int set);  // returns the previous on/off mode; set >= 0 changes it (PDT_CONV1X1 seeds it)
+// The same GEMM as the backward-data pass of a 1x1 256 -> 64 conv, with the fused block-output BN-backward epilogue
+// (conv_fwd.h EPI 3: + residual, ReLU bit of the block output, sum dz and sum dz * xhat1 into fp64 slots).
+void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res,
+                            const uint16_t* y1, const float* coef1, const uint8_t* mask, double* slots, int64_t M,
+                            int dtype, hipStream_t s);
 void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
                         hipStream_t s);
 

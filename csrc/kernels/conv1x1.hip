@@ -187,14 +187,234 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __r
   }
 }
 
-bool conv1x1_c64_supported(int C, int Kout) {
-  // PDT_CONV1X1=0: the generic implicit-GEMM kernels (A/B)
-  static const bool on = [] {
-    const char* e = getenv("PDT_CONV1X1");
-    return !(e && e[0] == '0');
-  }();
-  return on && C == kC && Kout == kK;
+// ------------------------------------------------------------------------------------------------
+// The same GEMM as the backward-data pass of ResNet-50 layer1's REDUCING 1x1 conv (256 -> 64 forward: dX[M][256] =
+// dY[M][64] x W^T), with the dgrad epilogue of a block-output BatchNorm fused (conv_fwd.h EPI 3): v = acc + res,
+// dz = v where the block output's ReLU bit is set (else 0), stored rounded, and per channel sum(dz) and
+// sum(dz * (y1 - mean1) * invstd1) into the block's statistics row.  The generic path runs this as the 512 x 128
+// ping-pong kernel with ONE K-step per tile (1.5-1.7 ms per call at B = 1200).
+// Tiles are 64 pixels (two 32-pixel sub-tiles): per tile and wave 24 epilogue operand loads (residual, y1: 16 B;
+// mask: 1 B per 8 channels) and 8 stores follow the next tile's input DMA, so the loop-top wait is vmcnt(32).
+namespace {
+constexpr int kBMb = 64;
+constexpr int kTileBb = kBMb * kRowB;  // 8 KB
+constexpr int kOpsPerTileB = 32;       // vector-memory ops per wave after the next tile's DMA (24 loads + 8 stores)
+}  // namespace
+
+template <int DT>
+__global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t* __restrict__ x,
+                                                                 const uint16_t* __restrict__ w,
+                                                                 uint16_t* __restrict__ y,
+                                                                 const uint16_t* __restrict__ res,
+                                                                 const uint16_t* __restrict__ y1,
+                                                                 const float* __restrict__ coef1,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 float* __restrict__ srows, int64_t M) {
+  static_assert(kOpsPerTileB == 32, "the loop-top s_waitcnt vmcnt(32) literal below");
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  __shared__ __attribute__((aligned(1024))) char smem[kWB + 2 * kTileBb];
+  char* const wl = smem;
+  char* const xl = smem + kWB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  const int sw = (fr >> 1) & 7;
+  const int tiles = (int)((M + kBMb - 1) / kBMb);
+  const int G = gridDim.x;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * kRowB));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)kWB);
+  auto wave_ch = [](int i, int row) { return (i >> 1) * 32 + (row >> 2) * 8 + (i & 1) * 4 + (row & 3); };
+
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ins = wave * 8 + j;
+    const int row = ins * 8 + lrow;
+    buf_lds16_asm(rw, wl + ins * 1024, (uint32_t)(row * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)));
+  }
+  // one tile's input: 8 instructions, 2 per wave
+  auto stage_x = [&](int t, int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ins = wave * 2 + j;
+      const int row = ins * 8 + lrow;
+      const int64_t m = (int64_t)t * kBMb + row;
+      const uint32_t off = m < M ? (uint32_t)(m * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
+      buf_lds16_asm(rx, xl + buf * kTileBb + ins * 1024, off);
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < tiles) stage_x(t, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  vec8 af[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int wr = wave * 64 + wave_ch(i, fr);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      af[i][kk] = *(const vec8*)(wl + wr * kRowB + (((kk * 4 + fq) ^ ((wr >> 1) & 7)) << 4));
+  }
+  // BN-1 mean / invstd of this lane's 16 output channels: pair p, element e -> channel wave*64 + p*32 + 8*fq + e
+  float mu[2][8], is[2][8];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = wave * 64 + p * 32 + 8 * fq + e;
+      mu[p][e] = coef1[2 * kK + c];
+      is[p][e] = coef1[3 * kK + c];
+    }
+  float s0[2][8], s1[2][8];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s0[p][e] = 0.f; s1[p][e] = 0.f; }
+
+  int buf = 0;
+  bool first = true;
+  for (; t < tiles; t += G) {
+    if (!first) {
+      // tile t's DMA was issued before the previous (full) tile's 24 operand loads and 8 stores: waiting down to 32
+      // outstanding retires it and leaves the stores in flight
+      asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    first = false;
+    if (t + G < tiles) stage_x(t + G, buf ^ 1);
+
+    const char* xb = xl + buf * kTileBb;
+    const int64_t mt = (int64_t)t * kBMb;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // epilogue operands first (independent of the MFMAs); rows past M load row M-1 and are not stored
+      uint4 rr[2][2], yy[2][2];
+      uint32_t mb[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        int64_t m = mt + (h * 2 + j) * 16 + fr;
+        m = m < M ? m : M - 1;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int64_t o = m * kK + wave * 64 + p * 32 + 8 * fq;
+          rr[j][p] = *(const uint4*)(res + o);
+          yy[j][p] = *(const uint4*)(y1 + o);
+          mb[j][p] = mask[o >> 3];
+        }
+      }
+      f32x4_t acc[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        vec8 bf[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bf[j] = *(const vec8*)(xb + ((h * 2 + j) * 16 + fr) * kRowB + (((kk * 4 + fq) ^ sw) << 4));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = E::mfma16x16x32(af[i][kk], bf[j], acc[i][j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t m = mt + (h * 2 + j) * 16 + fr;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint32_t rw4[4] = {rr[j][p].x, rr[j][p].y, rr[j][p].z, rr[j][p].w};
+          const uint32_t yw4[4] = {yy[j][p].x, yy[j][p].y, yy[j][p].z, yy[j][p].w};
+          uint16_t o[8];
+          float q1[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(rw4[e >> 1] >> (16 * (e & 1))));
+            if (!((mb[j][p] >> e) & 1u)) v = 0.f;
+            o[e] = E::from_f(v);
+            q1[e] = E::to_f((uint16_t)(yw4[e >> 1] >> (16 * (e & 1))));
+          }
+          uint4 pk;
+          pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+          pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+          pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
+          pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+          if (m < M) {
+            *(uint4*)(y + m * kK + wave * 64 + p * 32 + 8 * fq) = pk;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float dz = E::to_f(o[e]);
+              s0[p][e] += dz;
+              s1[p][e] += dz * (q1[e] - mu[p][e]) * is[p][e];
+            }
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+  // reduce over the 16 pixel lanes; lane fr == 15 owns channels wave*64 + p*32 + 8*fq + e of the block's row
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s0[p][e] = row16_sum(s0[p][e]);
+      s1[p][e] = row16_sum(s1[p][e]);
+    }
+  if (fr == 15) {
+    float* dst = srows + (int64_t)blockIdx.x * kK * 2;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = wave * 64 + p * 32 + 8 * fq + e;
+        *(float2*)(dst + c * 2) = make_float2(s0[p][e], s1[p][e]);
+      }
+  }
 }
+
+void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res,
+                            const uint16_t* y1, const float* coef1, const uint8_t* mask, double* slots, int64_t M,
+                            int dtype, hipStream_t s) {
+  if (M <= 0) return;
+  if (M * kK >= (int64_t(1) << 31))
+    pdt_hip_fail("conv1x1_c64_bnb: operands exceed 32-bit offsets", hipErrorInvalidValue, __FILE__, __LINE__);
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  const int tiles = (int)((M + kBMb - 1) / kBMb);
+  const int G = tiles < 2 * cus ? tiles : 2 * cus;
+  Scratch part((size_t)G * kK * 2 * sizeof(float), s);
+  float* srows = part.as<float>();
+  PDT_COUNT("conv1x1_c64_bnb");
+  if (dtype == kBF16)
+    hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<kBF16>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, mask, srows, M);
+  else
+    hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<kF16>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, mask, srows, M);
+  stat_rows_reduce_launch(srows, G, kK * 2, slots, s);
+}
+
+int conv1x1_c64_mode(int set) {
+  // PDT_CONV1X1=0: the generic implicit-GEMM kernels (A/B); set >= 0 switches at run time (tests)
+  static int on = [] {
+    const char* e = getenv("PDT_CONV1X1");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  const int prev = on;
+  if (set >= 0) on = set;
+  return prev;
+}
+
+bool conv1x1_c64_supported(int C, int Kout) { return conv1x1_c64_mode(-1) && C == kC && Kout == kK; }
 
 void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
                         hipStream_t s) {
