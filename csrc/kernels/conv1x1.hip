@@ -191,31 +191,38 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __r
 // The same GEMM as the backward-data pass of ResNet-50 layer1's REDUCING 1x1 conv (256 -> 64 forward: dX[M][256] =
 // dY[M][64] x W^T), with the dgrad epilogue of a block-output BatchNorm fused (conv_fwd.h EPI 3): v = acc + res,
 // dz = v where the block output's ReLU bit is set (else 0), stored rounded, and per channel sum(dz) and
-// sum(dz * (y1 - mean1) * invstd1) into the block's statistics row.  The generic path runs this as the 512 x 128
+// sum(dz * (y1 - mean1) * invstd1) into the block's statistics row; BR = 2 (EPI 4): a second BatchNorm branch on
+// the same block input (a downsample block's main and shortcut BN) adds sum(dz * (y2 - mean2) * invstd2).  The generic path runs this as the 512 x 128
 // ping-pong kernel with ONE K-step per tile (1.5-1.7 ms per call at B = 1200).
 // Tiles are 64 pixels (two 32-pixel sub-tiles): per tile and wave 24 epilogue operand loads (residual, y1: 16 B;
-// mask: 1 B per 8 channels) and 8 stores follow the next tile's input DMA, so the loop-top wait is vmcnt(32).
+// mask: 1 B per 8 channels; BR = 2: 8 more for y2) and 8 stores follow the next tile's input DMA, so the loop-top
+// wait is vmcnt(32) (BR = 2: vmcnt(40)).
 namespace {
 constexpr int kBMb = 64;
 constexpr int kTileBb = kBMb * kRowB;  // 8 KB
-constexpr int kOpsPerTileB = 32;       // vector-memory ops per wave after the next tile's DMA (24 loads + 8 stores)
+constexpr int kOpsPerTileB = 32;       // vector-memory ops per wave after the next tile's DMA (24 loads + 8 stores; +8)
 }  // namespace
 
-template <int DT>
+template <int DT, int BR>
 __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ w,
                                                                  uint16_t* __restrict__ y,
                                                                  const uint16_t* __restrict__ res,
                                                                  const uint16_t* __restrict__ y1,
                                                                  const float* __restrict__ coef1,
+                                                                 const uint16_t* __restrict__ y2,
+                                                                 const float* __restrict__ coef2,
                                                                  const uint8_t* __restrict__ mask,
                                                                  float* __restrict__ srows, int64_t M) {
-  static_assert(kOpsPerTileB == 32, "the loop-top s_waitcnt vmcnt(32) literal below");
+  static_assert(BR == 1 || BR == 2, "one or two BatchNorm branches");
+  static_assert(kOpsPerTileB == 32, "the loop-top s_waitcnt vmcnt(32 | 40) literals below");
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
-  __shared__ __attribute__((aligned(1024))) char smem[kWB + 2 * kTileBb];
+  __shared__ __attribute__((aligned(1024))) char smem[kWB + 2 * kTileBb + BR * 2 * kK * 4];
   char* const wl = smem;
   char* const xl = smem + kWB;
+  // per-branch BN mean / invstd of all 256 channels: cf[(branch * 2 + 0 | 1) * 256 + c]
+  float* const cf = (float*)(smem + kWB + 2 * kTileBb);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
@@ -247,6 +254,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
 
   int t = blockIdx.x;
   if (t < tiles) stage_x(t, 0);
+  cf[tid] = coef1[2 * kK + tid];
+  cf[kK + tid] = coef1[3 * kK + tid];
+  if constexpr (BR == 2) {
+    cf[2 * kK + tid] = coef2[2 * kK + tid];
+    cf[3 * kK + tid] = coef2[3 * kK + tid];
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -258,29 +271,27 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
     for (int kk = 0; kk < 2; ++kk)
       af[i][kk] = *(const vec8*)(wl + wr * kRowB + (((kk * 4 + fq) ^ ((wr >> 1) & 7)) << 4));
   }
-  // BN-1 mean / invstd of this lane's 16 output channels: pair p, element e -> channel wave*64 + p*32 + 8*fq + e
-  float mu[2][8], is[2][8];
+  // statistics of this lane's 16 output channels: pair p, element e -> channel wave*64 + p*32 + 8*fq + e
+  float s0[2][8], s1[2][8], s2[BR == 2 ? 2 : 1][8];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = wave * 64 + p * 32 + 8 * fq + e;
-      mu[p][e] = coef1[2 * kK + c];
-      is[p][e] = coef1[3 * kK + c];
+      s0[p][e] = 0.f;
+      s1[p][e] = 0.f;
+      if constexpr (BR == 2) s2[p][e] = 0.f;
     }
-  float s0[2][8], s1[2][8];
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s0[p][e] = 0.f; s1[p][e] = 0.f; }
 
   int buf = 0;
   bool first = true;
   for (; t < tiles; t += G) {
     if (!first) {
-      // tile t's DMA was issued before the previous (full) tile's 24 operand loads and 8 stores: waiting down to 32
-      // outstanding retires it and leaves the stores in flight
-      asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      // tile t's DMA was issued before the previous (full) tile's 24 | 32 operand loads and 8 stores: waiting down to
+      // that many outstanding retires it and leaves the stores in flight
+      if constexpr (BR == 1)
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -293,7 +304,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       // epilogue operands first (independent of the MFMAs); rows past M load row M-1 and are not stored
-      uint4 rr[2][2], yy[2][2];
+      uint4 rr[2][2], yy[2][2], yz[BR == 2 ? 2 : 1][2];
       uint32_t mb[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -304,6 +315,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
           const int64_t o = m * kK + wave * 64 + p * 32 + 8 * fq;
           rr[j][p] = *(const uint4*)(res + o);
           yy[j][p] = *(const uint4*)(y1 + o);
+          if constexpr (BR == 2) yz[j][p] = *(const uint4*)(y2 + o);
           mb[j][p] = mask[o >> 3];
         }
       }
@@ -331,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
           const uint32_t rw4[4] = {rr[j][p].x, rr[j][p].y, rr[j][p].z, rr[j][p].w};
           const uint32_t yw4[4] = {yy[j][p].x, yy[j][p].y, yy[j][p].z, yy[j][p].w};
           uint16_t o[8];
-          float q1[8];
+          float q1[8], q2[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(rw4[e >> 1] >> (16 * (e & 1))));
@@ -339,18 +351,36 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
             o[e] = E::from_f(v);
             q1[e] = E::to_f((uint16_t)(yw4[e >> 1] >> (16 * (e & 1))));
           }
+          if constexpr (BR == 2) {
+            const uint32_t zw4[4] = {yz[j][p].x, yz[j][p].y, yz[j][p].z, yz[j][p].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q2[e] = E::to_f((uint16_t)(zw4[e >> 1] >> (16 * (e & 1))));
+          }
           uint4 pk;
           pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
           pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
           pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
           pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
           if (m < M) {
-            *(uint4*)(y + m * kK + wave * 64 + p * 32 + 8 * fq) = pk;
+            const int c0 = wave * 64 + p * 32 + 8 * fq;
+            *(uint4*)(y + m * kK + c0) = pk;
+            const float4 ma = *(const float4*)(cf + c0), mb4 = *(const float4*)(cf + c0 + 4);
+            const float4 ia = *(const float4*)(cf + kK + c0), ib = *(const float4*)(cf + kK + c0 + 4);
+            const float mu[8] = {ma.x, ma.y, ma.z, ma.w, mb4.x, mb4.y, mb4.z, mb4.w};
+            const float is[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float dz = E::to_f(o[e]);
               s0[p][e] += dz;
-              s1[p][e] += dz * (q1[e] - mu[p][e]) * is[p][e];
+              s1[p][e] += dz * (q1[e] - mu[e]) * is[e];
+            }
+            if constexpr (BR == 2) {
+              const float4 na = *(const float4*)(cf + 2 * kK + c0), nb = *(const float4*)(cf + 2 * kK + c0 + 4);
+              const float4 ja = *(const float4*)(cf + 3 * kK + c0), jb = *(const float4*)(cf + 3 * kK + c0 + 4);
+              const float mu2[8] = {na.x, na.y, na.z, na.w, nb.x, nb.y, nb.z, nb.w};
+              const float is2[8] = {ja.x, ja.y, ja.z, ja.w, jb.x, jb.y, jb.z, jb.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) s2[p][e] += E::to_f(o[e]) * (q2[e] - mu2[e]) * is2[e];
             }
           }
         }
@@ -360,28 +390,34 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
   }
 
   // reduce over the 16 pixel lanes; lane fr == 15 owns channels wave*64 + p*32 + 8*fq + e of the block's row
+  // ([256][2] = (sum dz, sum dz*xhat1); two branches: [256][4] = (sum dz, sum dz*xhat1, sum dz, sum dz*xhat2))
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       s0[p][e] = row16_sum(s0[p][e]);
       s1[p][e] = row16_sum(s1[p][e]);
+      if constexpr (BR == 2) s2[p][e] = row16_sum(s2[p][e]);
     }
   if (fr == 15) {
-    float* dst = srows + (int64_t)blockIdx.x * kK * 2;
+    constexpr int KO = BR == 2 ? 4 : 2;
+    float* dst = srows + (int64_t)blockIdx.x * kK * KO;
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = wave * 64 + p * 32 + 8 * fq + e;
-        *(float2*)(dst + c * 2) = make_float2(s0[p][e], s1[p][e]);
+        if constexpr (BR == 2)
+          *(float4*)(dst + c * 4) = make_float4(s0[p][e], s1[p][e], s0[p][e], s2[p][e]);
+        else
+          *(float2*)(dst + c * 2) = make_float2(s0[p][e], s1[p][e]);
       }
   }
 }
 
 void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res,
-                            const uint16_t* y1, const float* coef1, const uint8_t* mask, double* slots, int64_t M,
-                            int dtype, hipStream_t s) {
+                            const uint16_t* y1, const float* coef1, const uint16_t* y2, const float* coef2,
+                            const uint8_t* mask, double* slots, int64_t M, int dtype, hipStream_t s) {
   if (M <= 0) return;
   if (M * kK >= (int64_t(1) << 31))
     pdt_hip_fail("conv1x1_c64_bnb: operands exceed 32-bit offsets", hipErrorInvalidValue, __FILE__, __LINE__);
@@ -393,14 +429,20 @@ void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   }();
   const int tiles = (int)((M + kBMb - 1) / kBMb);
   const int G = tiles < 2 * cus ? tiles : 2 * cus;
-  Scratch part((size_t)G * kK * 2 * sizeof(float), s);
+  const int KO = y2 ? 4 : 2;
+  Scratch part((size_t)G * kK * KO * sizeof(float), s);
   float* srows = part.as<float>();
   PDT_COUNT("conv1x1_c64_bnb");
-  if (dtype == kBF16)
-    hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<kBF16>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, mask, srows, M);
-  else
-    hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<kF16>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, mask, srows, M);
-  stat_rows_reduce_launch(srows, G, kK * 2, slots, s);
+#define PDT_CB(DT_, BR_)                                                                                    \
+  hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<DT_, BR_>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, y2, coef2, \
+                     mask, srows, M)
+  if (dtype == kBF16) {
+    if (y2) PDT_CB(kBF16, 2); else PDT_CB(kBF16, 1);
+  } else {
+    if (y2) PDT_CB(kF16, 2); else PDT_CB(kF16, 1);
+  }
+#undef PDT_CB
+  stat_rows_reduce_launch(srows, G, kK * KO, slots, s);
 }
 
 int conv1x1_c64_mode(int set) {

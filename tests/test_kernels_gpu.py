@@ -844,10 +844,12 @@ def test_conv_dgrad_fused_bn_bk32_ring_bit_identical(mode, bm, bn):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("NHW", [(4, 56, 56), (3, 13, 11)])
-def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW):
+@pytest.mark.parametrize("mode", [2, 3])
+def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode):
     """Backward-data of a 1x1 256 -> 64 conv with the fused block-output BN-backward epilogue (residual, ReLU bit of
-    the block output, sum dz, sum dz * xhat) on the persistent 1x1 kernel (conv1x1.hip) vs the generic implicit-GEMM
-    epilogue: dz bit-identical, statistics equal up to summation order; M tails (3 * 13 * 11 = 429 pixels)."""
+    the block output, sum dz, sum dz * xhat; mode 3: a second BN branch, sum dz * xhat2) on the persistent 1x1
+    kernel (conv1x1.hip) vs the generic implicit-GEMM epilogue: dz bit-identical, statistics equal up to summation
+    order; M tails (3 * 13 * 11 = 429 pixels)."""
     from pytorch_distributed_template_amd.ops import conv, native
     C = native.C
     N, H, W = NHW
@@ -855,19 +857,24 @@ def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW):
     dy = _rand16(N, H, W, 64, dtype=dtype)
     w = _rand16(64, 1, 1, 256, dtype=dtype, scale=0.125)
     res = _rand16(N, H, W, 256, dtype=dtype)
-    y1 = _rand16(N, H, W, 256, dtype=dtype)
-    coef1 = torch.cat([torch.rand(256, device=DEV) + 0.5, torch.randn(256, device=DEV) * 0.3,
-                       y1.float().view(-1, 256).mean(0), torch.rand(256, device=DEV) + 0.5]).contiguous()
+
+    def branch():
+        yb = _rand16(N, H, W, 256, dtype=dtype)
+        cb = torch.cat([torch.rand(256, device=DEV) + 0.5, torch.randn(256, device=DEV) * 0.3,
+                        yb.float().view(-1, 256).mean(0), torch.rand(256, device=DEV) + 0.5]).contiguous()
+        return yb, cb
+    y1, coef1 = branch()
+    y2, coef2 = branch() if mode == 3 else (None, None)
+    K_ = 4 if mode == 3 else 2
     om = conv.pack_relu_mask(torch.relu(_rand16(N, H, W, 256)))
     outs = []
     prev = C.conv1x1_c64_mode(0)
     try:
-        for mode in (0, 1):
-            C.conv1x1_c64_mode(mode)
-            slots = torch.zeros(C.stat_slots() * 256 * 2, dtype=torch.float64, device=DEV)
-            dz = torch.full((N, H, W, 256), float("nan"), dtype=dtype, device=DEV)
-            dz = conv.conv_dgrad(dy, w, H, W, 1, 0, residual=res, bnb=(2, y1, coef1, None, None, om, slots))
-            outs.append((dz, slots.view(-1, 256, 2).sum(0)))
+        for on in (0, 1):
+            C.conv1x1_c64_mode(on)
+            slots = torch.zeros(C.stat_slots() * 256 * K_, dtype=torch.float64, device=DEV)
+            dz = conv.conv_dgrad(dy, w, H, W, 1, 0, residual=res, bnb=(mode, y1, coef1, y2, coef2, om, slots))
+            outs.append((dz, slots.view(-1, 256, K_).sum(0)))
         torch.cuda.synchronize()
     finally:
         C.conv1x1_c64_mode(prev)
@@ -876,6 +883,9 @@ def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW):
     assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-3)
     # and against fp64 sums of the stored dz
     d = dz1.double().view(-1, 256)
-    xh = ((y1.float() - coef1[512:768]) * coef1[768:]).double().view(-1, 256)
-    assert torch.allclose(s1[:, 0], d.sum(0), rtol=1e-4, atol=1e-2)
-    assert torch.allclose(s1[:, 1], (d * xh).sum(0), rtol=1e-4, atol=1e-2)
+    for k, (yb, cb) in ((1, (y1, coef1)), (3, (y2, coef2))):
+        if yb is None:
+            continue
+        xh = ((yb.float() - cb[512:768]) * cb[768:]).double().view(-1, 256)
+        assert torch.allclose(s1[:, k - 1], d.sum(0), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(s1[:, k], (d * xh).sum(0), rtol=1e-4, atol=1e-2)

@@ -42,7 +42,7 @@ WINDOWS = {
     "wgrad_stem_kernel": {10: "dma", 8: "load"},
     "conv_wgrad_wide_kernel": {6: ("dma", 6), 3: ("dma", 3)},
     "conv1x1_c64_kernel": {16: "dma"},  # the previous tile's 16 stores stay in flight
-    "conv1x1_c64_bnb_kernel": {32: "dma"},  # the previous tile's 24 operand loads + 8 stores
+    "conv1x1_c64_bnb_kernel": {32: "dma", 40: "dma"},  # the previous tile's 24 (32) operand loads + 8 stores
 }
 COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "conv_pp_kernel",
             "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel",
