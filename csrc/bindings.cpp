@@ -332,14 +332,16 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     a.bn_mask = pmask(bn_mask, dx.numel(), "bn_mask");
     a.stats = pd(*bn_slots, "bn_slots");
   }
-  if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 && K == 64 && C == 256 && H == P && W == Q &&
-      pdt::conv1x1_c64_supported(K, C)) {
+  if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 &&
+      (K == 64 || (K == 128 && bnb == 2)) && C == 256 && H == P && W == Q && pdt::conv1x1_c64_supported(64, C)) {
     const auto& f = phases[0];
     if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
-      // 1x1 256 -> 64 conv's backward-data with the block-output BN-backward epilogue: persistent kernel (conv1x1.hip);
-      // its [256][64] weights start at the phase's offset (bounds checked with the phases above)
+      // 1x1 256 -> 64 | 128 conv's backward-data with the block-output BN-backward epilogue: persistent kernel
+      // (conv1x1.hip);
+      // its [256][K] weights start at the phase's offset (bounds checked with the phases above)
       pdt::conv1x1_c64_bnb_launch(a.x, a.w + f[6], a.y, a.res, a.bn_y1, a.bn_coef1, bnb == 3 ? a.bn_y2 : nullptr,
-                                  bnb == 3 ? a.bn_coef2 : nullptr, a.bn_mask, a.stats, N * P * Q, dt, cur_stream());
+                                  bnb == 3 ? a.bn_coef2 : nullptr, a.bn_mask, a.stats, N * P * Q, (int)K, dt,
+                                  cur_stream());
       launched("conv1x1_c64_bnb");
       return;
     }

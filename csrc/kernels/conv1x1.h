@@ -11,10 +11,11 @@ bool conv1x1_c64_supported(int C, int Kout);
 int conv1x1_c64_mode(int set);  // returns the previous on/off mode; set >= 0 changes it (PDT_CONV1X1 seeds it)
 // The same GEMM as the backward-data pass of a 1x1 256 -> 64 conv, with the fused block-output BN-backward epilogue
 // (conv_fwd.h EPI 3: + residual, ReLU bit of the block output, sum dz and sum dz * xhat1 into fp64 slots).
-// y2 / coef2 != nullptr: a second BN branch (EPI 4), slots [C][4] = (sum dz, sum dz*xhat1, sum dz, sum dz*xhat2)
+// y2 / coef2 != nullptr: a second BN branch (EPI 4), slots [C][4] = (sum dz, sum dz*xhat1, sum dz, sum dz*xhat2).
+// cin = reduction channels of x (64, or 128 with one branch: ResNet-50 layer2.0's 256 -> 128 conv1).
 void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res,
                             const uint16_t* y1, const float* coef1, const uint16_t* y2, const float* coef2,
-                            const uint8_t* mask, double* slots, int64_t M, int dtype, hipStream_t s);
+                            const uint8_t* mask, double* slots, int64_t M, int cin, int dtype, hipStream_t s);
 void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
                         hipStream_t s);
 

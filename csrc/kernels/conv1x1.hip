@@ -203,7 +203,7 @@ constexpr int kTileBb = kBMb * kRowB;  // 8 KB
 constexpr int kOpsPerTileB = 32;       // vector-memory ops per wave after the next tile's DMA (24 loads + 8 stores; +8)
 }  // namespace
 
-template <int DT, int BR>
+template <int DT, int BR, int KH>
 __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ w,
                                                                  uint16_t* __restrict__ y,
@@ -215,14 +215,20 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
                                                                  const uint8_t* __restrict__ mask,
                                                                  float* __restrict__ srows, int64_t M) {
   static_assert(BR == 1 || BR == 2, "one or two BatchNorm branches");
+  static_assert(KH == 1 || KH == 2, "64 or 128 reduction channels");
   static_assert(kOpsPerTileB == 32, "the loop-top s_waitcnt vmcnt(32 | 40) literals below");
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
-  __shared__ __attribute__((aligned(1024))) char smem[kWB + 2 * kTileBb + BR * 2 * kK * 4];
+  // KH 64-channel halves of the reduction, each in the 128-B-row layout of the K = 64 kernel.  KH = 2: the 64 KB of
+  // weights pass through LDS once (into registers) and the input ring then reuses that area (2 workgroups per CU)
+  constexpr int kXOff = KH == 1 ? kWB : 0;
+  constexpr int kCfOff = KH == 1 ? kWB + 2 * kTileBb : 2 * kWB;
+  static_assert(KH == 1 || 2 * KH * kTileBb <= KH * kWB, "input ring inside the weight staging area");
+  __shared__ __attribute__((aligned(1024))) char smem[kCfOff + BR * 2 * kK * 4];
   char* const wl = smem;
-  char* const xl = smem + kWB;
+  char* const xl = smem + kXOff;
   // per-branch BN mean / invstd of all 256 channels: cf[(branch * 2 + 0 | 1) * 256 + c]
-  float* const cf = (float*)(smem + kWB + 2 * kTileBb);
+  float* const cf = (float*)(smem + kCfOff);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
@@ -230,30 +236,39 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
   const int sw = (fr >> 1) & 7;
   const int tiles = (int)((M + kBMb - 1) / kBMb);
   const int G = gridDim.x;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * kRowB));
-  const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)kWB);
+  constexpr int kSrcRow = KH * kRowB;  // bytes per source row (x: pixel, w: output channel)
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * kSrcRow));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)(KH * kWB));
   auto wave_ch = [](int i, int row) { return (i >> 1) * 32 + (row >> 2) * 8 + (i & 1) * 4 + (row & 3); };
 
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int ins = wave * 8 + j;
-    const int row = ins * 8 + lrow;
-    buf_lds16_asm(rw, wl + ins * 1024, (uint32_t)(row * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)));
-  }
-  // one tile's input: 8 instructions, 2 per wave
+  for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ins = wave * 8 + j;
+      const int row = ins * 8 + lrow;
+      buf_lds16_asm(rw, wl + hh * kWB + ins * 1024,
+                    (uint32_t)(row * kSrcRow + hh * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)));
+    }
+  // one tile's input: 8 instructions per half, 2 per wave
   auto stage_x = [&](int t, int buf) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ins = wave * 2 + j;
-      const int row = ins * 8 + lrow;
-      const int64_t m = (int64_t)t * kBMb + row;
-      const uint32_t off = m < M ? (uint32_t)(m * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
-      buf_lds16_asm(rx, xl + buf * kTileBb + ins * 1024, off);
-    }
+    for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ins = wave * 2 + j;
+        const int row = ins * 8 + lrow;
+        const int64_t m = (int64_t)t * kBMb + row;
+        const uint32_t off =
+            m < M ? (uint32_t)(m * kSrcRow + hh * kRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
+        buf_lds16_asm(rx, xl + (buf * KH + hh) * kTileBb + ins * 1024, off);
+      }
   };
 
   int t = blockIdx.x;
-  if (t < tiles) stage_x(t, 0);
+  if constexpr (KH == 1) {
+    if (t < tiles) stage_x(t, 0);
+  }
   cf[tid] = coef1[2 * kK + tid];
   cf[kK + tid] = coef1[3 * kK + tid];
   if constexpr (BR == 2) {
@@ -263,13 +278,20 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  vec8 af[4][2];
+  vec8 af[4][2 * KH];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int wr = wave * 64 + wave_ch(i, fr);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      af[i][kk] = *(const vec8*)(wl + wr * kRowB + (((kk * 4 + fq) ^ ((wr >> 1) & 7)) << 4));
+    for (int kq = 0; kq < 2 * KH; ++kq)
+      af[i][kq] = *(const vec8*)(wl + (kq >> 1) * kWB + wr * kRowB + ((((kq & 1) * 4 + fq) ^ ((wr >> 1) & 7)) << 4));
+  }
+  if constexpr (KH == 2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave holds its weight fragments: the area becomes the input ring
+    if (t < tiles) stage_x(t, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
   // statistics of this lane's 16 output channels: pair p, element e -> channel wave*64 + p*32 + 8*fq + e
   float s0[2][8], s1[2][8], s2[BR == 2 ? 2 : 1][8];
@@ -299,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
     first = false;
     if (t + G < tiles) stage_x(t + G, buf ^ 1);
 
-    const char* xb = xl + buf * kTileBb;
+    const char* xb = xl + buf * KH * kTileBb;
     const int64_t mt = (int64_t)t * kBMb;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -325,15 +347,16 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kq = 0; kq < 2 * KH; ++kq) {
         vec8 bf[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          bf[j] = *(const vec8*)(xb + ((h * 2 + j) * 16 + fr) * kRowB + (((kk * 4 + fq) ^ sw) << 4));
+          bf[j] = *(const vec8*)(xb + (kq >> 1) * kTileBb + ((h * 2 + j) * 16 + fr) * kRowB +
+                                 ((((kq & 1) * 4 + fq) ^ sw) << 4));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = E::mfma16x16x32(af[i][kk], bf[j], acc[i][j]);
+          for (int j = 0; j < 2; ++j) acc[i][j] = E::mfma16x16x32(af[i][kq], bf[j], acc[i][j]);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -417,7 +440,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
 
 void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res,
                             const uint16_t* y1, const float* coef1, const uint16_t* y2, const float* coef2,
-                            const uint8_t* mask, double* slots, int64_t M, int dtype, hipStream_t s) {
+                            const uint8_t* mask, double* slots, int64_t M, int cin, int dtype, hipStream_t s) {
+  if (cin != 64 && !(cin == 128 && y2 == nullptr))
+    pdt_hip_fail("conv1x1_c64_bnb: 64 reduction channels, or 128 with one BN branch", hipErrorInvalidValue, __FILE__,
+                 __LINE__);
   if (M <= 0) return;
   if (M * kK >= (int64_t(1) << 31))
     pdt_hip_fail("conv1x1_c64_bnb: operands exceed 32-bit offsets", hipErrorInvalidValue, __FILE__, __LINE__);
@@ -433,13 +459,13 @@ void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   Scratch part((size_t)G * kK * KO * sizeof(float), s);
   float* srows = part.as<float>();
   PDT_COUNT("conv1x1_c64_bnb");
-#define PDT_CB(DT_, BR_)                                                                                    \
-  hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<DT_, BR_>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, y2, coef2, \
-                     mask, srows, M)
+#define PDT_CB(DT_, BR_, KH_)                                                                                     \
+  hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<DT_, BR_, KH_>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, y2,  \
+                     coef2, mask, srows, M)
   if (dtype == kBF16) {
-    if (y2) PDT_CB(kBF16, 2); else PDT_CB(kBF16, 1);
+    if (cin == 128) PDT_CB(kBF16, 1, 2); else if (y2) PDT_CB(kBF16, 2, 1); else PDT_CB(kBF16, 1, 1);
   } else {
-    if (y2) PDT_CB(kF16, 2); else PDT_CB(kF16, 1);
+    if (cin == 128) PDT_CB(kF16, 1, 2); else if (y2) PDT_CB(kF16, 2, 1); else PDT_CB(kF16, 1, 1);
   }
 #undef PDT_CB
   stat_rows_reduce_launch(srows, G, kK * KO, slots, s);

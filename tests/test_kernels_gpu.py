@@ -844,18 +844,19 @@ def test_conv_dgrad_fused_bn_bk32_ring_bit_identical(mode, bm, bn):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("NHW", [(4, 56, 56), (3, 13, 11)])
-@pytest.mark.parametrize("mode", [2, 3])
-def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode):
+@pytest.mark.parametrize("mode,cin", [(2, 64), (3, 64), (2, 128)])
+def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
     """Backward-data of a 1x1 256 -> 64 conv with the fused block-output BN-backward epilogue (residual, ReLU bit of
     the block output, sum dz, sum dz * xhat; mode 3: a second BN branch, sum dz * xhat2) on the persistent 1x1
     kernel (conv1x1.hip) vs the generic implicit-GEMM epilogue: dz bit-identical, statistics equal up to summation
-    order; M tails (3 * 13 * 11 = 429 pixels)."""
+    order; M tails (3 * 13 * 11 = 429 pixels); cin = 128: ResNet-50 layer2.0's 256 -> 128 conv1 (two reduction
+    halves, weights staged through the input-ring area)."""
     from pytorch_distributed_template_amd.ops import conv, native
     C = native.C
     N, H, W = NHW
     torch.manual_seed(29)
-    dy = _rand16(N, H, W, 64, dtype=dtype)
-    w = _rand16(64, 1, 1, 256, dtype=dtype, scale=0.125)
+    dy = _rand16(N, H, W, cin, dtype=dtype)
+    w = _rand16(cin, 1, 1, 256, dtype=dtype, scale=0.125)
     res = _rand16(N, H, W, 256, dtype=dtype)
 
     def branch():
