@@ -364,6 +364,7 @@ void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats,
   const int dt = dt16(x, "x");
   TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv1x1_c64: mixed dtypes");
   TORCH_CHECK(x.numel() >= M * 64 && w.numel() == 256 * 64 && y.numel() >= M * 256, "conv1x1_c64: size mismatch");
+  TORCH_CHECK(M * 256 < (int64_t(1) << 31), "conv1x1_c64: M*256 must be < 2^31 (32-bit buffer offsets)");
   double* st = nullptr;
   if (stats.has_value()) {
     TORCH_CHECK(stats->numel() >= pdt::kStatSlots * 256 * 2, "conv1x1_c64: stats buffer too small");

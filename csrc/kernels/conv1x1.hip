@@ -459,6 +459,12 @@ void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   Scratch part((size_t)G * kK * KO * sizeof(float), s);
   float* srows = part.as<float>();
   PDT_COUNT("conv1x1_c64_bnb");
+  if (cin == 128)
+    PDT_COUNT("conv1x1_c64_bnb_c128");
+  else if (y2)
+    PDT_COUNT("conv1x1_c64_bnb_2br");
+  else
+    PDT_COUNT("conv1x1_c64_bnb_1br");
 #define PDT_CB(DT_, BR_, KH_)                                                                                     \
   hipLaunchKernelGGL((conv1x1_c64_bnb_kernel<DT_, BR_, KH_>), dim3(G), dim3(256), 0, s, x, w, y, res, y1, coef1, y2,  \
                      coef2, mask, srows, M)

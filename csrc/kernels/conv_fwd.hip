@@ -930,6 +930,7 @@ static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_
       PDT_COUNT("conv_generic_fwd_window");
     else
       PDT_COUNT("conv_generic_fwd");
+    if (pp && bm == 512) PDT_COUNT("conv_pp_512x128");
     if (dg && a.res_phase >= 0) PDT_COUNT("conv_dgrad_compact_residual");
     if (dg && a.bnb) PDT_COUNT("conv_dgrad_bn_reduce_epilogue");
   }

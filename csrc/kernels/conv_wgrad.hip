@@ -479,15 +479,6 @@ int wgrad_ctiles(const ConvWgradArgs& a) {
 
 int wgrad_ktile(const ConvWgradArgs& a) { return a.tile == kWgradWide ? 128 : a.tile; }
 
-// pixels per K-step of the wide kernel (PDT_WGRAD_WIDE_BKP=32: two workgroups per CU)
-static int wide_bkp() {
-  static const int bkp = [] {
-    const char* e = getenv("PDT_WGRAD_WIDE_BKP");
-    return e && atoi(e) == 32 ? 32 : 64;
-  }();
-  return bkp;
-}
-
 template <int DT, bool PAIR>
 __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
@@ -640,13 +631,13 @@ PDT_DEVICE void wg_vm_wait() {
 // issued while K-step s computes, and each K-step waits only for its own stage (counted vmcnt(kWideDma): the 6
 // DMA instructions per wave of the stage behind it stay in flight) -- the 128 x 128 kernel drains its single
 // prefetch (vmcnt(0)) every K-step and is latency-bound at ~30 % MFMA busy.
-// BKP = 32 (PDT_WGRAD_WIDE_BKP=32): 24 KB stages, two workgroups per CU (4 waves per SIMD, <= 128 VGPRs).
+// (A BKP = 32 form with 24 KB stages and two workgroups per CU measured slower and was removed in round 5.)
 // DMA instructions per wave per stage: X 2 sub-tiles x BKP/4 rows-of-4 over 8 waves, dY BKP/4 over 8 waves.
 template <int BKP>
 constexpr int wide_dma() { return 2 * (BKP / 4) / 8 + (BKP / 4) / 8; }
 
 template <int DT, int BKP>
-__global__ __launch_bounds__(512, BKP == 32 ? 2 : 1) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
+__global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   constexpr int kWideDma = wide_dma<BKP>();
@@ -1318,8 +1309,7 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
     // one full round: each block then streams ~130 K-steps (ResNet-18 layer3/4), amortising its prologue
     // and its 256 KB fp32 partial; measured faster than two rounds (tools/conv_bench.py wgrad_256 column)
     (void)target_blocks;
-    const int per_cu = (a.tile == kWgradWide && wide_bkp() == 32) ? 2 : 1;
-    splits = per_cu * cus / tiles > 0 ? per_cu * cus / tiles : 1;
+    splits = cus / tiles > 0 ? cus / tiles : 1;
   }
   const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
@@ -1344,12 +1334,7 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad_pp_kernel<kF16>), dim3(nwg), dim3(512), 0, s, a);
   } else if (a.tile == kWgradWide) {
     PDT_COUNT("conv_wgrad_wide");
-    if (wide_bkp() == 32) {
-      if (dtype == kBF16)
-        hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16, 32>), dim3(nwg), dim3(512), 0, s, a);
-      else
-        hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16, 32>), dim3(nwg), dim3(512), 0, s, a);
-    } else if (dtype == kBF16) {
+    if (dtype == kBF16) {
       hipLaunchKernelGGL((conv_wgrad_wide_kernel<kBF16, 64>), dim3(nwg), dim3(512), 0, s, a);
     } else {
       hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16, 64>), dim3(nwg), dim3(512), 0, s, a);

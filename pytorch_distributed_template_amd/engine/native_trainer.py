@@ -35,6 +35,7 @@ class NativeTrainer:
                  grad_compress: str = "none", comm_transport: str = "auto"):
         self.device = torch.device(device)
         self.dtype = dtype
+        self.buffer_syncs = 0  # buffer broadcasts issued (tests: one per train step after the first + one per eval epoch)
         self.model = model
         self.pg = process_group
         self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
@@ -107,6 +108,7 @@ class NativeTrainer:
         self.broadcast_buffers = broadcast_buffers and (self.distributed or self.ncomm is not None)
         self.reduce_metrics = reduce_metrics and (self.distributed or self.ncomm is not None)
         self._steps = 0
+        self._eval_sync_pending = False  # a train step ran since the last eval-forward buffer broadcast
         # whole-step HIP graph (launch-bound small batches, e.g. the reference's -b 1200 split over 8 GPUs = 150
         # per GPU): single process, or any world on the native communicator, whose collectives (buffer
         # broadcast, gradient buckets, SyncBN statistics, metrics) are captured into the graph with the kernels
@@ -130,9 +132,18 @@ class NativeTrainer:
 
     def close(self) -> None:
         """Collective teardown of the native communicators (every rank, same point: runner._finish after its barrier,
-        bench.py after the timed steps): ncclCommDestroy, watchdog threads joined.  Idempotent."""
+        bench.py after the timed steps): ncclCommDestroy, watchdog threads joined.  Idempotent.
+
+        Captured step graphs hold collectives on these communicators, and RCCL's destroy waits until every graph
+        referencing a communicator is freed: release the graphs (after the device drained) BEFORE destroying."""
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+        if self._graphs:
+            self._graphs.clear()
+            import gc
+            gc.collect()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
         for c in (self.ncomm_bn, self.ncomm):
             if c is not None:
                 c.destroy()
@@ -180,6 +191,7 @@ class NativeTrainer:
         return met
 
     def _sync_buffers(self) -> None:
+        self.buffer_syncs += 1
         if self.ncomm is not None:
             # start of a step: every earlier collective was joined into the compute stream, so the broadcasts
             # go straight onto it (no comm-stream round trip; same RCCL order on every rank)
@@ -221,6 +233,7 @@ class NativeTrainer:
         if self.ncomm is not None:
             self.ncomm.track_compute("graph replay of a training step")
         self._steps += 1
+        self._eval_sync_pending = True
         self.optimizer.step_count += 1
         return out
 
@@ -247,12 +260,16 @@ class NativeTrainer:
                             found_inf=self.scaler.found_inf)
         self.scaler.update()
         self._steps += 1
+        self._eval_sync_pending = True
         return logits, met
 
     @torch.no_grad()
     def eval_step(self, images: torch.Tensor, target: torch.Tensor):
-        if self.broadcast_buffers and self._steps > 0:
+        if self.broadcast_buffers and self._eval_sync_pending:
+            # DDP: only the FIRST eval forward after training re-broadcasts the buffers; the following
+            # no-grad forwards see require_forward_param_sync = False (`T/nn/parallel/distributed.py:1557-1558`)
             self._sync_buffers()
+            self._eval_sync_pending = False
         if self._eval32 is not None:
             if self._eval32_at != self.optimizer.step_count:  # once per weight version, not per batch
                 self._eval32.update_derived()  # fp32 layouts of the current master weights

@@ -423,11 +423,14 @@ def _finish(writer, logger, distributed: bool, trainer=None) -> None:
         dist.barrier()
     close = getattr(trainer, "close", None)
     if close is not None:
-        close()
-        if os.environ.get("PDT_COMM_TRACE") == "1" and getattr(trainer, "ncomm", 1) is None:
+        trace = os.environ.get("PDT_COMM_TRACE") == "1"
+        if trace:  # (only the RCCL transport runs a watchdog thread; the host transport times out inside its waits)
             from ..parallel.comm import live_watchdogs
+            before = live_watchdogs() if getattr(trainer, "ncomm", None) is not None else 0
+        close()
+        if trace and getattr(trainer, "ncomm", 1) is None:
             sys.stderr.write(f"[pdt comm] rank {dist.get_rank() if dist.is_initialized() else 0}: trainer closed, "
-                             f"live watchdogs {live_watchdogs()}\n")
+                             f"live watchdogs {before} -> {live_watchdogs()}\n")
             sys.stderr.flush()
     if distributed and dist.is_initialized():
         dist.destroy_process_group()

@@ -31,7 +31,7 @@ class TorchTrainer:
                  bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0, broadcast_buffers: bool = True,
                  process_group=None, reduce_metrics: bool = True, channels_last: bool = True,
                  aux_loss_weight: float = 0.3, dp_device_ids=None, comm: str = "torch",
-                 comm_timeout_s: float = 0.0):
+                 comm_timeout_s: float = 0.0, rebuild_buckets: bool = True):
         self.device = torch.device(device)
         self.pg = process_group
         self.distributed = dist.is_initialized() and dist.get_world_size(process_group) > 1
@@ -49,7 +49,9 @@ class TorchTrainer:
         self.net = nn.DataParallel(model, device_ids=list(dp_device_ids)) if dp_device_ids else model
         self.buffers = FlatBuffers(model, self.device)
         broadcast_parameters(self.flat, self.buffers, process_group)
-        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed)
+        # autograd decides the gradient order: rebuild the buckets from step 1's observed order, like DDP
+        layout = GradBucketer(self.flat, process_group, bucket_cap_mb, first_bucket_mb, enabled=self.distributed,
+                              rebuild=rebuild_buckets and dp_device_ids is None)
         # --comm native: gradient buckets, buffer broadcasts and metric all-reduces through this framework's C++
         # communicator + bucketer (host shared-memory transport on the CPU, csrc/comm.cpp) instead of c10d
         self.ncomm = None
@@ -68,6 +70,8 @@ class TorchTrainer:
         # GoogLeNet / Inception-v3 return auxiliary logits in training; their CE losses are added with this weight
         self.aux_loss_weight = aux_loss_weight
         self._steps = 0
+        self._eval_sync_pending = False  # a train step ran since the last eval-forward buffer broadcast
+        self.buffer_syncs = 0  # buffer broadcasts issued (tests: one per train step after the first + one per eval epoch)
 
     def on_state_loaded(self) -> None:
         """Parameters are views of the flat buffer, so ``load_state_dict`` already updated them."""
@@ -90,6 +94,7 @@ class TorchTrainer:
         return torch.autocast(self.device.type, dtype=self.dtype)
 
     def _sync_buffers(self) -> None:
+        self.buffer_syncs += 1
         if self.ncomm is None:
             sync_buffers(self.buffers, self.pg)
             return
@@ -131,13 +136,16 @@ class TorchTrainer:
         self.optimizer.step(grad_scale=self.bucketer.grad_scale(), loss_scale=scale, found_inf=self.scaler.found_inf)
         self.scaler.update()
         self._steps += 1
+        self._eval_sync_pending = True
         return out.detach().float(), met
 
     @torch.no_grad()
     def eval_step(self, images, target):
         self.model.eval()
-        if self.broadcast_buffers and self._steps > 0:
+        if self.broadcast_buffers and self._eval_sync_pending:
+            # DDP: only the FIRST eval forward after training re-broadcasts the buffers
             self._sync_buffers()
+            self._eval_sync_pending = False
         out = self.net(self._inputs(images)).float()  # validation runs without autocast (`:316-317`)
         loss = F.cross_entropy(out, target)
         acc = accuracy(out, target, 1)

@@ -20,7 +20,6 @@ weights and gradients.  Reference call sites mirror
 """
 from __future__ import annotations
 
-import json
 import os
 
 from typing import Callable, Dict, List, Optional, Tuple
@@ -33,9 +32,6 @@ from ..ops.conv import conv_tile as _conv_tile, dgrad_phases, dgrad_weight_index
 from .resnet import BasicBlock, Bottleneck, ResNet
 
 _BUF_POISON = os.environ.get("PDT_BUF_POISON", "0") == "1"
-# PDT_DGRAD_BK32=s2|all: backward-data convs (stride-2 only | all) on the 3-stage BK=32 ring instead of the
-# 2-stage BK=64 one (A/B knob)
-_DGRAD_BK32 = os.environ.get("PDT_DGRAD_BK32", "0")
 
 
 def _load_tuned():
@@ -44,16 +40,11 @@ def _load_tuned():
     at B = 1200).  PDT_TUNED_TILES=0 ignores them."""
     if os.environ.get("PDT_TUNED_TILES", "1") != "1":
         return {}
-    out = {}
-    paths = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_tiles_mi355x.json")]
+    from .tuned import ARITY16, TABLE16, load_table
+    out = load_table(TABLE16, ARITY16)
     if os.environ.get("PDT_TUNED_EXTRA"):  # more tables (A/B of candidate entries); later files win
-        paths += os.environ["PDT_TUNED_EXTRA"].split(os.pathsep)
-    for path in paths:
-        try:
-            with open(path) as f:
-                out.update({tuple(k): tuple(v) for k, v in json.load(f)["tiles"]})
-        except (OSError, ValueError, KeyError):
-            pass
+        for path in os.environ["PDT_TUNED_EXTRA"].split(os.pathsep):
+            out.update(load_table(path, ARITY16, shipped=False))
     return out
 
 
@@ -490,8 +481,6 @@ class ResNetExecutor:
             return
         bk = 64 if c.cout % 64 == 0 else 32
         dst = c.st
-        if _DGRAD_BK32 == "all" or (_DGRAD_BK32 == "s2" and dst == 2 and not compact):
-            bk = 32  # 3-stage BK=32 ring: two K-steps in flight for the short sub-pixel-phase reductions
         if compact:
             ph0 = c.phases[0]
             assert c.R == 1 and c.S == 1 and c.pad == 0 and tuple(ph0[:6]) == (0, 0, 1, 1, 0, 0), "compact: 1x1 only"
@@ -506,11 +495,16 @@ class ResNetExecutor:
             else:
                 self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, dst, phases, bm, bn,
                                      bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
-        key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
-        if bk == 32 and c.cout % 64 == 0:
-            key = key + ("bk32",)  # not a tuned-table shape
-        bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
-        launch(bm, bn)
+        if (self._c1x1 and bnb is not None and bnb[0] in (2, 3) and res_phase < 0 and dst == 1 and len(phases) == 1
+                and c.R == 1 and c.S == 1 and c.cin == 256 and (c.cout == 64 or (c.cout == 128 and bnb[0] == 2))
+                and H == P and W == Q and self.C.conv1x1_c64_supported(64, 256)):
+            # the binding runs the persistent 1x1 backward-data kernel (conv1x1.hip), which has no tile: no tile
+            # choice (or autotune timing) for this shape
+            launch(0, 0)
+        else:
+            key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
+            bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
+            launch(bm, bn)
         if fin is not None and bnb is not None:  # fin = (count, bn1, bn2): the fused reduce's BN-backward finalize
             self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2])
 

@@ -21,7 +21,6 @@ tests/test_fp32_gpu.py judges against the fp64 gradients' own sensitivity to an 
 """
 from __future__ import annotations
 
-import json
 import os
 from typing import Callable, List, Optional
 
@@ -176,13 +175,8 @@ class ResNetExecutor32(ResNetExecutor):
         return 128, self._bn_tile(n)
 
     # shipped per-conv fp32 tiles (models/tuned_tiles32_mi355x.json; PDT_FP32_TUNED=0 ignores them)
-    _TUNED32 = {}
-    if os.environ.get("PDT_FP32_TUNED", "1") == "1":
-        try:
-            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_tiles32_mi355x.json")) as _f:
-                _TUNED32 = {tuple(k): tuple(v) for k, v in json.load(_f)["tiles"]}
-        except (OSError, ValueError, KeyError):
-            _TUNED32 = {}
+    from .tuned import ARITY32, TABLE32, load_table
+    _TUNED32 = load_table(TABLE32, ARITY32) if os.environ.get("PDT_FP32_TUNED", "1") == "1" else {}
 
     def _tile32c(self, kind: str, c: _Conv, N: int, H: int, n: int, m: int):
         return self._TUNED32.get((kind, N, H, c.cin, c.cout, c.R, c.st)) or self._tile32(n, m)

@@ -56,6 +56,7 @@ class FlatParams:
         from ..ops import validate
         guard = int(os.environ.get("PDT_VALIDATE_GUARD", "0") or 0) if validate.level_from_env() > 0 else 0
         self.guard = guard
+        self.align = align
         off = 0
         for name, p in model.named_parameters():
             if not p.requires_grad:
@@ -138,6 +139,37 @@ class FlatParams:
 
     def zero_grad(self) -> None:
         self.grad.zero_()
+
+    def reorder(self, mem_order: List[int]) -> None:
+        """Re-lay the flat buffers so slot ``mem_order[0]`` comes first, ``mem_order[1]`` next, ... (the DDP bucket
+        rebuild, parallel/ddp.py: a bucket must be a contiguous slice).  Contents of data / grad / momentum /
+        shadow move with their slots IN PLACE -- the buffer tensors stay the same objects, so everything holding
+        them (optimizer, C++ bucketer, scaler) stays valid; parameter and gradient views are re-pointed.  Slot
+        indices (the bucketer's parameter ids) do not change."""
+        assert sorted(mem_order) == list(range(len(self.slots))), "reorder needs a permutation of the slots"
+        assert self.guard == 0, "flat reorder with PDT_VALIDATE guard bands"
+        new_off, off = {}, 0
+        for i in mem_order:
+            new_off[i] = off
+            off += (self.slots[i].numel + self.align - 1) // self.align * self.align
+        assert off == self.total
+        with torch.no_grad():
+            for buf in (self.data, self.grad, self.momentum, self.shadow):
+                if buf is None:
+                    continue
+                src = buf.clone()
+                buf.zero_()
+                for s in self.slots:
+                    buf[new_off[s.index]:new_off[s.index] + s.numel].copy_(src[s.offset:s.offset + s.numel])
+            for s, p in zip(self.slots, self.params):
+                s.offset = new_off[s.index]
+                p.data = _phys_view(self.data, s.offset, s.shape, s.channels_last)
+                p.grad = _phys_view(self.grad, s.offset, s.shape, s.channels_last)
+
+    def canonical(self, buf: torch.Tensor) -> torch.Tensor:
+        """``buf`` (data / grad / momentum layout) with the slots concatenated in parameter-registration order and
+        without alignment gaps: comparable across processes whatever their flat layout (bucket rebuild)."""
+        return torch.cat([buf[s.offset:s.offset + s.numel] for s in self.slots])
 
     def reattach_grads(self) -> None:
         """Point every ``param.grad`` back at its flat view (after code that set grads to None)."""

@@ -179,19 +179,30 @@ class NativeBucketer:
         self.world = comm.world
         self.comm = comm
         self.compress = compress
+        self.layout = layout
+        self._make_impl()
+
+    def _make_impl(self) -> None:
+        layout = self.layout
         self.buckets = layout.buckets
         self.bucket_of = layout.bucket_of
         pb: List[int] = [0] * len(layout.flat.slots)
         for pid, bid in layout.bucket_of.items():
             pb[pid] = bid
-        self._impl = native.C.Bucketer(comm.comm, layout.flat.grad, [b["lo"] for b in self.buckets],
-                                       [b["hi"] for b in self.buckets], pb, 1 if compress == "bf16" else 0)
+        self._impl = native.C.Bucketer(self.comm.comm, layout.flat.grad, [b["lo"] for b in self.buckets],
+                                       [b["hi"] for b in self.buckets], pb, 1 if self.compress == "bf16" else 0)
 
     def grad_ready(self, pid: int) -> None:
+        if self.layout._observed is not None:  # step 1 of a rebuilding layout (GradBucketer rebuild=True)
+            self.layout._observed.append(pid)
         self._impl.ready(pid)
 
-    def finish(self) -> None:
+    def finish(self) -> bool:
         self._impl.finish()
+        if self.layout._observed is not None and self.layout._rebuild_from_observed():
+            self._make_impl()
+            return True
+        return False
 
     def grad_scale(self) -> float:
         return 1.0 / self.world

@@ -32,7 +32,8 @@ from ..optim.flat import FlatBuffers, FlatParams
 
 class GradBucketer:
     def __init__(self, flat: FlatParams, process_group=None, bucket_cap_mb: float = 25.0,
-                 first_bucket_mb: float = 1.0, enabled: Optional[bool] = None, last_bucket_mb: Optional[float] = None):
+                 first_bucket_mb: float = 1.0, enabled: Optional[bool] = None, last_bucket_mb: Optional[float] = None,
+                 rebuild: bool = False):
         """Buckets over parameters in the order their gradients are produced (reverse registration).
 
         ``last_bucket_mb=None``: DDP's policy -- the FIRST-produced bucket closes at ``first_bucket_mb``, the rest
@@ -40,35 +41,72 @@ class GradBucketer:
         layer1 side, ready only when backward ends, so its all-reduce is exposed) closes at ``x`` and the rest at
         the cap; every other bucket is launched while backward still has whole stages to run.  With DDP's policy
         on ResNet-18 the last bucket holds 15 MiB (part of layer4, layer3, layer2, layer1, stem) and its ring
-        all-reduce trails backward on every step."""
+        all-reduce trails backward on every step.
+
+        ``rebuild=True`` (the autograd / torch-engine path): like upstream DDP after its first iteration
+        (`distributed.py:144`; `T/nn/parallel/distributed.py:1195-1247`, Reducer::rebuild_buckets), the buckets are
+        rebuilt ONCE from the order in which gradients actually became ready in step 1 (rank 0's order, broadcast,
+        so every rank builds the same buckets), and the flat buffers are re-laid so each new bucket is again a
+        contiguous slice.  The native executor's production order is fixed by construction and needs no rebuild."""
         self.flat = flat
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.enabled = (self.world > 1) if enabled is None else enabled
+        self._policy = (bucket_cap_mb, first_bucket_mb, last_bucket_mb)
+        self._assign(list(range(len(flat.slots) - 1, -1, -1)))
+        self._works = []
+        self._observed: Optional[List[int]] = [] if (rebuild and self.enabled) else None
+        self.rebuilt = False
+
+    def _assign(self, production: List[int]) -> None:
+        """Buckets over ``production`` (parameter ids in gradient-production order); the flat buffer's memory order
+        must be its reverse (so every bucket is a contiguous slice)."""
+        bucket_cap_mb, first_bucket_mb, last_bucket_mb = self._policy
         cap = int(bucket_cap_mb * 1024 * 1024)
+        slots = self.flat.slots
         self.buckets: List[dict] = []
         self.bucket_of = {}
         groups: List[List[int]] = []
         cur: List[int] = []
         cur_bytes = 0
         if last_bucket_mb is None:
-            order, limit = list(reversed(flat.slots)), int(first_bucket_mb * 1024 * 1024)
+            order, limit = list(production), int(first_bucket_mb * 1024 * 1024)
         else:
-            order, limit = list(flat.slots), int(last_bucket_mb * 1024 * 1024)
-        for s in order:
-            cur.append(s.index)
-            cur_bytes += s.numel * 4
+            order, limit = list(reversed(production)), int(last_bucket_mb * 1024 * 1024)
+        for i in order:
+            cur.append(i)
+            cur_bytes += slots[i].numel * 4
             if cur_bytes >= limit:
                 groups.append(cur)
                 cur, cur_bytes, limit = [], 0, cap
         if cur:
             groups.append(cur)
-        if last_bucket_mb is not None:  # built stem-first: put them in production order
+        if last_bucket_mb is not None:  # built from the last-produced end: put them in production order
             groups = [list(reversed(g)) for g in reversed(groups)]
         for g in groups:
             self._close(g)
         self._pending = [len(b["params"]) for b in self.buckets]
-        self._works = []
+
+    def production_order(self) -> List[int]:
+        return [i for b in self.buckets for i in b["params"]]
+
+    def _rebuild_from_observed(self) -> bool:
+        """End of step 1: rank 0's observed gradient-ready order -> new buckets + flat re-layout (every rank).
+        Returns True when the layout changed."""
+        obs, self._observed = self._observed, None
+        seen = set(obs)
+        obs = obs + [i for i in self.production_order() if i not in seen]  # never-ready params last (unused)
+        if dist.is_initialized() and self.world > 1:
+            on_dev = dist.get_backend(self.pg) == "nccl"
+            t = torch.tensor(obs, dtype=torch.int64, device=self.flat.device if on_dev else "cpu")
+            dist.broadcast(t, src=0, group=self.pg)
+            obs = [int(v) for v in t.tolist()]
+        if obs == self.production_order():
+            return False
+        self.flat.reorder(list(reversed(obs)))
+        self._assign(obs)
+        self.rebuilt = True
+        return True
 
     def _close(self, idxs: List[int]) -> None:
         slots = [self.flat.slots[i] for i in idxs]
@@ -86,6 +124,8 @@ class GradBucketer:
     def grad_ready(self, pid: int) -> None:
         if not self.enabled:
             return
+        if self._observed is not None:
+            self._observed.append(pid)
         bid = self.bucket_of[pid]
         self._pending[bid] -= 1
         if self._pending[bid] == 0:
@@ -93,10 +133,11 @@ class GradBucketer:
             view = self.flat.grad[b["lo"]:b["hi"]]
             self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
-    def finish(self) -> None:
-        """Wait (stream-wise) for every bucket; launch any bucket whose params produced no grad."""
+    def finish(self) -> bool:
+        """Wait (stream-wise) for every bucket; launch any bucket whose params produced no grad.  After the first
+        step of a ``rebuild`` bucketer, rebuild the buckets from the observed order; returns True when it did."""
         if not self.enabled:
-            return
+            return False
         for bid, n in enumerate(self._pending):
             if n > 0:  # unused parameters: reduce whatever is in the buffer (zeros) to stay in lock-step
                 b = self.buckets[bid]
@@ -106,6 +147,9 @@ class GradBucketer:
             w.wait()
         self._works.clear()
         self._pending = [len(b["params"]) for b in self.buckets]
+        if self._observed is not None:
+            return self._rebuild_from_observed()
+        return False
 
     def grad_scale(self) -> float:
         """Factor the optimizer applies to the summed gradients (mean over ranks)."""

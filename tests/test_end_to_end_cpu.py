@@ -178,8 +178,7 @@ def test_entry_script_tears_down_native_comm(tmp_path):
     """Communicator lifecycle on the entry-script path (reference teardown `distributed_syncBN_amp.py:236-237`):
     distributed.py at world 2 on the CPU runs its gradient buckets / buffer broadcasts / metrics through the native
     C++ communicator (host shared-memory transport, --comm native); at the end every rank passes the barrier, then
-    destroys its communicator collectively (runner._finish -> trainer.close()), with no watchdog thread left, and
-    the job exits 0."""
+    destroys its communicator collectively (runner._finish -> trainer.close()) and the job exits 0."""
     out = str(tmp_path / "output_teardown")
     env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="1", PDT_COMM_TRACE="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc_per_node", "2", "--master-addr", "127.0.0.1",
@@ -190,7 +189,9 @@ def test_entry_script_tears_down_native_comm(tmp_path):
     assert r.returncode == 0, log[-3000:]
     for rk in (0, 1):
         assert f"[pdt comm] rank {rk}/2: host communicator destroyed" in log, log[-3000:]
-        assert f"[pdt comm] rank {rk}: trainer closed, live watchdogs 0" in log, log[-3000:]
+        # the host transport starts no watchdog thread (its timeout runs inside its waits): 0 before and after;
+        # the RCCL watchdog's teardown is covered by test_multigpu.py::test_entry_script_rccl_graph_teardown
+        assert f"[pdt comm] rank {rk}: trainer closed, live watchdogs 0 -> 0" in log, log[-3000:]
     assert "communicator aborted" not in log
 
 

@@ -111,11 +111,25 @@ R18_224_KERNELS = ("stem_fwd", "conv_l1_fwd", "conv_l1_dgrad", "wgrad3x3_c64", "
                    "conv_l1_fwd_fused_bn_relu", "wgrad3x3_c64_fused_bn_relu")
 
 
-@pytest.mark.parametrize("arch,N", [("resnet18", 16), ("resnet18", 32), ("resnet50", 8)])
-def test_train_step_matches_reference_224(arch, N):
-    """The bench geometry (224x224): gradients and running stats vs fp32 torch, judged against torch
-    autocast bf16, with the specialised kernels asserted to have run."""
+# ResNet-50's specialised kernels: the persistent 1x1 64->256 forward, the fused-BN 1x1 backward-data kernel in its
+# one-branch, two-branch (downsample block) and 128-reduction-channel forms, and the 512x128 ping-pong tile the shipped
+# tile table picks for its 1x1 convs (csrc/kernels/conv1x1.hip, conv_fwd.hip)
+R50_224_KERNELS = ("conv1x1_c64", "conv1x1_c64_bnb_1br", "conv1x1_c64_bnb_2br", "conv1x1_c64_bnb_c128",
+                   "conv_pp_512x128", "stem_fwd", "conv_pp_fwd", "conv_wgrad_pp", "wgrad_stem_fused")
+
+
+@pytest.mark.parametrize("arch,N", [("resnet18", 16), ("resnet18", 32), ("resnet50", 8), ("resnet34", 4),
+                                    ("resnet101", 3), ("resnet152", 2), ("wide_resnet50_2", 3),
+                                    ("wide_resnet101_2", 2)])
+def test_train_step_matches_reference_224(arch, N, monkeypatch):
+    """The bench geometry (224x224) for every arch the native engine accepts (engine/runner.py NATIVE_ARCHS):
+    gradients and running stats vs fp32 torch, judged against torch autocast bf16, with the specialised kernels
+    asserted to have run (ResNet-18 and ResNet-50; the shipped B = 1200 tile table re-keyed to this batch so its
+    tile choices are exercised)."""
+    from pytorch_distributed_template_amd.models import executor
     from pytorch_distributed_template_amd.ops import native
+    if arch == "resnet50":
+        monkeypatch.setattr(executor, "_TUNED", {(k[0], N) + k[2:]: v for k, v in executor._TUNED.items()})
     model, ref, flat, ex, x, t = _setup(arch, N=N, HW=224, dtype=torch.bfloat16)
     tb = copy.deepcopy(ref)
     native.C.reset_dispatch_counts()
@@ -123,9 +137,9 @@ def test_train_step_matches_reference_224(arch, N):
     torch.cuda.synchronize()
     counts = {k: v for k, v in native.C.dispatch_counts().items() if v}
     print("dispatch", arch, N, counts)
-    if arch == "resnet18":
-        missing = [k for k in R18_224_KERNELS if not counts.get(k)]
-        assert not missing, (missing, counts)
+    want = {"resnet18": R18_224_KERNELS, "resnet50": R50_224_KERNELS}.get(arch, ())
+    missing = [k for k in want if not counts.get(k)]
+    assert not missing, (missing, counts)
     out = ref(x)
     loss = F.cross_entropy(out, t)
     loss.backward()

@@ -126,7 +126,10 @@ def _setup(arch, N, HW, seed=0):
 
 
 @pytest.mark.parametrize("arch,N,HW,chunk", [("resnet18", 8, 64, None), ("resnet50", 4, 128, None),
-                                             ("resnet50", 4, 64, None), ("resnet18", 6, 224, 4)])
+                                             ("resnet50", 4, 64, None), ("resnet18", 6, 224, 4),
+                                             ("resnet34", 4, 128, None), ("resnet101", 2, 128, None),
+                                             ("resnet152", 2, 128, None), ("wide_resnet50_2", 2, 128, None),
+                                             ("wide_resnet101_2", 2, 128, None)])
 def test_executor32_train_step_matches_torch_fp32(arch, N, HW, chunk):
     """The whole fp32 step vs an fp64 PyTorch oracle, judged against PyTorch's own fp32 autograd: logits, loss,
     every gradient and the running statistics must be no worse than torch fp32 (+ a small absolute floor) --

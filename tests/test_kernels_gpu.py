@@ -814,7 +814,8 @@ def test_conv1x1_c64_matches_implicit_gemm(dtype, M):
 @pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("bm,bn", [(256, 64), (128, 128)])
 def test_conv_dgrad_fused_bn_bk32_ring_bit_identical(mode, bm, bn):
-    """The fused BN-backward dgrad epilogue on the 3-stage BK=32 ring (PDT_DGRAD_BK32) is bit-identical to the
+    """The fused BN-backward dgrad epilogue on the 3-stage BK=32 ring (the dgrad of convs whose Kout is not a
+    multiple of 64) is bit-identical to the
     2-stage BK=64 kernel (same MFMA K order, same epilogue): dz and the statistics slots, stride-2 phases with a
     compact residual on phase 0."""
     from pytorch_distributed_template_amd.ops import conv, native

@@ -130,3 +130,30 @@ def test_device_group_broadcast_and_reduce():
     g.reduce(ti, 0)
     torch.cuda.synchronize()
     assert torch.equal(ti[0].cpu(), torch.stack(ints).sum(0))  # integers in fp32: exact in any order
+
+
+def test_entry_script_rccl_graph_teardown(tmp_path):
+    """Communicator lifecycle on two real GPUs (reference teardown `distributed_syncBN_amp.py:236-237`): distributed.py
+    at world 2 on the native RCCL communicator with the whole step captured as a HIP graph (its collectives live in
+    the graph).  At the end every rank releases its graphs BEFORE ncclCommDestroy (RCCL's destroy waits for every
+    graph that references the communicator), the watchdog thread that was running stops, and the job exits 0 well
+    inside the time bound instead of hanging at exit."""
+    import re
+    import subprocess
+    root = os.path.dirname(HERE)
+    out = str(tmp_path / "output_rccl_teardown")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", PDT_COMM_TRACE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc_per_node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29641", "distributed.py", "--outpath", out, "-b", "16", "--comm", "native", "--graph",
+           "--dist-timeout", "120", "--synthetic", "--synthetic-train-size", "96", "--synthetic-val-size", "16",
+           "--image-size", "64", "--num-classes", "10", "-j", "0", "--epochs", "1", "--exist-policy", "delete",
+           "-p", "1"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    log = r.stdout + r.stderr
+    assert r.returncode == 0, log[-3000:]
+    for rk in (0, 1):
+        assert f"[pdt comm] rank {rk}/2: rccl communicator destroyed" in log, log[-3000:]
+        m = re.search(rf"\[pdt comm\] rank {rk}: trainer closed, live watchdogs (\d+) -> (\d+)", log)
+        assert m is not None, log[-3000:]
+        assert int(m.group(1)) > 0 and int(m.group(2)) == 0, m.group(0)
+    assert "communicator aborted" not in log

@@ -183,7 +183,14 @@ def check_windows(ins, labels, wins):
     is the target of backward branches (a loop header / latch block) may continue from any of those branches ("the
     previous iteration"); the window is the LARGEST count over these walks -- the kernel's steady-state path.  Paths
     through a latch that skips the epilogue (e.g. a tile with no rows to store) are guarded at run time by the
-    kernel's own flag and are not reported; a spill or a store scheduled out of the steady-state window is."""
+    kernel's own flag and are not reported; a spill or a store scheduled out of the steady-state window is.
+
+    Why the LARGEST and not the smallest count (round-5 review): a path-insensitive minimum over the real control-flow
+    graph was built and run over all 615 kernels -- it flags 20 of them, every one on a path the kernel's own
+    loop-carried flag makes infeasible (``stores_behind`` / ``n_st`` / ``first`` select ``vmcnt(0)`` exactly when the
+    previous tile issued no stores, and exec-mask store skips occur only on a partial last tile).  A checker that fails
+    on correct code gets disabled; the flag-guarded first / last tiles are covered by the GPU numerics tests of each
+    counted-wait kernel (bit-identity against the generic kernels, PDT_BUF_POISON on)."""
     latches = {}
     for j, t in enumerate(ins):
         b = branch(t)
