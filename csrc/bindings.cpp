@@ -445,6 +445,10 @@ void conv_wgrad_stem_fused(const Tensor& x, const Tensor& dp, const Tensor& idx,
   a.cs = 4; a.win = 1;
   a.tile = pdt::wgrad_tile(64, 64, 1);
   TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad_stem_fused: bad split plan");
+  {  // the kernel walks pixels in 2x2 quads: an odd height pads the count to whole quads (same splits, same ws)
+    const int64_t pq = N * ((Pm + 1) / 2) * 2 * Qm;
+    if (splits * a.pix_per_split < pq) a.pix_per_split = (int)(((pq + splits - 1) / splits + 127) / 128 * 128);
+  }
   a.f_y = p16(y0, "y0");
   a.f_dp = p16(dp, "dp");
   a.f_idx = idx.data_ptr<uint8_t>();

@@ -191,31 +191,71 @@ void bn_eval_coef_launch(const float* gamma, const float* beta, const float* rm,
 // out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift.
 // WM: also write the ReLU bitmask (bit e of mask[v] = out[8v+e] > 0) that the backward reads instead of
 // re-reading the 16-bit block output (1 bit instead of 16 per element).
-template <int DT, int RESMODE, bool RELU, bool WM, bool NT>
+//
+// Streaming structure (both apply kernels): a block owns U * 256 CONSECUTIVE 16-byte vectors, thread t the vectors
+// t, t + 256, ... (each wave-instruction one contiguous KiB), all U loads issued before any math.  256 vectors are
+// 2048 elements, so for C | 2048 (every power-of-two width up to 2048: all ResNet / ResNeXt widths) all of a
+// thread's vectors hold the SAME 8 channels and the per-channel coefficients are loaded once per thread into
+// registers (CH) instead of once per vector -- the coefficient traffic through the vector L1 was 3-6x the
+// streamed bytes.  Other widths (CH = false) index the coefficients per vector.
+template <int C8, bool CH>
+struct ChanCoef {  // C8 coefficient rows of 8 consecutive channels each
+  float v[C8][8];
+  PDT_DEVICE void load(const float* __restrict__ p, int C, int c0) {
+#pragma unroll
+    for (int k = 0; k < C8; ++k) {
+      const float4 a = *(const float4*)(p + k * C + c0), b = *(const float4*)(p + k * C + c0 + 4);
+      v[k][0] = a.x; v[k][1] = a.y; v[k][2] = a.z; v[k][3] = a.w;
+      v[k][4] = b.x; v[k][5] = b.y; v[k][6] = b.z; v[k][7] = b.w;
+    }
+  }
+};
+
+template <int DT, int RESMODE, bool RELU, bool WM, bool NT, int U, bool CH>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                        const uint16_t* __restrict__ res,
                                                        const float* __restrict__ rcoef, uint16_t* __restrict__ out,
                                                        uint8_t* __restrict__ mask, int64_t n8, int C) {
   using E = E16<DT>;
-  const bool cpow2 = (C & (C - 1)) == 0;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
-    const int c0 = cpow2 ? (int)(v * 8) & (C - 1) : (int)((v * 8) % C);
-    const uint4 yy = ld16<NT>(y + v * 8);
-    uint4 rr;
-    if constexpr (RESMODE != 0) rr = ld16<NT>(res + v * 8);
-    const uint32_t yw[4] = {yy.x, yy.y, yy.z, yy.w};
-    uint32_t rw[4];
-    if constexpr (RESMODE != 0) { rw[0] = rr.x; rw[1] = rr.y; rw[2] = rr.z; rw[3] = rr.w; }
+  const int64_t v0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  ChanCoef<2, CH> cf;
+  ChanCoef<RESMODE == 2 ? 2 : 1, CH> rf;
+  if constexpr (CH) {
+    const int c0 = (int)((v0 * 8) & (C - 1));
+    cf.load(coef, C, c0);
+    if constexpr (RESMODE == 2) rf.load(rcoef, C, c0);
+  }
+  uint4 yy[U], rr[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t v = v0 + u * 256;
+    if (v < n8) {
+      yy[u] = ld16<NT>(y + v * 8);
+      if constexpr (RESMODE != 0) rr[u] = ld16<NT>(res + v * 8);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t v = v0 + u * 256;
+    if (v >= n8) break;
+    if constexpr (!CH) {
+      const int c0 = (int)((v * 8) % C);
+      cf.load(coef, C, c0);
+      if constexpr (RESMODE == 2) rf.load(rcoef, C, c0);
+    }
+    const uint32_t yw[4] = {yy[u].x, yy[u].y, yy[u].z, yy[u].w};
+    uint32_t rw[4] = {0, 0, 0, 0};
+    if constexpr (RESMODE != 0) { rw[0] = rr[u].x; rw[1] = rr[u].y; rw[2] = rr[u].z; rw[3] = rr[u].w; }
     uint32_t ow[4], bits = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float o2[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int c = c0 + 2 * e + h;
-        float val = E::to_f((uint16_t)(yw[e] >> (16 * h))) * coef[c] + coef[C + c];
+        const int c = 2 * e + h;
+        float val = E::to_f((uint16_t)(yw[e] >> (16 * h))) * cf.v[0][c] + cf.v[1][c];
         if constexpr (RESMODE == 1) val += E::to_f((uint16_t)(rw[e] >> (16 * h)));
-        if constexpr (RESMODE == 2) val += E::to_f((uint16_t)(rw[e] >> (16 * h))) * rcoef[c] + rcoef[C + c];
+        if constexpr (RESMODE == 2) val += E::to_f((uint16_t)(rw[e] >> (16 * h))) * rf.v[0][c] + rf.v[1][c];
         if constexpr (RELU) val = fmaxf(val, 0.f);
         o2[h] = val;
       }
@@ -229,42 +269,58 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
   }
 }
 
-// Elementwise grids: one 16-byte vector per thread (a grid-stride loop only past 2^20 blocks) -- the
-// in-order block dispatch then keeps the concurrently streamed window contiguous; capping the grid at a
-// few thousand looping blocks cost ~20% of bandwidth (tools/bw_probe.py).  Streams larger than the L2s
-// and MALL use nontemporal loads/stores.  PDT_EW_CAP / PDT_EW_NT override both (A/B experiments).
+// Elementwise grids: one block per U * 256 consecutive 16-byte vectors, U = 4 (no grid-stride loop: the in-order
+// block dispatch keeps the concurrently streamed window contiguous; capping the grid at a few thousand looping
+// blocks cost ~20% of bandwidth, tools/bw_probe.py).  tools/ew_bench.py, ResNet shapes at B = 1200 (round 5):
+// U = 1 (one vector per thread, coefficients indexed per vector, the round-4 structure) 5.3-6.1 TB/s, U = 2 and 4
+// 6.2-6.7 TB/s (two-branch backward 7.3-7.6), U = 8 a few % below 4.  Streams larger than the L2s and MALL use
+// nontemporal loads/stores (PDT_EW_NT: threshold override for A/B experiments).
+constexpr int kEwU = 4;
 static int64_t env_i64(const char* name, int64_t dflt) {
   const char* e = getenv(name);
   return e && *e ? atoll(e) : dflt;
 }
-static int ew_blocks(int64_t n) {
-  static const int64_t cap = env_i64("PDT_EW_CAP", 1 << 20);
-  int64_t b = (n + 255) / 256;
-  if (b > cap) b = cap;
+static int ew_blocks(int64_t n8, int U) {
+  const int64_t b = (n8 + 256 * U - 1) / (256 * U);
+  if (b >= (int64_t(1) << 31)) pdt_hip_fail("elementwise pass: tensor too large", hipErrorInvalidValue, __FILE__, __LINE__);
   return (int)(b < 1 ? 1 : b);
 }
 static bool ew_nt(int64_t bytes) {
   static const int64_t thr = env_i64("PDT_EW_NT", 64ll << 20);
   return thr >= 0 && bytes >= thr;
 }
+static bool ew_ch(int C) { return C > 0 && C <= 2048 && (C & (C - 1)) == 0 && C % 8 == 0; }
+
+// dispatch an elementwise kernel template K<..., NT, U, CH> over (NT, CH): U = kEwU with hoisted coefficients,
+// one vector per thread otherwise
+#define PDT_EW_DISPATCH(KERNEL, TARGS, grid_of, nt, ch, ...)                                                     \
+  do {                                                                                                           \
+    const dim3 b_(256);                                                                                          \
+    if (!(ch)) {                                                                                                 \
+      if (nt) hipLaunchKernelGGL((KERNEL<TARGS, true, 1, false>), dim3(grid_of(1)), b_, 0, s, __VA_ARGS__);     \
+      else hipLaunchKernelGGL((KERNEL<TARGS, false, 1, false>), dim3(grid_of(1)), b_, 0, s, __VA_ARGS__);      \
+    } else {                                                                                                     \
+      if (nt) hipLaunchKernelGGL((KERNEL<TARGS, true, kEwU, true>), dim3(grid_of(kEwU)), b_, 0, s, __VA_ARGS__); \
+      else hipLaunchKernelGGL((KERNEL<TARGS, false, kEwU, true>), dim3(grid_of(kEwU)), b_, 0, s, __VA_ARGS__);  \
+    }                                                                                                            \
+  } while (0)
 
 template <int DT>
 static void bn_apply_dt(const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef, uint16_t* out,
                         uint8_t* mask, int64_t n, int C, int resmode, bool relu, hipStream_t s) {
   const int64_t n8 = n / 8;
-  dim3 g(ew_blocks(n8)), b(256);
-  const bool wm = mask != nullptr, nt = ew_nt(n * 2);
+  auto grid = [&](int U) { return ew_blocks(n8, U); };
+  const bool wm = mask != nullptr, nt = ew_nt(n * 2), ch = ew_ch(C);
 #define PDT_AP(RM, RL, WM)                                                                                       \
   if (resmode == RM && relu == RL && wm == WM) {                                                                 \
-    if (nt)                                                                                                      \
-      hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL, WM, true>), g, b, 0, s, y, coef, res, rcoef, out, mask, n8, C); \
-    else                                                                                                         \
-      hipLaunchKernelGGL((bn_apply_kernel<DT, RM, RL, WM, false>), g, b, 0, s, y, coef, res, rcoef, out, mask, n8, C); \
+    PDT_EW_DISPATCH(bn_apply_kernel, PDT_TARGS(DT, RM, RL, WM), grid, nt, ch, y, coef, res, rcoef, out, mask, n8, C); \
     return;                                                                                                      \
   }
+#define PDT_TARGS(...) __VA_ARGS__
   PDT_AP(0, true, false) PDT_AP(1, true, false) PDT_AP(2, true, false) PDT_AP(0, false, false)
   PDT_AP(1, false, false) PDT_AP(2, false, false) PDT_AP(1, true, true) PDT_AP(2, true, true)
 #undef PDT_AP
+#undef PDT_TARGS
 }
 
 void bn_apply_launch(int dtype, const uint16_t* y, const float* coef, const uint16_t* res, const float* rcoef,
@@ -450,8 +506,9 @@ void bn_bwd_finalize_slots_launch(const double* slots, int K, double count, cons
                        gamma1, dgamma1, dbeta1, bcoef1, coef2, gamma2, dgamma2, dbeta2, bcoef2, gscale, C);
 }
 
-// dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad)
-template <int DT, bool MASK, int NBR, bool WDZ, bool NT>
+// dy_b = A_b*dz + B_b*y_b + C_b for b = 1 (and 2); optionally also writes dz (identity branch grad).
+// Streaming structure and coefficient hoisting (CH) as bn_apply_kernel.
+template <int DT, bool MASK, int NBR, bool WDZ, bool NT, int U, bool CH>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ g,
                                                            const uint8_t* __restrict__ mask,
                                                            const uint16_t* __restrict__ y1,
@@ -460,30 +517,53 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            const float* __restrict__ b2, uint16_t* __restrict__ dy2,
                                                            uint16_t* __restrict__ dz_out, int64_t n8, int C) {
   using E = E16<DT>;
-  const bool cpow2 = (C & (C - 1)) == 0;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (int64_t)gridDim.x * 256) {
-    const int c0 = cpow2 ? (int)(v * 8) & (C - 1) : (int)((v * 8) % C);
-    const uint4 gv = ld16<NT>(g + v * 8);
-    const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
-    uint32_t mb = 0xffu;
-    if constexpr (MASK) mb = mask[v];
-    const uint4 y1v = ld16<NT>(y1 + v * 8);
-    const uint32_t y1w[4] = {y1v.x, y1v.y, y1v.z, y1v.w};
+  const int64_t v0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  ChanCoef<3, CH> f1;
+  ChanCoef<NBR == 2 ? 3 : 1, CH> f2;
+  if constexpr (CH) {
+    const int c0 = (int)((v0 * 8) & (C - 1));
+    f1.load(b1, C, c0);
+    if constexpr (NBR == 2) f2.load(b2, C, c0);
+  }
+  uint4 gv[U], y1v[U], y2v[U];
+  uint32_t mb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t v = v0 + u * 256;
+    if (v < n8) {
+      gv[u] = ld16<NT>(g + v * 8);
+      mb[u] = 0xffu;
+      if constexpr (MASK) mb[u] = mask[v];
+      y1v[u] = ld16<NT>(y1 + v * 8);
+      if constexpr (NBR == 2) y2v[u] = ld16<NT>(y2 + v * 8);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t v = v0 + u * 256;
+    if (v >= n8) break;
+    if constexpr (!CH) {
+      const int c0 = (int)((v * 8) % C);
+      f1.load(b1, C, c0);
+      if constexpr (NBR == 2) f2.load(b2, C, c0);
+    }
+    const uint32_t gw[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+    const uint32_t y1w[4] = {y1v[u].x, y1v[u].y, y1v[u].z, y1v[u].w};
     uint32_t y2w[4] = {0, 0, 0, 0};
-    if constexpr (NBR == 2) { const uint4 y2v = ld16<NT>(y2 + v * 8); y2w[0] = y2v.x; y2w[1] = y2v.y; y2w[2] = y2v.z; y2w[3] = y2v.w; }
+    if constexpr (NBR == 2) { y2w[0] = y2v[u].x; y2w[1] = y2v[u].y; y2w[2] = y2v[u].z; y2w[3] = y2v[u].w; }
     uint32_t o1[4], o2[4], oz[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       uint16_t r1[2], r2[2], rz[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int c = c0 + 2 * e + h;
+        const int c = 2 * e + h;
         float dz = E::to_f((uint16_t)(gw[e] >> (16 * h)));
-        if constexpr (MASK) dz = (mb >> (2 * e + h)) & 1u ? dz : 0.f;
+        if constexpr (MASK) dz = (mb[u] >> (2 * e + h)) & 1u ? dz : 0.f;
         rz[h] = E::from_f(dz);
-        r1[h] = E::from_f(b1[c] * dz + b1[C + c] * E::to_f((uint16_t)(y1w[e] >> (16 * h))) + b1[2 * C + c]);
+        r1[h] = E::from_f(f1.v[0][c] * dz + f1.v[1][c] * E::to_f((uint16_t)(y1w[e] >> (16 * h))) + f1.v[2][c]);
         if constexpr (NBR == 2)
-          r2[h] = E::from_f(b2[c] * dz + b2[C + c] * E::to_f((uint16_t)(y2w[e] >> (16 * h))) + b2[2 * C + c]);
+          r2[h] = E::from_f(f2.v[0][c] * dz + f2.v[1][c] * E::to_f((uint16_t)(y2w[e] >> (16 * h))) + f2.v[2][c]);
       }
       o1[e] = (uint32_t)r1[0] | ((uint32_t)r1[1] << 16);
       if constexpr (NBR == 2) o2[e] = (uint32_t)r2[0] | ((uint32_t)r2[1] << 16);
@@ -499,18 +579,15 @@ void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint8_t* out, const
                          uint16_t* dy1, const uint16_t* y2, const float* b2, uint16_t* dy2, uint16_t* dz_out, int64_t n,
                          int C, hipStream_t s) {
   const int64_t n8 = n / 8;
-  dim3 gr(ew_blocks(n8)), bl(256);
-  const bool mask = out != nullptr, wdz = dz_out != nullptr, nt = ew_nt(n * 2);
+  auto grid = [&](int U) { return ew_blocks(n8, U); };
+  const bool mask = out != nullptr, wdz = dz_out != nullptr, nt = ew_nt(n * 2), ch = ew_ch(C);
   const int nbr = y2 ? 2 : 1;
-#define PDT_BA(DT_, M_, NB_, WZ_)                                                                           \
-  if (mask == M_ && nbr == NB_ && wdz == WZ_) {                                                             \
-    if (nt)                                                                                                 \
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<DT_, M_, NB_, WZ_, true>), gr, bl, 0, s, g, out, y1, b1, dy1, \
-                         y2, b2, dy2, dz_out, n8, C);                                                       \
-    else                                                                                                    \
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<DT_, M_, NB_, WZ_, false>), gr, bl, 0, s, g, out, y1, b1, dy1, \
-                         y2, b2, dy2, dz_out, n8, C);                                                       \
-    return;                                                                                                 \
+#define PDT_TARGS(...) __VA_ARGS__
+#define PDT_BA(DT_, M_, NB_, WZ_)                                                                                \
+  if (mask == M_ && nbr == NB_ && wdz == WZ_) {                                                                  \
+    PDT_EW_DISPATCH(bn_bwd_apply_kernel, PDT_TARGS(DT_, M_, NB_, WZ_), grid, nt, ch, g, out, y1, b1, dy1, y2, b2, \
+                    dy2, dz_out, n8, C);                                                                         \
+    return;                                                                                                      \
   }
   if (dtype == kBF16) {
     PDT_BA(kBF16, true, 1, false) PDT_BA(kBF16, true, 1, true) PDT_BA(kBF16, true, 2, false)
@@ -520,6 +597,7 @@ void bn_bwd_apply_launch(int dtype, const uint16_t* g, const uint8_t* out, const
     PDT_BA(kF16, false, 1, false) PDT_BA(kF16, false, 2, false) PDT_BA(kF16, false, 1, true)
   }
 #undef PDT_BA
+#undef PDT_TARGS
   pdt_hip_fail("bn_bwd_apply: unsupported variant", hipErrorInvalidValue, __FILE__, __LINE__);
 }
 

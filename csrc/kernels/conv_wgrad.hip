@@ -193,16 +193,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
 // block stages the dY tile once plus the 4 pair-windows of X (64 pixels x 128 B each, 40 KB per stage,
 // 2 stages -> 2 blocks per CU) and wave t owns pair t's 64 (window column) x 64 (cout) tile over the
 // whole pixel range of its split.  The partial tile goes out through LDS as coalesced float4 rows.
-//
-// FUSE: the stem's whole backward tail in this kernel -- dY is never materialised.  Instead of a dY DMA,
-// every K-step's 64 x 64 dY tile is computed from the pooled gradient, the max-pool argmax, the conv
-// output y0 and the BatchNorm coefficients (max-pool backward + ReLU mask + BN-backward apply:
-// dY = A * relu'(sc*y0 + sh) * dz + B * y0 + C) and written to LDS.  A thread owns 8 channels of a
-// horizontal pixel pair (2s, 2s+1) of one conv-output row h: the pair's dz gathers from at most 4
-// pooling windows (rows h>>1 and, for odd h, h>>1 + 1; columns s and s+1).  The loads of step st+1 are
-// issued before step st's MFMAs and consumed after them, so they hide behind the matrix work.  This
-// removes the 1.9 GB dY write and re-read of ResNet-18 at B = 1200 (the separate apply pass).
-template <int DT, bool FUSE>
+// (The training path fuses the stem's backward tail into the weight gradient instead: wgrad_stem_rows_kernel /
+// wgrad_stem_quad_kernel below; this one serves a materialised dY, PDT_STEM_FUSED=0.)
+template <int DT>
 __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -222,13 +215,12 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
   const int lrow = lane >> 3, pch = lane & 7;
 
-  // 40 DMA instructions per stage (8 dY + 4 x 8 X), 10 per wave (FUSE: the 8 dY ones are replaced by
-  // dy_load / dy_store below; m < 2 <=> tile 0)
+  // 40 DMA instructions per stage (8 dY + 4 x 8 X), 10 per wave
   auto stage_load = [&](int step, int buf) {
     const int pbase = pix_begin + step * BKP;
     char* sb = smem + buf * STAGE;
 #pragma unroll
-    for (int m = FUSE ? 2 : 0; m < 10; ++m) {
+    for (int m = 0; m < 10; ++m) {
       const int ii = wave + 4 * m;
       const int tile = ii >> 3;                 // 0 = dY, 1..4 = pair tile-1
       const int row = (ii & 7) * 8 + lrow;      // pixel within the step
@@ -250,145 +242,13 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
 
-  // FUSE: the 8 X-tile DMAs of a wave cover only two pixel rows (wave*8 + lrow and (wave+4)*8 + lrow),
-  // once per kernel-row pair; the pairs differ by a constant image-row offset, so the pixel decode runs
-  // twice per step instead of once per DMA.  Same rows / LDS slots as stage_load's m = 2..9.
-  const uint32_t pair_step = (uint32_t)a.dil_h * a.W * a.cs * 2u;
-  auto stage_load_x = [&](int step, int buf) {
-    const int pbase = pix_begin + step * BKP;
-    char* sb = smem + buf * STAGE;
-    const int ra = wave * 8 + lrow, rb = ra + 32;
-    const int lch = pch ^ tr_swz(ra);  // == pch ^ tr_swz(rb): the swizzle reads row bits 1 and 3
-    uint32_t xa, xb, unused;
-    wgrad_rows<true>(a, pbase + ra, -a.pad_h, 0, 0, lch, 0, xa, unused);
-    wgrad_rows<true>(a, pbase + rb, -a.pad_h, 0, 0, lch, 0, xb, unused);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      buf_lds16_asm(rx, sb + (1 + t) * TB + wave * 1024, xa + t * pair_step);
-      buf_lds16_asm(rx, sb + (1 + t) * TB + (wave + 4) * 1024, xb + t * pair_step);
-    }
-  };
-
-  // ---- FUSE: dY tile rows 2*pr, 2*pr + 1 (a pixel pair), channels 8*c8 .. 8*c8 + 7 of this thread
-  const int pr = tid >> 3, c8 = tid & 7;
-  float fA[8], fB[8], fC[8], fsc[8], fsh[8];
-  u32x4v fy[2], fg[4];  // loaded through inline asm (gload*_asm): invisible to the compiler's waitcnt pass,
-  u32x2v fi[4];         // waited for by FUSE_WAIT, which also carries them as operands (see the loop)
-  int fkh = 0, fv = 0;  // fv: bit wi = window wi exists (applied in dy_store: a select right after the
-  bool fok = false;     // loads would make the wave wait for them before the MFMAs)
-  if constexpr (FUSE) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c8 * 8 + e;
-      fA[e] = a.f_bcoef[c]; fB[e] = a.f_bcoef[64 + c]; fC[e] = a.f_bcoef[128 + c];
-      fsc[e] = a.f_coef[c]; fsh[e] = a.f_coef[64 + c];
-    }
-  }
-  // issue the global loads of step `step`'s dY inputs (y0 of the pair, argmax + gradient of 4 windows)
-  auto dy_load = [&](int step) {
-    const int p0 = pix_begin + step * BKP + 2 * pr;
-    fok = p0 < a.P;  // P is even (Qm even), so the pair is all-in or all-out
-    const int p = fok ? p0 : 0;
-    const FastDiv dpq{a.div_pq_mul, a.div_pq_shift}, dq{a.div_q_mul, a.div_q_shift};
-    const int nimg = (int)fdiv((uint32_t)p, dpq);
-    const int rem = p - nimg * (a.Pm * a.Qm);
-    const int h = (int)fdiv((uint32_t)rem, dq), w = rem - h * a.Qm;  // w even
-    const int oh = h >> 1, s = w >> 1;
-    fkh = h & 1 ? 2 : 1;                        // kernel row of window oh that selects row h
-    const bool okb = (h & 1) && oh + 1 < a.f_OH;  // window oh+1 (kernel row 0) covers odd h
-    const bool oks = s + 1 < a.f_OW;             // window column s+1 (kernel column 0) covers w+1
-    fy[0] = gload16_asm(a.f_y + (uint32_t)p * 64u + c8 * 8);
-    fy[1] = gload16_asm(a.f_y + (uint32_t)(p + 1) * 64u + c8 * 8);
-#pragma unroll
-    for (int wi = 0; wi < 4; ++wi) {
-      const int wr = oh + (wi >> 1), wc = s + (wi & 1);
-      const bool ok = ((wi >> 1) == 0 || okb) && ((wi & 1) == 0 || oks);
-      const uint32_t o = (((uint32_t)nimg * a.f_OH + (ok ? wr : oh)) * a.f_OW + (ok ? wc : s)) * 64u + c8 * 8;
-      fi[wi] = gload8_asm(a.f_idx + o);
-      fg[wi] = gload16_asm(a.f_dp + o);
-    }
-    fv = 1 | (okb ? 4 : 0) | (oks ? 2 : 0) | (okb && oks ? 8 : 0);
-  };
-  // finish step's dY (max-pool backward, ReLU mask, BN-backward apply) into LDS buffer `buf`
-  auto dy_store = [&](int buf) {
-    char* sy = smem + buf * STAGE;
-    const uint32_t keep = fok ? 0xffffffffu : 0u;  // pixels past the end: zero rows (branch-free)
-    uint32_t ov[2][4];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int sh = 16 * (e & 1);
-      auto pos = [&](int wi) { return (int)(((e < 4 ? fi[wi].x : fi[wi].y) >> (8 * (e & 3))) & 0xffu); };
-      auto grd = [&](int wi) {
-        const uint32_t gw[4] = {fg[wi].x, fg[wi].y, fg[wi].z, fg[wi].w};
-        return E::to_f((uint16_t)(gw[e >> 1] >> sh));
-      };
-      // window (oh, s) selects (h, w) with tap (fkh, 1) and (h, w+1) with (fkh, 2); (oh, s+1) selects
-      // (h, w+1) with (fkh, 0); (oh+1, s): (h, w) with (0, 1), (h, w+1) with (0, 2); (oh+1, s+1): (h, w+1)
-      // with (0, 0)
-      const int p0 = pos(0), p1 = fv & 2 ? pos(1) : 255, p2 = fv & 4 ? pos(2) : 255, p3 = fv & 8 ? pos(3) : 255;
-      const float g0 = grd(0), g1 = grd(1), g2 = grd(2), g3 = grd(3);
-      float dz0 = 0.f, dz1 = 0.f;
-      if (p0 == fkh * 3 + 1) dz0 += g0;
-      if (p2 == 1) dz0 += g2;
-      if (p0 == fkh * 3 + 2) dz1 += g0;
-      if (p1 == fkh * 3) dz1 += g1;
-      if (p2 == 2) dz1 += g2;
-      if (p3 == 0) dz1 += g3;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const uint32_t yw[4] = {fy[q].x, fy[q].y, fy[q].z, fy[q].w};
-        const float yv = E::to_f((uint16_t)(yw[e >> 1] >> sh));
-        const float dz = yv * fsc[e] + fsh[e] > 0.f ? (q ? dz1 : dz0) : 0.f;
-        const uint32_t r = (uint32_t)E::from_f(__builtin_fmaf(fA[e], dz, __builtin_fmaf(fB[e], yv, fC[e])));
-        if (e & 1) ov[q][e >> 1] |= r << 16; else ov[q][e >> 1] = r;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int row = 2 * pr + q;
-      *(uint4*)(sy + row * ROWB + ((c8 ^ tr_swz(row)) << 4)) =
-          make_uint4(ov[q][0] & keep, ov[q][1] & keep, ov[q][2] & keep, ov[q][3] & keep);
-    }
-  };
-
-  // FUSE schedule: step st+1's dY inputs are loaded at the end of step st-1 (after that step's dY tile
-  // was stored), so they have all of step st (DMA issue + MFMAs) to arrive; step st ends with one
-  // vmcnt(0) covering both the X-tile DMA and those loads, then stores the dY tile of st+1 and issues
-  // the loads of st+2.  One register set suffices and no load is waited for ahead of the MFMAs.
-  // The dY-input loads are asm (the compiler would wait vmcnt(0) for them, draining the X-tile DMA
-  // too); FUSE_WAIT(n) waits for all but the n youngest vector-memory ops and takes the loaded
-  // registers as in/out operands, so no use of them can be scheduled ahead of it.  Per step st the
-  // queue is [loads(st+1): 10][DMA(st+1): 8] at the dY store (vmcnt(8): the DMA stays in flight under
-  // the dY math), then [DMA(st+1): 8][loads(st+2): 10] before the barrier (vmcnt(10)).
-#define FUSE_WAIT(n)                                                                                   \
-  asm volatile("s_waitcnt vmcnt(" #n ")"                                                               \
-               : "+v"(fy[0]), "+v"(fy[1]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]), "+v"(fi[3]), "+v"(fg[0]), \
-                 "+v"(fg[1]), "+v"(fg[2]), "+v"(fg[3])                                                 \
-               :                                                                                       \
-               : "memory")
   if (nsteps > 0) {
-    if constexpr (FUSE) {
-      dy_load(0);
-      stage_load_x(0, 0);
-    } else {
-      stage_load(0, 0);
-    }
-    if constexpr (FUSE) {
-      FUSE_WAIT(0);
-      dy_store(0);
-      if (nsteps > 1) dy_load(1);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    stage_load(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int st = 0; st < nsteps; ++st) {
       const int cur = st & 1;
-      if (st + 1 < nsteps) {
-        if constexpr (FUSE)
-          stage_load_x(st + 1, cur ^ 1);
-        else
-          stage_load(st + 1, cur ^ 1);
-      }
+      if (st + 1 < nsteps) stage_load(st + 1, cur ^ 1);
       const char* sy = smem + cur * STAGE;
       const char* sx = sy + (1 + wave) * TB;
 #pragma unroll
@@ -414,28 +274,10 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
       }
-      if constexpr (FUSE) {
-        __builtin_amdgcn_sched_barrier(0);  // the waits and the dY math stay behind the last MFMA
-        if (st + 1 < nsteps) {
-          FUSE_WAIT(8);
-          __builtin_amdgcn_sched_barrier(0);
-          dy_store(cur ^ 1);
-          if (st + 2 < nsteps) {
-            dy_load(st + 2);
-            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-          } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   }
-#undef FUSE_WAIT
   // acc[i][j]: rows (window column) c = 16i + 4*(lane>>4) + r, col k = 16j + (lane&15); transpose
   // through LDS ([4 pairs][64 k][64 c]) and write ws[split][k][pair*64 + c] as float4 rows
   float* red = (float*)smem;
@@ -455,6 +297,480 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(ConvWgradArgs a) {
     const int idx = (e * 256 + tid) * 4;  // 0..16383 over [k][pair][c]
     const int k = idx >> 8, pc = idx & 255, pr = pc >> 6, c = pc & 63;
     *(f32x4_t*)(dst + (int64_t)k * a.ldw + pc) = *(const f32x4_t*)(red + (pr * 64 + k) * 64 + c);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The fused stem weight gradient over 2x2 pixel QUADS (round 5).  The GEMM's reduction runs over pixels in any
+// order, so a K-step's 64 pixels are 16 quads (conv rows 2r, 2r+1 x columns 2s, 2s+1), in (image, r, s) order.
+// A quad's four pixels draw their max-pool gradient from exactly the four pooling windows (r | r+1, s | s+1) --
+// the same four windows a pixel-PAIR form (round 4) loaded for just two pixels -- and each window's
+// argmax can select at most one pixel of the quad:
+//     (2r, 2s)     <- (r, s) at tap 4
+//     (2r, 2s+1)   <- (r, s) tap 5, (r, s+1) tap 3
+//     (2r+1, 2s)   <- (r, s) tap 7, (r+1, s) tap 1
+//     (2r+1, 2s+1) <- (r, s) tap 8, (r, s+1) tap 6, (r+1, s) tap 2, (r+1, s+1) tap 0
+// so per element the max-pool backward is 9/4 compare-selects instead of 3, and the window loads and decodes are
+// shared by four pixels instead of two (the kernel is VALU-issue bound: r4_after_pmc.md, 53 % active / 11 % wait).
+// The sums add the windows in the same order as the separate apply pass (stem_pool_bwd_apply), so dY is
+// bit-identical to it.  A thread owns one quad x 4 channels.  An odd
+// conv-output height leaves the quads of the last row half dead (zero rows on both GEMM sides).  Pipeline, LDS
+// images and MFMA part as wgrad_stem_kernel: 12 operand loads per thread per step.  Serves the shapes the
+// raw-row kernel below does not (conv output not a multiple of 4 x 16 pixels).
+PDT_DEVICE uint32_t gload4_asm(const void* p) {
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void wgrad_stem_quad_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 64;         // pixels (16 quads) per K-step
+  constexpr int ROWB = 128;       // 64 elements * 2 B
+  constexpr int TB = BKP * ROWB;  // 8 KB per tile
+  constexpr int STAGE = 5 * TB;   // dY + 4 pair windows
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = kernel-row pair
+  const int split = blockIdx.x;
+  const int pix_begin = split * a.pix_per_split;
+  const int pix_end = min(a.P, pix_begin + a.pix_per_split);  // a.P: quad-padded pixel count (launcher)
+  const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int QR = (a.Pm + 1) >> 1, QC = a.Qm >> 1;  // quad rows / columns per image
+  const FastDiv dqimg{a.div_pq_mul, a.div_pq_shift}, dqc{a.div_q_mul, a.div_q_shift};  // by QR*QC, by QC
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+
+  // X DMA: rows ra = wave*8 + lrow and rb = ra + 32 of the step (pixel p = 4 * quad + sub), 4 pairs each
+  const uint32_t pair_step = (uint32_t)a.dil_h * a.W * a.cs * 2u;
+  auto x_off = [&](int p, int lch) -> uint32_t {
+    const int qd = p >> 2, sub = p & 3;
+    const int nimg = (int)fdiv((uint32_t)qd, dqimg);
+    const int rem = qd - nimg * (QR * QC);
+    const int r = (int)fdiv((uint32_t)rem, dqc), sc = rem - r * QC;
+    const int h = 2 * r + (sub >> 1), w = 2 * sc + (sub & 1);
+    // dead half-quad of an odd height: zero row (kOOB); pixels past the tensor land past num_records (zeros)
+    if (h >= a.Pm) return kOOB;
+    return (uint32_t)((((nimg * a.H + h * a.stride_h - a.pad_h + (lch >> 2)) * a.W + w * a.stride_w) * a.cs +
+                       (lch & 3) * 8) * 2);
+  };
+  auto stage_load_x = [&](int step, int buf) {
+    const int pbase = pix_begin + step * BKP;
+    char* sb = smem + buf * STAGE;
+    const int ra = wave * 8 + lrow, rb = ra + 32;
+    const int lch = pch ^ tr_swz(ra);  // == pch ^ tr_swz(rb)
+    const uint32_t xa = x_off(pbase + ra, lch), xb = x_off(pbase + rb, lch);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      buf_lds16_asm(rx, sb + (1 + t) * TB + wave * 1024, xa == kOOB ? kOOB : xa + t * pair_step);
+      buf_lds16_asm(rx, sb + (1 + t) * TB + (wave + 4) * 1024, xb == kOOB ? kOOB : xb + t * pair_step);
+    }
+  };
+
+  // ---- dY: quad qd of the step, channels 4*cg .. 4*cg + 3
+  const int qd = tid >> 4, cg = tid & 15;
+  float fA[4], fB[4], fC[4], fsc[4], fsh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = cg * 4 + e;
+    fA[e] = a.f_bcoef[c]; fB[e] = a.f_bcoef[64 + c]; fC[e] = a.f_bcoef[128 + c];
+    fsc[e] = a.f_coef[c]; fsh[e] = a.f_coef[64 + c];
+  }
+  u32x2v fy[4], fg[4];  // asm loads (common.h gload*_asm): waited for by QUAD_WAIT, which also carries them as
+                        // operands so no use can be scheduled ahead of it
+  uint32_t fi[4];
+  int fvalid = 0;       // bit 0: quad live, bit 1: row 2r+1 live, bit 2: window row r+1, bit 3: window column s+1
+  auto dy_load = [&](int step) {
+    const int qg = (pix_begin + step * BKP) / 4 + qd;
+    const bool live = qg * 4 < a.P;
+    const int qq = live ? qg : 0;
+    const int nimg = (int)fdiv((uint32_t)qq, dqimg);
+    const int rem = qq - nimg * (QR * QC);
+    const int r = (int)fdiv((uint32_t)rem, dqc), sc = rem - r * QC;
+    const bool row1 = 2 * r + 1 < a.Pm;
+    const bool okr = r + 1 < a.f_OH, oks = sc + 1 < a.f_OW;
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      const int h = min(2 * r + (sub >> 1), a.Pm - 1), w = 2 * sc + (sub & 1);
+      fy[sub] = gload8_asm(a.f_y + ((uint32_t)(nimg * a.Pm + h) * a.Qm + w) * 64u + cg * 4);
+    }
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const int wr = (wi >> 1) && okr ? r + 1 : r, wc = (wi & 1) && oks ? sc + 1 : sc;
+      const uint32_t o = (((uint32_t)nimg * a.f_OH + wr) * a.f_OW + wc) * 64u + cg * 4;
+      fi[wi] = gload4_asm(a.f_idx + o);
+      fg[wi] = gload8_asm(a.f_dp + o);
+    }
+    fvalid = (live ? 1 : 0) | (row1 ? 2 : 0) | (okr ? 4 : 0) | (oks ? 8 : 0);
+  };
+  auto dy_store = [&](int buf) {
+    char* sy = smem + buf * STAGE;
+    // missing windows select nothing (position 255); a dead quad or half-quad stores zero rows
+    const uint32_t i0 = fi[0], i1 = fvalid & 8 ? fi[1] : 0xffffffffu, i2 = fvalid & 4 ? fi[2] : 0xffffffffu;
+    const uint32_t i3 = (fvalid & 12) == 12 ? fi[3] : 0xffffffffu;
+    const uint32_t keep0 = fvalid & 1 ? 0xffffffffu : 0u, keep1 = (fvalid & 3) == 3 ? 0xffffffffu : 0u;
+    uint32_t ov[4][2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int sh = 16 * (e & 1);
+      const uint32_t p0 = (i0 >> (8 * e)) & 0xffu, p1 = (i1 >> (8 * e)) & 0xffu;
+      const uint32_t p2 = (i2 >> (8 * e)) & 0xffu, p3 = (i3 >> (8 * e)) & 0xffu;
+      const float g0 = E::to_f((uint16_t)(fg[0][e >> 1] >> sh)), g1 = E::to_f((uint16_t)(fg[1][e >> 1] >> sh));
+      const float g2 = E::to_f((uint16_t)(fg[2][e >> 1] >> sh)), g3 = E::to_f((uint16_t)(fg[3][e >> 1] >> sh));
+      float dz[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p0 == 4) dz[0] += g0;
+      if (p0 == 5) dz[1] += g0;
+      if (p1 == 3) dz[1] += g1;
+      if (p0 == 7) dz[2] += g0;
+      if (p2 == 1) dz[2] += g2;
+      if (p0 == 8) dz[3] += g0;
+      if (p1 == 6) dz[3] += g1;
+      if (p2 == 2) dz[3] += g2;
+      if (p3 == 0) dz[3] += g3;
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        const float yv = E::to_f((uint16_t)(fy[sub][e >> 1] >> sh));
+        const float d = yv * fsc[e] + fsh[e] > 0.f ? dz[sub] : 0.f;
+        const uint32_t rr = (uint32_t)E::from_f(__builtin_fmaf(fA[e], d, __builtin_fmaf(fB[e], yv, fC[e])));
+        if (e & 1) ov[sub][e >> 1] |= rr << 16; else ov[sub][e >> 1] = rr;
+      }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      const int row = 4 * qd + sub;
+      const uint32_t keep = sub < 2 ? keep0 : keep1;
+      *(uint2*)(sy + row * ROWB + (((cg >> 1) ^ tr_swz(row)) << 4) + (cg & 1) * 8) =
+          make_uint2(ov[sub][0] & keep, ov[sub][1] & keep);
+    }
+  };
+  // step st+1's dY inputs are loaded at the end of step st-1 (after that step's dY tile was stored), so they have
+  // all of step st to arrive: [loads(st+1): 12][DMA(st+1): 8] at the dY store (vmcnt(8): the DMA stays in flight
+  // under the dY math), then [DMA(st+1): 8][loads(st+2): 12] before the barrier (vmcnt(12))
+#define QUAD_WAIT(n)                                                                                     \
+  asm volatile("s_waitcnt vmcnt(" #n ")"                                                                 \
+               : "+v"(fy[0]), "+v"(fy[1]), "+v"(fy[2]), "+v"(fy[3]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]), \
+                 "+v"(fi[3]), "+v"(fg[0]), "+v"(fg[1]), "+v"(fg[2]), "+v"(fg[3])                         \
+               :                                                                                         \
+               : "memory")
+  if (nsteps > 0) {
+    dy_load(0);
+    stage_load_x(0, 0);
+    QUAD_WAIT(0);
+    dy_store(0);
+    if (nsteps > 1) dy_load(1);
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+      const int cur = st & 1;
+      if (st + 1 < nsteps) stage_load_x(st + 1, cur ^ 1);
+      const char* sy = smem + cur * STAGE;
+      const char* sx = sy + (1 + wave) * TB;
+#pragma unroll
+      for (int kk = 0; kk < BKP / 32; ++kk) {
+        const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+        const int sw0 = tr_swz(r0), sw1 = tr_swz(r1);
+        vec8 af[4], bfr[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int col = f * 16 + 4 * p4;
+          const int ch = col >> 3, off = (col & 7) * 2;
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sx + r0 * ROWB + ((ch ^ sw0) << 4) + off));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(sx + r1 * ROWB + ((ch ^ sw1) << 4) + off));
+          af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r0 * ROWB + ((ch ^ sw0) << 4) + off));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r1 * ROWB + ((ch ^ sw1) << 4) + off));
+          bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the waits and the dY math stay behind the last MFMA
+      if (st + 1 < nsteps) {
+        QUAD_WAIT(8);
+        __builtin_amdgcn_sched_barrier(0);
+        dy_store(cur ^ 1);
+        if (st + 2 < nsteps) {
+          dy_load(st + 2);
+          asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+  }
+#undef QUAD_WAIT
+  // acc[i][j]: rows (window column) c = 16i + 4*(lane>>4) + r, col k = 16j + (lane&15); transpose through LDS
+  float* red = (float*)smem;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 16 * j + (lane & 15);
+      const int c = 16 * i + 4 * (lane >> 4);
+      *(f32x4_t*)(red + (wave * 64 + k) * 64 + c) = acc[i][j];
+    }
+  __syncthreads();
+  float* dst = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int idx = (e * 256 + tid) * 4;  // 0..16383 over [k][pair][c]
+    const int k = idx >> 8, pc = idx & 255, pr = pc >> 6, c = pc & 63;
+    *(f32x4_t*)(dst + (int64_t)k * a.ldw + pc) = *(const f32x4_t*)(red + (pr * 64 + k) * 64 + c);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The fused stem weight gradient on RAW IMAGE ROWS (round 5).  PMC on the window-staged kernels above: the vector
+// data-return path (TD) is ~80 % busy, and 60 % of what it returns is the window image: every pixel's 4 x 128 B
+// of kernel-row-pair windows are DMA'd separately although neighbouring windows overlap 3/4 (stride 2, 8 pixels
+// wide).  Here a K-step is a 4-row x 16-column block of conv-output pixels and stages just the padded image rows
+// it touches -- 14 rows x 38 pixels x 4 channels, 4.2 KB instead of 32 KB -- and the MFMA A fragments are read
+// straight out of them: the transposed LDS read only needs each lane's 8-byte address of 4 consecutive elements of
+// its pixel's window row, and window column j of pixel (dh, wl) for kernel-row pair t is element 8 wl + (j & 31) of
+// staged row 2 dh + 2 t + (j >> 5).  dY is computed per 2x2 quad as in wgrad_stem_quad_kernel (same arithmetic,
+// same summation order) into the [pixel][64] tile.  Needs Pm % 4 == 0 and Qm % 16 == 0 (the ResNet stem at
+// 224 px: 112 x 112); other shapes take the pixel-pair kernel.  12 operand loads + 2 DMA instructions per thread /
+// wave per step; pixel p of a step = 16 dh + wl.
+template <int DT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void wgrad_stem_rows_kernel(ConvWgradArgs a) {
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int BKP = 64;             // pixels per K-step: 4 conv rows x 16 conv columns
+  constexpr int ROWB = 128;           // dY tile: 64 channels * 2 B
+  constexpr int TB = BKP * ROWB;      // 8 KB
+  constexpr int XROWB = 38 * 4 * 2;   // one staged image row: 2 * 15 + 8 pixels x 4 channels (304 B)
+  constexpr int XCH = XROWB / 16;     // 19 16-byte DMA chunks per row
+  constexpr int XROWS = 14;           // image rows of a step: 2 * 3 + 2 * 3 + 1 + 1
+  constexpr int XB = 512 * 16;        // 2 DMA instructions per wave x 4 waves x 64 lanes x 16 B (266 chunks live)
+  constexpr int STAGE = TB + XB;      // 16 KB
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = kernel-row pair
+  const int split = blockIdx.x;
+  const int steps_total = a.P / BKP;
+  const int s_begin = split * (a.pix_per_split / BKP);
+  const int s_end = min(steps_total, s_begin + a.pix_per_split / BKP);
+  const int nsteps = max(0, s_end - s_begin);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
+  const int SW = a.Qm / 16, SPI = (a.Pm / 4) * SW;  // steps per 4-row band, per image
+  const FastDiv dspi{a.div_pq_mul, a.div_pq_shift}, dsw{a.div_q_mul, a.div_q_shift};
+  const uint32_t img_row_b = (uint32_t)a.W * a.cs * 2u;
+
+  // step -> (image, first conv row h0, first conv column w0), wave-uniform
+  auto step_geom = [&](int st, int& n, int& h0, int& w0) {
+    n = (int)fdiv((uint32_t)st, dspi);
+    const int rem = st - n * SPI;
+    const int hb = (int)fdiv((uint32_t)rem, dsw);
+    h0 = 4 * hb;
+    w0 = 16 * (rem - hb * SW);
+  };
+  // X DMA: lane slot L = j * 256 + wave * 64 + lane of the stage's 512 16-byte slots; slot L holds chunk L % 19 of
+  // staged row L / 19 (slots past 14 rows read zeros)
+  uint32_t xlane[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int L = j * 256 + wave * 64 + lane, k = L / XCH, c = L - k * XCH;
+    xlane[j] = k < XROWS ? (uint32_t)k * img_row_b + (uint32_t)c * 16u : kOOB;
+  }
+  auto stage_load_x = [&](int st, int buf) {
+    int n, h0, w0;
+    step_geom(st, n, h0, w0);
+    const uint32_t base = (((uint32_t)n * a.H + 2u * h0) * a.W + 2u * w0) * a.cs * 2u;
+    char* sx = smem + buf * STAGE + TB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      buf_lds16_asm(rx, sx + (j * 256 + wave * 64) * 16, xlane[j] == kOOB ? kOOB : base + xlane[j]);
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+  // A-fragment addresses (per kk, r0 | r1, column half): row 2 dh + 2 wave + half, element 8 wl + 4 p4 (+ 16 for
+  // the odd fragment of a half)
+  int xa[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = kk * 32 + 8 * g + q + 4 * h, dh = p >> 4, wl = p & 15;
+      xa[kk][h] = (2 * dh + 2 * wave) * XROWB + wl * 16 + p4 * 8;
+    }
+
+  // ---- dY: quad (qr, qc) = (qd >> 3, qd & 7) of the step, channels 4*cg .. 4*cg + 3
+  const int qd = tid >> 4, cg = tid & 15, qr = qd >> 3, qc = qd & 7;
+  float fA[4], fB[4], fC[4], fsc[4], fsh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = cg * 4 + e;
+    fA[e] = a.f_bcoef[c]; fB[e] = a.f_bcoef[64 + c]; fC[e] = a.f_bcoef[128 + c];
+    fsc[e] = a.f_coef[c]; fsh[e] = a.f_coef[64 + c];
+  }
+  u32x2v fy[4], fg[4];  // asm loads: waited for by ROWS_WAIT
+  uint32_t fi[4];
+  int fvalid = 0;       // bit 2: window row r+1 exists, bit 3: window column s+1 exists
+  auto dy_load = [&](int st) {
+    int n, h0, w0;
+    step_geom(st, n, h0, w0);
+    const int r = (h0 >> 1) + qr, sc = (w0 >> 1) + qc;
+    const bool okr = r + 1 < a.f_OH, oks = sc + 1 < a.f_OW;
+    const uint32_t pix = ((uint32_t)(n * a.Pm + 2 * r) * a.Qm + 2 * sc) * 64u + cg * 4;
+    fy[0] = gload8_asm(a.f_y + pix);
+    fy[1] = gload8_asm(a.f_y + pix + 64u);
+    fy[2] = gload8_asm(a.f_y + pix + (uint32_t)a.Qm * 64u);
+    fy[3] = gload8_asm(a.f_y + pix + (uint32_t)a.Qm * 64u + 64u);
+    const uint32_t w00 = (((uint32_t)n * a.f_OH + r) * a.f_OW + sc) * 64u + cg * 4;
+    const uint32_t dr = okr ? (uint32_t)a.f_OW * 64u : 0u, dc = oks ? 64u : 0u;
+    fi[0] = gload4_asm(a.f_idx + w00);
+    fg[0] = gload8_asm(a.f_dp + w00);
+    fi[1] = gload4_asm(a.f_idx + w00 + dc);
+    fg[1] = gload8_asm(a.f_dp + w00 + dc);
+    fi[2] = gload4_asm(a.f_idx + w00 + dr);
+    fg[2] = gload8_asm(a.f_dp + w00 + dr);
+    fi[3] = gload4_asm(a.f_idx + w00 + dr + dc);
+    fg[3] = gload8_asm(a.f_dp + w00 + dr + dc);
+    fvalid = (okr ? 4 : 0) | (oks ? 8 : 0);
+  };
+  auto dy_store = [&](int buf) {
+    char* sy = smem + buf * STAGE;
+    const uint32_t i0 = fi[0], i1 = fvalid & 8 ? fi[1] : 0xffffffffu, i2 = fvalid & 4 ? fi[2] : 0xffffffffu;
+    const uint32_t i3 = (fvalid & 12) == 12 ? fi[3] : 0xffffffffu;
+    uint32_t ov[4][2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int sh = 16 * (e & 1);
+      const uint32_t p0 = (i0 >> (8 * e)) & 0xffu, p1 = (i1 >> (8 * e)) & 0xffu;
+      const uint32_t p2 = (i2 >> (8 * e)) & 0xffu, p3 = (i3 >> (8 * e)) & 0xffu;
+      const float g0 = E::to_f((uint16_t)(fg[0][e >> 1] >> sh)), g1 = E::to_f((uint16_t)(fg[1][e >> 1] >> sh));
+      const float g2 = E::to_f((uint16_t)(fg[2][e >> 1] >> sh)), g3 = E::to_f((uint16_t)(fg[3][e >> 1] >> sh));
+      float dz[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p0 == 4) dz[0] += g0;
+      if (p0 == 5) dz[1] += g0;
+      if (p1 == 3) dz[1] += g1;
+      if (p0 == 7) dz[2] += g0;
+      if (p2 == 1) dz[2] += g2;
+      if (p0 == 8) dz[3] += g0;
+      if (p1 == 6) dz[3] += g1;
+      if (p2 == 2) dz[3] += g2;
+      if (p3 == 0) dz[3] += g3;
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        const float yv = E::to_f((uint16_t)(fy[sub][e >> 1] >> sh));
+        const float d = yv * fsc[e] + fsh[e] > 0.f ? dz[sub] : 0.f;
+        const uint32_t rr = (uint32_t)E::from_f(__builtin_fmaf(fA[e], d, __builtin_fmaf(fB[e], yv, fC[e])));
+        if (e & 1) ov[sub][e >> 1] |= rr << 16; else ov[sub][e >> 1] = rr;
+      }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      const int row = (2 * qr + (sub >> 1)) * 16 + 2 * qc + (sub & 1);
+      *(uint2*)(sy + row * ROWB + (((cg >> 1) ^ tr_swz(row)) << 4) + (cg & 1) * 8) = make_uint2(ov[sub][0], ov[sub][1]);
+    }
+  };
+  // per step the queue is [loads(st+1): 12][DMA(st+1): 2] at the dY store (vmcnt(2): the DMA stays in flight
+  // under the dY math), then [DMA(st+1): 2][loads(st+2): 12] before the barrier (vmcnt(12))
+#define ROWS_WAIT(n)                                                                                     \
+  asm volatile("s_waitcnt vmcnt(" #n ")"                                                                 \
+               : "+v"(fy[0]), "+v"(fy[1]), "+v"(fy[2]), "+v"(fy[3]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]), \
+                 "+v"(fi[3]), "+v"(fg[0]), "+v"(fg[1]), "+v"(fg[2]), "+v"(fg[3])                         \
+               :                                                                                         \
+               : "memory")
+  if (nsteps > 0) {
+    dy_load(s_begin);
+    stage_load_x(s_begin, 0);
+    ROWS_WAIT(0);
+    dy_store(0);
+    if (nsteps > 1) dy_load(s_begin + 1);
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+      const int cur = st & 1;
+      if (st + 1 < nsteps) stage_load_x(s_begin + st + 1, cur ^ 1);
+      const char* sy = smem + cur * STAGE;
+      const char* sx = sy + TB;
+#pragma unroll
+      for (int kk = 0; kk < BKP / 32; ++kk) {
+        const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
+        const int sw0 = tr_swz(r0), sw1 = tr_swz(r1);
+        vec8 af[4], bfr[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int xo = (f >> 1) * XROWB + (f & 1) * 32;  // column half -> next staged row; odd fragment +16 el
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sx + xa[kk][0] + xo));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sx + xa[kk][1] + xo));
+          af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          const int col = f * 16 + 4 * p4;
+          const int ch = col >> 3, off = (col & 7) * 2;
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r0 * ROWB + ((ch ^ sw0) << 4) + off));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r1 * ROWB + ((ch ^ sw1) << 4) + off));
+          bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the waits and the dY math stay behind the last MFMA
+      if (st + 1 < nsteps) {
+        ROWS_WAIT(2);
+        __builtin_amdgcn_sched_barrier(0);
+        dy_store(cur ^ 1);
+        if (st + 2 < nsteps) {
+          dy_load(s_begin + st + 2);
+          asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+  }
+#undef ROWS_WAIT
+  // acc[i][j]: rows (window column) c = 16i + 4*(lane>>4) + r, col k = 16j + (lane&15); transposed through the
+  // 32 KB of LDS two pairs at a time ([2 pairs][64 k][64 c] fp32), written as ws[split][k][pair*64 + c] rows
+  float* red = (float*)smem;
+  float* dst = a.ws + (int64_t)split * a.Kout * a.ldw;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+    if ((wave >> 1) == half) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = 16 * j + (lane & 15);
+          const int c = 16 * i + 4 * (lane >> 4);
+          *(f32x4_t*)(red + ((wave & 1) * 64 + k) * 64 + c) = acc[i][j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = (e * 256 + tid) * 4;  // 0..8191 over [k][pair of the half][c]
+      const int k = idx >> 7, pc = idx & 127, pr = pc >> 6, c = pc & 63;
+      *(f32x4_t*)(dst + (int64_t)k * a.ldw + half * 128 + pc) = *(const f32x4_t*)(red + (pr * 64 + k) * 64 + c);
+    }
   }
 }
 
@@ -1311,6 +1627,18 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
     (void)target_blocks;
     splits = cus / tiles > 0 ? cus / tiles : 1;
   }
+  if (a.win && a.T == 4 && a.U == 1 && a.C == 64 && a.Kout == 64) {
+    // the ResNet stem (one block per split covers all 4 pairs): the raw-row kernel runs 3 workgroups per CU
+    // (wgrad_stem_rows_kernel: 168 registers, 32 KB LDS) -- one full round of them
+    static const int cus3 = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return 3 * (n > 0 ? n : 256);
+    }();
+    (void)target_blocks;
+    splits = cus3;
+  }
   const int max_splits = (a.P + 511) / 512;  // keep >= 4 K-steps per block
   splits = splits < 1 ? 1 : (splits > max_splits ? max_splits : splits);
   int pps = (a.P + splits - 1) / splits;
@@ -1357,15 +1685,40 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       PDT_COUNT("wgrad_stem_fused");
     else
       PDT_COUNT("wgrad_stem");
-    if (a.f_y != nullptr) {
+    static const bool rows = [] {  // PDT_STEM_ROWS=0: the window-staged quad kernel (A/B)
+      const char* e = getenv("PDT_STEM_ROWS");
+      return !(e && e[0] == '0');
+    }();
+    if (a.f_y != nullptr && rows && a.Pm % 4 == 0 && a.Qm % 16 == 0 && a.pix_per_split % 64 == 0 &&
+               a.stride_h == 2 && a.dil_h == 2 && a.pad_h == 0 && a.cs == 4) {
+      // raw-image-row staging (wgrad_stem_rows_kernel): steps are 4 x 16 pixel blocks, divisions by steps per
+      // image and per 4-row band
+      const int SW = a.Qm / 16, SPI = (a.Pm / 4) * SW;
+      const FastDiv dspi = make_fastdiv((uint32_t)SPI), dsw = make_fastdiv((uint32_t)SW);
+      a.div_pq_mul = dspi.mul; a.div_pq_shift = dspi.shift; a.div_q_mul = dsw.mul; a.div_q_shift = dsw.shift;
+      PDT_COUNT("wgrad_stem_rows");
       if (dtype == kBF16)
-        hipLaunchKernelGGL((wgrad_stem_kernel<kBF16, true>), dim3(a.splits), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((wgrad_stem_rows_kernel<kBF16>), dim3(a.splits), dim3(256), 0, s, a);
       else
-        hipLaunchKernelGGL((wgrad_stem_kernel<kF16, true>), dim3(a.splits), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((wgrad_stem_rows_kernel<kF16>), dim3(a.splits), dim3(256), 0, s, a);
+    } else if (a.f_y != nullptr) {
+      // quad order (wgrad_stem_quad_kernel): the divisions are by quads per image and quads per row, and the
+      // pixel count is padded to whole quads (an odd height's last quad row is half dead)
+      const int QR = (a.Pm + 1) / 2, QC = a.Qm / 2;
+      const FastDiv dqi = make_fastdiv((uint32_t)(QR * QC)), dqc = make_fastdiv((uint32_t)QC);
+      a.div_pq_mul = dqi.mul; a.div_pq_shift = dqi.shift; a.div_q_mul = dqc.mul; a.div_q_shift = dqc.shift;
+      a.P = a.N * QR * QC * 4;
+      if (a.Qm % 2 != 0 || (int64_t)a.splits * a.pix_per_split < a.P)
+        pdt_hip_fail("wgrad_stem_quad: needs an even width and a split plan over the quad-padded pixels",
+                     hipErrorInvalidValue, __FILE__, __LINE__);
+      if (dtype == kBF16)
+        hipLaunchKernelGGL((wgrad_stem_quad_kernel<kBF16>), dim3(a.splits), dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((wgrad_stem_quad_kernel<kF16>), dim3(a.splits), dim3(256), 0, s, a);
     } else if (dtype == kBF16) {
-      hipLaunchKernelGGL((wgrad_stem_kernel<kBF16, false>), dim3(a.splits), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_stem_kernel<kBF16>), dim3(a.splits), dim3(256), 0, s, a);
     } else {
-      hipLaunchKernelGGL((wgrad_stem_kernel<kF16, false>), dim3(a.splits), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_stem_kernel<kF16>), dim3(a.splits), dim3(256), 0, s, a);
     }
   } else if (a.win) {
     PDT_COUNT("conv_wgrad_window");

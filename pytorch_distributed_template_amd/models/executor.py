@@ -499,8 +499,8 @@ class ResNetExecutor:
                 and c.R == 1 and c.S == 1 and c.cin == 256 and (c.cout == 64 or (c.cout == 128 and bnb[0] == 2))
                 and H == P and W == Q and self.C.conv1x1_c64_supported(64, 256)):
             # the binding runs the persistent 1x1 backward-data kernel (conv1x1.hip), which has no tile: no tile
-            # choice (or autotune timing) for this shape
-            launch(0, 0)
+            # choice (or autotune timing) for this shape (the static tile only satisfies the binding's checks)
+            launch(*_conv_tile(c.cin))
         else:
             key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
             bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)

@@ -147,7 +147,12 @@ def test_train_step_matches_reference_224(arch, N, monkeypatch):
         ob = tb(x)
         lb = F.cross_entropy(ob, t)
     lb.backward()
-    assert abs(met[0].item() - loss.item()) / loss.item() < 5e-3
+    # loss within 5e-3 (ResNet-18/50); the deeper archs at N = 2-4 carry ~14 % bf16 logits error vs fp32 in BOTH
+    # engines (tools/deep_arch_probe.py: wide_resnet101_2 logits rel 0.138 ours / 0.135 autocast, loss off by up to
+    # 0.8 % ours / 0.8 % autocast depending on the seed), so their loss is held to 1.5e-2 and the logits / gradient
+    # checks below carry the comparison with autocast
+    tol = 5e-3 if arch in ("resnet18", "resnet50") else 1.5e-2
+    assert abs(met[0].item() - loss.item()) / loss.item() < tol
     assert _relnorm(logits, out.detach()) < 1.5 * _relnorm(ob.detach(), out.detach()) + 0.02
     bad = []
     for (n, p), (_, p2), (_, p3) in zip(model.named_parameters(), ref.named_parameters(), tb.named_parameters()):

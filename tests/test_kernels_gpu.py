@@ -322,12 +322,13 @@ def test_stem_pool_backward_fused():
     assert _rel(dy.permute(0, 3, 1, 2), xin.grad) < 2e-2
 
 
-@pytest.mark.parametrize("geom", [(2, 29, 28), (3, 28, 36)])
+@pytest.mark.parametrize("geom", [(2, 29, 28), (3, 28, 36), (2, 64, 64), (2, 224, 224)])
 def test_stem_wgrad_fused_dy(geom):
     """Stem weight gradient with dY computed in-kernel (max-pool bwd + ReLU + BN-bwd apply) vs the two-pass
     path (stem_pool_bwd_apply -> window-mode conv_wgrad) and vs an fp32 autograd reference.  The second
     geometry has an even conv-output height and a pooled width whose last window column is out of range
-    for the last pixel pair (boundary windows), both have a partial last K-step."""
+    for the last pixel pair (boundary windows), both have a partial last K-step; those two run the 2x2-quad kernel,
+    the 64 and 224 px ones (conv output a multiple of 4 x 16) the raw-image-row kernel."""
     from pytorch_distributed_template_amd.ops import native
     torch.manual_seed(9)
     N, H, W = geom

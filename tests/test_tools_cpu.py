@@ -104,5 +104,6 @@ def test_isa_hazards_every_kernel():
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     m = re.search(r"(\d+) kernels checked, 0 with violations", r.stdout)
     assert m and int(m.group(1)) > 300, r.stdout[-2000:]
-    for k in ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel"):
+    for k in ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_quad_kernel",
+              "wgrad_stem_rows_kernel"):
         assert k in r.stdout  # the designated windows were found and checked

@@ -39,12 +39,14 @@ WINDOWS = {
     "conv_l1pp_kernel": {14: "dma", 11: "load", 8: "load"},
     "conv_l1_kernel": {16: "dma", 12: "dma"},
     "stem_fwd_kernel": {24: "dma"},
-    "wgrad_stem_kernel": {10: "dma", 8: "load"},
+    "wgrad_stem_quad_kernel": {12: "dma", 8: "load"},
+    "wgrad_stem_rows_kernel": {12: "dma", 2: "load"},
     "conv_wgrad_wide_kernel": {6: ("dma", 6), 3: ("dma", 3)},
     "conv1x1_c64_kernel": {16: "dma"},  # the previous tile's 16 stores stay in flight
     "conv1x1_c64_bnb_kernel": {32: "dma", 40: "dma"},  # the previous tile's 24 (32) operand loads + 8 stores
 }
-COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "conv_pp_kernel",
+COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "wgrad_stem_quad_kernel",
+            "wgrad_stem_rows_kernel", "conv_pp_kernel",
             "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel",
             "conv1x1_c64_kernel", "conv1x1_c64_bnb_kernel")
 
