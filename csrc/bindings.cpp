@@ -415,6 +415,128 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   launched("conv_wgrad_launch");
 }
 
+// ---------------------------------------------------------------------------- grouped convolution (ResNeXt)
+// A grouped conv (groups g of cg channels, width = g * cg in and out) runs as width / S channel SLICES of S = 64:
+// slice j is the dense S -> S conv of channels [j*S, (j+1)*S) with a block-diagonal weight (S / cg groups on the
+// diagonal, zeros elsewhere: a derived layout gathered by the executor), on the generic implicit-GEMM kernels with
+// strided operands (input pixel stride ``cs`` = width, output / BN-operand stride ``ldy`` = width, statistics slot
+// row stride = the full width's).  The MFMA work is S / cg times the grouped FLOPs (16x at cg = 4 ... 2x at 32), in
+// exchange for running on the tuned tiles with the fused statistics / BN-backward epilogues.
+static constexpr int64_t kGSlice = 64;
+#define PDT_BCOUNT(name)                                                  \
+  do {                                                                    \
+    static long long* _c = pdt::dispatch_counter(name);                   \
+    __atomic_fetch_add(_c, 1LL, __ATOMIC_RELAXED);                        \
+  } while (0)
+
+void gconv_fwd(const Tensor& x, const Tensor& wslice, Tensor& y, const OptT& stats, int64_t N, int64_t H, int64_t W,
+               int64_t width, int64_t R, int64_t stride, int64_t pad, int64_t P, int64_t Q, int64_t j, int64_t bm,
+               int64_t bn) {
+  const int dt = dt16(x, "x");
+  const int64_t S = kGSlice;
+  TORCH_CHECK(dt16(wslice, "w") == dt && dt16(y, "y") == dt, "gconv_fwd: mixed dtypes");
+  TORCH_CHECK(width % S == 0 && j >= 0 && j < width / S, "gconv_fwd: bad slice");
+  TORCH_CHECK(x.numel() == N * H * W * width && y.numel() == N * P * Q * width && wslice.numel() == S * R * R * S,
+              "gconv_fwd: size mismatch");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && y.numel() < (int64_t(1) << 30), "gconv_fwd: operands exceed 2 GiB");
+  TORCH_CHECK(S % bn == 0 && N * P * Q < (int64_t(1) << 31), "gconv_fwd: tile / size");
+  pdt::ConvFwdArgs a{};
+  a.x = p16(x, "x") + j * S;
+  a.w = p16(wslice, "w");
+  a.y = p16(y, "y") + j * S;
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * width * 2, "gconv_fwd: stats buffer too small");
+    a.stats = pd(*stats, "stats") + j * S * 2;
+    a.stats_ld = (int)(width * 2);
+  }
+  a.N = N; a.H = H; a.W = W; a.C = S; a.Kout = S; a.T = R; a.U = R; a.Pm = P; a.Qm = Q; a.cs = width;
+  a.ldy = (int)width;
+  a.ist_h = stride; a.ist_w = stride; a.ioff_h = -pad; a.ioff_w = -pad; a.tstep_h = 1; a.tstep_w = 1;
+  a.OH = P; a.OW = Q; a.ost_h = 1; a.ost_w = 1; a.ooff_h = 0; a.ooff_w = 0;
+  a.M = N * P * Q;
+  pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, 64, cur_stream());
+  launched("gconv_fwd");
+  PDT_BCOUNT("gconv_fwd");
+}
+
+// backward data of slice j (phases and their derived-weight offsets as conv_dgrad), optionally with the fused
+// reduce of the BatchNorm + ReLU that produced the conv's input (bnb 1: y1 / coef1 / slots of the full width)
+void gconv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, int64_t N, int64_t P, int64_t Q, int64_t width,
+                 int64_t H, int64_t W, int64_t stride, const std::vector<std::vector<int64_t>>& phases, int64_t j,
+                 int64_t bm, int64_t bn, const OptT& bn_y1, const OptT& bn_coef1, const OptT& bn_slots) {
+  const int dt = dt16(dy, "dy");
+  const int64_t S = kGSlice;
+  TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "gconv_dgrad: mixed dtypes");
+  TORCH_CHECK(width % S == 0 && j >= 0 && j < width / S, "gconv_dgrad: bad slice");
+  TORCH_CHECK(dy.numel() == N * P * Q * width && dx.numel() == N * H * W * width, "gconv_dgrad: size mismatch");
+  TORCH_CHECK(dy.numel() < (int64_t(1) << 30) && dx.numel() < (int64_t(1) << 30), "gconv_dgrad: operands exceed 2 GiB");
+  TORCH_CHECK(!phases.empty() && phases.size() <= 4 && S % bn == 0, "gconv_dgrad: 1..4 phases / tile");
+  pdt::ConvFwdArgs a{};
+  a.x = p16(dy, "dy") + j * S;
+  a.w = p16(wt, "wt");
+  a.y = p16(dx, "dx") + j * S;
+  a.N = N; a.H = P; a.W = Q; a.C = S; a.cs = width; a.Kout = S; a.ldy = (int)width;
+  a.ist_h = 1; a.ist_w = 1; a.tstep_h = -1; a.tstep_w = -1;
+  a.OH = H; a.OW = W; a.ost_h = stride; a.ost_w = stride;
+  a.nphase = (int)phases.size();
+  a.res_phase = -1;
+  int64_t maxM = 0;
+  for (size_t i = 0; i < phases.size(); ++i) {
+    const auto& f = phases[i];
+    TORCH_CHECK(f.size() == 7, "gconv_dgrad: phase = (ph, pw, T, U, ioff_h, ioff_w, woff)");
+    const int64_t ph = f[0], pw = f[1];
+    const int64_t Pm = (H - ph + stride - 1) / stride, Qm = (W - pw + stride - 1) / stride;
+    TORCH_CHECK(Pm > 0 && Qm > 0 && f[6] + S * f[2] * f[3] * S <= wt.numel(), "gconv_dgrad: bad phase");
+    a.pooff_h[i] = (int)ph; a.pooff_w[i] = (int)pw; a.pT[i] = (int)f[2]; a.pU[i] = (int)f[3];
+    a.pioff_h[i] = (int)f[4]; a.pioff_w[i] = (int)f[5]; a.pwoff[i] = f[6];
+    a.pPm[i] = (int)Pm; a.pQm[i] = (int)Qm;
+    maxM = std::max(maxM, N * Pm * Qm);
+  }
+  TORCH_CHECK(maxM < (int64_t(1) << 31), "gconv_dgrad: 32-bit pixel indexing");
+  a.M = maxM;
+  if (bn_y1.has_value()) {  // bnb 1: ReLU mask from y1 and the forward coefficients; dx holds dz
+    TORCH_CHECK(bn_coef1.has_value() && bn_slots.has_value() && bn_y1->numel() == dx.numel() &&
+                    dt16(*bn_y1, "bn_y1") == dt && bn_coef1->numel() >= 4 * width &&
+                    bn_slots->numel() >= pdt::kStatSlots * width * 2,
+                "gconv_dgrad: bnb needs y1 / coef1 (4 x width) / slots of the full width");
+    a.bnb = 1;
+    a.bn_y1 = p16(*bn_y1, "bn_y1") + j * S;
+    a.bn_coef1 = pf(*bn_coef1, "bn_coef1") + j * S;
+    a.coef_ld = (int)width;
+    a.stats = pd(*bn_slots, "bn_slots") + j * S * 2;
+    a.stats_ld = (int)(width * 2);
+  }
+  pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, 64, cur_stream());
+  launched("gconv_dgrad");
+  PDT_BCOUNT("gconv_dgrad");
+}
+
+// weight gradient of slice j: the dense S x (R*R*S) partials [splits][S][ldw] (the executor keeps the diagonal blocks)
+void gconv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t width,
+                 int64_t R, int64_t P, int64_t Q, int64_t stride, int64_t pad, int64_t j, int64_t ldw, int64_t splits,
+                 int64_t pix_per_split) {
+  const int dt = dt16(x, "x");
+  const int64_t S = kGSlice;
+  TORCH_CHECK(dt16(dy, "dy") == dt, "gconv_wgrad: mixed dtypes");
+  TORCH_CHECK(width % S == 0 && j >= 0 && j < width / S, "gconv_wgrad: bad slice");
+  TORCH_CHECK(x.numel() == N * H * W * width && dy.numel() == N * P * Q * width, "gconv_wgrad: size mismatch");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30), "gconv_wgrad: operands exceed 2 GiB");
+  TORCH_CHECK(ldw >= R * R * S && ws.numel() >= splits * S * ldw, "gconv_wgrad: workspace too small");
+  pdt::ConvWgradArgs a{};
+  a.x = p16(x, "x") + j * S;
+  a.dy = p16(dy, "dy") + j * S;
+  a.ws = pf(ws, "ws");
+  a.N = N; a.H = H; a.W = W; a.C = S; a.Kout = S; a.T = R; a.U = R; a.Pm = P; a.Qm = Q;
+  a.stride_h = stride; a.stride_w = stride; a.pad_h = pad; a.pad_w = pad; a.dil_h = 1; a.dil_w = 1;
+  a.P = N * P * Q; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
+  a.cs = width; a.ldy = (int)width; a.win = 0;
+  a.tile = pdt::wgrad_tile((int)S, (int)S, 0);
+  TORCH_CHECK(a.tile == 64 && pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "gconv_wgrad: bad plan");
+  pdt::conv_wgrad_launch(a, dt, cur_stream());
+  launched("gconv_wgrad");
+  PDT_BCOUNT("gconv_wgrad");
+}
+
 // ResNet stem weight gradient with its dY computed in-kernel (max-pool backward + ReLU mask + BN-backward
 // apply from the pooled gradient dp, the argmax idx, the conv output y0 and the BN coefficients): the
 // window-mode conv_wgrad above without the [P][64] dY tensor.  x: padded NHWC4 image [N][Hp][Wp][4].
@@ -1206,6 +1328,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_c64_mode", [](int64_t set) { return (int64_t)pdt::conv1x1_c64_mode((int)set); });
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_wgrad_stem_fused", &conv_wgrad_stem_fused);
+  m.def("gconv_fwd", &gconv_fwd);
+  m.def("gconv_dgrad", &gconv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("P"),
+        py::arg("Q"), py::arg("width"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("phases"), py::arg("j"),
+        py::arg("bm"), py::arg("bn"), py::arg("bn_y1") = py::none(), py::arg("bn_coef1") = py::none(),
+        py::arg("bn_slots") = py::none());
+  m.def("gconv_wgrad", &gconv_wgrad);
+  m.def("gconv_slice", []() { return kGSlice; });
   m.def("wgrad_reduce", &wgrad_reduce);
   m.def("wgrad_blocks_3x3c64", &wgrad_blocks_3x3c64);
   m.def("wgrad_3x3c64_supported", &wgrad_3x3c64_supported);

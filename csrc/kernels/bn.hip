@@ -23,7 +23,7 @@ namespace pdt {
 // LDS in a fixed order.  (R grows with the conv's M tiles -- ~30k rows x 256 channels for a ResNet-50 layer1
 // conv -- so the reduction must stream at HBM rate, not walk 64 long dependent chains.)
 __global__ __launch_bounds__(256) void stat_rows_reduce_kernel(const float* __restrict__ rows, int R, int CK,
-                                                               double* __restrict__ slots) {
+                                                               double* __restrict__ slots, int LD) {
   __shared__ double part[3][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63), lane4 = threadIdx.x >> 6;
   const int s = blockIdx.y;
@@ -45,11 +45,13 @@ __global__ __launch_bounds__(256) void stat_rows_reduce_kernel(const float* __re
   if (lane4 > 0) part[lane4 - 1][threadIdx.x & 63] = a;
   __syncthreads();
   if (lane4 == 0 && col < CK)
-    slots[(int64_t)s * CK + col] = ((a + part[0][threadIdx.x]) + part[1][threadIdx.x]) + part[2][threadIdx.x];
+    slots[(int64_t)s * LD + col] = ((a + part[0][threadIdx.x]) + part[1][threadIdx.x]) + part[2][threadIdx.x];
 }
 
-void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s) {
-  hipLaunchKernelGGL(stat_rows_reduce_kernel, dim3((CK + 63) / 64, kStatSlots), dim3(256), 0, s, rows, R, CK, slots);
+// slots_ld: row stride of the slots (0 = CK; a channel slice of a wider tensor's statistics: the wider row)
+void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s, int slots_ld) {
+  hipLaunchKernelGGL(stat_rows_reduce_kernel, dim3((CK + 63) / 64, kStatSlots), dim3(256), 0, s, rows, R, CK, slots,
+                     slots_ld ? slots_ld : CK);
 }
 
 // slots [kStatSlots][C][K] double (the fixed-order row sums of stat_rows_reduce)

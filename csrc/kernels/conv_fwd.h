@@ -13,7 +13,7 @@ constexpr int kStatSlots = 64;  // slot copies of per-channel statistics accumul
 // stat_rows_reduce sums the rows in a FIXED order (slot s <- contiguous row range s*R/64.., fp64)
 // into slots[kStatSlots][CK], the layout the finalize kernels and the SyncBN all-reduce read.  Every slot
 // is written, so the slots need no zeroing.
-void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s);
+void stat_rows_reduce_launch(const float* rows, int R, int CK, double* slots, hipStream_t s, int slots_ld = 0);
 
 
 // Generalised implicit-GEMM convolution (see conv_fwd.hip for the geometry contract).
@@ -55,6 +55,12 @@ struct ConvFwdArgs {
   // pre_coef != nullptr: x is the RAW output of a producer conv and the kernel applies that BatchNorm + ReLU
   // (scale[C] | shift[C]) to the staged input tile itself (conv_l1 forward only; zero padding stays zero)
   const float* pre_coef = nullptr;
+  // Channel slices of wider tensors (grouped convolution, models/executor.py): output pixel stride ``ldy`` (y, res,
+  // bn_y1/bn_y2 and the ReLU mask are [pixels][ldy] with this conv's Kout channels at the caller's pointer offset),
+  // stride ``coef_ld`` of the bn_coef1/bn_coef2 quantity rows, and row stride ``stats_ld`` of the fp64 statistics
+  // slots ([kStatSlots][stats_ld]); 0 = Kout / Kout / Kout * quantities (dense tensors).  The input's pixel stride
+  // is ``cs``.
+  int ldy = 0, coef_ld = 0, stats_ld = 0;
   int pT[4], pU[4], pioff_h[4], pioff_w[4], pPm[4], pQm[4], pooff_h[4], pooff_w[4], pmt[4];
   int64_t pwoff[4];
   uint32_t ppq_mul[4], ppq_shift[4], pq1_mul[4], pq1_shift[4];

@@ -76,16 +76,18 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
   // Layout [quantity][BN]: 0 scale, 1 shift, 2 mean, 3 invstd (branch 1); 4 mean, 5 invstd (branch 2).
   constexpr int RED_BYTES = WAVES_M * BN * 3 * 4;
   float* cf = (float*)(smem + RED_BYTES);
+  const int64_t LDY = a.ldy ? a.ldy : a.Kout;  // output pixel stride (channel slices of a wider tensor)
   if constexpr (EPI >= 2) {
+    const int CL = a.coef_ld ? a.coef_ld : a.Kout;
     for (int c = tid; c < BN; c += NW_ * 64) {
       const int n = n0 + c;
       cf[0 * BN + c] = a.bn_coef1[n];
-      cf[1 * BN + c] = a.bn_coef1[a.Kout + n];
-      cf[2 * BN + c] = a.bn_coef1[2 * a.Kout + n];
-      cf[3 * BN + c] = a.bn_coef1[3 * a.Kout + n];
+      cf[1 * BN + c] = a.bn_coef1[CL + n];
+      cf[2 * BN + c] = a.bn_coef1[2 * CL + n];
+      cf[3 * BN + c] = a.bn_coef1[3 * CL + n];
       if constexpr (EPI == 4) {
-        cf[4 * BN + c] = a.bn_coef2[2 * a.Kout + n];
-        cf[5 * BN + c] = a.bn_coef2[3 * a.Kout + n];
+        cf[4 * BN + c] = a.bn_coef2[2 * CL + n];
+        cf[5 * BN + c] = a.bn_coef2[3 * CL + n];
       }
     }
     __syncthreads();
@@ -139,7 +141,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
         const int rem = mm - nimg * PQ;
         const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
         const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
-        const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout + n0 + ch * 8;
+        const int64_t ob = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * LDY + n0 + ch * 8;
         *(uint4*)(a.y + ob) = *(const uint4*)(stg + row * SPITCH + ch * 16);
       }
     }
@@ -168,8 +170,8 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
       const int rem = mm - nimg * PQ;
       const int i_ = (int)fdiv((uint32_t)rem, fd_q), j_ = rem - i_ * a.Qm;
       const int oh = i_ * a.ost_h + a.ooff_h, ow = j_ * a.ost_w + a.ooff_w;
-      obase[jj] = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * a.Kout;
-      if constexpr (RC) rbase[jj] = (uint32_t)mm * (uint32_t)a.Kout;
+      obase[jj] = (((int64_t)nimg * a.OH + oh) * a.OW + ow) * LDY;
+      if constexpr (RC) rbase[jj] = (uint32_t)mm * (uint32_t)LDY;
     }
     uint2 p_res[RES ? JC : 1][RES ? FN : 1], p_y1[LY1 ? JC : 1][LY1 ? FN : 1], p_y2[LY2 ? JC : 1][LY2 ? FN : 1];
     uint64_t p_m[LM ? JC : 1][MW];
@@ -894,7 +896,7 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
   Scratch part(a.stats ? (size_t)srows * a.Kout * KO * sizeof(float) : 0, s);
   a.srows = part.as<float>();
   launch_tile<DT>(a, bm, bn, bk, s);
-  if (a.stats) stat_rows_reduce_launch(a.srows, srows, a.Kout * KO, a.stats, s);
+  if (a.stats) stat_rows_reduce_launch(a.srows, srows, a.Kout * KO, a.stats, s, a.stats_ld);
 }
 
 template <int DT>
@@ -942,11 +944,12 @@ static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_
   PDT_CFG(256, 64, 32, 1, 3)
   PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
-  if (bk == 64 && bm == 256 && bn == 256 && a.C % 64 == 0) {
+  const bool sliced = (a.ldy && a.ldy != a.Kout) || a.cs != a.C;
+  if (bk == 64 && bm == 256 && bn == 256 && a.C % 64 == 0 && !sliced) {
     launch_pp<DT, 256, 256>(a, s);
     return;
   }
-  if (bk == 64 && bm == 512 && bn == 128 && a.C % 64 == 0) {
+  if (bk == 64 && bm == 512 && bn == 128 && a.C % 64 == 0 && !sliced) {
     launch_pp<DT, 512, 128>(a, s);
     return;
   }

@@ -794,6 +794,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
 bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
   // H % 4 == 0: whole 4-row tiles only (the epilogue has no per-pixel range checks; see conv_l1_kernel)
   if (a.C != 64 || a.Kout != 64 || a.cs != 64 || a.W != kW || a.OW != kW || a.bnb == 3 || a.H % 4 != 0) return false;
+  if ((a.ldy && a.ldy != a.Kout) || (a.coef_ld && a.coef_ld != a.Kout) || a.stats_ld) return false;  // slices
   if (a.nphase == 0) {
     if (a.T == 3 && a.U == 3 && a.ist_h == 1 && a.ist_w == 1 && a.ioff_h == -1 && a.ioff_w == -1 &&
         a.tstep_h == 1 && a.tstep_w == 1 && a.ost_h == 1 && a.ost_w == 1 && a.ooff_h == 0 && a.ooff_w == 0 &&

@@ -47,7 +47,7 @@ PDT_DEVICE void wgrad_rows(const ConvWgradArgs& a, int p, int th, int tw, int xc
     const uint32_t off = (uint32_t)((((nimg * a.H + h) * a.W + w) * a.cs + xcol + lch * 8) * 2);
     xoff = ok ? off : kOOB;
   }
-  yoff = (uint32_t)(p * a.Kout + ycol + lch * 8) * 2u;
+  yoff = (uint32_t)(p * (a.ldy ? a.ldy : a.Kout) + ycol + lch * 8) * 2u;
 }
 
 // WIN: the ResNet stem's "window" mode.  X is the zero-padded NHWC4 image and a 64-wide tile column
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
 
   const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * (a.ldy ? a.ldy : a.Kout) * 2u);
 
   // DMA lane geometry: 8 rows x 8 chunks per 1 KiB instruction
   const int lrow = lane >> 3, pch = lane & 7;
@@ -1149,7 +1149,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_pp_kernel(ConvWgradArgs a) {
   const int nsteps = (pix_end - pix_begin + BKP - 1) / BKP;
   const int th = t * a.dil_h - a.pad_h, tw = u * a.dil_w - a.pad_w;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * (a.ldy ? a.ldy : a.Kout) * 2u);
 
   // DMA lane geometry: 4 pixel rows x 16 chunks per 1 KiB instruction, 2 instructions per wave per half
   const int lrow = lane >> 4, pch = lane & 15;
@@ -1650,6 +1650,9 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
 
 void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   ConvWgradArgs a = args;
+  if (a.ldy && a.ldy != a.Kout && (a.tile != 64 || a.win))
+    pdt_hip_fail("conv_wgrad: a strided dY (channel slice) runs on the 64x64 tile only", hipErrorInvalidValue,
+                 __FILE__, __LINE__);
   const int nwg = (a.Kout / wgrad_ktile(a)) * wgrad_ctiles(a) * a.splits;
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);

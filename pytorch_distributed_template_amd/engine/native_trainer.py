@@ -98,6 +98,11 @@ class NativeTrainer:
         # validates without autocast, `distributed_syncBN_amp.py:311-317`), whatever the training dtype
         self._eval32 = None
         self._eval32_at = -1  # optimizer step count its derived layouts were gathered at
+        if eval_fp32 and dtype != torch.float32 and getattr(model, "groups", 1) > 1:
+            # grouped convs (ResNeXt) have no fp32 native kernels: validate in the training dtype
+            import warnings
+            warnings.warn("--eval-precision fp32: no native fp32 grouped convolution; validating in the compute dtype")
+            eval_fp32 = False
         if eval_fp32 and dtype != torch.float32:
             from ..models.executor32 import ResNetExecutor32
             self._eval32 = ResNetExecutor32(model, self.flat, self.device)

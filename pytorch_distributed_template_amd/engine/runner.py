@@ -37,7 +37,10 @@ from ..utils.meters import AverageMeter, get_learning_rate
 from ..utils.profiling import roctx_range
 from ..utils.tensorboard import SummaryWriter
 
-NATIVE_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2")
+NATIVE_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2",
+                "resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d")
+# grouped-conv archs: 16-bit executor only (models/executor.py channel slices); fp32 runs them on the torch engine
+NATIVE_ARCHS_16BIT_ONLY = ("resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d")
 
 
 def seed_everything(seed: int) -> None:
@@ -64,6 +67,8 @@ def resolve_engine(args, device: torch.device, dtype: torch.dtype) -> str:
     e = args.engine
     native_ok = device.type == "cuda" and args.arch in NATIVE_ARCHS and dtype in (torch.bfloat16, torch.float16,
                                                                                   torch.float32)
+    if args.arch in NATIVE_ARCHS_16BIT_ONLY and dtype == torch.float32:
+        native_ok = False
     if e == "auto":
         return "native" if native_ok else "torch"
     if e == "native" and not native_ok:

@@ -20,6 +20,7 @@ weights and gradients.  Reference call sites mirror
 """
 from __future__ import annotations
 
+import json
 import os
 
 from typing import Callable, Dict, List, Optional, Tuple
@@ -53,10 +54,14 @@ _TUNED = _load_tuned()
 class _Conv:
     """Static description of one convolution and its derived (dgrad) weight layouts."""
 
-    def __init__(self, conv: nn.Conv2d, flat, derived_maps: List[torch.Tensor], derived_off: List[int]):
-        assert conv.groups == 1 and conv.dilation == (1, 1), "native executor: groups/dilation unsupported"
+    def __init__(self, conv: nn.Conv2d, flat, derived_maps: List[torch.Tensor], derived_off: List[int],
+                 fwd_maps: Optional[list] = None):
+        """``fwd_maps``: grouped convs append (conv, map) pairs of their FORWARD weight layouts here; the executor
+        places those where the forward-read layouts are gathered (update_derived)."""
+        assert conv.dilation == (1, 1), "native executor: dilation unsupported"
         self.mod = conv
         self.cin, self.cout = conv.in_channels, conv.out_channels
+        self.groups = conv.groups
         self.R, self.S = conv.kernel_size
         self.st = conv.stride[0]
         self.pad = conv.padding[0]
@@ -65,11 +70,49 @@ class _Conv:
         self.pid = self.slot.index
         self.phases = []  # (ph, pw, T, U, ioff_h, ioff_w, derived offset, derived numel)
         base = self.slot.offset
+        if self.groups > 1:
+            self._init_grouped(base, derived_maps, derived_off, fwd_maps)
+            return
         for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(self.R, self.S, self.st, self.pad):
             m = (base + dgrad_weight_index(self.cout, self.cin, self.R, self.S, rs, ss)).to(torch.int32)
             self.phases.append((ph, pw, len(rs), len(ss), ioff_h, ioff_w, derived_off[0], m.numel()))
             derived_maps.append(m)
             derived_off[0] += m.numel()
+
+    GSLICE = 64  # channel slice of the grouped convolutions (csrc/bindings.cpp gconv_*)
+
+    def _init_grouped(self, base: int, derived_maps, derived_off, fwd_maps) -> None:
+        """Grouped conv (ResNeXt) as width / 64 dense channel slices with block-diagonal weights: per slice j the
+        forward layout [64][R][S][64] and the backward-data phase layouts, gathered from the grouped parameter
+        [cout][R][S][cg] (zeros off the diagonal blocks); the weight gradient keeps the diagonal blocks of the dense
+        slice gradients (``gidx``)."""
+        G, cg, S_, R, S = self.groups, self.cin // self.groups, self.GSLICE, self.R, self.S
+        if not (self.cin == self.cout and self.cin % S_ == 0 and S_ % cg == 0):
+            raise NotImplementedError(f"native executor: grouped conv {self.cin}->{self.cout} / {G} groups needs "
+                                      "equal widths, width % 64 == 0 and 64 % (channels per group) == 0")
+        self.cg, self.nslice = cg, self.cin // S_
+        k = torch.arange(S_).view(-1, 1, 1, 1)
+        t = torch.arange(R).view(1, -1, 1, 1)
+        u = torch.arange(S).view(1, 1, -1, 1)
+        c = torch.arange(S_).view(1, 1, 1, -1)
+        self.gfwd = []     # per slice: (derived offset) of its forward layout, filled by the executor
+        self.gphases = []  # per slice: list of phases (ph, pw, T, U, ioff_h, ioff_w, derived offset)
+        for j in range(self.nslice):
+            src = base + (((j * S_ + k) * R + t) * S + u) * cg + c % cg
+            dense = torch.where(k // cg == c // cg, src, torch.full_like(src, -1)).reshape(-1)
+            fwd_maps.append((self, j, dense.to(torch.int32)))
+            ph_list = []
+            for ph, pw, rs, ss, ioff_h, ioff_w in dgrad_phases(R, S, self.st, self.pad):
+                m = dense[dgrad_weight_index(S_, S_, R, S, rs, ss)].to(torch.int32)
+                ph_list.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, derived_off[0]])
+                derived_maps.append(m)
+                derived_off[0] += m.numel()
+            self.gphases.append(ph_list)
+        # weight gradient: grouped [cout][R][S][cg] <- dense slice partials [nslice][64][R*S*64]
+        kk = torch.arange(self.cout).view(-1, 1, 1, 1)
+        cl = torch.arange(cg).view(1, 1, 1, -1)
+        jj, kl = kk // S_, kk % S_
+        self.gidx = ((jj * S_ + kl) * (R * S * S_) + (t * S + u) * S_ + (kl // cg) * cg + cl).reshape(-1).to(torch.int32)
 
     def out_hw(self, H: int, W: int) -> Tuple[int, int]:
         return (H + 2 * self.pad - self.R) // self.st + 1, (W + 2 * self.pad - self.S) // self.st + 1
@@ -104,8 +147,8 @@ class ResNetExecutor:
                  syncbn_allreduce_fwd: Optional[Callable[[torch.Tensor], None]] = None):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
-        if not isinstance(model, ResNet) or model.groups != 1:
-            raise NotImplementedError("native executor supports torchvision-style ResNets with groups=1")
+        if not isinstance(model, ResNet):
+            raise NotImplementedError("native executor supports torchvision-style ResNets / ResNeXts")
         self.C = native.C
         self.n_slots = self.C.stat_slots()
         self.model = model
@@ -172,9 +215,10 @@ class ResNetExecutor:
         self._tiles: Dict[tuple, Tuple[int, int]] = {}
         derived_maps: List[torch.Tensor] = []
         off = [0]
+        gfwd_maps: list = []  # forward layouts of the grouped convs (gathered with the stem / fc ones, see below)
 
         def conv(c):
-            return _Conv(c, flat, derived_maps, off)
+            return _Conv(c, flat, derived_maps, off, gfwd_maps)
 
         self.stem = conv(model.conv1)
         self.stem_bn = _BN(model.bn1, flat, self.device)
@@ -210,6 +254,12 @@ class ResNetExecutor:
         self.stem_w_off = off[0]
         derived_maps.append(m.reshape(-1).to(torch.int32))
         off[0] += m.numel()
+        # grouped convs' forward layouts right behind the stem's: inside the range update_derived gathers on the
+        # compute stream ahead of the forward
+        for gc, j, gm in gfwd_maps:
+            gc.gfwd.append(off[0])
+            derived_maps.append(gm)
+            off[0] += gm.numel()
         # stem weight-gradient scatter: [Cout][R/2 pairs][2][32] (wgrad window tile) -> KRSC [Cout][R][S][Cin]
         kk = torch.arange(st.cout).view(-1, 1, 1, 1)
         rr = torch.arange(st.R).view(1, -1, 1, 1)
@@ -235,6 +285,10 @@ class ResNetExecutor:
         off[0] += mt.numel()
         self.derived_idx = torch.cat([m.to(torch.int32) for m in derived_maps]).to(self.device)
         self.derived = torch.zeros(off[0], dtype=dtype, device=self.device)
+        for b in self.blocks:
+            for c in b["convs"]:
+                if c.groups > 1:
+                    c.gidx = c.gidx.to(self.device)
         self._bufs: Dict[Tuple, torch.Tensor] = {}
         self._plans: Dict[Tuple, Tuple[int, int]] = {}
         from ..ops import validate
@@ -348,13 +402,16 @@ class ResNetExecutor:
     def _pre_ok(self, nxt: _Conv, N: int, H: int, W: int, train: bool) -> bool:
         """Can ``nxt`` (the conv consuming a block-internal BN + ReLU) apply that BN itself (conv_fwd_pre +
         the fused layer1 weight gradient)?"""
-        return (self.fuse_pre and train and self.wgrad_l1 and hasattr(self.C, "conv_fwd_pre") and nxt.R == 3 and nxt.S == 3 and nxt.st == 1 and
+        return (self.fuse_pre and train and self.wgrad_l1 and hasattr(self.C, "conv_fwd_pre") and nxt.groups == 1 and
+                nxt.R == 3 and nxt.S == 3 and nxt.st == 1 and
                 nxt.pad == 1 and nxt.cin == 64 and nxt.cout == 64 and self.C.conv_fwd_pre_supported(N, H, W) and
                 self.C.wgrad_3x3c64_supported(64, 64, 3, 3, W, 1, 1))
 
     def conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, w=None, cin=None, R=None, S=None, st=None, pad=None,
                  pre=None, stats_tag=None, fin: Optional[_BN] = None):
         """``fin``: the BatchNorm consuming y -- its training finalize is launched right behind the conv."""
+        if c.groups > 1:
+            return self._gconv_fwd(c, x, N, H, W, y, stats, stats_tag, fin)
         if pre is not None:  # x is the producer conv's raw output; pre = its BN coefficients (layer1 only)
             key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
             sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
@@ -397,6 +454,58 @@ class ResNetExecutor:
             self.bn_train_finalize(fin, sp, 0, M)
         return P, Q, sp, M
 
+    def _gconv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, stats_tag, fin):
+        """Grouped conv forward: one launch per 64-channel slice (block-diagonal dense weights, strided operands);
+        the slices' BN statistics land in their channel ranges of ONE statistics buffer."""
+        P, Q = c.out_hw(H, W)
+        sp = None
+        if stats:
+            key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
+            sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
+        bm, bn = _conv_tile(c.GSLICE, c.GSLICE * c.R * c.S)
+        n = c.GSLICE * c.R * c.S * c.GSLICE
+        for j in range(c.nslice):
+            o = c.gfwd[j]
+            self.C.gconv_fwd(x, self.derived[o:o + n], y, sp, N, H, W, c.cout, c.R, c.st, c.pad, P, Q, j, bm, bn)
+        if stats and fin is not None:
+            self.bn_train_finalize(fin, sp, 0, N * P * Q)
+        return P, Q, sp, N * P * Q
+
+    def _gconv_bwd(self, c: _Conv, x, N, H, W, dy, P, Q, dx, bnb, fin):
+        """Grouped conv backward: per 64-channel slice the dense weight-gradient partials (diagonal blocks gathered
+        into the grouped gradient) and the backward data with the producer BN's fused reduce (bnb mode 1)."""
+        def wg():
+            R, S, S_ = c.R, c.S, c.GSLICE
+            ldw = R * S * S_
+            key = (S_, R, S, S_, N * P * Q, False)
+            plan = self._plans.get(key)
+            if plan is None:
+                plan = tuple(self.C.conv_wgrad_plan(S_, R, S, S_, N * P * Q, self.wgrad_blocks, False))[:2]
+                self._plans[key] = plan
+            splits, pps = plan
+            ws = self._buf("ws", splits * S_ * ldw, torch.float32)
+            tmp = self._buf("gconv_dw", c.nslice * S_ * ldw, torch.float32)
+            for j in range(c.nslice):
+                self.C.gconv_wgrad(x, dy, ws, N, H, W, c.cin, R, P, Q, c.st, c.pad, j, ldw, splits, pps)
+                self.C.wgrad_reduce(ws, splits, S_, ldw, ldw, S_ * ldw, tmp[j * S_ * ldw:(j + 1) * S_ * ldw], ldw,
+                                    1.0, False)
+            self.C.gather32(tmp, c.gidx, self._g(c.slot))
+            self.grad_ready(c.pid)
+        self._side_wgrad((dy, x), wg)
+        if dx is None:
+            return
+        assert bnb is None or bnb[0] == 1, "grouped conv backward-data: inner-BN epilogue only"
+        bm, bn = _conv_tile(c.GSLICE, c.GSLICE * c.R * c.S)
+        for j in range(c.nslice):
+            phases = [p for p in c.gphases[j] if H - p[0] > 0 and W - p[1] > 0]
+            if bnb is None:
+                self.C.gconv_dgrad(dy, self.derived, dx, N, P, Q, c.cin, H, W, c.st, phases, j, bm, bn)
+            else:
+                self.C.gconv_dgrad(dy, self.derived, dx, N, P, Q, c.cin, H, W, c.st, phases, j, bm, bn,
+                                   bn_y1=bnb[1], bn_coef1=bnb[2], bn_slots=bnb[6])
+        if fin is not None and bnb is not None:
+            self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2])
+
     # per-shape tile choice: the static table (ops.conv.conv_tile), or -- with autotune on, the analogue of
     # the reference's cudnn.benchmark=True (`distributed.py:104`) -- the fastest candidate timed once per shape
     _CANDIDATES = ((128, 128), (256, 64), (128, 64), (64, 128), (256, 128), (256, 256), (512, 128))
@@ -421,6 +530,10 @@ class ResNetExecutor:
                 if best is None or ms < best[0]:
                     best = (ms, (bm, bn))
             choice = best[1]
+            dump = os.environ.get("PDT_AUTOTUNE_DUMP")  # tuned-table candidates: shapes where the static rule lost
+            if dump and choice != _conv_tile(n_dim, kdim if bk == 64 else 0):
+                with open(dump, "a") as f:
+                    f.write(json.dumps([list(key), list(choice)]) + "\n")
         self._tiles[key] = choice
         return choice
 
@@ -467,6 +580,9 @@ class ResNetExecutor:
         ``compact``: a 1x1 strided conv's data gradient written only on its nonzero phase (0, 0), as a dense
         [N, P, Q, Cin] tensor -- a stride-1 GEMM over the P x Q pixels (the zeros of the other phases are
         neither written nor re-read by the consumer)."""
+        if c.groups > 1:
+            assert res is None and res_phase < 0 and not compact and pre is None and wgrad_geom is None
+            return self._gconv_bwd(c, x, N, H, W, dy, P, Q, dx, bnb, fin)
         # --- wgrad
         if wgrad_geom is None:
             xg, Hx, Wx, Cx, R, S, st, pad = x, H, W, c.cin, c.R, c.S, c.st, c.pad

@@ -892,3 +892,93 @@ def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
         xh = ((yb.float() - cb[512:768]) * cb[768:]).double().view(-1, 256)
         assert torch.allclose(s1[:, k - 1], d.sum(0), rtol=1e-4, atol=1e-2)
         assert torch.allclose(s1[:, k], (d * xh).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("width,groups,stride,H", [(128, 32, 1, 14), (256, 32, 2, 14), (128, 2, 1, 9),
+                                                   (256, 64, 2, 8)])
+def test_grouped_conv_slices_match_torch(width, groups, stride, H):
+    """ResNeXt grouped 3x3 conv on the channel-slice kernels (gconv_fwd / gconv_dgrad / gconv_wgrad: 64-channel
+    slices with block-diagonal weights, strided operands) vs fp32 torch F.conv2d(groups=...): forward with the BN
+    statistics of the slices in one buffer, backward data (stride-2: sub-pixel phases) with and without the fused
+    inner-BN reduce, and the weight gradient's diagonal blocks."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    C_ = native.C
+    torch.manual_seed(3)
+    N, W, R, pad, S = 2, H, 3, 1, 64
+    cg = width // groups
+    P, Q = conv.out_hw(H, W, R, R, stride, pad)
+    x = _rand16(N, H, W, width)
+    wg = _rand16(width, R, R, cg, scale=(1.0 / (cg * 9)) ** 0.5)  # grouped KRSC weight
+    # dense block-diagonal slice weights [nslice][64][R][R][64]
+    nsl = width // S
+    dense = torch.zeros(nsl, S, R, R, S, dtype=wg.dtype, device=DEV)
+    for j in range(nsl):
+        for k in range(S):
+            g0 = (k // cg) * cg
+            dense[j, k, :, :, g0:g0 + cg] = wg[j * S + k]
+    # forward + statistics
+    y = torch.full((N, P, Q, width), float("nan"), dtype=x.dtype, device=DEV)
+    st = torch.zeros(C_.stat_slots() * width * 2, dtype=torch.float64, device=DEV)
+    for j in range(nsl):
+        C_.gconv_fwd(x, dense[j].reshape(-1), y, st, N, H, W, width, R, stride, pad, P, Q, j, 256, 64)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wg.float().permute(0, 3, 1, 2), stride=stride, padding=pad,
+                   groups=groups).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2
+    s = st.view(-1, width, 2).sum(0)
+    yf = y.double().reshape(-1, width)
+    assert torch.allclose(s[:, 0], yf.sum(0), rtol=1e-6, atol=1e-3)
+    assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
+    # backward data: per slice the phase weights of the dense slice weight
+    dy = _rand16(N, P, Q, width)
+    derived, phases_of = [], []
+    off = 0
+    for j in range(nsl):
+        pl = []
+        flat_j = dense[j].reshape(-1)
+        for ph, pw, rs, ss, ioff_h, ioff_w in conv.dgrad_phases(R, R, stride, pad):
+            m = conv.dgrad_weight_index(S, S, R, R, rs, ss)
+            if m.numel() == 0 or H - ph <= 0 or W - pw <= 0:
+                continue
+            derived.append(flat_j[m.to(DEV)])
+            pl.append([ph, pw, len(rs), len(ss), ioff_h, ioff_w, off])
+            off += m.numel()
+        phases_of.append(pl)
+    derived = torch.cat(derived)
+    dx = torch.full((N, H, W, width), float("nan"), dtype=x.dtype, device=DEV)
+    for j in range(nsl):
+        C_.gconv_dgrad(dy, derived, dx, N, P, Q, width, H, W, stride, phases_of[j], j, 256, 64)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = wg.float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(xr, wr, stride=stride, padding=pad, groups=groups).backward(dy.float().permute(0, 3, 1, 2))
+    torch.cuda.synchronize()
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    # fused inner-BN reduce (mode 1): dz = dx * relu'(y1 * scale + shift), sums of dz and dz * xhat
+    y1 = _rand16(N, H, W, width)
+    coef = torch.cat([torch.rand(width, device=DEV) + 0.5, torch.randn(width, device=DEV) * 0.3,
+                      y1.float().view(-1, width).mean(0), torch.rand(width, device=DEV) + 0.5]).contiguous()
+    slots = torch.zeros(C_.stat_slots() * width * 2, dtype=torch.float64, device=DEV)
+    dz = torch.full_like(dx, float("nan"))
+    for j in range(nsl):
+        C_.gconv_dgrad(dy, derived, dz, N, P, Q, width, H, W, stride, phases_of[j], j, 256, 64, bn_y1=y1,
+                       bn_coef1=coef, bn_slots=slots)
+    torch.cuda.synchronize()
+    mask = (y1.float() * coef[:width] + coef[width:2 * width]) > 0
+    dz_ref = torch.where(mask, dx.float(), torch.zeros_like(dx.float()))
+    assert torch.equal(dz, dz_ref.to(dz.dtype))
+    sums = slots.view(-1, width, 2).sum(0)
+    xhat = (y1.float() - coef[2 * width:3 * width]) * coef[3 * width:]
+    assert torch.allclose(sums[:, 0].float(), dz.float().view(-1, width).sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sums[:, 1].float(), (dz.float() * xhat).view(-1, width).sum(0), rtol=1e-3, atol=1e-2)
+    # weight gradient: dense slice partials, diagonal blocks == the grouped weight gradient
+    splits, pps, _ = C_.conv_wgrad_plan(S, R, R, S, N * P * Q, 256, False)
+    ldw = R * R * S
+    ws = torch.full((splits * S * ldw,), float("nan"), device=DEV)
+    dwd = torch.empty(nsl, S, ldw, device=DEV)
+    for j in range(nsl):
+        C_.gconv_wgrad(x, dy, ws, N, H, W, width, R, P, Q, stride, pad, j, ldw, splits, pps)
+        C_.wgrad_reduce(ws, splits, S, ldw, ldw, S * ldw, dwd[j].view(-1), ldw, 1.0, False)
+    torch.cuda.synchronize()
+    dwd = dwd.view(nsl, S, R, R, S)
+    got = torch.stack([dwd[j, k, :, :, (k // cg) * cg:(k // cg) * cg + cg] for j in range(nsl) for k in range(S)])
+    assert _rel(got, wr.grad.permute(0, 2, 3, 1)) < 1e-2

@@ -10,8 +10,11 @@ sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
 from test_executor_gpu import _relnorm, _setup  # noqa: E402
 
-for arch, N, seed in [("wide_resnet101_2", 2, 0), ("wide_resnet101_2", 2, 1), ("wide_resnet101_2", 4, 0),
-                      ("resnet152", 2, 0), ("wide_resnet50_2", 3, 0)]:
+CASES = [("wide_resnet101_2", 2, 0), ("wide_resnet101_2", 2, 1), ("wide_resnet101_2", 4, 0),
+         ("resnet152", 2, 0), ("wide_resnet50_2", 3, 0)]
+if len(sys.argv) > 1:  # arch:N:seed ...
+    CASES = [(a.split(":")[0], int(a.split(":")[1]), int(a.split(":")[2])) for a in sys.argv[1:]]
+for arch, N, seed in CASES:
     model, ref, flat, ex, x, t = _setup(arch, N=N, HW=224, dtype=torch.bfloat16, seed=seed)
     tb = copy.deepcopy(ref)
     logits, met = ex.train_step(x, t)
