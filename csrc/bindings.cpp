@@ -932,27 +932,9 @@ void scatter32(const Tensor& src, const Tensor& idx, Tensor& dst) {
 const float* pfc(const OptT& t, const char* name) { return t.has_value() ? pf(*t, name) : nullptr; }
 
 // forward conv over fp32 NHWC / KRSC (same geometry arguments as conv_fwd; stats -> fp64 slots)
-void conv32_fwd_impl(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N,
-                     int64_t H, int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm,
-                     int64_t stride, int64_t pad, int64_t bm, int64_t bn, const OptT& pre);
-
 void conv32_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N, int64_t H,
                 int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride,
                 int64_t pad, int64_t bm, int64_t bn) {
-  conv32_fwd_impl(x, w, y, res, stats, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, bm, bn, {});
-}
-
-// conv32_fwd over the RAW output of the producer conv: its BatchNorm + ReLU (pre = coef [scale | shift | ...] x C) is
-// applied to the activation fragments in the kernel (relu(bn(x)) is never written)
-void conv32_fwd_pre(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t N, int64_t H, int64_t W,
-                    int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad,
-                    int64_t bm, int64_t bn, const Tensor& pre) {
-  conv32_fwd_impl(x, w, y, {}, stats, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, bm, bn, pre);
-}
-
-void conv32_fwd_impl(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, const OptT& stats, int64_t N,
-                     int64_t H, int64_t W, int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm,
-                     int64_t stride, int64_t pad, int64_t bm, int64_t bn, const OptT& pre) {
   TORCH_CHECK(x.numel() == N * H * W * C && w.numel() == Kout * T * U * C && y.numel() == N * Pm * Qm * Kout,
               "conv32_fwd: size mismatch");
   TORCH_CHECK(C % 32 == 0 && Kout % bn == 0, "conv32_fwd: C % 32 / Kout % bn must be 0");
@@ -972,10 +954,6 @@ void conv32_fwd_impl(const Tensor& x, const Tensor& w, Tensor& y, const OptT& re
   a.ist_h = stride; a.ist_w = stride; a.ioff_h = -pad; a.ioff_w = -pad; a.tstep_h = 1; a.tstep_w = 1;
   a.OH = Pm; a.OW = Qm; a.ost_h = 1; a.ost_w = 1; a.ooff_h = 0; a.ooff_w = 0;
   a.M = N * Pm * Qm;
-  if (pre.has_value()) {
-    TORCH_CHECK(pre->numel() >= 2 * C, "conv32_fwd_pre: pre needs scale and shift for every input channel");
-    a.pre_coef = pf(*pre, "pre");
-  }
   pdt::conv32_launch(a, (int)bm, (int)bn, cur_stream());
   launched("conv32_launch");
 }
@@ -1036,27 +1014,9 @@ void conv32_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& re
   launched("conv32_launch");
 }
 
-void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                  int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw,
-                  int64_t splits, int64_t pix_per_split, int64_t tile, const OptT& pre);
-
 void wgrad32(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
              int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw, int64_t splits,
              int64_t pix_per_split, int64_t tile) {
-  wgrad32_impl(x, dy, ws, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, ldw, splits, pix_per_split, tile, {});
-}
-
-// wgrad32 with x the producer conv's raw output and its BatchNorm + ReLU (pre = coef) applied in the kernel
-// (tile 128 or 3 only)
-void wgrad32_pre(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                 int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw,
-                 int64_t splits, int64_t pix_per_split, int64_t tile, const Tensor& pre) {
-  wgrad32_impl(x, dy, ws, N, H, W, C, Kout, T, U, Pm, Qm, stride, pad, ldw, splits, pix_per_split, tile, pre);
-}
-
-void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                  int64_t Kout, int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride, int64_t pad, int64_t ldw,
-                  int64_t splits, int64_t pix_per_split, int64_t tile, const OptT& pre) {
   TORCH_CHECK(tile == 64 || tile == 128 || tile == 3, "wgrad32: tile must be 64, 128 or 3 (3x3 halo kernel)");
   const int64_t cb = tile == 3 ? 64 : tile;
   TORCH_CHECK(C % cb == 0 && Kout % cb == 0, "wgrad32: C and Kout must be multiples of the tile");
@@ -1075,10 +1035,6 @@ void wgrad32_impl(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int6
   a.N = N; a.H = H; a.W = W; a.C = C; a.Kout = Kout; a.T = T; a.U = U; a.Pm = Pm; a.Qm = Qm;
   a.stride = stride; a.pad = pad; a.ldw = ldw; a.splits = splits; a.pix_per_split = pix_per_split;
   a.P = N * Pm * Qm;
-  if (pre.has_value()) {
-    TORCH_CHECK(pre->numel() >= 2 * C && (tile == 128 || tile == 3), "wgrad32_pre: coef size / tile (128 or 3)");
-    a.pre_coef = pf(*pre, "pre");
-  }
   pdt::wgrad32_launch(a, cur_stream());
   launched("wgrad32_launch");
 }
@@ -1390,8 +1346,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_coef") = py::none(), py::arg("stats") = py::none(), py::arg("bn_y2") = py::none(),
         py::arg("bn_coef2") = py::none());
   m.def("wgrad32", &wgrad32);
-  m.def("wgrad32_pre", &wgrad32_pre);
-  m.def("conv32_fwd_pre", &conv32_fwd_pre);
   m.def("bn_apply32", &bn_apply32);
   m.def("bn_bwd_reduce32_blocks", &bn_bwd_reduce32_blocks);
   m.def("bn_bwd_reduce32", &bn_bwd_reduce32);

@@ -23,9 +23,6 @@ struct Conv32Args {
   // receive 4 quantities per channel: (sum dz, sum dz * xhat1, sum dz, sum dz * xhat2)
   const float* bn_y2 = nullptr;
   const float* bn_coef2 = nullptr;
-  // forward only: x is the RAW output of the producer conv; its BatchNorm + ReLU (scale[C] | shift[C]) is applied to
-  // every activation fragment as it is read (zero padding stays zero), so relu(bn(x)) is never written
-  const float* pre_coef = nullptr;
   float* srows;
   int srows_pp;
   int N, H, W, C, Kout, T, U;
@@ -60,9 +57,6 @@ struct Wgrad32Args {
   // are 8 pixels x 4 channels of row 2t (chunks 0..7) then of row 2t+1 (chunks 8..15 read element sc * 4 + pair_skip:
   // pair_skip = one padded row - 32)
   int cs = 0, pair_skip = 0, tstep = 1;
-  // 128-wide and 3x3-halo kernels: x is the producer conv's raw output, its BatchNorm + ReLU (scale[C] | shift[C]) is
-  // applied to the staged input elements as they are read (padding rows stay zero)
-  const float* pre_coef = nullptr;
   // 4-pair stem kernel only (f_y != nullptr): dY is not read but computed per staged chunk from the max-pool backward,
   // the ReLU mask and the BN-backward apply (the math of stem_pool_bwd_apply32): f_dp / f_idx pooled gradient and
   // argmax [N][f_OH][f_OW][64], f_y the conv output [P][64], f_coef the forward BN coefficients (scale | shift),

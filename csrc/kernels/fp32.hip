@@ -155,11 +155,7 @@ PDT_DEVICE void conv32_epilogue(const Conv32Args& a, f32x4_t (&acc)[BN / WAVES_N
 // the 4-wave tile does not get (52 % of fp32 MFMA peak, profiles/r2_fp32_path.md).  256 x 256 / 8 waves (and
 // 256 x 128 / 8 waves for 128-channel GEMMs) double / 1.3x that intensity; one 128 KB-LDS block per CU with two
 // waves per SIMD, each wave running 256 MFMAs (8192 cycles) per K-step behind the next stage's DMA.
-// PRE (forward): Conv32Args::pre_coef -- the activation fragments get relu(x * scale + shift) as they are read, with
-// the rows that fall into the image padding (zero-filled by the DMA) kept zero; C <= kPre32MaxC.
-constexpr int kPre32MaxC = 512;
-
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool RES, bool PRE = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool RES>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Args args) {
   Conv32Args a = args;
   if (args.nphase > 0) {  // multi-phase launch (strided backward-data): this block's phase geometry
@@ -189,7 +185,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
   constexpr int STAGE = (BN + BM) * ROWB;
   static_assert(A_INSTR * RPI * NW == BN && B_INSTR * RPI * NW == BM, "conv32 tile/instr mismatch");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-  __shared__ __attribute__((aligned(16))) float pre_s[PRE ? 2 * kPre32MaxC : 4];  // scale | shift
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -269,34 +264,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
   for (int j = 0; j < FM; ++j) b_off[j] = A_BYTES + (wm * WM + j * 16 + fr) * ROWB;
   const int sw = (fr >> 1) & 7;  // row swizzle: every fragment base is a multiple of 16 rows
 
-  // PRE: this lane's activation rows (pixel m0 + wm*WM + j*16 + fr): input position before the tap offset
-  int ph[PRE ? FM : 1], pw[PRE ? FM : 1];
-  if constexpr (PRE) {
-    for (int i = tid; i < 2 * a.C; i += 64 * NW) pre_s[i] = a.pre_coef[i];  // visible after the prologue barrier
-#pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const int64_t m = m0 + wm * WM + j * 16 + fr;
-      if (m < a.M) {
-        const int nimg = (int)fdiv((uint32_t)m, fd_pq);
-        const int rem = (int)m - nimg * PQ;
-        const int i = (int)fdiv((uint32_t)rem, fd_q), jj = rem - i * a.Qm;
-        ph[j] = i * a.ist_h + a.ioff_h;
-        pw[j] = jj * a.ist_w + a.ioff_w;
-      } else {
-        ph[j] = -(1 << 29);
-        pw[j] = 0;
-      }
-    }
-  }
-  int ct = 0, cu = 0, cc = 0;  // (tap, channel) of the stage being computed
-
   auto compute_stage = [&](const char* sb) {
-    const int dh = ct * a.tstep_h, dw = cu * a.tstep_w;
-    bool rok[PRE ? FM : 1];
-    if constexpr (PRE) {
-#pragma unroll
-      for (int j = 0; j < FM; ++j) rok[j] = (unsigned)(ph[j] + dh) < (unsigned)a.H && (unsigned)(pw[j] + dw) < (unsigned)a.W;
-    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       f32x4v af[FN], bfr[FM];
@@ -304,16 +272,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
       for (int i = 0; i < FN; ++i) af[i] = *(const f32x4v*)(sb + a_off[i] + (((kk * 4 + fq) ^ sw) << 4));
 #pragma unroll
       for (int j = 0; j < FM; ++j) bfr[j] = *(const f32x4v*)(sb + b_off[j] + (((kk * 4 + fq) ^ sw) << 4));
-      if constexpr (PRE) {  // channels cc + (kk*4 + fq)*4 .. +3 of every row fragment
-        const int ch = cc + (kk * 4 + fq) * 4;
-        const f32x4v s4 = *(const f32x4v*)(pre_s + ch), h4 = *(const f32x4v*)(pre_s + a.C + ch);
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-          const f32x4v v = bfr[j] * s4 + h4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bfr[j][e] = rok[j] ? fmaxf(v[e], 0.f) : 0.f;
-        }
-      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -331,11 +289,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
       const int cur = ks & 1;
       if (ks + 1 < ksteps) stage_load(cur ^ 1);
       compute_stage(smem + cur * STAGE);
-      cc += 32;  // the order of stage_load
-      if (cc == a.C) {
-        cc = 0;
-        if (++cu == a.U) { cu = 0; ++ct; }
-      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -356,7 +309,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv32_kernel(Conv32Ar
 // K order: chunk-major (chunk, tap), so the fp32 sums differ from conv32_kernel's (tap, chunk) order in rounding.
 constexpr int kHalo32Rows = 464;  // LDS rows of one halo chunk: ((W + 254) / W + 3) * (W + 2) <= 464 (W = 56: 8 x 58)
 
-template <int EPI, bool RES, bool PRE = false>
+template <int EPI, bool RES>
 __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
   Conv32Args a = args;
   if (args.nphase > 0) {  // single-phase (stride-1) backward-data launch: the phase's weights and tap offsets
@@ -373,7 +326,6 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
   constexpr int HI = (NHI + NW - 1) / NW;            // ... per wave
   static_assert(A_BYTES == NW * 1024, "one weight DMA instruction per wave");
   __shared__ __attribute__((aligned(1024))) char smem[OFF_Z + ROWB];
-  __shared__ __attribute__((aligned(16))) float pre_s[PRE ? 2 * 256 : 4];  // PRE (C <= 256): scale | shift
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -421,7 +373,7 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
 
   // per-lane output pixel geometry: halo base row and the pixel's row within its image
   const int fr = lane & 15, fq = lane >> 4;
-  int hb[FM], hin[FM], win[PRE ? FM : 1];
+  int hb[FM], hin[FM];
 #pragma unroll
   for (int j = 0; j < FM; ++j) {
     const int64_t m = m0 + wm * WM + j * 16 + fr;
@@ -430,15 +382,11 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
       const int nimg = (int)fdiv((uint32_t)m, fd_pq);
       hb[j] = (g - gA + 1) * W2 + ((int)m - g * Wd) + 1;
       hin[j] = g - nimg * a.H;
-      if constexpr (PRE) win[j] = (int)m - g * Wd;
     } else {  // past the end: any in-range LDS row (the result is not stored)
       hb[j] = W2 + 1;
       hin[j] = 0;
-      if constexpr (PRE) win[j] = 0;
     }
   }
-  if constexpr (PRE)
-    for (int i = tid; i < 2 * C; i += 512) pre_s[i] = a.pre_coef[i];  // visible after the prologue barrier
   int a_off[FN];
 #pragma unroll
   for (int i = 0; i < FN; ++i) a_off[i] = (wn * WN + i * 16 + fr) * ROWB;
@@ -450,19 +398,17 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf, int tap, int kc) {
+  auto compute = [&](int buf, int tap) {
     const int t = tap / 3, u = tap - 3 * t;
     const int dh = a.ioff_h + t * a.tstep_h, dw = a.ioff_w + u * a.tstep_w;
     const int delta = dh * W2 + dw;
     int bo[FM], bsw[FM];
-    bool rok[PRE ? FM : 1];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int hr = hb[j] + delta;
       const bool ok = (unsigned)(hin[j] + dh) < (unsigned)a.H;
       bo[j] = ok ? OFF_H + hr * ROWB : OFF_Z;
       bsw[j] = ok ? (hr >> 1) & 7 : 0;
-      if constexpr (PRE) rok[j] = ok && (unsigned)(win[j] + dw) < (unsigned)Wd;  // the halo's zero columns too
     }
     const char* sa = smem + buf * A_BYTES;
 #pragma unroll
@@ -472,16 +418,6 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
       for (int i = 0; i < FN; ++i) af[i] = *(const f32x4v*)(sa + a_off[i] + (((kk * 4 + fq) ^ sw) << 4));
 #pragma unroll
       for (int j = 0; j < FM; ++j) bfr[j] = *(const f32x4v*)(smem + bo[j] + (((kk * 4 + fq) ^ bsw[j]) << 4));
-      if constexpr (PRE) {
-        const int ch = kc * 32 + (kk * 4 + fq) * 4;
-        const f32x4v s4 = *(const f32x4v*)(pre_s + ch), h4 = *(const f32x4v*)(pre_s + C + ch);
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-          const f32x4v v = bfr[j] * s4 + h4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bfr[j][e] = rok[j] ? fmaxf(v[e], 0.f) : 0.f;
-        }
-      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -502,7 +438,7 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
     const int nkc = tap == 8 ? kc + 1 : kc, ntap = tap == 8 ? 0 : tap + 1;
     const bool more = nkc < nchunks;
     if (more) stage_w(nkc, ntap, (ks + 1) & 1);  // the other ring slot: its last reader passed the last barrier
-    compute(ks & 1, tap, kc);
+    compute(ks & 1, tap);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (more && nkc != kc) {  // next chunk: restage the halo once every wave is past its last read of it
@@ -584,19 +520,10 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
                  __FILE__, __LINE__);
   if (a.bnb) PDT_COUNT("conv32_dgrad_bn_reduce_epilogue");
   const int two = a.bn_y2 != nullptr;
-  const bool pre = a.pre_coef != nullptr;
-  if (pre) {
-    if (a.bnb || rs || a.nphase > 0 || (a.cs != 0 && a.cs != a.C) || a.C > (halo ? 256 : kPre32MaxC))
-      pdt_hip_fail("conv32: the fused producer BN + ReLU (pre_coef) is a forward-only prologue (no residual, C <= 512)",
-                   hipErrorInvalidValue, __FILE__, __LINE__);
-    PDT_COUNT("conv32_fwd_pre");
-  }
   if (halo) {
     PDT_COUNT("conv32_halo");
     dim3 grid(gx, 1), block(512);
-    if (pre && st) hipLaunchKernelGGL((conv32_halo_kernel<1, false, true>), grid, block, 0, s, a);
-    else if (pre) hipLaunchKernelGGL((conv32_halo_kernel<0, false, true>), grid, block, 0, s, a);
-    else if (a.bnb && two && rs) hipLaunchKernelGGL((conv32_halo_kernel<3, true>), grid, block, 0, s, a);
+    if (a.bnb && two && rs) hipLaunchKernelGGL((conv32_halo_kernel<3, true>), grid, block, 0, s, a);
     else if (a.bnb && two) hipLaunchKernelGGL((conv32_halo_kernel<3, false>), grid, block, 0, s, a);
     else if (a.bnb && rs) hipLaunchKernelGGL((conv32_halo_kernel<2, true>), grid, block, 0, s, a);
     else if (a.bnb) hipLaunchKernelGGL((conv32_halo_kernel<2, false>), grid, block, 0, s, a);
@@ -610,9 +537,7 @@ void conv32_launch(Conv32Args a, int bm, int bn, hipStream_t s) {
 #define PDT_C32(BM_, BN_, WM_, WN_)                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                          \
     dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(64 * WM_ * WN_);                                   \
-    if (pre && st) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 1, false, true>), grid, block, 0, s, a); \
-    else if (pre) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 0, false, true>), grid, block, 0, s, a); \
-    else if (a.bnb && two && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 3, true>), grid, block, 0, s, a); \
+    if (a.bnb && two && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 3, true>), grid, block, 0, s, a); \
     else if (a.bnb && two) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 3, false>), grid, block, 0, s, a); \
     else if (a.bnb && rs) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 2, true>), grid, block, 0, s, a);   \
     else if (a.bnb) hipLaunchKernelGGL((conv32_kernel<BM_, BN_, WM_, WN_, 2, false>), grid, block, 0, s, a);  \
@@ -925,15 +850,11 @@ __global__ __launch_bounds__(512) void wgrad32_stem4_kernel(Wgrad32Args a) {
 // CU).  32 FLOP per staged byte against the 64 x 64 kernel's 16: the 64 x 64 tile needs ~10 TB/s of L2 traffic at
 // the fp32 MFMA rate, this one half that.  Rows are 32 chunks of 16 B; source chunk = LDS chunk ^ ((row & 3) << 2),
 // so the 4 pixel rows one MFMA reads (lane / 16) land on 4 disjoint 16-bank groups (ds_read_b32 conflict free).
-// PRE (Wgrad32Args::pre_coef): X is the producer's raw output; every X element read gets relu(x * scale + shift), and
-// the rows the DMA zero-filled (image padding, past the split) stay zero through a per-row flag written at staging.
-template <bool PRE>
 __global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
   constexpr int PIX = 32;
   constexpr int ROW = 512;              // 128 fp32 channels
   constexpr int TILE = PIX * ROW;       // 16 KiB per operand tile
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * TILE];
-  __shared__ float rowok[PRE ? 2 : 1][PRE ? PIX : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wave >> 2, wc = wave & 3;
@@ -969,9 +890,6 @@ __global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
       }
       buf_lds16(rd, dyb + ins * 1024, od);
       buf_lds16(rx, xb + ins * 1024, ox);
-      if constexpr (PRE) {
-        if (pc == 0) rowok[buf][row] = ox != kOOB ? 1.f : 0.f;  // read after the stage's barrier
-      }
     }
   };
   f32x4_t acc[4][2];
@@ -993,15 +911,6 @@ __global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
     const int col = wc * 32 + j * 16 + fr;
     boff[j] = TILE + fq * ROW + ((((col >> 2) ^ (fq << 2))) << 4) + (col & 3) * 4;
   }
-  float psc[2], psh[2];  // PRE: this lane's two X channels c0 + wc*32 + j*16 + fr
-  if constexpr (PRE) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = c0 + wc * 32 + j * 16 + fr;
-      psc[j] = a.pre_coef[c];
-      psh[j] = a.pre_coef[a.C + c];
-    }
-  }
   const int nchunks = p_end > p_begin ? (int)((p_end - p_begin + PIX - 1) / PIX) : 0;
   if (nchunks > 0) {
     stage(p_begin, 0);
@@ -1019,11 +928,6 @@ __global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
         for (int i = 0; i < 4; ++i) av[i] = *(const float*)(sb + aoff[i]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) bv[j] = *(const float*)(sb + boff[j]);
-        if constexpr (PRE) {
-          const bool ok = rowok[cur][s4 * 4 + fq] != 0.f;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) bv[j] = ok ? fmaxf(bv[j] * psc[j] + psh[j], 0.f) : 0.f;
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1055,8 +959,6 @@ __global__ __launch_bounds__(512) void wgrad32w_kernel(Wgrad32Args a) {
 // (Q + Q + 2 + 2) x 256 B.  Rows: the pixel-row swizzle of wgrad32 (chunk ^ (row & 3) << 2) keeps the four rows one
 // MFMA reads (lane / 16, plus the tap shift) on distinct bank groups.
 constexpr int kHaloMaxQ = 62;
-// PRE: as wgrad32w_kernel's; the zero rows here are the image padding (input row ih or column iw outside the image).
-template <bool PRE>
 __global__ __launch_bounds__(256) void wgrad32_halo_kernel(Wgrad32Args a) {
   constexpr int ROW = 256;                       // 64 fp32 channels
   constexpr int XR = kHaloMaxQ + 2;               // staged input rows (halo included), 64
@@ -1118,14 +1020,6 @@ __global__ __launch_bounds__(256) void wgrad32_halo_kernel(Wgrad32Args a) {
     bsh[j] = cc / 64;                   // tap s: the input tile shifted by s rows
     bcol[j] = (cc & 63) + fr;
   }
-  float psc[3], psh[3];  // PRE: this lane's X channels c0 + bcol[j]
-  if constexpr (PRE) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      psc[j] = a.pre_coef[c0 + bcol[j]];
-      psh[j] = a.pre_coef[a.C + c0 + bcol[j]];
-    }
-  }
   const int steps = (Q + 3) / 4;
   if (r_end > r_begin) {
     stage(r_begin, 0);
@@ -1136,11 +1030,6 @@ __global__ __launch_bounds__(256) void wgrad32_halo_kernel(Wgrad32Args a) {
       if (orow + 1 < r_end) stage(orow + 1, cur ^ 1);
       const char* db = smem + cur * STAGE;
       const char* xb = db + TILE_D;
-      bool rok = true;  // PRE: the staged input row ih = h + rt - 1 lies inside the image
-      if constexpr (PRE) {
-        const int n = orow / a.Pm, h = orow - n * a.Pm;
-        rok = (unsigned)(h + rt - 1) < (unsigned)a.H;
-      }
       for (int s4 = 0; s4 < steps; ++s4) {
         float av[4], bv[3];
 #pragma unroll
@@ -1149,10 +1038,6 @@ __global__ __launch_bounds__(256) void wgrad32_halo_kernel(Wgrad32Args a) {
         for (int j = 0; j < 3; ++j) {
           const int row = s4 * 4 + fq + bsh[j];
           bv[j] = *(const float*)(xb + row * ROW + ((((bcol[j] >> 2) ^ ((row & 3) << 2))) << 4) + (bcol[j] & 3) * 4);
-          if constexpr (PRE) {  // staged row `row` = input column row - 1
-            const bool ok = rok && (unsigned)(row - 1) < (unsigned)a.W;
-            bv[j] = ok ? fmaxf(bv[j] * psc[j] + psh[j], 0.f) : 0.f;
-          }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1182,21 +1067,13 @@ bool wgrad32_halo_supported(const Wgrad32Args& a) {
 }
 
 void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
-  const bool pre = a.pre_coef != nullptr;
-  if (pre && a.tile != 3 && a.tile != 128)
-    pdt_hip_fail("wgrad32: the fused producer BN + ReLU (pre_coef) needs the 128-wide or the 3x3 halo kernel",
-                 hipErrorInvalidValue, __FILE__, __LINE__);
-  if (pre) PDT_COUNT("wgrad32_pre");
   if (a.tile == 3) {  // halo kernel (wgrad32_halo_supported): splits over output rows
     if (!wgrad32_halo_supported(a))
       pdt_hip_fail("wgrad32: halo kernel needs a 3x3/s1/p1 conv, 64-channel blocks and W <= 62", hipErrorInvalidValue,
                    __FILE__, __LINE__);
     PDT_COUNT("wgrad32_halo");
     dim3 grid(a.splits, 3, (a.Kout / 64) * (a.C / 64)), block(256);
-    if (pre)
-      hipLaunchKernelGGL(wgrad32_halo_kernel<true>, grid, block, 0, s, a);
-    else
-      hipLaunchKernelGGL(wgrad32_halo_kernel<false>, grid, block, 0, s, a);
+    hipLaunchKernelGGL(wgrad32_halo_kernel, grid, block, 0, s, a);
     return;
   }
   if (a.tile == 4) {  // window-pair stem, all 4 pairs per block
@@ -1219,10 +1096,7 @@ void wgrad32_launch(const Wgrad32Args& a, hipStream_t s) {
   if (a.tile == 128) {
     PDT_COUNT("wgrad32_wide");
     dim3 grid(a.splits, a.Kout / 128, a.T * a.U * (a.C / 128)), block(512);
-    if (pre)
-      hipLaunchKernelGGL(wgrad32w_kernel<true>, grid, block, 0, s, a);
-    else
-      hipLaunchKernelGGL(wgrad32w_kernel<false>, grid, block, 0, s, a);
+    hipLaunchKernelGGL(wgrad32w_kernel, grid, block, 0, s, a);
     return;
   }
   PDT_COUNT("wgrad32");

@@ -13,7 +13,7 @@ all-reduce) without its 16-bit-specific fusions: BN-backward reductions are sepa
 as an im2col GEMM (K = 7*7*3 padded to 192), processed in image chunks so every operand stays within the
 32-bit buffer offsets of the LDS-DMA loads.
 
-Accuracy (tools/diag_fp32.py, ResNet-50): the forward activations track an fp64 forward exactly as closely as
+Accuracy (measured in round 4 against an fp64 forward, ResNet-50): the forward activations track an fp64 forward exactly as closely as
 PyTorch's own fp32 does (relative error 2e-7 after the stem, 7e-5 at the last block, both), and conv weight
 gradients of the later layers match fp64 to ~5e-6.  Where a gradient differs more it is a discrete effect of
 fp32 rounding itself -- a near-zero pre-activation landing on the other side of a ReLU than in fp64 -- which
@@ -181,34 +181,16 @@ class ResNetExecutor32(ResNetExecutor):
     def _tile32c(self, kind: str, c: _Conv, N: int, H: int, n: int, m: int):
         return self._TUNED32.get((kind, N, H, c.cin, c.cout, c.R, c.st)) or self._tile32(n, m)
 
-    def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool, pre=None):
-        """``pre``: x is the producer conv's raw output and ``pre`` its BN coefficients -- BN + ReLU applied to the
-        activation fragments inside the kernel (``_pre_ok``)."""
+    def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool):
         P, Q = c.out_hw(H, W)
         sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
         tile = self._tile32c("fwd", c, N, H, c.cout, N * P * Q)
-        if pre is not None:
-            self.C.conv32_fwd_pre(x, self._w32(c), y, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, *tile,
-                                  pre)
-        else:
-            self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, *tile)
+        self.C.conv32_fwd(x, self._w32(c), y, None, sp, N, H, W, c.cin, c.cout, c.R, c.S, P, Q, c.st, c.pad, *tile)
         return P, Q, sp
 
-    # PDT_FP32_PRE=1: the inner BatchNorms' BN + ReLU (SURVEY §7.2 P5) applied by their consumer conv's kernels --
-    # forward fragments and the weight gradient's staged input -- instead of a bn_apply32 pass writing relu(bn(y));
-    # the backward's ReLU mask comes from y and the BN coefficients.  Bit-identical to the separate pass, but OFF by
-    # default: measured 126.1 -> 129.7 ms/step (the fused kernels run 14-21 % slower, +4.6 ms, against the 1.2 ms of
-    # bn_apply32 passes removed: the transform sits between the fragment reads and the MFMAs; profiles/r4_fp32_pre.md)
-    _PRE = os.environ.get("PDT_FP32_PRE", "0") == "1"
-
-    def _pre_ok(self, c: _Conv, H: int, W: int) -> bool:
-        """Can conv ``c`` (input H x W) consume its producer's raw output: its weight gradient must run on a kernel with
-        the fused prologue (3x3 halo or 128-wide tile), the backward's BN reduce must be the fused dgrad epilogue
-        (its ReLU mask is recomputed from y), and the input channels fit the kernels' coefficient tables."""
-        if not (self._PRE and self._FUSE_BN) or c.cin > 256:
-            return False
-        P, Q = c.out_hw(H, W)
-        return self._wgrad_tile(c.cout, c.R, c.S, c.cin, H, W, P, Q, c.st, c.pad) in (3, 128)
+    # (the inner BatchNorms' BN + ReLU applied inside the consumer conv's fp32 kernels -- round 4's PDT_FP32_PRE --
+    # measured 126.1 -> 129.7 ms/step, the fused kernels 14-21 % slower than the 1.2 ms of bn_apply32 passes they
+    # remove, and was deleted in round 5; profiles/r4_fp32_pre.md)
 
     def _dgrad(self, c: _Conv, dy, N, H, W, P, Q, dx, res=None, bnb=None):
         """``bnb = (mref, y1, coef, slots)``: the consumer BatchNorm's backward reduce fused into the epilogue (dx then
@@ -245,7 +227,7 @@ class ResNetExecutor32(ResNetExecutor):
         return 128 if (self._WIDE and C % 128 == 0 and cout % 128 == 0) else 64
 
     def _wgrad(self, cout, x, dy, N, H, W, C, R, S, P, Q, st, pad, gout, ldo, rows=None, cols=None,
-               accumulate=False, pre=None):
+               accumulate=False):
         ldw = R * S * C
         npix = N * P * Q
         tile = self._wgrad_tile(cout, R, S, C, H, W, P, Q, st, pad)
@@ -266,10 +248,7 @@ class ResNetExecutor32(ResNetExecutor):
             plan = self._plans[key] = (splits, pps)
         splits, pps = plan
         ws = self._buf("ws", splits * cout * ldw, torch.float32)
-        if pre is not None:
-            self.C.wgrad32_pre(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile, pre)
-        else:
-            self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile)
+        self.C.wgrad32(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, pad, ldw, splits, pps, tile)
         self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, accumulate)
 
     def _stem_chunk(self, N: int) -> int:
@@ -341,11 +320,11 @@ class ResNetExecutor32(ResNetExecutor):
         recs = []
         for bi, b in enumerate(self.blocks):
             rec = {"x": x, "H": Hc, "W": Wc, "C": Cc, "ys": [], "as": [], "hw": []}
-            cur, h, w, pre = x, Hc, Wc, None
+            cur, h, w = x, Hc, Wc
             for ci, (c, bn) in enumerate(zip(b["convs"], b["bns"])):
                 P, Q = c.out_hw(h, w)
                 y = self._buf(("y", bi, ci), N * P * Q * c.cout, torch.float32)
-                _, _, sp = self._conv_fwd(c, cur, N, h, w, y, train, pre=pre)
+                _, _, sp = self._conv_fwd(c, cur, N, h, w, y, train)
                 if train:
                     self.bn_train_finalize(bn, sp, 0, N * P * Q)
                 else:
@@ -353,14 +332,10 @@ class ResNetExecutor32(ResNetExecutor):
                 rec["ys"].append(y)
                 rec["hw"].append((h, w, P, Q))
                 if ci < len(b["convs"]) - 1:
-                    if self._pre_ok(b["convs"][ci + 1], P, Q):  # the consumer applies BN + ReLU: no activation
-                        rec["as"].append(None)
-                        cur, pre = y, bn.coef
-                    else:
-                        a = self._buf(("a", bi, ci), y.numel(), torch.float32)
-                        Cn.bn_apply32(y, bn.coef, None, None, a, c.cout, 0, True)
-                        rec["as"].append(a)
-                        cur, pre = a, None
+                    a = self._buf(("a", bi, ci), y.numel(), torch.float32)
+                    Cn.bn_apply32(y, bn.coef, None, None, a, c.cout, 0, True)
+                    rec["as"].append(a)
+                    cur = a
                 h, w = P, Q
             cl, bnl = b["convs"][-1], b["bns"][-1]
             out = self._buf(("out", bi), N * h * w * cl.cout, torch.float32)
@@ -464,17 +439,15 @@ class ResNetExecutor32(ResNetExecutor):
             for ci in range(len(convs) - 1, -1, -1):
                 c = convs[ci]
                 h, w, P, Q = rec["hw"][ci]
-                xin, pre = (rec["as"][ci - 1], None) if ci > 0 else (x, None)
-                if ci > 0 and xin is None:  # fused producer BN + ReLU (forward): x = the raw conv output
-                    xin, pre = rec["ys"][ci - 1], bns[ci - 1].coef
+                xin = rec["as"][ci - 1] if ci > 0 else x
                 self._wgrad(c.cout, xin, dy, N, h, w, c.cin, c.R, c.S, P, Q, c.st, c.pad, self._g(c.slot),
-                            c.R * c.S * c.cin, pre=pre)
+                            c.R * c.S * c.cin)
                 self.grad_ready(c.pid)
                 if ci > 0:
                     da = self._buf("da", N * h * w * c.cin, torch.float32)
                     bnp, yp, ap = bns[ci - 1], rec["ys"][ci - 1], rec["as"][ci - 1]
                     if self._FUSE_BN:  # dgrad epilogue writes dz and reduces the inner BN's backward sums (ReLU
-                        # mask from ap, or -- fused producer BN, ap is None -- from yp * scale + shift)
+                        # mask from ap)
                         slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
                         self._dgrad(c, dy, N, h, w, P, Q, da, bnb=(ap, yp, bnp.coef, slots))
                         self._bn_bwd_finish(slots, N * h * w, bnp)

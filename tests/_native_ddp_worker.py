@@ -75,7 +75,7 @@ def main():
                    os.environ["PDT_TEST_OUT"])
     from pytorch_distributed_template_amd.ops import validate
     v = validate.validator()
-    if v is not None:  # PDT_VALIDATE runs (tools/diag_run.sh): report replay-determinism findings of this rank
+    if v is not None:  # PDT_VALIDATE runs (bench.py / pytest under PDT_VALIDATE=1): report replay-determinism findings of this rank
         print(f"[rank {rank}] validator: {v.replayed} launches replayed, {len(v.findings)} findings", flush=True)
         for f in v.findings:
             print(f"[rank {rank}] NONDETERMINISTIC: {f}", flush=True)

@@ -136,7 +136,7 @@ def test_executor32_train_step_matches_torch_fp32(arch, N, HW, chunk):
     random-init ResNets amplify rounding differences through the backward chain, so a fixed fp32 tolerance
     would be meaningless.  (ResNet-50 at 64 px, i.e. BatchNorm over 4 x 2 x 2 = 16 values per channel in
     layer4, is ill-conditioned enough that a single ReLU-mask flip of a near-zero pre-activation in the last
-    block moves that block's gradients by ~1 %: tools/diag_fp32.py.  128 px keeps the comparison meaningful.)
+    block moves that block's gradients by ~1 % (round-4 fp64 comparison).  128 px keeps the comparison meaningful.)
     (chunk: the im2col stem processed in several image chunks.)"""
     model, ref, flat, ex, x, t = _setup(arch, N, HW)
     if chunk:
@@ -152,7 +152,7 @@ def test_executor32_train_step_matches_torch_fp32(arch, N, HW, chunk):
     F.cross_entropy(out64, t).backward()
     # sensitivity floor: the fp64 gradients themselves under a 1e-4 relative input nudge -- the size of fp32's
     # own forward rounding at ResNet-50 depth (torch fp32 and ours both reach ~7e-5 vs fp64 at the last block,
-    # tools/diag_fp32.py); ReLU-mask flips of near-zero pre-activations move whole blocks' gradients by ~1 %
+    # the round-4 fp64 comparison); ReLU-mask flips of near-zero pre-activations move whole blocks' gradients by ~1 %
     # (an additive random nudge: BatchNorm normalises a uniform input scaling away)
     g = torch.Generator(device=DEV).manual_seed(5)
     F.cross_entropy(ref64b(x.double() + 1e-4 * torch.randn(x.shape, device=DEV, generator=g).double()), t).backward()
@@ -473,31 +473,3 @@ def test_stem_pool_bwd_reduce_out32_matches_window_gather():
     r, g = ref.view(64, ch, 2).sum(0), got.view(64, ch, 2).sum(0)
     scale = dp.abs().view(-1, ch).sum(0).double()  # sum |dz| bounds both sums' rounding
     assert ((r - g).abs() <= 1e-5 * scale[:, None] + 1e-9).all(), ((r - g).abs() / scale[:, None]).max()
-
-
-@pytest.mark.parametrize("arch,HW", [("resnet18", 112), ("resnet50", 64)])
-def test_fp32_fused_producer_bn_equals_separate_pass(monkeypatch, arch, HW):
-    """SURVEY P5 in fp32: the inner BatchNorms' BN + ReLU applied by the consumer conv's kernels (forward activation
-    fragments, the weight gradient's staged input; the backward's ReLU mask recomputed from y) gives the logits, loss,
-    every gradient and the running statistics of the separate bn_apply32 pass BIT FOR BIT -- the same fma + max on
-    the same values, summed in the same order -- and really runs (dispatch counts)."""
-    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
-    from pytorch_distributed_template_amd.models import registry
-    from pytorch_distributed_template_amd.models.executor32 import ResNetExecutor32
-    from pytorch_distributed_template_amd.ops import native
-    torch.manual_seed(3)
-    model = registry.create(arch)
-    x = torch.randn(4, 3, HW, HW, device=DEV)
-    t = torch.randint(0, 1000, (4,), device=DEV)
-    outs = []
-    for pre in (False, True):
-        monkeypatch.setattr(ResNetExecutor32, "_PRE", pre)
-        tr = NativeTrainer(copy.deepcopy(model), torch.device(DEV), dtype=torch.float32, lr=0.0)
-        native.C.reset_dispatch_counts()
-        logits, met = tr.train_step(x, t)
-        torch.cuda.synchronize()
-        cnt = dict(native.C.dispatch_counts())
-        assert (cnt.get("conv32_fwd_pre", 0) > 0 and cnt.get("wgrad32_pre", 0) > 0) == pre, cnt
-        outs.append((logits.clone(), met.clone(), tr.flat.grad.clone(), tr.buffers.fdata.clone()))
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b), _rel(b, a)
