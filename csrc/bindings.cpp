@@ -346,6 +346,19 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
       return;
     }
   }
+  if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 && H == P && W == Q &&
+      pdt::conv1x1x_supported((int)K, (int)C)) {
+    const auto& f = phases[0];
+    if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
+      // ResNet-50 layers 2-4: 1x1 C -> 4C backward-data (conv1 of a bottleneck) with the block-output BN-backward
+      // epilogue on the persistent sliced kernel (conv1x1x.hip); [C][K] weights at the phase's offset
+      pdt::conv1x1x_bnb_launch(a.x, a.w + f[6], a.y, a.res, a.bn_y1, a.bn_coef1, bnb == 3 ? a.bn_y2 : nullptr,
+                               bnb == 3 ? a.bn_coef2 : nullptr, a.bn_mask, a.stats, N * P * Q, (int)K, (int)C, dt,
+                               cur_stream());
+      launched("conv1x1x_bnb");
+      return;
+    }
+  }
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, (int)bk, cur_stream());
   launched("conv_fwd_launch");
 }
@@ -372,6 +385,27 @@ void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats,
   }
   pdt::conv1x1_c64_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), st, M, dt, cur_stream());
   launched("conv1x1_c64");
+}
+
+// 1x1 / stride-1 expanding conv with C = 128 / 256 / 512 input channels (ResNet-50 layers 2-4 conv3): the persistent
+// sliced kernel (conv1x1x.hip); y[M][N] from x[M][C] and w[N][C], optional BN statistics (fp64 slots)
+bool conv1x1x_supported(int64_t C, int64_t N) { return pdt::conv1x1x_supported((int)C, (int)N); }
+int64_t conv1x1x_mode(int64_t set) { return pdt::conv1x1x_mode((int)set); }
+
+void conv1x1x(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M, int64_t C, int64_t N) {
+  const int dt = dt16(x, "x");
+  TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv1x1x: mixed dtypes");
+  TORCH_CHECK(pdt::conv1x1x_supported((int)C, (int)N), "conv1x1x: unsupported C / N (or PDT_CONV1X1X=0)");
+  TORCH_CHECK(x.numel() >= M * C && w.numel() == N * C && y.numel() >= M * N, "conv1x1x: size mismatch");
+  TORCH_CHECK(M * N < (int64_t(1) << 30) && M * C < (int64_t(1) << 30),
+              "conv1x1x: operands exceed 2 GiB (32-bit buffer offsets)");
+  double* st = nullptr;
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->numel() >= pdt::kStatSlots * N * 2, "conv1x1x: stats buffer too small");
+    st = pd(*stats, "stats");
+  }
+  pdt::conv1x1x_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), st, M, (int)C, (int)N, dt, cur_stream());
+  launched("conv1x1x");
 }
 
 std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t C, int64_t P, int64_t target_blocks,
@@ -1297,6 +1331,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_3x3c64", &conv_wgrad_3x3c64, py::arg("x"), py::arg("dy"), py::arg("ws"), py::arg("N"), py::arg("H"),
         py::arg("W"), py::arg("pre_coef") = py::none());
   m.def("conv_fwd_pre", &conv_fwd_pre);
+  m.def("conv1x1x", &conv1x1x);
+  m.def("conv1x1x_supported", &conv1x1x_supported);
+  m.def("conv1x1x_mode", &conv1x1x_mode);
   m.def("conv_fwd_pre_supported", &conv_fwd_pre_supported);
   m.def("bn_slot_sum", &bn_slot_sum);
   m.def("stat_slots", &stat_slots);

@@ -19,4 +19,14 @@ void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, c
 void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
                         hipStream_t s);
 
+// The same two GEMMs for C = 128 / 256 / 512 reduction channels and N output channels (ResNet-50 layers 2-4: conv3
+// forward, conv1 backward-data), N split into slices of 256 (C = 128) or 128 channels (conv1x1x.hip).  w is [N][C].
+bool conv1x1x_supported(int C, int N);
+int conv1x1x_mode(int set);  // PDT_CONV1X1X seeds it; set >= 0 changes it, returns the previous mode
+void conv1x1x_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int C, int N,
+                     int dtype, hipStream_t s);
+void conv1x1x_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res, const uint16_t* y1,
+                         const float* coef1, const uint16_t* y2, const float* coef2, const uint8_t* mask,
+                         double* slots, int64_t M, int C, int N, int dtype, hipStream_t s);
+
 }  // namespace pdt

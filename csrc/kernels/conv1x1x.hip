@@ -1,0 +1,513 @@
+// Expanding 1x1 / stride-1 GEMMs of ResNet-50 layers 2-4 (K = 128 / 256 / 512 reduction channels, N = 4K output
+// channels) as persistent, store-overlapped kernels: the generalisation of conv1x1.hip (K = 64, N = 256) to
+// reductions whose weights no longer fit in one block's registers.
+//
+// Two GEMMs have this shape: every bottleneck's conv3 forward (y[M][4C] = x[M][C] * W^T, + BN statistics) and the
+// backward-data pass of its conv1 (dX[M][4C] = dY[M][C] * W, with the block-output BN-backward epilogue of
+// conv_fwd.h EPI 3 / 4).  On the generic ping-pong kernel (one 512 x 128 tile per workgroup, 2-8 K-steps) they run
+// at 2.1-2.8 TB/s of HBM traffic: each workgroup's life is load latency -> a few MFMAs -> an epilogue writing 4x the
+// bytes it read, with nothing of the next tile in flight (profiles/r5_resnet50_bs1200_kernels.md).  Here:
+//   * the N output channels are split into S slices of NS = 4 waves x 16*NF channels; a block owns one slice and
+//     keeps that slice's weights (NS x K) resident in registers as MFMA A fragments, staged once through LDS in
+//     64-channel K pieces;
+//   * blocks are persistent (2 per CU) and walk BM-pixel tiles; a tile's input (BM x K) is DMA'd into a 2-deep LDS
+//     ring one tile ahead, and the per-tile wait is COUNTED: the next tile's DMA is issued before this tile's
+//     epilogue operand loads and stores, so waiting for it leaves them in flight;
+//   * the S blocks of one tile sequence sit on the SAME XCD (block b runs on XCD b % 8 under the round-robin
+//     dispatch): the input is fetched from HBM once and re-read by the other slices from that XCD's L2;
+//   * statistics accumulate in registers over all of a block's tiles; one partial row per tile walker (the S slices
+//     of a walker write disjoint channel ranges of the same row), reduced in fixed order (conv_fwd.h).
+// Configurations (register budget: 2 waves per SIMD): K = 128: 64 channels per wave, BM = 64 (S = N / 256);
+// K = 256: 32 channels per wave, BM = 64 (S = N / 128); K = 512: 32 channels per wave, BM = 32 (S = N / 128).
+#include <cstdlib>
+
+#include "../common.h"
+#include "conv1x1.h"
+#include "conv_fwd.h"
+
+namespace pdt {
+
+namespace {
+constexpr int kXRowB = 128;  // 64 16-bit channels per LDS row
+
+template <int KH, int NF, int BM>
+struct X1 {
+  static constexpr int WCH = 16 * NF;              // output channels per wave
+  static constexpr int NS = 4 * WCH;               // per block (slice)
+  static constexpr int TILE = BM * KH * kXRowB;    // one tile's input, all 64-channel K pieces
+  static constexpr int WPIECE = NS * kXRowB;       // one K piece of the slice's weights
+  static constexpr int AREA = 2 * TILE > WPIECE ? 2 * TILE : WPIECE;
+  static constexpr int XI = TILE / 1024 / 4;       // input DMA instructions per wave per tile
+  static constexpr int WI = WPIECE / 1024 / 4;     // weight DMA instructions per wave per piece
+  static_assert(XI * 4096 == TILE && WI * 4096 == WPIECE && BM % 32 == 0, "conv1x1x geometry");
+  static_assert(NF == 2 || NF == 4, "fragment pairs");
+};
+
+// fragments 2p and 2p+1 give a lane 8 consecutive channels of its pixel (one 16-byte store per pixel and pair)
+PDT_DEVICE int x1_wave_ch(int i, int row) { return (i >> 1) * 32 + (row >> 2) * 8 + (i & 1) * 4 + (row & 3); }
+
+template <int N>
+PDT_DEVICE void x1_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// block -> (slice, tile walker): blocks b and b + 8 share an XCD; the S slices of walker l are consecutive there
+struct X1Map {
+  int slice, walker;
+};
+PDT_DEVICE X1Map x1_map(int b, int S) {
+  const int xcd = b & 7, q = b >> 3;
+  return X1Map{q % S, (q / S) * 8 + xcd};
+}
+
+// the slice's weights [n0, n0 + NS) x [0, 64 KH) into registers (af[i][kq]: fragment i, 32-channel K step kq),
+// through the LDS area in 64-channel pieces
+template <int DT, int KH, int NF, int BM>
+PDT_DEVICE void x1_load_weights(typename E16<DT>::vec8 (&af)[NF][2 * KH], const __amdgpu_buffer_rsrc_t& rw,
+                                char* wl, int n0, int wave, int lane) {
+  using C = X1<KH, NF, BM>;
+  typedef typename E16<DT>::vec8 vec8;
+  const int fr = lane & 15, fq = lane >> 4, lrow = lane >> 3, pchunk = lane & 7;
+#pragma unroll
+  for (int hh = 0; hh < KH; ++hh) {
+#pragma unroll
+    for (int j = 0; j < C::WI; ++j) {
+      const int ins = wave * C::WI + j;
+      const int row = ins * 8 + lrow;
+      buf_lds16_asm(rw, wl + ins * 1024,
+                    (uint32_t)((n0 + row) * (KH * kXRowB) + hh * kXRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int wr = wave * C::WCH + x1_wave_ch(i, fr);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[i][2 * hh + kk] = *(const vec8*)(wl + wr * kXRowB + (((kk * 4 + fq) ^ ((wr >> 1) & 7)) << 4));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave holds this piece: the area is free again
+  }
+}
+
+// one tile's input: XI DMA instructions per wave; rows past M read zeros (their results are not stored)
+template <int KH, int NF, int BM>
+PDT_DEVICE void x1_stage(const __amdgpu_buffer_rsrc_t& rx, char* xl, int64_t t, int buf, int64_t M, int wave,
+                         int lane) {
+  using C = X1<KH, NF, BM>;
+  const int lrow = lane >> 3, pchunk = lane & 7;
+#pragma unroll
+  for (int j = 0; j < C::XI; ++j) {
+    const int ins = wave * C::XI + j;
+    const int hh = ins / (BM / 8), row = (ins % (BM / 8)) * 8 + lrow;
+    const int64_t m = t * BM + row;
+    const uint32_t off =
+        m < M ? (uint32_t)(m * (KH * kXRowB) + hh * kXRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
+    buf_lds16_asm(rx, xl + buf * C::TILE + ins * 1024, off);
+  }
+}
+
+// acc[i][j] (fragment i of the wave's channels, pixel fragment j of the PJ*16-pixel sub-tile s) over the whole
+// reduction
+template <int DT, int KH, int NF, int BM, int PJ>
+PDT_DEVICE void x1_mma(f32x4_t (&acc)[NF][PJ], const typename E16<DT>::vec8 (&af)[NF][2 * KH], const char* xb, int s,
+                       int lane) {
+  typedef typename E16<DT>::vec8 vec8;
+  const int fr = lane & 15, fq = lane >> 4, sw = (fr >> 1) & 7;
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kq = 0; kq < 2 * KH; ++kq) {
+    vec8 bf[PJ];
+#pragma unroll
+    for (int j = 0; j < PJ; ++j)
+      bf[j] = *(const vec8*)(xb + (kq >> 1) * BM * kXRowB + ((s * PJ + j) * 16 + fr) * kXRowB +
+                             ((((kq & 1) * 4 + fq) ^ sw) << 4));
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) acc[i][j] = E16<DT>::mfma16x16x32(af[i][kq], bf[j], acc[i][j]);
+  }
+}
+
+PDT_DEVICE uint4 x1_pack(const uint16_t (&o)[8]) {
+  uint4 pk;
+  pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+  pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+  pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
+  pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+  return pk;
+}
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------ forward
+template <int DT, bool STATS, int KH, int NF, int BM>
+__global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                          float* __restrict__ srows, int64_t M, int N, int S) {
+  using C = X1<KH, NF, BM>;
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  constexpr int OPS = (BM / 16) * (NF / 2);  // vector-memory ops per wave after the next tile's DMA (stores)
+  __shared__ __attribute__((aligned(1024))) char smem[C::AREA];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const X1Map mp = x1_map(blockIdx.x, S);
+  const int Gs = gridDim.x / S;
+  const int n0 = mp.slice * C::NS;
+  const int64_t tiles = (M + BM - 1) / BM;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * KH * kXRowB));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)((int64_t)N * KH * kXRowB));
+
+  vec8 af[NF][2 * KH];
+  x1_load_weights<DT, KH, NF, BM>(af, rw, smem, n0, wave, lane);
+
+  float ssum[NF][4], ssq[NF][4];
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { ssum[i][r] = 0.f; ssq[i][r] = 0.f; }
+
+  int64_t t = mp.walker;
+  if (t < tiles) x1_stage<KH, NF, BM>(rx, smem, t, 0, M, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int buf = 0;
+  bool first = true;
+  for (; t < tiles; t += Gs) {
+    if (!first) {
+      // tile t's DMA was issued before the previous (full: only a walker's last tile can be the M tail) tile's OPS
+      // stores; vector-memory ops retire in order, so waiting down to OPS outstanding retires the DMA only
+      x1_vm_wait<OPS>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    first = false;
+    if (t + Gs < tiles) x1_stage<KH, NF, BM>(rx, smem, t + Gs, buf ^ 1, M, wave, lane);
+    const char* xb = smem + buf * C::TILE;
+#pragma unroll
+    for (int s = 0; s < BM / 32; ++s) {
+      f32x4_t acc[NF][2];
+      x1_mma<DT, KH, NF, BM, 2>(acc, af, xb, s, lane);
+      // pair p gives the lane channels n0 + wave*WCH + p*32 + 8*fq + [0, 8) of pixel t*BM + (2s + j)*16 + fr
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t m = t * BM + (s * 2 + j) * 16 + fr;
+        uint16_t* yp = y + m * N + n0 + wave * C::WCH + 8 * fq;
+#pragma unroll
+        for (int p = 0; p < NF / 2; ++p) {
+          uint16_t o[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = E::from_f(acc[2 * p + (r >> 2)][j][r & 3]);
+          if (m < M) {
+            *(uint4*)(yp + p * 32) = x1_pack(o);
+            if constexpr (STATS) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                const float q = E::to_f(o[r]);
+                ssum[2 * p + (r >> 2)][r & 3] += q;
+                ssq[2 * p + (r >> 2)][r & 3] += q * q;
+              }
+            }
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+  if constexpr (STATS) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ssum[i][r] = row16_sum(ssum[i][r]);
+        ssq[i][r] = row16_sum(ssq[i][r]);
+      }
+    if (fr == 15) {
+      float* dst = srows + (int64_t)mp.walker * N * 2;
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = n0 + wave * C::WCH + x1_wave_ch(i, 4 * fq + r);
+          *(float2*)(dst + c * 2) = make_float2(ssum[i][r], ssq[i][r]);
+        }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ backward data
+// dX = dY * W with the block-output BN-backward epilogue (conv1x1.hip's conv1x1_c64_bnb_kernel, generalised):
+// v = acc + res, dz = v where the block output's ReLU bit is set (else 0), stored rounded; per channel sum(dz) and
+// sum(dz * (y1 - mean1) * invstd1) (BR = 2: + sum(dz * (y2 - mean2) * invstd2)) into the walker's statistics row.
+// PJ: pixel fragments per sub-tile (1 where 2 would not fit the register budget).
+template <int DT, int BR, int KH, int NF, int BM, int PJ>
+__global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+    const uint16_t* __restrict__ res, const uint16_t* __restrict__ y1, const float* __restrict__ coef1,
+    const uint16_t* __restrict__ y2, const float* __restrict__ coef2, const uint8_t* __restrict__ mask,
+    float* __restrict__ srows, int64_t M, int N, int S) {
+  static_assert(BR == 1 || BR == 2, "one or two BatchNorm branches");
+  using C = X1<KH, NF, BM>;
+  using E = E16<DT>;
+  typedef typename E::vec8 vec8;
+  // per wave and tile, after the next tile's DMA: residual + y1 (+ y2) 16-B loads, one mask byte, one store per
+  // (pixel fragment, channel pair)
+  constexpr int OPS = (BM / 16) * (NF / 2) * (BR == 2 ? 5 : 4);
+  __shared__ __attribute__((aligned(1024))) char smem[C::AREA + BR * 2 * C::NS * 4];
+  float* const cf = (float*)(smem + C::AREA);  // cf[(branch * 2 + 0 | 1) * NS + c]: mean | invstd of the slice
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const X1Map mp = x1_map(blockIdx.x, S);
+  const int Gs = gridDim.x / S;
+  const int n0 = mp.slice * C::NS;
+  const int64_t tiles = (M + BM - 1) / BM;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * KH * kXRowB));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)((int64_t)N * KH * kXRowB));
+
+  if (tid < C::NS) {
+    cf[tid] = coef1[2 * N + n0 + tid];
+    cf[C::NS + tid] = coef1[3 * N + n0 + tid];
+    if constexpr (BR == 2) {
+      cf[2 * C::NS + tid] = coef2[2 * N + n0 + tid];
+      cf[3 * C::NS + tid] = coef2[3 * N + n0 + tid];
+    }
+  }
+  vec8 af[NF][2 * KH];
+  x1_load_weights<DT, KH, NF, BM>(af, rw, smem, n0, wave, lane);  // (its barriers also publish cf)
+
+  float s0[NF / 2][8], s1[NF / 2][8], s2[BR == 2 ? NF / 2 : 1][8];
+#pragma unroll
+  for (int p = 0; p < NF / 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s0[p][e] = 0.f;
+      s1[p][e] = 0.f;
+      if constexpr (BR == 2) s2[p][e] = 0.f;
+    }
+
+  int64_t t = mp.walker;
+  if (t < tiles) x1_stage<KH, NF, BM>(rx, smem, t, 0, M, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int buf = 0;
+  bool first = true;
+  for (; t < tiles; t += Gs) {
+    if (!first) {
+      x1_vm_wait<OPS>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    first = false;
+    if (t + Gs < tiles) x1_stage<KH, NF, BM>(rx, smem, t + Gs, buf ^ 1, M, wave, lane);
+    const char* xb = smem + buf * C::TILE;
+#pragma unroll
+    for (int s = 0; s < BM / (16 * PJ); ++s) {
+      // epilogue operands first (independent of the MFMAs); rows past M load row M-1 and are not stored
+      uint4 rr[PJ][NF / 2], yy[PJ][NF / 2], yz[BR == 2 ? PJ : 1][NF / 2];
+      uint32_t mb[PJ][NF / 2];
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) {
+        int64_t m = t * BM + (s * PJ + j) * 16 + fr;
+        m = m < M ? m : M - 1;
+#pragma unroll
+        for (int p = 0; p < NF / 2; ++p) {
+          const int64_t o = m * N + n0 + wave * C::WCH + p * 32 + 8 * fq;
+          rr[j][p] = *(const uint4*)(res + o);
+          yy[j][p] = *(const uint4*)(y1 + o);
+          if constexpr (BR == 2) yz[j][p] = *(const uint4*)(y2 + o);
+          mb[j][p] = mask[o >> 3];
+        }
+      }
+      f32x4_t acc[NF][PJ];
+      x1_mma<DT, KH, NF, BM, PJ>(acc, af, xb, s, lane);
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) {
+        const int64_t m = t * BM + (s * PJ + j) * 16 + fr;
+#pragma unroll
+        for (int p = 0; p < NF / 2; ++p) {
+          const uint32_t rw4[4] = {rr[j][p].x, rr[j][p].y, rr[j][p].z, rr[j][p].w};
+          const uint32_t yw4[4] = {yy[j][p].x, yy[j][p].y, yy[j][p].z, yy[j][p].w};
+          uint16_t o[8];
+          float q1[8], q2[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(rw4[e >> 1] >> (16 * (e & 1))));
+            if (!((mb[j][p] >> e) & 1u)) v = 0.f;
+            o[e] = E::from_f(v);
+            q1[e] = E::to_f((uint16_t)(yw4[e >> 1] >> (16 * (e & 1))));
+          }
+          if constexpr (BR == 2) {
+            const uint32_t zw4[4] = {yz[j][p].x, yz[j][p].y, yz[j][p].z, yz[j][p].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q2[e] = E::to_f((uint16_t)(zw4[e >> 1] >> (16 * (e & 1))));
+          }
+          if (m < M) {
+            const int cl = wave * C::WCH + p * 32 + 8 * fq;  // slice-local channel
+            *(uint4*)(y + m * N + n0 + cl) = x1_pack(o);
+            const float4 ma = *(const float4*)(cf + cl), mb4 = *(const float4*)(cf + cl + 4);
+            const float4 ia = *(const float4*)(cf + C::NS + cl), ib = *(const float4*)(cf + C::NS + cl + 4);
+            const float mu[8] = {ma.x, ma.y, ma.z, ma.w, mb4.x, mb4.y, mb4.z, mb4.w};
+            const float is[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float dz = E::to_f(o[e]);
+              s0[p][e] += dz;
+              s1[p][e] += dz * (q1[e] - mu[e]) * is[e];
+            }
+            if constexpr (BR == 2) {
+              const float4 na = *(const float4*)(cf + 2 * C::NS + cl), nb = *(const float4*)(cf + 2 * C::NS + cl + 4);
+              const float4 ja = *(const float4*)(cf + 3 * C::NS + cl), jb = *(const float4*)(cf + 3 * C::NS + cl + 4);
+              const float mu2[8] = {na.x, na.y, na.z, na.w, nb.x, nb.y, nb.z, nb.w};
+              const float is2[8] = {ja.x, ja.y, ja.z, ja.w, jb.x, jb.y, jb.z, jb.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) s2[p][e] += E::to_f(o[e]) * (q2[e] - mu2[e]) * is2[e];
+            }
+          }
+        }
+      }
+    }
+    buf ^= 1;
+  }
+
+#pragma unroll
+  for (int p = 0; p < NF / 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s0[p][e] = row16_sum(s0[p][e]);
+      s1[p][e] = row16_sum(s1[p][e]);
+      if constexpr (BR == 2) s2[p][e] = row16_sum(s2[p][e]);
+    }
+  if (fr == 15) {
+    constexpr int KO = BR == 2 ? 4 : 2;
+    float* dst = srows + (int64_t)mp.walker * N * KO;
+#pragma unroll
+    for (int p = 0; p < NF / 2; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = n0 + wave * C::WCH + p * 32 + 8 * fq + e;
+        if constexpr (BR == 2)
+          *(float4*)(dst + c * 4) = make_float4(s0[p][e], s1[p][e], s0[p][e], s2[p][e]);
+        else
+          *(float2*)(dst + c * 2) = make_float2(s0[p][e], s1[p][e]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ host
+namespace {
+int x1_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+int x1_slice(int C) { return C == 128 ? 256 : 128; }  // NS of the configuration for C reduction channels
+
+// grid: 2 blocks per CU, a multiple of 8 * S (every XCD holds whole walkers), at least one walker per XCD
+int x1_grid(int S, int64_t tiles) {
+  const int unit = 8 * S;
+  int g = (2 * x1_cus()) / unit * unit;
+  if (g < unit) g = unit;
+  const int64_t need = (tiles + 7) / 8 * 8 * S;  // no more walkers than tiles (rounded up to whole XCD rows)
+  if ((int64_t)g > need) g = (int)((need + unit - 1) / unit * unit);
+  return g;
+}
+
+void x1_check(int64_t M, int C, int N, const char* what) {
+  if (!conv1x1x_supported(C, N))
+    pdt_hip_fail(what, hipErrorInvalidValue, __FILE__, __LINE__);
+  if (M * N >= (int64_t(1) << 30) || M * C >= (int64_t(1) << 30))
+    pdt_hip_fail("conv1x1x: operands exceed 32-bit buffer offsets", hipErrorInvalidValue, __FILE__, __LINE__);
+}
+}  // namespace
+
+int conv1x1x_mode(int set) {
+  // PDT_CONV1X1X=0: the generic implicit-GEMM kernels for these shapes (A/B); set >= 0 switches at run time (tests)
+  static int on = [] {
+    const char* e = getenv("PDT_CONV1X1X");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  const int prev = on;
+  if (set >= 0) on = set;
+  return prev;
+}
+
+bool conv1x1x_supported(int C, int N) {
+  if (!conv1x1x_mode(-1) || !(C == 128 || C == 256 || C == 512) || N <= 0) return false;
+  const int ns = x1_slice(C);
+  return N % ns == 0 && N / ns <= 32;
+}
+
+void conv1x1x_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int C, int N,
+                     int dtype, hipStream_t s) {
+  if (M <= 0) return;
+  x1_check(M, C, N, "conv1x1x: C must be 128 / 256 / 512 and N a multiple of the slice width");
+  const int S = N / x1_slice(C);
+  const int bm = C == 512 ? 32 : 64;
+  const int G = x1_grid(S, (M + bm - 1) / bm);
+  const int walkers = G / S;
+  Scratch part(stats ? (size_t)walkers * N * 2 * sizeof(float) : 0, s);
+  float* srows = part.as<float>();
+  PDT_COUNT("conv1x1x");
+#define PDT_X1(DT_, ST_, KH_, NF_, BM_) \
+  hipLaunchKernelGGL((conv1x1x_kernel<DT_, ST_, KH_, NF_, BM_>), dim3(G), dim3(256), 0, s, x, w, y, srows, M, N, S)
+#define PDT_X1C(DT_, ST_)                                   \
+  if (C == 128) PDT_X1(DT_, ST_, 2, 4, 64);                \
+  else if (C == 256) PDT_X1(DT_, ST_, 4, 2, 64);           \
+  else PDT_X1(DT_, ST_, 8, 2, 32)
+  if (dtype == kBF16) {
+    if (stats) { PDT_X1C(kBF16, true); } else { PDT_X1C(kBF16, false); }
+  } else {
+    if (stats) { PDT_X1C(kF16, true); } else { PDT_X1C(kF16, false); }
+  }
+#undef PDT_X1C
+#undef PDT_X1
+  if (stats) stat_rows_reduce_launch(srows, walkers, N * 2, stats, s);
+}
+
+void conv1x1x_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res, const uint16_t* y1,
+                         const float* coef1, const uint16_t* y2, const float* coef2, const uint8_t* mask,
+                         double* slots, int64_t M, int C, int N, int dtype, hipStream_t s) {
+  if (M <= 0) return;
+  x1_check(M, C, N, "conv1x1x_bnb: C must be 128 / 256 / 512 and N a multiple of the slice width");
+  const int S = N / x1_slice(C);
+  const int bm = C == 512 ? 32 : 64;
+  const int G = x1_grid(S, (M + bm - 1) / bm);
+  const int walkers = G / S;
+  const int KO = y2 ? 4 : 2;
+  Scratch part((size_t)walkers * N * KO * sizeof(float), s);
+  float* srows = part.as<float>();
+  PDT_COUNT("conv1x1x_bnb");
+  if (y2) PDT_COUNT("conv1x1x_bnb_2br");
+#define PDT_XB(DT_, BR_, KH_, NF_, BM_, PJ_)                                                                      \
+  hipLaunchKernelGGL((conv1x1x_bnb_kernel<DT_, BR_, KH_, NF_, BM_, PJ_>), dim3(G), dim3(256), 0, s, x, w, y, res, \
+                     y1, coef1, y2, coef2, mask, srows, M, N, S)
+#define PDT_XBC(DT_, BR_)                                 \
+  if (C == 128) PDT_XB(DT_, BR_, 2, 4, 64, 3 - BR_);     \
+  else if (C == 256) PDT_XB(DT_, BR_, 4, 2, 64, 2);      \
+  else PDT_XB(DT_, BR_, 8, 2, 32, 1)
+  if (dtype == kBF16) {
+    if (y2) { PDT_XBC(kBF16, 2); } else { PDT_XBC(kBF16, 1); }
+  } else {
+    if (y2) { PDT_XBC(kF16, 2); } else { PDT_XBC(kF16, 1); }
+  }
+#undef PDT_XBC
+#undef PDT_XB
+  stat_rows_reduce_launch(srows, walkers, N * KO, slots, s);
+}
+
+}  // namespace pdt

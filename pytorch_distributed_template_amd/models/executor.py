@@ -190,6 +190,7 @@ class ResNetExecutor:
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
         self.bk32_short = os.environ.get("PDT_BK32_SHORT", "1") == "1"
         self._c1x1 = hasattr(self.C, "conv1x1_c64")
+        self._c1x1x = hasattr(self.C, "conv1x1x")
         # a layer1 block's inner BN + ReLU applied by its consumers (conv2 forward and conv2 weight
         # gradient) to their staged input tiles in LDS; the activation relu(bn(z1)) is never written or re-read
         self.fuse_pre = os.environ.get("PDT_FUSE_PRE", "1") == "1"
@@ -444,6 +445,13 @@ class ResNetExecutor:
             if stats and fin is not None:
                 self.bn_train_finalize(fin, sp, 0, M)
             return P, Q, sp, M
+        if (R == 1 and S == 1 and st == 1 and pad == 0 and c.cout == 4 * cin and self._c1x1x and
+                self.C.conv1x1x_supported(cin, c.cout)):
+            # layers 2-4's expanding 1x1 convs (bottleneck conv3): the persistent sliced kernel (conv1x1x.hip)
+            self.C.conv1x1x(x, wt, y, sp, M, cin, c.cout)
+            if stats and fin is not None:
+                self.bn_train_finalize(fin, sp, 0, M)
+            return P, Q, sp, M
 
         def launch(bm, bn):
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
@@ -611,11 +619,15 @@ class ResNetExecutor:
             else:
                 self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, dst, phases, bm, bn,
                                      bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
-        if (self._c1x1 and bnb is not None and bnb[0] in (2, 3) and res_phase < 0 and dst == 1 and len(phases) == 1
-                and c.R == 1 and c.S == 1 and c.cin == 256 and (c.cout == 64 or (c.cout == 128 and bnb[0] == 2))
-                and H == P and W == Q and self.C.conv1x1_c64_supported(64, 256)):
-            # the binding runs the persistent 1x1 backward-data kernel (conv1x1.hip), which has no tile: no tile
-            # choice (or autotune timing) for this shape (the static tile only satisfies the binding's checks)
+        persistent = bnb is not None and bnb[0] in (2, 3) and res_phase < 0 and dst == 1 and len(phases) == 1 and \
+            c.R == 1 and c.S == 1 and H == P and W == Q and (
+                (self._c1x1 and c.cin == 256 and (c.cout == 64 or (c.cout == 128 and bnb[0] == 2)) and
+                 self.C.conv1x1_c64_supported(64, 256)) or
+                (self._c1x1x and self.C.conv1x1x_supported(c.cout, c.cin)))
+        if persistent:
+            # the binding runs a persistent 1x1 backward-data kernel (conv1x1.hip / conv1x1x.hip), which has no
+            # tile: no tile choice (or autotune timing) for this shape (the static tile only satisfies the binding's
+            # checks)
             launch(*_conv_tile(c.cin))
         else:
             key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)

@@ -116,7 +116,8 @@ R18_224_KERNELS = ("stem_fwd", "conv_l1_fwd", "conv_l1_dgrad", "wgrad3x3_c64", "
 # one-branch, two-branch (downsample block) and 128-reduction-channel forms, and the 512x128 ping-pong tile the shipped
 # tile table picks for its 1x1 convs (csrc/kernels/conv1x1.hip, conv_fwd.hip)
 R50_224_KERNELS = ("conv1x1_c64", "conv1x1_c64_bnb_1br", "conv1x1_c64_bnb_2br", "conv1x1_c64_bnb_c128",
-                   "conv_pp_512x128", "stem_fwd", "conv_pp_fwd", "conv_wgrad_pp", "wgrad_stem_fused")
+                   "conv_pp_512x128", "stem_fwd", "conv_pp_fwd", "conv_wgrad_pp", "wgrad_stem_fused", "conv1x1x",
+                   "conv1x1x_bnb", "conv1x1x_bnb_2br")
 
 
 @pytest.mark.parametrize("arch,N", [("resnet18", 16), ("resnet18", 32), ("resnet50", 8), ("resnet34", 4),

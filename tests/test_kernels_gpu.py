@@ -894,6 +894,93 @@ def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
         assert torch.allclose(s1[:, k], (d * xh).sum(0), rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cin", [128, 256, 512])
+@pytest.mark.parametrize("M", [3000 + 37, 40000 + 5])
+def test_conv1x1x_matches_implicit_gemm(dtype, cin, M):
+    """Persistent sliced 1x1 cin -> 4 cin conv (conv1x1x.hip: ResNet-50 layers 2-4 conv3) vs the implicit-GEMM conv_fwd
+    on the same operands: outputs bit-identical (same MFMA K order), BN statistics equal to fp64 sums of the stored
+    outputs; M tails and walkers with several tiles (M = 40005)."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    N = 4 * cin
+    if not C.conv1x1x_supported(cin, N):
+        pytest.skip("PDT_CONV1X1X=0")
+    torch.manual_seed(23)
+    x = _rand16(M, cin, dtype=dtype)
+    w = _rand16(N, cin, dtype=dtype, scale=(1.0 / cin) ** 0.5)
+    y_ref = torch.empty(M, N, dtype=dtype, device=DEV)
+    C.conv_fwd(x, w, y_ref, None, None, 1, 1, M, cin, N, 1, 1, 1, M, 1, 1, 0, 0, 1, 1, 1, M, 1, 1, 0, 0,
+               128, 128, 64, 0)
+    cnt0 = dict(C.dispatch_counts()).get("conv1x1x", 0)
+    for stats in (False, True):
+        y = torch.full((M, N), float("nan"), dtype=dtype, device=DEV)
+        st = torch.zeros(C.stat_slots() * N * 2, dtype=torch.float64, device=DEV) if stats else None
+        C.conv1x1x(x, w, y, st, M, cin, N)
+        torch.cuda.synchronize()
+        assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
+        if stats:
+            s = st.view(-1, N, 2).sum(0)
+            yf = y.double()
+            assert torch.allclose(s[:, 0], yf.sum(0), rtol=1e-6, atol=1e-3)
+            assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
+    assert dict(C.dispatch_counts()).get("conv1x1x", 0) == cnt0 + 2
+    ref = x.float() @ w.float().t()
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("NHW", [(2, 28, 28), (3, 13, 11)])
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("cin", [128, 256, 512])
+def test_conv1x1x_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
+    """Backward-data of a 1x1 4c -> c conv (ResNet-50 layers 2-4 conv1) with the fused block-output BN-backward
+    epilogue (residual, ReLU bit of the block output, sum dz, sum dz * xhat; mode 3: a second BN branch) on the
+    persistent sliced kernel (conv1x1x.hip) vs the generic implicit-GEMM epilogue: dz bit-identical, statistics
+    equal up to summation order (and to fp64 sums of the stored dz); M tails (3 * 13 * 11 = 429 pixels)."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    C = native.C
+    N, H, W = NHW
+    Co = 4 * cin
+    torch.manual_seed(31)
+    dy = _rand16(N, H, W, cin, dtype=dtype)
+    w = _rand16(cin, 1, 1, Co, dtype=dtype, scale=(1.0 / cin) ** 0.5)
+    res = _rand16(N, H, W, Co, dtype=dtype)
+
+    def branch():
+        yb = _rand16(N, H, W, Co, dtype=dtype)
+        cb = torch.cat([torch.rand(Co, device=DEV) + 0.5, torch.randn(Co, device=DEV) * 0.3,
+                        yb.float().view(-1, Co).mean(0), torch.rand(Co, device=DEV) + 0.5]).contiguous()
+        return yb, cb
+    y1, coef1 = branch()
+    y2, coef2 = branch() if mode == 3 else (None, None)
+    K_ = 4 if mode == 3 else 2
+    om = conv.pack_relu_mask(torch.relu(_rand16(N, H, W, Co)))
+    outs = []
+    prev = C.conv1x1x_mode(0)
+    try:
+        for on in (0, 1):
+            C.conv1x1x_mode(on)
+            cnt0 = dict(C.dispatch_counts()).get("conv1x1x_bnb", 0)
+            slots = torch.zeros(C.stat_slots() * Co * K_, dtype=torch.float64, device=DEV)
+            dz = conv.conv_dgrad(dy, w, H, W, 1, 0, residual=res, bnb=(mode, y1, coef1, y2, coef2, om, slots))
+            outs.append((dz, slots.view(-1, Co, K_).sum(0)))
+            assert dict(C.dispatch_counts()).get("conv1x1x_bnb", 0) == cnt0 + on
+        torch.cuda.synchronize()
+    finally:
+        C.conv1x1x_mode(prev)
+    (dz0, s0), (dz1, s1) = outs
+    assert torch.equal(dz0.view(torch.int16), dz1.view(torch.int16))
+    assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-3)
+    d = dz1.double().view(-1, Co)
+    for k, (yb, cb) in ((1, (y1, coef1)), (3, (y2, coef2))):
+        if yb is None:
+            continue
+        xh = ((yb.float() - cb[2 * Co:3 * Co]) * cb[3 * Co:]).double().view(-1, Co)
+        assert torch.allclose(s1[:, k - 1], d.sum(0), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(s1[:, k], (d * xh).sum(0), rtol=1e-4, atol=1e-2)
+
+
 @pytest.mark.parametrize("width,groups,stride,H", [(128, 32, 1, 14), (256, 32, 2, 14), (128, 2, 1, 9),
                                                    (256, 64, 2, 8)])
 def test_grouped_conv_slices_match_torch(width, groups, stride, H):

@@ -44,11 +44,14 @@ WINDOWS = {
     "conv_wgrad_wide_kernel": {6: ("dma", 6), 3: ("dma", 3)},
     "conv1x1_c64_kernel": {16: "dma"},  # the previous tile's 16 stores stay in flight
     "conv1x1_c64_bnb_kernel": {32: "dma", 40: "dma"},  # the previous tile's 24 (32) operand loads + 8 stores
+    # conv1x1x.hip: the previous tile's stores (forward: (BM/16)*(NF/2) per wave) / operand loads + stores
+    "conv1x1x_kernel": {8: "dma", 4: "dma", 2: "dma"},
+    "conv1x1x_bnb_kernel": {32: "dma", 40: "dma", 16: "dma", 20: "dma", 8: "dma", 10: "dma"},
 }
 COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "wgrad_stem_quad_kernel",
             "wgrad_stem_rows_kernel", "conv_pp_kernel",
             "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel",
-            "conv1x1_c64_kernel", "conv1x1_c64_bnb_kernel")
+            "conv1x1_c64_kernel", "conv1x1_c64_bnb_kernel", "conv1x1x_kernel", "conv1x1x_bnb_kernel")
 
 
 def hip_flags():
