@@ -392,19 +392,26 @@ void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats,
 bool conv1x1x_supported(int64_t C, int64_t N) { return pdt::conv1x1x_supported((int)C, (int)N); }
 int64_t conv1x1x_mode(int64_t set) { return pdt::conv1x1x_mode((int)set); }
 
-void conv1x1x(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M, int64_t C, int64_t N) {
+// st > 1: stride-st 1x1 conv over nimg x H x W input images (M = nimg * P * Q)
+void conv1x1x(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M, int64_t C, int64_t N,
+              int64_t st, int64_t nimg, int64_t H, int64_t W) {
   const int dt = dt16(x, "x");
   TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv1x1x: mixed dtypes");
   TORCH_CHECK(pdt::conv1x1x_supported((int)C, (int)N), "conv1x1x: unsupported C / N (or PDT_CONV1X1X=0)");
-  TORCH_CHECK(x.numel() >= M * C && w.numel() == N * C && y.numel() >= M * N, "conv1x1x: size mismatch");
+  const int64_t xr = st > 1 ? nimg * H * W : M;
+  TORCH_CHECK(st >= 1 && (st == 1 || nimg * ((H - 1) / st + 1) * ((W - 1) / st + 1) == M),
+              "conv1x1x: strided geometry");
+  TORCH_CHECK(x.numel() >= xr * C && w.numel() == N * C && y.numel() >= M * N, "conv1x1x: size mismatch");
   TORCH_CHECK(M * N < (int64_t(1) << 30) && M * C < (int64_t(1) << 30),
               "conv1x1x: operands exceed 2 GiB (32-bit buffer offsets)");
-  double* st = nullptr;
+  TORCH_CHECK(xr * C < (int64_t(1) << 30), "conv1x1x: input exceeds 2 GiB (32-bit buffer offsets)");
+  double* sp = nullptr;
   if (stats.has_value()) {
     TORCH_CHECK(stats->numel() >= pdt::kStatSlots * N * 2, "conv1x1x: stats buffer too small");
-    st = pd(*stats, "stats");
+    sp = pd(*stats, "stats");
   }
-  pdt::conv1x1x_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), st, M, (int)C, (int)N, dt, cur_stream());
+  pdt::conv1x1x_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), sp, M, (int)C, (int)N, dt, cur_stream(), (int)st,
+                       (int)nimg, (int)H, (int)W);
   launched("conv1x1x");
 }
 

@@ -23,8 +23,9 @@ void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, doubl
 // forward, conv1 backward-data), N split into slices of 256 (C = 128) or 128 channels (conv1x1x.hip).  w is [N][C].
 bool conv1x1x_supported(int C, int N);
 int conv1x1x_mode(int set);  // PDT_CONV1X1X seeds it; set >= 0 changes it, returns the previous mode
+// st > 1: a 1x1 / stride-st conv over nimg H x W images (M = nimg * P * Q output pixels; the downsample convs)
 void conv1x1x_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int C, int N,
-                     int dtype, hipStream_t s);
+                     int dtype, hipStream_t s, int st = 1, int nimg = 0, int H = 0, int W = 0);
 void conv1x1x_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res, const uint16_t* y1,
                          const float* coef1, const uint16_t* y2, const float* coef2, const uint8_t* mask,
                          double* slots, int64_t M, int C, int N, int dtype, hipStream_t s);

@@ -18,7 +18,8 @@
 //   * statistics accumulate in registers over all of a block's tiles; one partial row per tile walker (the S slices
 //     of a walker write disjoint channel ranges of the same row), reduced in fixed order (conv_fwd.h).
 // Configurations (register budget: 2 waves per SIMD): K = 128: 64 channels per wave, BM = 64 (S = N / 256);
-// K = 256: 32 channels per wave, BM = 64 (S = N / 128); K = 512: 32 channels per wave, BM = 32 (S = N / 128).
+// K = 256: 64 (forward) / 32 (backward-data) channels per wave, BM = 64; K = 512: 32 channels per wave, BM = 32.
+// The forward also takes stride-2 input (the downsample convs of layers 2-3: 256 -> 512, 512 -> 1024).
 #include <cstdlib>
 
 #include "../common.h"
@@ -92,10 +93,17 @@ PDT_DEVICE void x1_load_weights(typename E16<DT>::vec8 (&af)[NF][2 * KH], const 
   }
 }
 
+// strided input (a 1x1 / stride-st conv, st > 1: the downsample convs): output pixel m = (n, i, j) reads input pixel
+// (n, st*i, st*j) of an H x W image; P*Q and Q as exact reciprocals
+struct X1Geo {
+  int st, H, W, PQ, Q;
+  uint32_t pq_mul, pq_shift, q_mul, q_shift;
+};
+
 // one tile's input: XI DMA instructions per wave; rows past M read zeros (their results are not stored)
-template <int KH, int NF, int BM>
+template <int KH, int NF, int BM, bool SD = false>
 PDT_DEVICE void x1_stage(const __amdgpu_buffer_rsrc_t& rx, char* xl, int64_t t, int buf, int64_t M, int wave,
-                         int lane) {
+                         int lane, const X1Geo& g = X1Geo{}) {
   using C = X1<KH, NF, BM>;
   const int lrow = lane >> 3, pchunk = lane & 7;
 #pragma unroll
@@ -103,8 +111,16 @@ PDT_DEVICE void x1_stage(const __amdgpu_buffer_rsrc_t& rx, char* xl, int64_t t, 
     const int ins = wave * C::XI + j;
     const int hh = ins / (BM / 8), row = (ins % (BM / 8)) * 8 + lrow;
     const int64_t m = t * BM + row;
+    int64_t src = m;
+    if constexpr (SD) {
+      const uint32_t mu = (uint32_t)m;
+      const uint32_t n = fdiv(mu, FastDiv{g.pq_mul, g.pq_shift});
+      const uint32_t rem = mu - n * (uint32_t)g.PQ;
+      const uint32_t i = fdiv(rem, FastDiv{g.q_mul, g.q_shift}), jj = rem - i * (uint32_t)g.Q;
+      src = ((int64_t)n * g.H + (int64_t)g.st * i) * g.W + (int64_t)g.st * jj;
+    }
     const uint32_t off =
-        m < M ? (uint32_t)(m * (KH * kXRowB) + hh * kXRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
+        m < M ? (uint32_t)(src * (KH * kXRowB) + hh * kXRowB + ((pchunk ^ ((row >> 1) & 7)) << 4)) : kOOB;
     buf_lds16_asm(rx, xl + buf * C::TILE + ins * 1024, off);
   }
 }
@@ -145,10 +161,12 @@ PDT_DEVICE uint4 x1_pack(const uint16_t (&o)[8]) {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------ forward
-template <int DT, bool STATS, int KH, int NF, int BM>
+// SD: strided input (X1Geo; x holds x_rows pixels)
+template <int DT, bool STATS, int KH, int NF, int BM, bool SD>
 __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __restrict__ x,
                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                                                          float* __restrict__ srows, int64_t M, int N, int S) {
+                                                          float* __restrict__ srows, int64_t M, int N, int S,
+                                                          int64_t x_rows, X1Geo geo) {
   using C = X1<KH, NF, BM>;
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -161,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __rest
   const int Gs = gridDim.x / S;
   const int n0 = mp.slice * C::NS;
   const int64_t tiles = (M + BM - 1) / BM;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * KH * kXRowB));
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(x_rows * KH * kXRowB));
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)((int64_t)N * KH * kXRowB));
 
   vec8 af[NF][2 * KH];
@@ -174,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __rest
     for (int r = 0; r < 4; ++r) { ssum[i][r] = 0.f; ssq[i][r] = 0.f; }
 
   int64_t t = mp.walker;
-  if (t < tiles) x1_stage<KH, NF, BM>(rx, smem, t, 0, M, wave, lane);
+  if (t < tiles) x1_stage<KH, NF, BM, SD>(rx, smem, t, 0, M, wave, lane, geo);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int buf = 0;
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __rest
       __builtin_amdgcn_sched_barrier(0);
     }
     first = false;
-    if (t + Gs < tiles) x1_stage<KH, NF, BM>(rx, smem, t + Gs, buf ^ 1, M, wave, lane);
+    if (t + Gs < tiles) x1_stage<KH, NF, BM, SD>(rx, smem, t + Gs, buf ^ 1, M, wave, lane, geo);
     const char* xb = smem + buf * C::TILE;
 #pragma unroll
     for (int s = 0; s < BM / 32; ++s) {
@@ -415,7 +433,17 @@ int x1_cus() {
   return cus;
 }
 
-int x1_slice(int C) { return C == 128 ? 256 : 128; }  // NS of the configuration for C reduction channels
+// forward, C = 256: 64 channels per wave as for C = 128 (slices of 256: half the L2 re-reads of the input; ResNet-50
+// 72.68 -> 72.27 ms/step, same box); PDT_X1_WIDE=0: 32 channels per wave (A/B)
+bool x1_wide() {
+  static const bool on = [] {
+    const char* e = getenv("PDT_X1_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// NS of C's configuration (the backward-data kernel has no register room for the wide C = 256 variant)
+int x1_slice(int C, bool fwd) { return C == 128 || (C == 256 && fwd && x1_wide()) ? 256 : 128; }
 
 // grid: 2 blocks per CU, a multiple of 8 * S (every XCD holds whole walkers), at least one walker per XCD
 int x1_grid(int S, int64_t tiles) {
@@ -448,33 +476,52 @@ int conv1x1x_mode(int set) {
 
 bool conv1x1x_supported(int C, int N) {
   if (!conv1x1x_mode(-1) || !(C == 128 || C == 256 || C == 512) || N <= 0) return false;
-  const int ns = x1_slice(C);
+  const int ns = x1_slice(C, false);  // (the narrower slice: N must suit both kernels)
   return N % ns == 0 && N / ns <= 32;
 }
 
 void conv1x1x_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int C, int N,
-                     int dtype, hipStream_t s) {
+                     int dtype, hipStream_t s, int st, int nimg, int H, int W) {
   if (M <= 0) return;
   x1_check(M, C, N, "conv1x1x: C must be 128 / 256 / 512 and N a multiple of the slice width");
-  const int S = N / x1_slice(C);
+  X1Geo geo{};
+  int64_t x_rows = M;
+  const bool sd = st > 1;
+  if (sd) {
+    const int P = (H - 1) / st + 1, Q = (W - 1) / st + 1;
+    if ((int64_t)nimg * P * Q != M || (int64_t)nimg * H * W * C >= (int64_t(1) << 30))
+      pdt_hip_fail("conv1x1x: strided geometry (M != N * P * Q, or input past 32-bit offsets)", hipErrorInvalidValue,
+                   __FILE__, __LINE__);
+    const FastDiv f1 = make_fastdiv((uint32_t)(P * Q)), f2 = make_fastdiv((uint32_t)Q);
+    geo = X1Geo{st, H, W, P * Q, Q, f1.mul, f1.shift, f2.mul, f2.shift};
+    x_rows = (int64_t)nimg * H * W;
+  }
+  const bool wide = C == 256 && N % 256 == 0 && x1_slice(C, true) == 256;
+  const int S = N / (wide ? 256 : x1_slice(C, false));
   const int bm = C == 512 ? 32 : 64;
   const int G = x1_grid(S, (M + bm - 1) / bm);
   const int walkers = G / S;
   Scratch part(stats ? (size_t)walkers * N * 2 * sizeof(float) : 0, s);
   float* srows = part.as<float>();
   PDT_COUNT("conv1x1x");
-#define PDT_X1(DT_, ST_, KH_, NF_, BM_) \
-  hipLaunchKernelGGL((conv1x1x_kernel<DT_, ST_, KH_, NF_, BM_>), dim3(G), dim3(256), 0, s, x, w, y, srows, M, N, S)
-#define PDT_X1C(DT_, ST_)                                   \
-  if (C == 128) PDT_X1(DT_, ST_, 2, 4, 64);                \
-  else if (C == 256) PDT_X1(DT_, ST_, 4, 2, 64);           \
-  else PDT_X1(DT_, ST_, 8, 2, 32)
+  if (sd) PDT_COUNT("conv1x1x_strided");
+#define PDT_X1(DT_, ST_, KH_, NF_, BM_, SD_)                                                                     \
+  hipLaunchKernelGGL((conv1x1x_kernel<DT_, ST_, KH_, NF_, BM_, SD_>), dim3(G), dim3(256), 0, s, x, w, y, srows, M, \
+                     N, S, x_rows, geo)
+#define PDT_X1S(DT_, ST_, SD_)                                \
+  if (C == 128) PDT_X1(DT_, ST_, 2, 4, 64, SD_);             \
+  else if (wide) PDT_X1(DT_, ST_, 4, 4, 64, SD_);           \
+  else if (C == 256) PDT_X1(DT_, ST_, 4, 2, 64, SD_);        \
+  else PDT_X1(DT_, ST_, 8, 2, 32, SD_)
+#define PDT_X1C(DT_, ST_) \
+  if (sd) { PDT_X1S(DT_, ST_, true); } else { PDT_X1S(DT_, ST_, false); }
   if (dtype == kBF16) {
     if (stats) { PDT_X1C(kBF16, true); } else { PDT_X1C(kBF16, false); }
   } else {
     if (stats) { PDT_X1C(kF16, true); } else { PDT_X1C(kF16, false); }
   }
 #undef PDT_X1C
+#undef PDT_X1S
 #undef PDT_X1
   if (stats) stat_rows_reduce_launch(srows, walkers, N * 2, stats, s);
 }
@@ -484,7 +531,7 @@ void conv1x1x_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
                          double* slots, int64_t M, int C, int N, int dtype, hipStream_t s) {
   if (M <= 0) return;
   x1_check(M, C, N, "conv1x1x_bnb: C must be 128 / 256 / 512 and N a multiple of the slice width");
-  const int S = N / x1_slice(C);
+  const int S = N / x1_slice(C, false);
   const int bm = C == 512 ? 32 : 64;
   const int G = x1_grid(S, (M + bm - 1) / bm);
   const int walkers = G / S;

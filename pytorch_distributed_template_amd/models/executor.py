@@ -445,10 +445,12 @@ class ResNetExecutor:
             if stats and fin is not None:
                 self.bn_train_finalize(fin, sp, 0, M)
             return P, Q, sp, M
-        if (R == 1 and S == 1 and st == 1 and pad == 0 and c.cout == 4 * cin and self._c1x1x and
+        if (R == 1 and S == 1 and pad == 0 and self._c1x1x and (
+                (st == 1 and c.cout == 4 * cin) or (st == 2 and c.cout == 2 * cin)) and
                 self.C.conv1x1x_supported(cin, c.cout)):
-            # layers 2-4's expanding 1x1 convs (bottleneck conv3): the persistent sliced kernel (conv1x1x.hip)
-            self.C.conv1x1x(x, wt, y, sp, M, cin, c.cout)
+            # layers 2-4's expanding 1x1 convs (bottleneck conv3 and the stride-2 downsample convs of layers 2-3):
+            # the persistent sliced kernel (conv1x1x.hip)
+            self.C.conv1x1x(x, wt, y, sp, M, cin, c.cout, st, N, H, W)
             if stats and fin is not None:
                 self.bn_train_finalize(fin, sp, 0, M)
             return P, Q, sp, M

@@ -916,7 +916,7 @@ def test_conv1x1x_matches_implicit_gemm(dtype, cin, M):
     for stats in (False, True):
         y = torch.full((M, N), float("nan"), dtype=dtype, device=DEV)
         st = torch.zeros(C.stat_slots() * N * 2, dtype=torch.float64, device=DEV) if stats else None
-        C.conv1x1x(x, w, y, st, M, cin, N)
+        C.conv1x1x(x, w, y, st, M, cin, N, 1, 0, 0, 0)
         torch.cuda.synchronize()
         assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
         if stats:
@@ -926,6 +926,41 @@ def test_conv1x1x_matches_implicit_gemm(dtype, cin, M):
             assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
     assert dict(C.dispatch_counts()).get("conv1x1x", 0) == cnt0 + 2
     ref = x.float() @ w.float().t()
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cin,NHW", [(256, (2, 56, 56)), (512, (3, 28, 28)), (256, (3, 13, 11)), (128, (2, 9, 10))])
+def test_conv1x1x_strided_matches_implicit_gemm(dtype, cin, NHW):
+    """The downsample conv geometry (1x1, stride 2, cin -> 2 cin) on the sliced persistent kernel's strided-input
+    path vs the implicit-GEMM conv_fwd: outputs bit-identical, statistics equal to fp64 sums (odd H / W: the last
+    input row / column is read, P = ceil(H / 2))."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    Nimg, H, W = NHW
+    Co = 2 * cin
+    if not C.conv1x1x_supported(cin, Co):
+        pytest.skip("PDT_CONV1X1X=0")
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    M = Nimg * P * Q
+    torch.manual_seed(27)
+    x = _rand16(Nimg, H, W, cin, dtype=dtype)
+    w = _rand16(Co, cin, dtype=dtype, scale=(1.0 / cin) ** 0.5)
+    y_ref = torch.empty(M, Co, dtype=dtype, device=DEV)
+    C.conv_fwd(x, w, y_ref, None, None, Nimg, H, W, cin, Co, 1, 1, P, Q, 2, 2, 0, 0, 1, 1, P, Q, 1, 1, 0, 0,
+               128, 128, 64, 0)
+    y = torch.full((M, Co), float("nan"), dtype=dtype, device=DEV)
+    st = torch.zeros(C.stat_slots() * Co * 2, dtype=torch.float64, device=DEV)
+    cnt0 = dict(C.dispatch_counts()).get("conv1x1x_strided", 0)
+    C.conv1x1x(x, w, y, st, M, cin, Co, 2, Nimg, H, W)
+    torch.cuda.synchronize()
+    assert dict(C.dispatch_counts()).get("conv1x1x_strided", 0) == cnt0 + 1
+    assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
+    s = st.view(-1, Co, 2).sum(0)
+    yf = y.double()
+    assert torch.allclose(s[:, 0], yf.sum(0), rtol=1e-6, atol=1e-3)
+    assert torch.allclose(s[:, 1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
+    ref = x[:, ::2, ::2].reshape(M, cin).float() @ w.float().t()
     assert _rel(y, ref) < 1e-2
 
 
