@@ -333,7 +333,8 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     a.stats = pd(*bn_slots, "bn_slots");
   }
   if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 &&
-      (K == 64 || (K == 128 && bnb == 2)) && C == 256 && H == P && W == Q && pdt::conv1x1_c64_supported(64, C)) {
+      (K == 64 || (K == 128 && bnb == 2)) && C == 256 && H == P && W == Q && pdt::conv1x1_c64_supported(64, C) &&
+      !(pdt::conv1x1x_prefer_l1() && pdt::conv1x1x_bnb_supported((int)K, (int)C))) {
     const auto& f = phases[0];
     if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
       // 1x1 256 -> 64 | 128 conv's backward-data with the block-output BN-backward epilogue: persistent kernel
@@ -347,7 +348,7 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     }
   }
   if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 && H == P && W == Q &&
-      pdt::conv1x1x_supported((int)K, (int)C)) {
+      pdt::conv1x1x_bnb_supported((int)K, (int)C)) {
     const auto& f = phases[0];
     if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
       // ResNet-50 layers 2-4: 1x1 C -> 4C backward-data (conv1 of a bottleneck) with the block-output BN-backward
@@ -391,6 +392,7 @@ void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats,
 // sliced kernel (conv1x1x.hip); y[M][N] from x[M][C] and w[N][C], optional BN statistics (fp64 slots)
 bool conv1x1x_supported(int64_t C, int64_t N) { return pdt::conv1x1x_supported((int)C, (int)N); }
 int64_t conv1x1x_mode(int64_t set) { return pdt::conv1x1x_mode((int)set); }
+int64_t conv1x1x_l1_mode(int64_t set) { return pdt::conv1x1x_l1_mode((int)set); }
 
 // st > 1: stride-st 1x1 conv over nimg x H x W input images (M = nimg * P * Q)
 void conv1x1x(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M, int64_t C, int64_t N,
@@ -1341,6 +1343,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1x", &conv1x1x);
   m.def("conv1x1x_supported", &conv1x1x_supported);
   m.def("conv1x1x_mode", &conv1x1x_mode);
+  m.def("conv1x1x_l1_mode", &conv1x1x_l1_mode);
   m.def("conv_fwd_pre_supported", &conv_fwd_pre_supported);
   m.def("bn_slot_sum", &bn_slot_sum);
   m.def("stat_slots", &stat_slots);

@@ -21,6 +21,7 @@
 // K = 256: 64 (forward) / 32 (backward-data) channels per wave, BM = 64; K = 512: 32 channels per wave, BM = 32.
 // The forward also takes stride-2 input (the downsample convs of layers 2-3: 256 -> 512, 512 -> 1024).
 #include <cstdlib>
+#include <type_traits>
 
 #include "../common.h"
 #include "conv1x1.h"
@@ -100,8 +101,9 @@ struct X1Geo {
   uint32_t pq_mul, pq_shift, q_mul, q_shift;
 };
 
-// one tile's input: XI DMA instructions per wave; rows past M read zeros (their results are not stored)
-template <int KH, int NF, int BM, bool SD = false>
+// one tile's input: XI DMA instructions per wave; rows past M read zeros (their results are not stored) -- CL: row
+// M - 1 instead (every DMA piece a real access: counted waits that assume in-order retirement)
+template <int KH, int NF, int BM, bool SD = false, bool CL = false>
 PDT_DEVICE void x1_stage(const __amdgpu_buffer_rsrc_t& rx, char* xl, int64_t t, int buf, int64_t M, int wave,
                          int lane, const X1Geo& g = X1Geo{}) {
   using C = X1<KH, NF, BM>;
@@ -110,7 +112,8 @@ PDT_DEVICE void x1_stage(const __amdgpu_buffer_rsrc_t& rx, char* xl, int64_t t, 
   for (int j = 0; j < C::XI; ++j) {
     const int ins = wave * C::XI + j;
     const int hh = ins / (BM / 8), row = (ins % (BM / 8)) * 8 + lrow;
-    const int64_t m = t * BM + row;
+    const int64_t m0 = t * BM + row;
+    const int64_t m = CL && m0 >= M ? M - 1 : m0;
     int64_t src = m;
     if constexpr (SD) {
       const uint32_t mu = (uint32_t)m;
@@ -265,7 +268,57 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __rest
 // dX = dY * W with the block-output BN-backward epilogue (conv1x1.hip's conv1x1_c64_bnb_kernel, generalised):
 // v = acc + res, dz = v where the block output's ReLU bit is set (else 0), stored rounded; per channel sum(dz) and
 // sum(dz * (y1 - mean1) * invstd1) (BR = 2: + sum(dz * (y2 - mean2) * invstd2)) into the walker's statistics row.
-// PJ: pixel fragments per sub-tile (1 where 2 would not fit the register budget).
+//
+// Every vector-memory operation of the loop is issued through inline asm and waited for with COUNTED vmcnt: with
+// compiler-visible operand loads, the compiler's own waits (exact only for the operations it knows of) also retire
+// the next tile's LDS-DMA issued ahead of them, and a partial-tile branch makes it fall back to vmcnt(0) at the loop
+// top -- the DMA latency was exposed on every tile.  Here the epilogue operands (residual, BN inputs, the mask byte)
+// of sub-tile s + 1 are loaded while sub-tile s computes (the next tile's first sub-tile during the last one), and a
+// walker's last tile still issues the DMA and operand prefetch of the tile after it, so every wait count is a constant.
+// Loads and DMA pieces of rows past M read row M - 1 (never an out-of-range access, whose early retirement would break
+// the in-order count); stores keep the true row, and the range check drops those past M.  The counts cover LOADS only
+// (per sub-tile NL operand loads): the wait for sub-tile s's operands leaves the younger DMA pieces / loads in flight,
+// the loop-top wait for the tile's DMA the previous tile's SUB * NL loads; stores never relax a wait.
+// (Counting the stores too -- vmcnt(NS + NL) -- gave stale operands on the C = 64 configuration: round 5.)
+// PJ: pixel fragments per sub-tile (two operand sets must fit the register budget).
+namespace {
+PDT_DEVICE u32x4v x1_ld16(const __amdgpu_buffer_rsrc_t& r, uint32_t off) {
+  u32x4v v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+  return v;
+}
+PDT_DEVICE uint32_t x1_ld1(const __amdgpu_buffer_rsrc_t& r, uint32_t off) {
+  uint32_t v;
+  asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+  return v;
+}
+// (s_nop 1: a >8-byte store reads its data VGPRs after issue -- the next instructions hipcc places behind the opaque
+// asm may overwrite them; it pads only the stores it emits itself)
+PDT_DEVICE void x1_st16(const __amdgpu_buffer_rsrc_t& r, uint32_t off, u32x4v v) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" : : "v"(v), "v"(off), "s"(r) : "memory");
+}
+template <int SET, int PJ, int NP, int BR>
+PDT_DEVICE void x1_pin(u32x4v (&rr)[2][PJ][NP], u32x4v (&yy)[2][PJ][NP], u32x4v (&yz)[2][BR == 2 ? PJ : 1][NP],
+                       uint32_t (&mb)[2][PJ][NP]) {
+#pragma unroll
+  for (int j = 0; j < PJ; ++j)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      asm volatile("" : "+v"(rr[SET][j][p]), "+v"(yy[SET][j][p]), "+v"(mb[SET][j][p]));
+      if constexpr (BR == 2) asm volatile("" : "+v"(yz[SET][j][p]));
+    }
+}
+template <int N>
+PDT_DEVICE void x1_vm_wait_asm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+#ifdef PDT_X1_WAIT0
+  asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+#else
+  asm volatile("s_waitcnt vmcnt(%0)" : : "n"(N) : "memory");
+#endif
+}
+}  // namespace
+
 template <int DT, int BR, int KH, int NF, int BM, int PJ>
 __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
@@ -276,9 +329,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
   using C = X1<KH, NF, BM>;
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
-  // per wave and tile, after the next tile's DMA: residual + y1 (+ y2) 16-B loads, one mask byte, one store per
-  // (pixel fragment, channel pair)
-  constexpr int OPS = (BM / 16) * (NF / 2) * (BR == 2 ? 5 : 4);
+  constexpr int NP = NF / 2;                          // channel pairs (8 consecutive channels each) per lane
+  constexpr int SUB = BM / (16 * PJ);                 // sub-tiles per tile
+  constexpr int NL = PJ * NP * (BR == 2 ? 4 : 3);     // operand loads per sub-tile (16-B res, y1 (, y2); mask byte)
+  constexpr int NS = PJ * NP;                         // stores per sub-tile
+  constexpr int TOP = SUB * NL;                       // loads in flight behind the next tile's DMA at the loop top
+  static_assert(SUB % 2 == 0 && TOP < 64 && C::XI + NL < 64, "conv1x1x_bnb wait counts");
   __shared__ __attribute__((aligned(1024))) char smem[C::AREA + BR * 2 * C::NS * 4];
   float* const cf = (float*)(smem + C::AREA);  // cf[(branch * 2 + 0 | 1) * NS + c]: mean | invstd of the slice
   const int tid = threadIdx.x, lane = tid & 63;
@@ -290,6 +346,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
   const int64_t tiles = (M + BM - 1) / BM;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (uint32_t)(M * KH * kXRowB));
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (uint32_t)((int64_t)N * KH * kXRowB));
+  const uint32_t obytes = (uint32_t)(M * N * 2);  // < 2^31 (host check): rows past M are out of range
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(res, obytes), ry1 = make_rsrc(y1, obytes);
+  const __amdgpu_buffer_rsrc_t ry2 = make_rsrc(BR == 2 ? y2 : y1, obytes), rdz = make_rsrc(y, obytes);
+  const __amdgpu_buffer_rsrc_t rmask = make_rsrc(mask, (uint32_t)(M * N / 8));
 
   if (tid < C::NS) {
     cf[tid] = coef1[2 * N + n0 + tid];
@@ -302,9 +362,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
   vec8 af[NF][2 * KH];
   x1_load_weights<DT, KH, NF, BM>(af, rw, smem, n0, wave, lane);  // (its barriers also publish cf)
 
-  float s0[NF / 2][8], s1[NF / 2][8], s2[BR == 2 ? NF / 2 : 1][8];
+  float s0[NP][8], s1[NP][8], s2[BR == 2 ? NP : 1][8];
 #pragma unroll
-  for (int p = 0; p < NF / 2; ++p)
+  for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       s0[p][e] = 0.f;
@@ -312,66 +372,97 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
       if constexpr (BR == 2) s2[p][e] = 0.f;
     }
 
+  // operand sets: [set][pixel fragment j][pair p]
+  u32x4v rr[2][PJ][NP], yy[2][PJ][NP], yz[2][BR == 2 ? PJ : 1][NP];
+  uint32_t mb[2][PJ][NP];
+  // element offset of (pixel fragment j of sub-tile s of tile t, pair p); CLAMP: operand loads read row M - 1 for
+  // rows past M (every load a real access -- out-of-range ones could retire ahead of older loads), stores use the
+  // true row and the range check drops them
+  auto eoff = [&](int64_t t, int s, int j, int p, bool clamp) -> uint32_t {
+    int64_t m = t * BM + (s * PJ + j) * 16 + fr;
+    if (clamp) m = m < M ? m : M - 1;
+    return (uint32_t)(m * N + n0 + wave * C::WCH + p * 32 + 8 * fq);
+  };
+  auto load_ops = [&](auto SETc, int64_t t, int s) {
+    constexpr int SET = decltype(SETc)::value;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const uint32_t o = eoff(t, s, j, p, true);
+        rr[SET][j][p] = x1_ld16(rres, o * 2u);
+        yy[SET][j][p] = x1_ld16(ry1, o * 2u);
+        if constexpr (BR == 2) yz[SET][j][p] = x1_ld16(ry2, o * 2u);
+        mb[SET][j][p] = x1_ld1(rmask, o >> 3);
+      }
+  };
+  auto pin_ops = [&](auto SETc) {  // after the covering wait: no use may be scheduled ahead of it
+    x1_pin<decltype(SETc)::value, PJ, NP, BR>(rr, yy, yz, mb);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
   int64_t t = mp.walker;
-  if (t < tiles) x1_stage<KH, NF, BM>(rx, smem, t, 0, M, wave, lane);
+  if (t < tiles) {
+    x1_stage<KH, NF, BM, false, true>(rx, smem, t, 0, M, wave, lane);
+    load_ops(I0{}, t, 0);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  pin_ops(I0{});
   int buf = 0;
   bool first = true;
   for (; t < tiles; t += Gs) {
     if (!first) {
-      x1_vm_wait<OPS>();
+      x1_vm_wait_asm<TOP>();  // this tile's DMA; the previous tile's prefetch loads stay in flight
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     }
     first = false;
-    if (t + Gs < tiles) x1_stage<KH, NF, BM>(rx, smem, t + Gs, buf ^ 1, M, wave, lane);
+    // the next tile's DMA (past the walker's last tile: all rows out of range, zeros into the free ring slot)
+    x1_stage<KH, NF, BM, false, true>(rx, smem, t + Gs, buf ^ 1, M, wave, lane);
     const char* xb = smem + buf * C::TILE;
-#pragma unroll
-    for (int s = 0; s < BM / (16 * PJ); ++s) {
-      // epilogue operands first (independent of the MFMAs); rows past M load row M-1 and are not stored
-      uint4 rr[PJ][NF / 2], yy[PJ][NF / 2], yz[BR == 2 ? PJ : 1][NF / 2];
-      uint32_t mb[PJ][NF / 2];
-#pragma unroll
-      for (int j = 0; j < PJ; ++j) {
-        int64_t m = t * BM + (s * PJ + j) * 16 + fr;
-        m = m < M ? m : M - 1;
-#pragma unroll
-        for (int p = 0; p < NF / 2; ++p) {
-          const int64_t o = m * N + n0 + wave * C::WCH + p * 32 + 8 * fq;
-          rr[j][p] = *(const uint4*)(res + o);
-          yy[j][p] = *(const uint4*)(y1 + o);
-          if constexpr (BR == 2) yz[j][p] = *(const uint4*)(y2 + o);
-          mb[j][p] = mask[o >> 3];
-        }
-      }
+    auto sub = [&](auto SETc, int s) {
+      constexpr int SET = decltype(SETc)::value;
+      // prefetch the next sub-tile's operands (the next tile's first one during the last sub-tile)
+      if (s + 1 < SUB)
+        load_ops(std::integral_constant<int, SET ^ 1>{}, t, s + 1);
+      else
+        load_ops(std::integral_constant<int, SET ^ 1>{}, t + Gs, 0);
       f32x4_t acc[NF][PJ];
       x1_mma<DT, KH, NF, BM, PJ>(acc, af, xb, s, lane);
+      // wait for this sub-tile's operands: younger than them are the next tile's DMA (s == 0) or the previous
+      // sub-tile's stores (s > 0), and the prefetch just issued
+      if (s == 0)
+        x1_vm_wait_asm<C::XI + NL>();
+      else
+        x1_vm_wait_asm<NL>();
+      pin_ops(SETc);
 #pragma unroll
       for (int j = 0; j < PJ; ++j) {
         const int64_t m = t * BM + (s * PJ + j) * 16 + fr;
 #pragma unroll
-        for (int p = 0; p < NF / 2; ++p) {
-          const uint32_t rw4[4] = {rr[j][p].x, rr[j][p].y, rr[j][p].z, rr[j][p].w};
-          const uint32_t yw4[4] = {yy[j][p].x, yy[j][p].y, yy[j][p].z, yy[j][p].w};
+        for (int p = 0; p < NP; ++p) {
+          const u32x4v r4 = rr[SET][j][p], y4 = yy[SET][j][p];
           uint16_t o[8];
           float q1[8], q2[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(rw4[e >> 1] >> (16 * (e & 1))));
-            if (!((mb[j][p] >> e) & 1u)) v = 0.f;
+            float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(r4[e >> 1] >> (16 * (e & 1))));
+            if (!((mb[SET][j][p] >> e) & 1u)) v = 0.f;
             o[e] = E::from_f(v);
-            q1[e] = E::to_f((uint16_t)(yw4[e >> 1] >> (16 * (e & 1))));
+            q1[e] = E::to_f((uint16_t)(y4[e >> 1] >> (16 * (e & 1))));
           }
           if constexpr (BR == 2) {
-            const uint32_t zw4[4] = {yz[j][p].x, yz[j][p].y, yz[j][p].z, yz[j][p].w};
+            const u32x4v z4 = yz[SET][j][p];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) q2[e] = E::to_f((uint16_t)(zw4[e >> 1] >> (16 * (e & 1))));
+            for (int e = 0; e < 8; ++e) q2[e] = E::to_f((uint16_t)(z4[e >> 1] >> (16 * (e & 1))));
           }
+          const uint4 pk = x1_pack(o);
+          x1_st16(rdz, eoff(t, s, j, p, false) * 2u, u32x4v{pk.x, pk.y, pk.z, pk.w});  // rows past M: dropped
           if (m < M) {
             const int cl = wave * C::WCH + p * 32 + 8 * fq;  // slice-local channel
-            *(uint4*)(y + m * N + n0 + cl) = x1_pack(o);
             const float4 ma = *(const float4*)(cf + cl), mb4 = *(const float4*)(cf + cl + 4);
             const float4 ia = *(const float4*)(cf + C::NS + cl), ib = *(const float4*)(cf + C::NS + cl + 4);
             const float mu[8] = {ma.x, ma.y, ma.z, ma.w, mb4.x, mb4.y, mb4.z, mb4.w};
@@ -393,12 +484,21 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
           }
         }
       }
+    };
+#pragma unroll
+    for (int s2i = 0; s2i < SUB; s2i += 2) {
+      sub(I0{}, s2i);
+      sub(I1{}, s2i + 1);
     }
     buf ^= 1;
   }
+  // the last stores and the last (unused) operand prefetch -- set 0, pinned behind the wait: until then its registers
+  // may not be handed to the statistics reduction below (a late load would overwrite it; found in round 5)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pin_ops(I0{});
 
 #pragma unroll
-  for (int p = 0; p < NF / 2; ++p)
+  for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       s0[p][e] = row16_sum(s0[p][e]);
@@ -409,7 +509,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
     constexpr int KO = BR == 2 ? 4 : 2;
     float* dst = srows + (int64_t)mp.walker * N * KO;
 #pragma unroll
-    for (int p = 0; p < NF / 2; ++p)
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = n0 + wave * C::WCH + p * 32 + 8 * fq + e;
@@ -443,7 +543,7 @@ bool x1_wide() {
   return on;
 }
 // NS of C's configuration (the backward-data kernel has no register room for the wide C = 256 variant)
-int x1_slice(int C, bool fwd) { return C == 128 || (C == 256 && fwd && x1_wide()) ? 256 : 128; }
+int x1_slice(int C, bool fwd) { return C <= 128 || (C == 256 && fwd && x1_wide()) ? 256 : 128; }
 
 // grid: 2 blocks per CU, a multiple of 8 * S (every XCD holds whole walkers), at least one walker per XCD
 int x1_grid(int S, int64_t tiles) {
@@ -474,11 +574,35 @@ int conv1x1x_mode(int set) {
   return prev;
 }
 
+bool x1_n_ok(int C, int N);
+
 bool conv1x1x_supported(int C, int N) {
   if (!conv1x1x_mode(-1) || !(C == 128 || C == 256 || C == 512) || N <= 0) return false;
+  return x1_n_ok(C, N);
+}
+
+// the backward-data kernel also takes C = 64 (ResNet-50 layer1's conv1 backward-data; the binding prefers it over
+// conv1x1_c64_bnb when PDT_X1_L1=1)
+bool conv1x1x_bnb_supported(int C, int N) {
+  if (!conv1x1x_mode(-1) || !(C == 64 || C == 128 || C == 256 || C == 512) || N <= 0) return false;
+  return x1_n_ok(C, N);
+}
+
+bool x1_n_ok(int C, int N) {
   const int ns = x1_slice(C, false);  // (the narrower slice: N must suit both kernels)
   return N % ns == 0 && N / ns <= 32;
 }
+
+int conv1x1x_l1_mode(int set) {
+  static int on = [] {
+    const char* e = getenv("PDT_X1_L1");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  const int prev = on;
+  if (set >= 0) on = set;
+  return prev;
+}
+bool conv1x1x_prefer_l1() { return conv1x1x_l1_mode(-1) != 0; }
 
 void conv1x1x_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int C, int N,
                      int dtype, hipStream_t s, int st, int nimg, int H, int W) {
@@ -530,8 +654,12 @@ void conv1x1x_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
                          const float* coef1, const uint16_t* y2, const float* coef2, const uint8_t* mask,
                          double* slots, int64_t M, int C, int N, int dtype, hipStream_t s) {
   if (M <= 0) return;
-  x1_check(M, C, N, "conv1x1x_bnb: C must be 128 / 256 / 512 and N a multiple of the slice width");
-  const int S = N / x1_slice(C, false);
+  if (!conv1x1x_bnb_supported(C, N))
+    pdt_hip_fail("conv1x1x_bnb: C must be 64 / 128 / 256 / 512 and N a multiple of the slice width",
+                 hipErrorInvalidValue, __FILE__, __LINE__);
+  if (M * N >= (int64_t(1) << 30) || M * C >= (int64_t(1) << 30))
+    pdt_hip_fail("conv1x1x_bnb: operands exceed 32-bit buffer offsets", hipErrorInvalidValue, __FILE__, __LINE__);
+  const int S = N / (C <= 128 && !y2 ? 256 : 128);  // the configuration's slice (PDT_XBC below)
   const int bm = C == 512 ? 32 : 64;
   const int G = x1_grid(S, (M + bm - 1) / bm);
   const int walkers = G / S;
@@ -544,7 +672,10 @@ void conv1x1x_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
   hipLaunchKernelGGL((conv1x1x_bnb_kernel<DT_, BR_, KH_, NF_, BM_, PJ_>), dim3(G), dim3(256), 0, s, x, w, y, res, \
                      y1, coef1, y2, coef2, mask, srows, M, N, S)
 #define PDT_XBC(DT_, BR_)                                 \
-  if (C == 128) PDT_XB(DT_, BR_, 2, 4, 64, 3 - BR_);     \
+  if (C == 64 && BR_ == 1) PDT_XB(DT_, BR_, 1, 4, 64, 1); \
+  else if (C == 64) PDT_XB(DT_, BR_, 1, 2, 64, 2);       \
+  else if (C == 128 && BR_ == 1) PDT_XB(DT_, BR_, 2, 4, 64, 1); \
+  else if (C == 128) PDT_XB(DT_, BR_, 2, 2, 64, 2);      \
   else if (C == 256) PDT_XB(DT_, BR_, 4, 2, 64, 2);      \
   else PDT_XB(DT_, BR_, 8, 2, 32, 1)
   if (dtype == kBF16) {

@@ -93,7 +93,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     no_pk = [] if os.environ.get("PDT_PACKED_FP32") == "1" else ["-Xclang", "-target-feature", "-Xclang",
                                                                   "-packed-fp32-ops"]  # PDT_PACKED_FP32=1: A/B only
     hip_flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-                 "-munsafe-fp-atomics"] + no_pk + [f"-I{CSRC}"]
+                 "-munsafe-fp-atomics"] + no_pk + [f"-I{CSRC}"] + os.environ.get("PDT_HIP_EXTRA", "").split()
     py_inc = sysconfig.get_paths()["include"]
     cxx_flags = ["-O2", "-std=c++17", "-fPIC", f"-I{CSRC}", f"-I{py_inc}", "-D__HIP_PLATFORM_AMD__=1",
                  "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",

@@ -871,7 +871,7 @@ def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
     K_ = 4 if mode == 3 else 2
     om = conv.pack_relu_mask(torch.relu(_rand16(N, H, W, 256)))
     outs = []
-    prev = C.conv1x1_c64_mode(0)
+    prev, prev_x = C.conv1x1_c64_mode(0), C.conv1x1x_mode(0)  # off: the generic implicit-GEMM epilogue
     try:
         for on in (0, 1):
             C.conv1x1_c64_mode(on)
@@ -881,6 +881,7 @@ def test_conv1x1_c64_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
         torch.cuda.synchronize()
     finally:
         C.conv1x1_c64_mode(prev)
+        C.conv1x1x_mode(prev_x)
     (dz0, s0), (dz1, s1) = outs
     assert torch.equal(dz0.view(torch.int16), dz1.view(torch.int16))
     assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-3)
@@ -1014,6 +1015,47 @@ def test_conv1x1x_dgrad_bnb_matches_generic(dtype, NHW, mode, cin):
         xh = ((yb.float() - cb[2 * Co:3 * Co]) * cb[3 * Co:]).double().view(-1, Co)
         assert torch.allclose(s1[:, k - 1], d.sum(0), rtol=1e-4, atol=1e-2)
         assert torch.allclose(s1[:, k], (d * xh).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("mode,cin", [(2, 64), (3, 64), (2, 128)])
+@pytest.mark.parametrize("NHW", [(2, 56, 56), (3, 13, 11)])
+def test_conv1x1x_bnb_layer1_matches_c64(mode, cin, NHW):
+    """ResNet-50 layer1's 1x1 256 -> 64 | 128 backward-data with the block-output BN epilogue on the generic sliced
+    kernel (conv1x1x_l1_mode 1, the C = 64 configurations) vs the dedicated conv1x1_c64_bnb kernel: dz bit-identical,
+    statistics equal up to summation order."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    C = native.C
+    N, H, W = NHW
+    torch.manual_seed(37)
+    dy = _rand16(N, H, W, cin)
+    w = _rand16(cin, 1, 1, 256, scale=0.125)
+    res = _rand16(N, H, W, 256)
+
+    def branch():
+        yb = _rand16(N, H, W, 256)
+        cb = torch.cat([torch.rand(256, device=DEV) + 0.5, torch.randn(256, device=DEV) * 0.3,
+                        yb.float().view(-1, 256).mean(0), torch.rand(256, device=DEV) + 0.5]).contiguous()
+        return yb, cb
+    y1, coef1 = branch()
+    y2, coef2 = branch() if mode == 3 else (None, None)
+    K_ = 4 if mode == 3 else 2
+    om = conv.pack_relu_mask(torch.relu(_rand16(N, H, W, 256)))
+    outs = []
+    prev = C.conv1x1x_l1_mode(0)
+    try:
+        for on in (0, 1):
+            C.conv1x1x_l1_mode(on)
+            cnt0 = dict(C.dispatch_counts()).get("conv1x1x_bnb", 0)
+            slots = torch.zeros(C.stat_slots() * 256 * K_, dtype=torch.float64, device=DEV)
+            dz = conv.conv_dgrad(dy, w, H, W, 1, 0, residual=res, bnb=(mode, y1, coef1, y2, coef2, om, slots))
+            outs.append((dz, slots.view(-1, 256, K_).sum(0)))
+            assert dict(C.dispatch_counts()).get("conv1x1x_bnb", 0) == cnt0 + on
+        torch.cuda.synchronize()
+    finally:
+        C.conv1x1x_l1_mode(prev)
+    (dz0, s0), (dz1, s1) = outs
+    assert torch.equal(dz0.view(torch.int16), dz1.view(torch.int16))
+    assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize("width,groups,stride,H", [(128, 32, 1, 14), (256, 32, 2, 14), (128, 2, 1, 9),

@@ -16,6 +16,9 @@ result under GPU contention, not a crash):
    the youngest LDS-DMA piece (or asm operand load) it is meant to cover and the wait, on the kernel's loop path
    (walking back in layout order; entering a loop header continues from its latch: "the previous iteration").
    A spill or a reordered store inside the window breaks the count.  Windows: WINDOWS below.
+4. **store data** -- a ``..._store_dwordx3/x4`` reads its data VGPRs after issue: no VALU instruction in the next two
+   wait states may write them (hipcc pads the stores it emits; an asm store must end with ``s_nop 1`` itself -- found in
+   round 5, where the missing pad corrupted stored rows of conv1x1x_bnb).
 3. **packed FP32** -- no ``v_pk_{fma,mul,add}_f32`` anywhere: an LDS load into the source VGPRs of a packed FP32
    op issued right behind it raced on the last quarter-wave (profiles/r3_nondeterminism_root_cause.md); the build
    disables the feature (ops/_build.py), this checks it stays disabled.
@@ -46,8 +49,28 @@ WINDOWS = {
     "conv1x1_c64_bnb_kernel": {32: "dma", 40: "dma"},  # the previous tile's 24 (32) operand loads + 8 stores
     # conv1x1x.hip: the previous tile's stores (forward: (BM/16)*(NF/2) per wave) / operand loads + stores
     "conv1x1x_kernel": {8: "dma", 4: "dma", 2: "dma"},
-    "conv1x1x_bnb_kernel": {32: "dma", 40: "dma", 16: "dma", 20: "dma", 8: "dma", 10: "dma"},
 }
+
+
+def _x1_bnb_windows():
+    """conv1x1x_bnb_kernel<DT, BR, KH, NF, BM, PJ> (conv1x1x.hip): per configuration, the loop-top wait covers the
+    tile's DMA (SUB * NL younger loads; stores are not counted on), and the sub-tile waits cover that sub-tile's
+    operand loads with the NL-load prefetch of the next sub-tile left in flight (skip NL), behind the next tile's DMA
+    (XI, sub-tile 0).  (The walk counts stores too, so a window is >= the loads-only count.)"""
+    out = {}
+    for kh, nf, bm, pj, brs in ((1, 4, 64, 1, (1,)), (1, 2, 64, 2, (2,)), (2, 4, 64, 1, (1,)), (2, 2, 64, 2, (2,)),
+                                (4, 2, 64, 2, (1, 2)),
+                                (8, 2, 32, 1, (1, 2))):
+        for br in brs:
+            np_, sub = nf // 2, bm // (16 * pj)
+            nl, ns, xi = pj * np_ * (4 if br == 2 else 3), pj * np_, bm * kh * 128 // 4096
+            wins = {sub * nl: "dma", xi + nl: ("load", nl), nl: ("load", nl)}
+            for dt in (0, 1):
+                out[f"conv1x1x_bnb_kernelILi{dt}ELi{br}ELi{kh}ELi{nf}ELi{bm}ELi{pj}EE"] = wins
+    return out
+
+
+WINDOWS.update(_x1_bnb_windows())
 COUNTING = ("conv_l1pp_kernel", "conv_l1_kernel", "stem_fwd_kernel", "wgrad_stem_kernel", "wgrad_stem_quad_kernel",
             "wgrad_stem_rows_kernel", "conv_pp_kernel",
             "conv_wgrad_pp_kernel", "wgrad3x3_c64_kernel", "conv_fwd_kernel", "conv_wgrad_wide_kernel",
@@ -183,6 +206,34 @@ def check_register_hazards(ins, labels):
     return probs
 
 
+def check_store_data(ins):
+    """Module docstring, check 4: a >8-byte vector-memory store followed, within two wait states, by an instruction
+    whose destination overlaps the store's data registers."""
+    probs = []
+    for i, t in enumerate(ins):
+        op = t.split()[0]
+        if not (is_vm(t) and "store" in op and op.endswith(("dwordx3", "dwordx4"))):
+            continue
+        ops = [o.strip() for o in t.split(None, 1)[1].split(",")]
+        data = regs(ops[0] if op.startswith("buffer_") else ops[1])  # global_/flat_: vaddr first, then vdata
+        states, j = 0, i + 1
+        while states < 2 and j < len(ins):
+            u = ins[j]
+            m = re.match(r"s_nop\s+(\d+)", u)
+            if m:
+                states += int(m.group(1)) + 1
+            else:
+                parts = u.split(None, 1)
+                dest = regs(parts[1].split(",")[0]) if len(parts) > 1 and u.startswith("v_") else set()  # VALU
+                if dest & data:
+                    probs.append(f"store data hazard: '{u}' (instruction {j}) overwrites the data of '{t}' "
+                                 f"(instruction {i}) {states} wait state(s) after it")
+                    break
+                states += 1
+            j += 1
+    return probs
+
+
 def check_windows(ins, labels, wins):
     """Designated counted waits (module docstring, check 2).  Walking back from the wait in layout order, a label that
     is the target of backward branches (a loop header / latch block) may continue from any of those branches ("the
@@ -229,7 +280,7 @@ def check_windows(ins, labels, wins):
         if n is None or n == 0 or n not in wins:
             continue
         what, skip = wins[n] if isinstance(wins[n], tuple) else (wins[n], 0)
-        cnt = walk(i - 1, 0, what, 0, skip)
+        cnt = walk(i, 0, what, 0, skip)  # from the wait itself: its block may be a loop header (latch walks)
         if cnt is None:
             probs.append(f"vmcnt({n}) at instruction {i}: no {what} found before it")
             continue
@@ -250,6 +301,7 @@ def check_kernel(name, body):
         if nsp:
             probs.append(f"{nsp} scratch (spill) instructions in a kernel that counts its own waits")
     probs += check_register_hazards(ins, labels)
+    probs += check_store_data(ins)
     windows = []
     for key, wins in WINDOWS.items():
         if key in name:
