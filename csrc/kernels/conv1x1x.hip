@@ -279,7 +279,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __rest
 // the in-order count); stores keep the true row, and the range check drops those past M.  The counts cover LOADS only
 // (per sub-tile NL operand loads): the wait for sub-tile s's operands leaves the younger DMA pieces / loads in flight,
 // the loop-top wait for the tile's DMA the previous tile's SUB * NL loads; stores never relax a wait.
-// (Counting the stores too -- vmcnt(NS + NL) -- gave stale operands on the C = 64 configuration: round 5.)
+// (Round 5: with the stores counted and out-of-range operand rows, the C = 64 configuration read stale operands; the
+// two changes were made together, so which one it needed is not isolated.)
 // PJ: pixel fragments per sub-tile (two operand sets must fit the register budget).
 namespace {
 PDT_DEVICE u32x4v x1_ld16(const __amdgpu_buffer_rsrc_t& r, uint32_t off) {
