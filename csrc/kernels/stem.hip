@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // retire in issue order, so a counted wait leaves those stores in flight.  Then a raw barrier
     // (no vmcnt(0) drain): every wave's DMA landed and every wave finished reading the other buffer.
     if (stores_behind)
-      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -118,9 +118,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // scheduling barriers: read right before their MFMAs, each row's 11 LDS reads were exposed -- PMC: 63 % of the
     // wave cycles issue-stalled, 28 % MFMA busy)
     vec8 af[2][4], bf[2][kGroups];
+    // A fragment i row fr = output channel (fr >> 2) * 16 + i * 4 + (fr & 3): a lane's 4 fragments x 4 rows are then
+    // the 16 CONSECUTIVE channels 16 * fq .. +15 of its pixel -- two 16-byte stores per pixel instead of four 8-byte
+    // ones (round 5, same box: ResNet-18 19.93/19.93/20.34 -> 19.86/19.80/20.24 ms, ResNet-50 72.67/72.64 ->
+    // 72.56/72.51 ms)
     auto load = [&](int r, int sl) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[sl][i] = *(const vec8*)(wl + (i * 16 + fr) * kWPitch + (r * 4 + fq) * 16);
+      for (int i = 0; i < 4; ++i)
+        af[sl][i] = *(const vec8*)(wl + ((fr >> 2) * 16 + i * 4 + (fr & 3)) * kWPitch + (r * 4 + fq) * 16);
 #pragma unroll
       for (int g = 0; g < kGroups; ++g) bf[sl][g] = *(const vec8*)(sb + r * row_bytes + g * 256);
     };
@@ -136,37 +141,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- epilogue: lane holds couts i*16 + 4*fq + r of pixel (oh, g*16 + fr) ----
+    // ---- epilogue: lane holds couts 16*fq + 4*i + r of pixel (oh, g*16 + fr) ----
     int n, oh0;
     tile_n_oh(t, n, oh0);
     const int oh = oh0 + wave;
-    stores_behind = oh < a.P && a.Q == kGroups * 16;  // then 28 stores follow the next DMA
+    stores_behind = oh < a.P && a.Q == kGroups * 16;  // then 14 stores follow the next DMA
     float csum[4][4], csq[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
     if (oh < a.P) {
-      uint16_t* yrow = a.y + ((int64_t)(n * a.P + oh) * a.Q) * kCout + 4 * fq;
+      uint16_t* yrow = a.y + ((int64_t)(n * a.P + oh) * a.Q) * kCout + 16 * fq;
 #pragma unroll
       for (int g = 0; g < kGroups; ++g) {
         const int ow = g * 16 + fr;
         if (ow < a.Q) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            uint16_t o[4];
+          for (int h = 0; h < 2; ++h) {  // channels 16*fq + 8h .. +7 = fragments 2h, 2h+1
+            uint16_t o[8];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = E::from_f(acc[i][g][r]);
-            uint2 pk;
+            for (int e = 0; e < 8; ++e) o[e] = E::from_f(acc[2 * h + (e >> 2)][g][e & 3]);
+            uint4 pk;
             pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
             pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-            *(uint2*)(yrow + (int64_t)ow * kCout + i * 16) = pk;
+            pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
+            pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+            *(uint4*)(yrow + (int64_t)ow * kCout + 8 * h) = pk;
             if constexpr (STATS) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float q = E::to_f(o[r]);
-                csum[i][r] += q;
-                csq[i][r] += q * q;
+              for (int e = 0; e < 8; ++e) {
+                const float q = E::to_f(o[e]);
+                csum[2 * h + (e >> 2)][e & 3] += q;
+                csq[2 * h + (e >> 2)][e & 3] += q * q;
               }
             }
           }
@@ -188,7 +195,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int c = i * 16 + 4 * fq + r;
+            const int c = 16 * fq + 4 * i + r;
             red[wave][c * 2 + 0] += csum[i][r];  // lanes fr == 15 of distinct fq own distinct c
             red[wave][c * 2 + 1] += csq[i][r];
           }

@@ -41,7 +41,7 @@ VM_PREFIX = ("global_", "buffer_", "scratch_", "flat_")
 WINDOWS = {
     "conv_l1pp_kernel": {14: "dma", 11: "load", 8: "load"},
     "conv_l1_kernel": {16: "dma", 12: "dma"},
-    "stem_fwd_kernel": {24: "dma"},
+    "stem_fwd_kernel": {14: "dma"},
     "wgrad_stem_quad_kernel": {12: "dma", 8: "load"},
     "wgrad_stem_rows_kernel": {12: "dma", 2: "load"},
     "conv_wgrad_wide_kernel": {6: ("dma", 6), 3: ("dma", 3)},
