@@ -45,6 +45,10 @@ PDT_DEVICE int hswz(int R) { return R & 7; }
 // lanes 4..11 -> pixels 8..15 (matches the ds_read_b128 lane groups {0-3,12-15,20-27}, ...)
 PDT_DEVICE int pix_of_lane(int fr) { return fr < 4 ? fr : (fr >= 12 ? fr - 8 : fr + 4); }
 PDT_DEVICE int wswz(int co, int c) { return (c & ~7) | ((c & 7) ^ ((co >> 1) & 7)); }  // weight chunk
+// conv_l1pp_kernel's weight rows are read permuted (A fragment i row fr = output channel 8 * (fr >> 2) + 4 * i +
+// (fr & 3) of the wave's 32): its swizzle is the same function of the READING lane's fr as wswz's, so the fragment
+// reads stay conflict-free
+PDT_DEVICE int wswz_pp(int co, int c) { return (c & ~7) | ((c & 7) ^ ((((co >> 3) & 3) << 1) | ((co & 3) >> 1))); }
 }  // namespace
 
 // PRE: the input is the raw output of the block's first conv; its BatchNorm + ReLU is applied to each staged
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     const int ii = wave + 8 * m;
     const int L = ii * 64 + lrow * 8 + pch;
     const int co = L / 72, p = L - co * 72;
-    buf_lds16_asm(rw, wl + ii * 1024, (uint32_t)(co * 72 + wswz(co, p)) * 16u);
+    buf_lds16_asm(rw, wl + ii * 1024, (uint32_t)(co * 72 + wswz_pp(co, p)) * 16u);
   }
   // ---- a group's halo DMA: 44 instructions, 11 per wave, the last one half-masked ----
   auto stage_tile = [&](int t) {
@@ -474,7 +478,10 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     for (int tu = 0; tu < 3; ++tu)
       baddr[j][tu] = (uint32_t)(kWB + grp * kStageB + R0 * 128 + ((fq ^ ((w + tu) & 7)) << 4));
   }
-  const uint32_t abase0 = (uint32_t)((wn * 32 + fr) * 1152 + ((fq ^ ((fr >> 1) & 7)) << 4));
+  // permuted weight rows: fragment i row fr = channel wn*32 + 8*(fr >> 2) + 4*i + (fr & 3), so a lane's two fragments
+  // hold the 8 CONSECUTIVE channels wn*32 + 8*fq .. +7 of its pixel: one 16-byte store / operand load per pixel group
+  // (round 5, same box: ResNet-18 20.32/20.31/20.28 -> 20.15/20.16/20.14 ms, ResNet-50 73.07/73.15 -> 72.94/72.92 ms)
+  const uint32_t abase0 = (uint32_t)((wn * 32 + 8 * (fr >> 2) + (fr & 3)) * 1152 + ((fq ^ ((fr >> 1) & 7)) << 4));
   const uint32_t abase1 = abase0 ^ 64u;
   auto xor64 = [](uint32_t x) {
     uint32_t r;
@@ -499,7 +506,8 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     if (tid < 128) cfl[tid] = a.pre_coef[tid];  // scale[64] | shift[64]
     __syncthreads();                            // the prologue transform reads them
   }
-  auto coef = [&](int q, int i) { return *(const float4*)(cfl + q * 64 + wn * 32 + i * 16 + 4 * fq); };
+  // coefficient q of channels wn*32 + 8*fq + 4*h .. +3
+  auto coef = [&](int q, int h) { return *(const float4*)(cfl + q * 64 + wn * 32 + 8 * fq + 4 * h); };
 
   f32x4_t acc[2][NJ];
   // epilogue operands of the tile being computed: loaded at the start of its compute phase (latency hidden
@@ -509,7 +517,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
   // operands of at most NJO = 4 groups at once: all 7 would spill (~70 registers beside the accumulators), so its
   // epilogue runs in two halves (groups 0-3, then 4-6), each with its own operand loads (see memphase)
   constexpr int NJO = EPI == 3 ? 4 : NJ;
-  u32x2v pre_res[RES ? NJO : 1][RES ? 2 : 1], pre_y1[EPI >= 2 ? NJO : 1][EPI >= 2 ? 2 : 1];
+  u32x4v pre_res[RES ? NJO : 1], pre_y1[EPI >= 2 ? NJO : 1];
   u32x2v pre_m[EPI == 3 ? NJO : 1];
   // a tile's 4 x 56 output pixels are one contiguous block: pixel px of tile t is element (t's first pixel + px) * 64
   const int lpx0 = pix_of_lane(fr) * 64;
@@ -532,7 +540,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
       const int dR = tr * kXP + tu;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        af[sl][i] = *(const vec8*)(smem + (kk ? abase1 : abase0) + i * 16 * 1152 + wtap * 128);
+        af[sl][i] = *(const vec8*)(smem + (kk ? abase1 : abase0) + i * 4 * 1152 + wtap * 128);
       // (volatile xor: computed here, not hoisted out of the tile loop as 49 more live registers)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
@@ -553,11 +561,11 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // epilogue: lane holds couts wn*32 + i*16 + 4*fq + r of pixel (wm*7 + j)*16 + pix_of_lane(fr); exactly
-  // 2 * NJ = 14 stores per lane (every pixel of a tile is in range: H % 4 == 0)
-  constexpr int kStores = 2 * NJ;
-  // HOLD: the packed outputs go to held[j - J0][i] instead of memory (stored later by store_held)
-  uint2 held[NJO][2];
+  // epilogue: lane holds couts wn*32 + 8*fq + 4*i + r of pixel (wm*7 + j)*16 + pix_of_lane(fr); exactly
+  // NJ = 7 16-byte stores per lane (every pixel of a tile is in range: H % 4 == 0)
+  constexpr int kStores = NJ;
+  // HOLD: the packed outputs go to held[j - J0] instead of memory (stored later by store_held)
+  uint4 held[NJO];
   auto epilogue = [&](int t, auto J0c, auto J1c, auto HOLDc) {  // pixel groups [J0, J1); operands in pre_*[j - J0]
     constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
     constexpr bool HOLD = decltype(HOLDc)::value;
@@ -565,65 +573,69 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     (void)pre_m; (void)pre_res; (void)pre_y1;
     lpx = lpx0;
     asm volatile("" : "+v"(lpx));
+    const int c0 = wn * 32 + 8 * fq;
 #pragma unroll
     for (int j = J0; j < J1; ++j) {
       const int jo = j - J0;
       const int64_t ob = obase_of(t, j);
+      float v[8];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c0 = wn * 32 + i * 16 + 4 * fq;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (RES) {
-          const u32x2v rr = pre_res[jo][i];
-          v[0] += E::to_f((uint16_t)(rr[0] & 0xffff));
-          v[1] += E::to_f((uint16_t)(rr[0] >> 16));
-          v[2] += E::to_f((uint16_t)(rr[1] & 0xffff));
-          v[3] += E::to_f((uint16_t)(rr[1] >> 16));
-        }
-        float y1[4];
-        if constexpr (EPI >= 2) {
-          const u32x2v q1 = pre_y1[jo][i];
-          y1[0] = E::to_f((uint16_t)(q1[0] & 0xffff)); y1[1] = E::to_f((uint16_t)(q1[0] >> 16));
-          y1[2] = E::to_f((uint16_t)(q1[1] & 0xffff)); y1[3] = E::to_f((uint16_t)(q1[1] >> 16));
-          if constexpr (EPI == 2) {
-            const float4 sc = coef(0, i), sh = coef(1, i);
-            if (!(y1[0] * sc.x + sh.x > 0.f)) v[0] = 0.f;
-            if (!(y1[1] * sc.y + sh.y > 0.f)) v[1] = 0.f;
-            if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
-            if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
-          } else {
-            const uint32_t mb = c0 < 32 ? pre_m[jo][0] >> c0 : pre_m[jo][1] >> (c0 - 32);
-            if (!(mb & 1u)) v[0] = 0.f;
-            if (!(mb & 2u)) v[1] = 0.f;
-            if (!(mb & 4u)) v[2] = 0.f;
-            if (!(mb & 8u)) v[3] = 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = acc[e >> 2][j][e & 3];
+      if constexpr (RES) {
+        const u32x4v rr = pre_res[jo];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += E::to_f((uint16_t)(rr[e >> 1] >> (16 * (e & 1))));
+      }
+      float y1[8];
+      if constexpr (EPI >= 2) {
+        const u32x4v q1 = pre_y1[jo];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y1[e] = E::to_f((uint16_t)(q1[e >> 1] >> (16 * (e & 1))));
+        if constexpr (EPI == 2) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float4 sc = coef(0, h), sh = coef(1, h);
+            const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (!(y1[4 * h + r] * scv[r] + shv[r] > 0.f)) v[4 * h + r] = 0.f;
           }
+        } else {
+          const uint32_t mb = c0 < 32 ? pre_m[jo][0] >> c0 : pre_m[jo][1] >> (c0 - 32);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (!((mb >> e) & 1u)) v[e] = 0.f;
         }
-        uint16_t o[4];
+      }
+      uint16_t o[8];
 #pragma unroll
-        for (int r2 = 0; r2 < 4; ++r2) o[r2] = E::from_f(v[r2]);
-        uint2 packed;
-        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-        if constexpr (HOLD)
-          held[jo][i] = packed;
-        else
-          *(uint2*)(a.y + ob + c0) = packed;
-        if constexpr (EPI == 1) {
+      for (int e = 0; e < 8; ++e) o[e] = E::from_f(v[e]);
+      uint4 packed;
+      packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+      packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+      packed.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
+      packed.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+      if constexpr (HOLD)
+        held[jo] = packed;
+      else
+        *(uint4*)(a.y + ob + c0) = packed;
+      if constexpr (EPI == 1) {
 #pragma unroll
-          for (int r2 = 0; r2 < 4; ++r2) {
-            const float q = E::to_f(o[r2]);
-            sacc[i][r2][0] += q;
-            sacc[i][r2][1] += q * q;
-          }
-        } else if constexpr (EPI >= 2) {
-          const float4 mu = coef(2, i), is = coef(3, i);
+        for (int e = 0; e < 8; ++e) {
+          const float q = E::to_f(o[e]);
+          sacc[e >> 2][e & 3][0] += q;
+          sacc[e >> 2][e & 3][1] += q * q;
+        }
+      } else if constexpr (EPI >= 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 mu = coef(2, h), is = coef(3, h);
           const float m1[4] = {mu.x, mu.y, mu.z, mu.w}, i1[4] = {is.x, is.y, is.z, is.w};
 #pragma unroll
-          for (int r2 = 0; r2 < 4; ++r2) {
-            const float dz = E::to_f(o[r2]);
-            sacc[i][r2][0] += dz;
-            sacc[i][r2][1] += dz * (y1[r2] - m1[r2]) * i1[r2];
+          for (int r = 0; r < 4; ++r) {
+            const float dz = E::to_f(o[4 * h + r]);
+            sacc[h][r][0] += dz;
+            sacc[h][r][1] += dz * (y1[4 * h + r] - m1[r]) * i1[r];
           }
         }
       }
@@ -638,8 +650,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = J0; j < J1; ++j) {
       const int64_t ob = obase_of(t, j);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) *(uint2*)(a.y + ob + wn * 32 + i * 16 + 4 * fq) = held[j - J0][i];
+      *(uint4*)(a.y + ob + wn * 32 + 8 * fq) = held[j - J0];
     }
   };
 
@@ -659,15 +670,11 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     for (int j = J0; j < J1; ++j) {
       const int jo = j - J0;
       const uint32_t e = tb + (uint32_t)(lpx + (wm * NJ + j) * 1024);
-      const uint32_t yo = (e + wn * 32 + 4 * fq) * 2u;
-      if constexpr (RES) {
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_res[jo][0]) : "v"(yo), "s"(rres));
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_res[jo][1]) : "v"(yo), "s"(rres));
-      }
-      if constexpr (EPI >= 2) {
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_y1[jo][0]) : "v"(yo), "s"(ry1));
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen offset:32" : "=v"(pre_y1[jo][1]) : "v"(yo), "s"(ry1));
-      }
+      const uint32_t yo = (e + wn * 32 + 8 * fq) * 2u;
+      if constexpr (RES)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(pre_res[jo]) : "v"(yo), "s"(rres));
+      if constexpr (EPI >= 2)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(pre_y1[jo]) : "v"(yo), "s"(ry1));
       if constexpr (EPI == 3)
         asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(pre_m[jo]) : "v"(e >> 3), "s"(rmask));
     }
@@ -677,8 +684,8 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     (void)pre_m; (void)pre_res; (void)pre_y1;
 #pragma unroll
     for (int jo = 0; jo < NO; ++jo) {
-      if constexpr (RES) asm volatile("" : "+v"(pre_res[jo][0]), "+v"(pre_res[jo][1]));
-      if constexpr (EPI >= 2) asm volatile("" : "+v"(pre_y1[jo][0]), "+v"(pre_y1[jo][1]));
+      if constexpr (RES) asm volatile("" : "+v"(pre_res[jo]));
+      if constexpr (EPI >= 2) asm volatile("" : "+v"(pre_y1[jo]));
       if constexpr (EPI == 3) asm volatile("" : "+v"(pre_m[jo]));
     }
   };
@@ -703,15 +710,15 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     }
     if constexpr (NJO < NJ) {
       // EPI 3, two halves: groups 0-3 computed into registers (held, not stored yet), the operands of groups 4-6
-      // loaded into the freed operand registers, THEN the first half's 8 stores: the second half's loads are older
-      // than those stores, so vmcnt(8) waits for the loads (and the DMA) without draining the stores
+      // loaded into the freed operand registers, THEN the first half's 4 stores: the second half's loads are older
+      // than those stores, so vmcnt(4) waits for the loads (and the DMA) without draining the stores
       if (k_epi >= 0) {
         epilogue(te, I0{}, IH{}, std::true_type{});
         load_ops(te, IH{}, IN{});
         __builtin_amdgcn_sched_barrier(0);
         store_held(te, I0{}, IH{});
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         pin_ops(std::integral_constant<int, NJ - NJO>{});
         epilogue(te, IH{}, IN{}, std::false_type{});
       }
@@ -773,7 +780,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int lc = i * 16 + 4 * fq + r;
+          const int lc = 8 * fq + 4 * i + r;
           red[(wave * 32 + lc) * 2 + 0] = sacc[i][r][0];
           red[(wave * 32 + lc) * 2 + 1] = sacc[i][r][1];
         }

@@ -39,7 +39,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VM_PREFIX = ("global_", "buffer_", "scratch_", "flat_")
 # kernel-name substring -> {N: what the window must cover} (mangled names contain the plain kernel name)
 WINDOWS = {
-    "conv_l1pp_kernel": {14: "dma", 11: "load", 8: "load"},
+    "conv_l1pp_kernel": {7: "dma", 11: "load", 4: "load"},
     "conv_l1_kernel": {16: "dma", 12: "dma"},
     "stem_fwd_kernel": {14: "dma"},
     "wgrad_stem_quad_kernel": {12: "dma", 8: "load"},
