@@ -48,7 +48,13 @@ PDT_DEVICE int swz(int row) { return (row >> 1) & (CHUNKS - 1); }
 // SMEM > 0 (the kernel's LDS bytes): with a.stage_out the output tile is staged in LDS and written back as
 // whole 16-byte-per-lane rows; a lane's accumulators otherwise hold 4 channels of one pixel, so every store
 // instruction writes 16 rows x 32 B.
-template <int DT, int EPI, int RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_, int SMEM = 0>
+// PERM (conv_pp_kernel: its weight rows are staged permuted): fragment i row 4*fq + r is channel
+// wn*WN + (i >> 1)*32 + 8*fq + 4*(i & 1) + r, so fragments 2p and 2p+1 give a lane 8 CONSECUTIVE channels of its pixel
+// -- one 16-byte operand load / store (staged or not) per pair instead of two 8-byte ones.  Round 5, same box:
+// ResNet-18 20.66/20.69/20.68 -> 20.53/20.58/20.51 ms, ResNet-50 74.05/74.04 -> 73.64/73.42 ms (an earlier variant
+// with 8-byte staged writes at the permuted offsets was 0.1 ms SLOWER on ResNet-18: LDS write conflicts).
+template <int DT, int EPI, int RES, int FN, int FM, int WN, int WM, int BN, int WAVES_M, int NW_, int SMEM = 0,
+          bool PERM = false>
 PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int64_t m0, int n0, int tile_m, int wn,
                               int wm, int tid, int lane, char* smem) {
   using E = E16<DT>;
@@ -92,7 +98,10 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
     }
     __syncthreads();
   }
-  auto coef4 = [&](int q, int i) { return *(const float4*)(cf + q * BN + wn * WN + i * 16 + 4 * fq); };
+  // channel of fragment i, row 4*fq + r, within the wave's WN (PERM: see above)
+  auto chan = [&](int i, int r) { return PERM ? (i >> 1) * 32 + 8 * fq + 4 * (i & 1) + r : i * 16 + 4 * fq + r; };
+  static_assert(!PERM || FN % 2 == 0, "PERM pairs fragments");
+  auto coef4 = [&](int q, int i) { return *(const float4*)(cf + q * BN + wn * WN + chan(i, 0)); };
 
   // Two-phase chunks of JC pixel fragments: every epilogue operand load of the chunk (residual, BN input(s),
   // ReLU mask) is issued before any arithmetic or store, so the chunk pays ONE memory latency instead of
@@ -177,13 +186,28 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
     uint64_t p_m[LM ? JC : 1][MW];
 #pragma unroll
     for (int jj = 0; jj < JC; ++jj) {
+      if constexpr (PERM) {  // one 16-byte load per fragment pair
 #pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int64_t o = obase[jj] + n0 + wn * WN + i * 16 + 4 * fq;
-        if constexpr (RES == 1) p_res[jj][i] = *(const uint2*)(a.res + o);
-        if constexpr (RC) p_res[jj][i] = *(const uint2*)(a.res + rbase[jj] + (uint32_t)(n0 + wn * WN + i * 16 + 4 * fq));
-        if constexpr (LY1) p_y1[jj][i] = *(const uint2*)(a.bn_y1 + o);
-        if constexpr (LY2) p_y2[jj][i] = *(const uint2*)(a.bn_y2 + o);
+        for (int i = 0; i < FN; i += 2) {
+          const int64_t o = obase[jj] + n0 + wn * WN + chan(i, 0);
+          auto split = [&](uint2 (&dst)[FN], const uint4 v) {
+            dst[i] = make_uint2(v.x, v.y);
+            dst[i + 1] = make_uint2(v.z, v.w);
+          };
+          if constexpr (RES == 1) split(p_res[jj], *(const uint4*)(a.res + o));
+          if constexpr (RC) split(p_res[jj], *(const uint4*)(a.res + rbase[jj] + (uint32_t)(n0 + wn * WN + chan(i, 0))));
+          if constexpr (LY1) split(p_y1[jj], *(const uint4*)(a.bn_y1 + o));
+          if constexpr (LY2) split(p_y2[jj], *(const uint4*)(a.bn_y2 + o));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int64_t o = obase[jj] + n0 + wn * WN + i * 16 + 4 * fq;
+          if constexpr (RES == 1) p_res[jj][i] = *(const uint2*)(a.res + o);
+          if constexpr (RC) p_res[jj][i] = *(const uint2*)(a.res + rbase[jj] + (uint32_t)(n0 + wn * WN + i * 16 + 4 * fq));
+          if constexpr (LY1) p_y1[jj][i] = *(const uint2*)(a.bn_y1 + o);
+          if constexpr (LY2) p_y2[jj][i] = *(const uint2*)(a.bn_y2 + o);
+        }
       }
       if constexpr (LM) {
 #pragma unroll
@@ -195,9 +219,10 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
     for (int jj = 0; jj < JC; ++jj) {
       if (!valid[jj]) continue;
       const int j = jc + jj;
+      uint2 held = make_uint2(0u, 0u);  // PERM: fragment 2p's packed output, stored with 2p + 1's
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + 4 * fq;
+        const int n = n0 + wn * WN + chan(i, 0);
         const int64_t o = obase[jj] + n;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if constexpr (RES) {
@@ -223,7 +248,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
             if (!(y1[2] * sc.z + sh.z > 0.f)) v[2] = 0.f;
             if (!(y1[3] * sc.w + sh.w > 0.f)) v[3] = 0.f;
           } else {
-            const uint32_t mb = (uint32_t)(p_m[jj][i >> 2] >> ((i & 3) * 16 + 4 * fq));
+            const uint32_t mb = (uint32_t)(p_m[jj][chan(i, 0) >> 6] >> (chan(i, 0) & 63));
             if (!(mb & 1u)) v[0] = 0.f;
             if (!(mb & 2u)) v[1] = 0.f;
             if (!(mb & 4u)) v[2] = 0.f;
@@ -241,10 +266,24 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
         uint2 packed;
         packed.x = (uint32_t)ov[0] | ((uint32_t)ov[1] << 16);
         packed.y = (uint32_t)ov[2] | ((uint32_t)ov[3] << 16);
-        if (CAN_STAGE && stage)
-          *(uint2*)(stg + (srow0 + j * 16 + fr) * SPITCH + (wn * WN + i * 16 + 4 * fq) * 2) = packed;
-        else
+        if (CAN_STAGE && stage) {
+          if constexpr (PERM) {  // 16 B per pair: a pixel's 4 fq lanes write 64 contiguous bytes
+            if (i & 1)
+              *(uint4*)(stg + (srow0 + j * 16 + fr) * SPITCH + (wn * WN + chan(i, 0) - 4) * 2) =
+                  make_uint4(held.x, held.y, packed.x, packed.y);
+            else
+              held = packed;
+          } else {
+            *(uint2*)(stg + (srow0 + j * 16 + fr) * SPITCH + (wn * WN + chan(i, 0)) * 2) = packed;
+          }
+        } else if constexpr (PERM) {
+          if (i & 1)
+            *(uint4*)(a.y + o - 4) = make_uint4(held.x, held.y, packed.x, packed.y);
+          else
+            held = packed;
+        } else {
           *(uint2*)(a.y + o) = packed;
+        }
         if constexpr (EPI == 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -305,7 +344,7 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int nl = wn * WN + i * 16 + 4 * fq + r;
+          const int nl = wn * WN + chan(i, r);
 #pragma unroll
           for (int k = 0; k < KS; ++k) red[(wm * BN + nl) * KS + k] = sacc[i][r][k];
         }
@@ -665,7 +704,10 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
 #pragma unroll
     for (int j = 0; j < NWI; ++j) {
       const int hr = (wave * NWI + j) * 8 + lrow;
-      const int n = n0 + (hr >> 5) * 64 + h * 32 + (hr & 31);
+      // permuted channel order inside each 32-row half (conv_epilogue PERM): LDS row f2*16 + m of the half holds
+      // channel (m >> 2)*8 + f2*4 + (m & 3) -- the row swizzle stays a function of the LDS row, conflict-free as before
+      const int lr = hr & 31;
+      const int n = n0 + (hr >> 5) * 64 + h * 32 + ((lr & 15) >> 2) * 8 + (lr >> 4) * 4 + (lr & 3);
       woff[h][j] = (uint32_t)((n * TU * a.C + (pchunk ^ ((hr >> 1) & 7)) * 8) * 2);
     }
 
@@ -783,8 +825,8 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
     __builtin_amdgcn_s_barrier();
   }
 
-  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW, PP_STAGE ? 2 * BUF : 0>(a, acc, m0, n0, tile_m, wn, wm, tid,
-                                                                                  lane, smem);
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW, PP_STAGE ? 2 * BUF : 0, true>(a, acc, m0, n0, tile_m, wn,
+                                                                                        wm, tid, lane, smem);
 }
 
 template <int DT, int BM, int BN>
