@@ -464,11 +464,16 @@ void conv_fwd_kernel(ConvFwdArgs args) {
       brow_off[j] = 0;
     }
   }
+  // PERM (conv_epilogue): LDS weight row wn*WN + 16*i + m holds channel wn*WN + (i >> 1)*32 + (m >> 2)*8 + 4*(i & 1) +
+  // (m & 3), so fragment pairs give a lane 8 consecutive channels; the row swizzle stays a function of the LDS row
+  constexpr bool PERM = WN % 32 == 0;
   uint32_t arow_off[A_INSTR];
 #pragma unroll
   for (int j = 0; j < A_INSTR; ++j) {
     const int row = (wave * A_INSTR + j) * RPI + lrow;
-    arow_off[j] = (uint32_t)(((n0 + row) * TU * a.C + (pchunk ^ swz<CHUNKS>(row)) * 8) * 2);
+    const int lw = row % WN, fi = lw >> 4, fm = lw & 15;
+    const int ch = PERM ? row - lw + (fi >> 1) * 32 + (fm >> 2) * 8 + (fi & 1) * 4 + (fm & 3) : row;
+    arow_off[j] = (uint32_t)(((n0 + ch) * TU * a.C + (pchunk ^ swz<CHUNKS>(row)) * 8) * 2);
   }
 
   // load cursor over (t, u, c0) in K-step order: advanced incrementally (no per-step divisions)
@@ -585,7 +590,7 @@ void conv_fwd_kernel(ConvFwdArgs args) {
     }
   }
 
-  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW, STAGES * STAGE>(a, acc, m0, n0, tile_m, wn, wm, tid,
+  conv_epilogue<DT, EPI, RES, FN, FM, WN, WM, BN, WAVES_M, NW, STAGES * STAGE, PERM>(a, acc, m0, n0, tile_m, wn, wm, tid,
                                                                              lane, smem);
 }
 
