@@ -77,6 +77,9 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
   }
 }
 
+// (Round 5: a row-pair variant -- one block per pooled row, a thread per two adjacent outputs sharing their middle
+// window column, 15 loads for 2 outputs, no index divisions -- measured SLOWER on the same box: ResNet-18
+// 20.16 -> 20.24 ms, ResNet-50 71.7 -> 72.0 ms; not kept.)
 // eval / generic variant without index output is the same kernel with idx == nullptr handled by caller
 void bn_relu_maxpool_launch(int dtype, const uint16_t* y, const float* coef, uint16_t* out, uint8_t* idx, int N, int H,
                             int W, int C, hipStream_t s) {
