@@ -41,7 +41,7 @@ def test_timeline_gaps_busy_union_and_gaps(tmp_path):
 
 
 def test_counted_waits_in_layer1_pingpong_kernel():
-    """The 8-wave layer1 kernel counts its asm DMA / operand loads itself (s_waitcnt vmcnt(11) / vmcnt(14)); a spill
+    """The 8-wave layer1 kernel counts its asm DMA / operand loads itself (s_waitcnt vmcnt(11) / vmcnt(7)); a spill
     or a store scheduled into those windows would be a silent race.  Compile it (hipcc -S, gfx950) and check every
     instantiation's ISA: no scratch instructions, each counted window holds at least its count of younger ops."""
     import shutil

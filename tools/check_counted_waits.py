@@ -5,10 +5,11 @@ operand loads through inline asm, invisible to the compiler's waitcnt pass, and 
 
 * ``vmcnt(11)`` after the operand loads + the 11 DMA pieces: the loads are done once at most 11 younger
   vector-memory operations remain -- safe iff at least 11 vm operations follow the last operand load;
-* ``vmcnt(14)`` after the DMA + the epilogue's 14 stores: the DMA is done once at most 14 younger remain --
-  safe iff at least 14 vm operations follow the last DMA piece;
-* ``vmcnt(8)`` (EPI 3, the block-output BN-backward epilogue in two halves) after the second half's operand loads
-  + the first half's 8 held stores: safe iff at least 8 vm operations follow the last operand load.
+* ``vmcnt(7)`` after the DMA + the epilogue's 7 (16-byte) stores: the DMA is done once at most 7 younger remain --
+  safe iff at least 7 vm operations follow the last DMA piece;
+* ``vmcnt(4)`` (EPI 3, the block-output BN-backward epilogue in two halves) after the second half's operand loads
+  + the first half's 4 held stores: safe iff at least 4 vm operations follow the last operand load.
+(Round 5: 16-byte epilogue stores and operand loads -- the counts were 14 and 8 with 8-byte ones.)
 
 A compiler-inserted spill (``scratch_*``) or a reordered store inside those windows would break the count
 silently (a race, not a crash), so this walks every instantiation's ISA backwards from each such wait and
@@ -52,15 +53,15 @@ def check(lines):
         probs.append(f"{nspill} scratch (spill) instructions")
     for i, l in enumerate(ins):
         m = re.match(r"s_waitcnt vmcnt\((\d+)\)$", l)
-        if not m or m.group(1) not in ("8", "11", "14"):
+        if not m or m.group(1) not in ("4", "11", "7"):
             continue
         need = int(m.group(1))
         n = 0
         for k in range(i - 1, -1, -1):
             t = ins[k]
-            if need == 14 and t.startswith("buffer_load_dwordx4") and t.endswith(" lds"):
+            if need == 7 and t.startswith("buffer_load_dwordx4") and t.endswith(" lds"):
                 break
-            if need in (8, 11) and t.startswith("buffer_load_dwordx2"):
+            if need in (4, 11) and t.startswith("buffer_load_dwordx") and not t.endswith(" lds"):
                 break
             if t.startswith(VM):
                 n += 1
