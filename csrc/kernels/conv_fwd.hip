@@ -838,9 +838,11 @@ template <int DT, int BM, int BN>
 static void launch_pp(const ConvFwdArgs& args, hipStream_t s) {
   // PDT_PP_STAGE=0: the ping-pong kernel stores straight from the accumulators (A/B); default: LDS-staged row stores,
   // one wave row-group at a time (conv_epilogue PERGRP)
+  // (round 5: OFF by default -- with the PERM epilogue the direct stores are 16 bytes per lane, and the same box
+  // measured PDT_PP_STAGE=1 -> 0 at 20.45/20.43 -> 20.33/20.32 ms for ResNet-18, 73.23/73.36 -> 73.09/73.19 for ResNet-50)
   static const bool pp_stage = [] {
     const char* e = getenv("PDT_PP_STAGE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   ConvFwdArgs a = args;
   if (!pp_stage) a.stage_out = 0;
@@ -906,10 +908,12 @@ static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_
 
 template <int DT>
 static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
-  // LDS-staged output write-back (PDT_STAGE_OUT=0: direct 8-byte stores from the accumulators)
+  // LDS-staged output write-back, PDT_STAGE_OUT=1 (default off since round 5: the PERM epilogue's direct stores are
+  // 16 bytes per lane; with both staging knobs off the same box measured ResNet-18 20.33/20.32 -> 20.23/20.23 ms and
+  // ResNet-50 73.09/73.19 -> 73.05/73.00 ms against PP staging off alone)
   static const bool stage_env = [] {
     const char* e = getenv("PDT_STAGE_OUT");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   a.stage_out = stage_env && a.Kout % 8 == 0 ? 1 : 0;
   a.m_tiles = (int)((a.M + bm - 1) / bm);
