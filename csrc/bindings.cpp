@@ -624,8 +624,8 @@ void conv_wgrad_stem_fused(const Tensor& x, const Tensor& dp, const Tensor& idx,
   launched("conv_wgrad_launch");
 }
 
-// ResNet layer1 weight gradient (3x3/s1/p1, C = Kout = 64, W = 56): all 9 taps per block; writes
-// `blocks` fp32 partials [blocks][64][576] into ws and returns blocks (sum them with wgrad_reduce).
+// ResNet layer1 weight gradient (3x3/s1/p1, C = Kout = 64, W = 56): all 9 taps per block; writes at most
+// wgrad_blocks_3x3c64() fp32 partials [.][64][576] into ws and returns how many it wrote (sum them with wgrad_reduce).
 int64_t wgrad_blocks_3x3c64() { return pdt::wgrad3x3_c64_blocks(); }
 
 bool wgrad_3x3c64_supported(int64_t C, int64_t Kout, int64_t T, int64_t U, int64_t W, int64_t stride, int64_t pad) {
@@ -650,9 +650,9 @@ int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t
     TORCH_CHECK(pre_coef->numel() >= 128, "conv_wgrad_3x3c64: pre_coef needs scale[64] | shift[64]");
     a.pre_coef = pf(*pre_coef, "pre_coef");
   }
-  pdt::wgrad3x3_c64_launch(a, blocks, dt, cur_stream());
+  const int written = pdt::wgrad3x3_c64_launch(a, blocks, dt, cur_stream());
   launched("wgrad3x3_c64_launch");
-  return blocks;
+  return written;
 }
 
 void wgrad_reduce(const Tensor& ws, int64_t splits, int64_t rows, int64_t cols, int64_t ldw, int64_t split_stride,

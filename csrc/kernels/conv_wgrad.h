@@ -42,7 +42,7 @@ void conv_wgrad_launch(const ConvWgradArgs& a, int dtype, hipStream_t s);
 // writes `blocks` fp32 partials [blocks][64][ldw] (ldw >= 576) for wgrad_reduce.
 bool wgrad3x3_c64_supported(int C, int Kout, int T, int U, int W, int stride, int pad, int win);
 int wgrad3x3_c64_blocks();
-void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s);
+int wgrad3x3_c64_launch(const ConvWgradArgs& a, int partials, int dtype, hipStream_t s);  // partials written
 void wgrad_reduce_launch(const float* ws, int splits, int rows, int cols, int ldw, int64_t split_stride,
                          float* out, int ldo, float scale, bool accumulate, hipStream_t s);
 

@@ -1304,15 +1304,20 @@ PDT_DEVICE int l1_swz(int row2d, int col) { return (((col >> 1) & 1) << 1) | ((r
 
 // PRE: x is the raw output of the block's first conv; its BatchNorm + ReLU is applied to each staged X halo in
 // LDS (conv_l1.hip, PRE) -- the activation is never materialised.
-template <int DT, bool PRE = false, bool kL1Pipe = true>
-__global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
+// NWV = 8 (no PRE): two waves per SIMD on the same staged tile -- waves w and w + 4 take the even / odd column
+// blocks of the same 32 k x 32 c quadrant and write separate partials (2 per block), so a SIMD has a second wave to
+// issue from while the other waits on its transposed LDS reads (one wave per SIMD: ~36 % MFMA busy, r4_after_pmc.md).
+template <int DT, bool PRE = false, bool kL1Pipe = true, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
+  static_assert(NWV == 4 || (NWV == 8 && !kL1Pipe && !PRE), "8-wave form: straight tap loop, no PRE");
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   __shared__ __attribute__((aligned(1024))) char smem[2 * kL1Stage];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kh = wave & 1, chh = wave >> 1;  // this wave's k half and c half
+  const int kh = wave & 1, chh = (wave >> 1) & 1;  // this wave's k half and c half
+  const int jp = wave >> 2;                          // NWV = 8: column-block parity
 
   const int TH = (a.H + 3) / 4;  // row tiles per image
   const int tiles = a.N * TH;
@@ -1325,13 +1330,13 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.N * a.H * kL1W * 128u);
   const int lrow = lane >> 3, pch = lane & 7;
 
-  // 72 DMA instructions per stage (44 X + 28 dY), 18 per wave
+  // 72 DMA instructions per stage (44 X + 28 dY), 72 / NWV per wave
   auto stage_tile = [&](int t, int buf) {
     const int n = t / TH, h0 = (t - n * TH) * 4;
     char* sb = smem + buf * kL1Stage;
 #pragma unroll
-    for (int m = 0; m < 18; ++m) {
-      const int ii = wave + 4 * m;
+    for (int m = 0; m < 72 / NWV; ++m) {
+      const int ii = wave + NWV * m;
       if (ii < 44) {
         const int R = ii * 8 + lrow;
         const int hr = R / kL1XP, wc = R - (R / kL1XP) * kL1XP;
@@ -1455,7 +1460,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
       continue;
     }
 #pragma unroll 1
-    for (int j = 0; j < kL1W / 8; ++j) {
+    for (int j = jp; j < kL1W / 8; j += NWV / 4) {
       // A = dY^T (rows k): output row g, columns 8j + q (+4)
       const int ycol = 8 * j + q;
       const char* yb = sy + (g * kL1W + ycol) * 128;
@@ -1483,7 +1488,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
   }
 
   // partial dW[k][tap][c]: lane holds rows k = kb*16 + 4*(lane>>4) + r, column c = cb*16 + (lane&15)
-  float* dst = a.ws + (int64_t)blockIdx.x * 64 * a.ldw;
+  float* dst = a.ws + ((int64_t)blockIdx.x * (NWV / 4) + jp) * 64 * a.ldw;
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
@@ -1501,14 +1506,29 @@ bool wgrad3x3_c64_supported(int C, int Kout, int T, int U, int W, int stride, in
   return !win && C == 64 && Kout == 64 && T == 3 && U == 3 && W == kL1W && stride == 1 && pad == 1;
 }
 
+// The 8-wave form (two partials per block) for the calls without PRE; PDT_WGRAD_L1_W8=0 selects 4 waves.
+// Same box, ResNet-18 bf16 B = 1200: 20.166 / 20.111 / 20.064 (4 waves) vs 20.017 / 20.050 / 20.038 ms (8 waves).
+static bool wgrad_l1_w8() {
+  static const bool on = [] {
+    const char* e = getenv("PDT_WGRAD_L1_W8");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// number of fp32 partials the kernel writes (blocks x partials per block)
 int wgrad3x3_c64_blocks() {
   int dev = 0, cus = 256;
   PDT_HIP_CHECK(hipGetDevice(&dev));
   PDT_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  return (cus + 7) / 8 * 8;
+  return (cus + 7) / 8 * 8 * (wgrad_l1_w8() ? 2 : 1);
 }
 
-void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStream_t s) {
+int wgrad3x3_c64_launch(const ConvWgradArgs& a, int partials, int dtype, hipStream_t s) {
+  // the 8-wave form is built without PRE (with it the tap loop's 144 accumulators + the halo transform exceed the
+  // 256 registers of two waves per SIMD and spill inside the DMA window): PRE calls write one partial per block
+  const bool w8 = wgrad_l1_w8();
+  const int blocks = w8 ? partials / 2 : partials;
   PDT_COUNT("wgrad3x3_c64");
   // PDT_WGRAD_L1_PIPE=1: the software-pipelined tap loop.  Off by default: in isolation it ran 682 vs 758 TF/s
   // (tools/conv_bench.py) and the whole step measured 20.97 / 20.82 vs 21.03 / 21.00 ms with it (same box)
@@ -1519,7 +1539,9 @@ void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStrea
   if (a.pre_coef) PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
 #define PDT_W3(DT_, P_)                                                                         \
   do {                                                                                          \
-    if (pipe)                                                                                   \
+    if (w8 && !P_)                                                                              \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, false, false, 8>), dim3(blocks), dim3(512), 0, s, a); \
+    else if (pipe)                                                                              \
       hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, true>), dim3(blocks), dim3(256), 0, s, a);  \
     else                                                                                        \
       hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, false>), dim3(blocks), dim3(256), 0, s, a); \
@@ -1530,6 +1552,7 @@ void wgrad3x3_c64_launch(const ConvWgradArgs& a, int blocks, int dtype, hipStrea
     if (a.pre_coef) PDT_W3(kF16, true); else PDT_W3(kF16, false);
   }
 #undef PDT_W3
+  return w8 && !a.pre_coef ? partials : blocks;  // partials written
 }
 
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)

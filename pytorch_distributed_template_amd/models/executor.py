@@ -647,10 +647,10 @@ class ResNetExecutor:
             blocks = self.C.wgrad_blocks_3x3c64()
             ws = self._buf("ws", blocks * 64 * 576, torch.float32)
             if pre is None:
-                self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W)
+                parts = self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W)
             else:
-                self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W, pre)
-            self.C.wgrad_reduce(ws, blocks, 64, 576, 576, 64 * 576, gout, ldo, 1.0, False)
+                parts = self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W, pre)
+            self.C.wgrad_reduce(ws, parts, 64, 576, 576, 64 * 576, gout, ldo, 1.0, False)
             return
         assert pre is None, "fused producer BN only on the layer1 weight-gradient kernel"
         key = (cout, R, S, C, N * P * Q, win)
