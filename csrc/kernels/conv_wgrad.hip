@@ -1304,12 +1304,16 @@ PDT_DEVICE int l1_swz(int row2d, int col) { return (((col >> 1) & 1) << 1) | ((r
 
 // PRE: x is the raw output of the block's first conv; its BatchNorm + ReLU is applied to each staged X halo in
 // LDS (conv_l1.hip, PRE) -- the activation is never materialised.
-// NWV = 8 (no PRE): two waves per SIMD on the same staged tile -- waves w and w + 4 take the even / odd column
-// blocks of the same 32 k x 32 c quadrant and write separate partials (2 per block), so a SIMD has a second wave to
-// issue from while the other waits on its transposed LDS reads (one wave per SIMD: ~36 % MFMA busy, r4_after_pmc.md).
-template <int DT, bool PRE = false, bool kL1Pipe = true, int NWV = 4>
+// NWV = 8: two waves per SIMD on the same staged tile, so a SIMD has a second wave to issue from while the other
+// waits on its transposed LDS reads (one wave per SIMD: ~36 % MFMA busy, r4_after_pmc.md).  Waves w and w + 4 share
+// one 32 k x 32 c quadrant and split either
+//  - the column blocks (TSPL = false: even / odd blocks, separate partials, 2 per block; 144 accumulators per lane,
+//    too many registers left for PRE's halo transform), or
+//  - the taps (TSPL = true: taps 0-4 / 5-8 into one partial per block; 80 accumulators per lane).
+template <int DT, bool PRE = false, bool kL1Pipe = true, int NWV = 4, bool TSPL = false>
 __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
-  static_assert(NWV == 4 || (NWV == 8 && !kL1Pipe && !PRE), "8-wave form: straight tap loop, no PRE");
+  static_assert(NWV == 4 ? !TSPL : (NWV == 8 && !kL1Pipe && (TSPL || !PRE)), "unsupported wgrad3x3_c64 form");
+  constexpr int NT = TSPL ? 5 : 9;  // taps per wave
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   __shared__ __attribute__((aligned(1024))) char smem[2 * kL1Stage];
@@ -1317,7 +1321,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = wave & 1, chh = (wave >> 1) & 1;  // this wave's k half and c half
-  const int jp = wave >> 2;                          // NWV = 8: column-block parity
+  const int jp = wave >> 2;                          // NWV = 8: column-block parity / tap half
 
   const int TH = (a.H + 3) / 4;  // row tiles per image
   const int tiles = a.N * TH;
@@ -1356,9 +1360,9 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
     }
   };
 
-  f32x4_t acc[9][2][2];
+  f32x4_t acc[NT][2][2];
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp)
+  for (int tp = 0; tp < NT; ++tp)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1377,7 +1381,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
     return __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
-  // PRE: thread tid transforms logical chunk tid % 8 (8 fixed channels) of halo rows R = tid/8 + 32k; the
+  // PRE: thread tid transforms logical chunk tid % 8 (8 fixed channels) of halo rows R = tid/8 + 8*NWV*k; the
   // physical chunk follows the row's swizzle, so each 8-thread group covers one whole 128-B row
   float pre_sc[8], pre_sh[8];
   if constexpr (PRE) {
@@ -1399,17 +1403,18 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
     if constexpr (PRE) {
       const int n = t / TH, h0 = (t - n * TH) * 4;
       char* sxw = smem + buf * kL1Stage;
-      int off[11];
-      bool ok[11];
+      constexpr int KP = (kL1XRows + 8 * NWV - 1) / (8 * NWV);
+      int off[KP];
+      bool ok[KP];
 #pragma unroll
-      for (int k = 0; k < 11; ++k) {
-        const int R = min((tid >> 3) + 32 * k, kL1XRows - 1);
+      for (int k = 0; k < KP; ++k) {
+        const int R = min((tid >> 3) + 8 * NWV * k, kL1XRows - 1);
         const int hr = R / kL1XP, wc = R - (R / kL1XP) * kL1XP;
         const int h = h0 - 1 + hr, w = wc - 1;
-        ok[k] = (tid >> 3) + 32 * k < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W;
+        ok[k] = (tid >> 3) + 8 * NWV * k < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W;
         off[k] = R * 128 + (((tid & 7) ^ l1_swz(hr, wc)) << 4);
       }
-      pre_act_chunks<DT, 11>(sxw, off, ok, pre_sc, pre_sh);
+      pre_act_chunks<DT, KP>(sxw, off, ok, pre_sc, pre_sh);
       __syncthreads();
     }
     const char* sx = smem + buf * kL1Stage;
@@ -1460,7 +1465,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
       continue;
     }
 #pragma unroll 1
-    for (int j = jp; j < kL1W / 8; j += NWV / 4) {
+    for (int j = TSPL ? 0 : jp; j < kL1W / 8; j += TSPL ? 1 : NWV / 4) {
       // A = dY^T (rows k): output row g, columns 8j + q (+4)
       const int ycol = 8 * j + q;
       const char* yb = sy + (g * kL1W + ycol) * 128;
@@ -1468,29 +1473,32 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = frag(yb, g, ycol, kh * 2 + i);
 #pragma unroll
-      for (int tr = 0; tr < 3; ++tr)
+      for (int u = 0; u < NT; ++u) {
+        const int tp = TSPL ? jp * 5 + u : u;  // TSPL: wave-uniform
+        if (TSPL && tp >= 9) break;
+        const int tr = tp / 3, tu = tp - tr * 3;
+        // B = X (cols c): halo row g + tr, halo column 8j + tu + q (+4)
+        const int xcol = 8 * j + tu + q;
+        const char* xb = sx + ((g + tr) * kL1XP + xcol) * 128;
+        vec8 bf[2];
 #pragma unroll
-        for (int tu = 0; tu < 3; ++tu) {
-          // B = X (cols c): halo row g + tr, halo column 8j + tu + q (+4)
-          const int xcol = 8 * j + tu + q;
-          const char* xb = sx + ((g + tr) * kL1XP + xcol) * 128;
-          vec8 bf[2];
+        for (int c = 0; c < 2; ++c) bf[c] = frag(xb, g + tr, xcol, chh * 2 + c);
 #pragma unroll
-          for (int c = 0; c < 2; ++c) bf[c] = frag(xb, g + tr, xcol, chh * 2 + c);
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-              acc[tr * 3 + tu][i][c] = E::mfma16x16x32(af[i], bf[c], acc[tr * 3 + tu][i][c]);
-        }
+          for (int c = 0; c < 2; ++c) acc[u][i][c] = E::mfma16x16x32(af[i], bf[c], acc[u][i][c]);
+      }
     }
     buf ^= 1;
   }
 
   // partial dW[k][tap][c]: lane holds rows k = kb*16 + 4*(lane>>4) + r, column c = cb*16 + (lane&15)
-  float* dst = a.ws + ((int64_t)blockIdx.x * (NWV / 4) + jp) * 64 * a.ldw;
+  const int64_t part = TSPL ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * (NWV / 4) + jp;
+  float* dst = a.ws + part * 64 * a.ldw;
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp)
+  for (int u = 0; u < NT; ++u) {
+    const int tp = TSPL ? jp * 5 + u : u;
+    if (TSPL && tp >= 9) break;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1498,22 +1506,27 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
         const int k = (kh * 2 + i) * 16 + 4 * (lane >> 4);
         const int cc = (chh * 2 + c) * 16 + (lane & 15);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(int64_t)(k + r) * a.ldw + tp * 64 + cc] = acc[tp][i][c][r];
+        for (int r = 0; r < 4; ++r) dst[(int64_t)(k + r) * a.ldw + tp * 64 + cc] = acc[u][i][c][r];
       }
+  }
 }
 
 bool wgrad3x3_c64_supported(int C, int Kout, int T, int U, int W, int stride, int pad, int win) {
   return !win && C == 64 && Kout == 64 && T == 3 && U == 3 && W == kL1W && stride == 1 && pad == 1;
 }
 
-// The 8-wave form (two partials per block) for the calls without PRE; PDT_WGRAD_L1_W8=0 selects 4 waves.
-// Same box, ResNet-18 bf16 B = 1200: 20.166 / 20.111 / 20.064 (4 waves) vs 20.017 / 20.050 / 20.038 ms (8 waves).
-static bool wgrad_l1_w8() {
-  static const bool on = [] {
+// PDT_WGRAD_L1_W8: 0 = 4 waves; 1 = 8 waves splitting the column blocks (two partials per block; calls with PRE
+// stay on 4 waves); 2 = 8 waves splitting the taps (one partial per block, PRE included); 3 (default) = the column
+// split without PRE, the tap split with PRE.
+// Same box, ResNet-18 bf16 B = 1200: 20.166 / 20.111 / 20.064 (0) vs 20.017 / 20.050 / 20.038 ms (1).
+// Kernel times, same box (tools/r5_w8_prof.sh): without PRE 268 us (1) vs 301 us (2); with PRE 442 us (4 waves)
+// vs 390 us (2).
+static int wgrad_l1_w8() {
+  static const int mode = [] {
     const char* e = getenv("PDT_WGRAD_L1_W8");
-    return !(e && e[0] == '0');
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 3;
   }();
-  return on;
+  return mode;
 }
 
 // number of fp32 partials the kernel writes (blocks x partials per block)
@@ -1521,13 +1534,16 @@ int wgrad3x3_c64_blocks() {
   int dev = 0, cus = 256;
   PDT_HIP_CHECK(hipGetDevice(&dev));
   PDT_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  return (cus + 7) / 8 * 8 * (wgrad_l1_w8() ? 2 : 1);
+  const int mode = wgrad_l1_w8();
+  return (cus + 7) / 8 * 8 * (mode == 1 || mode == 3 ? 2 : 1);
 }
 
 int wgrad3x3_c64_launch(const ConvWgradArgs& a, int partials, int dtype, hipStream_t s) {
-  // the 8-wave form is built without PRE (with it the tap loop's 144 accumulators + the halo transform exceed the
-  // 256 registers of two waves per SIMD and spill inside the DMA window): PRE calls write one partial per block
-  const bool w8 = wgrad_l1_w8();
+  // the column-split form is built without PRE (its 144 accumulators + the halo transform exceed the 256 registers
+  // of two waves per SIMD and spill inside the DMA window): PRE calls then run 4 waves, one partial per block
+  const int mode = wgrad_l1_w8();
+  const bool w8 = mode == 1 || mode == 3;  // column split for the calls without PRE
+  const bool tspl = mode == 2 || (mode == 3 && a.pre_coef);
   const int blocks = w8 ? partials / 2 : partials;
   PDT_COUNT("wgrad3x3_c64");
   // PDT_WGRAD_L1_PIPE=1: the software-pipelined tap loop.  Off by default: in isolation it ran 682 vs 758 TF/s
@@ -1539,7 +1555,9 @@ int wgrad3x3_c64_launch(const ConvWgradArgs& a, int partials, int dtype, hipStre
   if (a.pre_coef) PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
 #define PDT_W3(DT_, P_)                                                                         \
   do {                                                                                          \
-    if (w8 && !P_)                                                                              \
+    if (tspl)                                                                                   \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, false, 8, true>), dim3(blocks), dim3(512), 0, s, a); \
+    else if (w8 && !P_)                                                                         \
       hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, false, false, 8>), dim3(blocks), dim3(512), 0, s, a); \
     else if (pipe)                                                                              \
       hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, true>), dim3(blocks), dim3(256), 0, s, a);  \
@@ -1552,7 +1570,7 @@ int wgrad3x3_c64_launch(const ConvWgradArgs& a, int partials, int dtype, hipStre
     if (a.pre_coef) PDT_W3(kF16, true); else PDT_W3(kF16, false);
   }
 #undef PDT_W3
-  return w8 && !a.pre_coef ? partials : blocks;  // partials written
+  return w8 && !a.pre_coef ? partials : blocks;  // partials written (the tap split: one per block)
 }
 
 // out[r][c] = scale * sum_s ws[s][r][c]   (r < rows, c < cols; ws row stride ldw, out row stride ldo)
