@@ -1084,10 +1084,14 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
                 (lds_s16x4*)(sy + r1 * ROWB + (((kc >> 3) ^ sw1) << 4) + (kc & 7) * 2));
             bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
           }
+          // raised priority while this wave's 16 MFMAs issue: the SIMD's other wave then slots its fragment reads
+          // in between instead of both waves reading at once
+          __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+          __builtin_amdgcn_s_setprio(0);
         }
       }
     }
