@@ -492,12 +492,10 @@ __global__ __launch_bounds__(256) void wgrad_stem_quad_kernel(ConvWgradArgs a) {
           hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r1 * ROWB + ((ch ^ sw1) << 4) + off));
           bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
-        __builtin_amdgcn_s_setprio(1);  // as conv_wgrad_wide_kernel: the SIMD's other waves read meanwhile
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
-        __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);  // the waits and the dY math stay behind the last MFMA
       if (st + 1 < nsteps) {
@@ -726,12 +724,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sy + r1 * ROWB + ((ch ^ sw1) << 4) + off));
           bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
-        __builtin_amdgcn_s_setprio(1);  // as conv_wgrad_wide_kernel: the SIMD's other waves read meanwhile
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
-        __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);  // the waits and the dY math stay behind the last MFMA
       if (st + 1 < nsteps) {
