@@ -256,6 +256,28 @@ void stem_fwd(const Tensor& xp, const Tensor& w, Tensor& y, const OptT& stats, i
 
 int64_t conv_m_tiles(int64_t M, int64_t bm) { return pdt::conv_fwd_m_tiles(M, (int)bm); }
 
+// Which persistent 1x1 backward-data kernel conv_dgrad_impl runs for a launch, if any: 0 none (tiled implicit GEMM),
+// 1 conv1x1.hip (C = 256 -> K = 64 | 128), 2 conv1x1x.hip (sliced, layers 2-4).  The ONE source of this dispatch: the
+// executor asks it (conv_dgrad_persistent) before choosing / autotuning a tile, so the two cannot drift apart.
+static int dgrad_persistent_kind(int64_t K, int64_t C, int64_t bnb, int64_t stride,
+                                 const std::vector<std::vector<int64_t>>& phases, int64_t H, int64_t W, int64_t P,
+                                 int64_t Q, int64_t res_phase) {
+  if (!(bnb == 2 || bnb == 3) || res_phase >= 0 || stride != 1 || phases.size() != 1 || H != P || W != Q) return 0;
+  const auto& f = phases[0];
+  if (f.size() < 6 || f[0] != 0 || f[1] != 0 || f[2] != 1 || f[3] != 1 || f[4] != 0 || f[5] != 0) return 0;
+  const bool x_ok = pdt::conv1x1x_bnb_supported((int)K, (int)C);
+  if ((K == 64 || (K == 128 && bnb == 2)) && C == 256 && pdt::conv1x1_c64_supported(64, C) &&
+      !(pdt::conv1x1x_prefer_l1() && x_ok))
+    return 1;
+  return x_ok ? 2 : 0;
+}
+
+int64_t conv_dgrad_persistent(int64_t K, int64_t C, int64_t bnb, int64_t stride,
+                              const std::vector<std::vector<int64_t>>& phases, int64_t H, int64_t W, int64_t P,
+                              int64_t Q, int64_t res_phase) {
+  return dgrad_persistent_kind(K, C, bnb, stride, phases, H, W, P, Q, res_phase);
+}
+
 // Backward-data of a (strided) conv in ONE launch: phases = [(ph, pw, T, U, ioff_h, ioff_w, woff), ...]
 // over dY [N,P,Q,K] -> dX [N,H,W,C] (+ residual), wt = concatenated per-phase [C][T][U][K] weights.
 void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res, int64_t N, int64_t P,
@@ -332,11 +354,10 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
     a.bn_mask = pmask(bn_mask, dx.numel(), "bn_mask");
     a.stats = pd(*bn_slots, "bn_slots");
   }
-  if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 &&
-      (K == 64 || (K == 128 && bnb == 2)) && C == 256 && H == P && W == Q && pdt::conv1x1_c64_supported(64, C) &&
-      !(pdt::conv1x1x_prefer_l1() && pdt::conv1x1x_bnb_supported((int)K, (int)C))) {
+  const int pk = dgrad_persistent_kind(K, C, bnb, stride, phases, H, W, P, Q, res_phase);
+  if (pk == 1) {
     const auto& f = phases[0];
-    if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
+    {
       // 1x1 256 -> 64 | 128 conv's backward-data with the block-output BN-backward epilogue: persistent kernel
       // (conv1x1.hip);
       // its [256][K] weights start at the phase's offset (bounds checked with the phases above)
@@ -347,10 +368,9 @@ void conv_dgrad_impl(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT&
       return;
     }
   }
-  if ((bnb == 2 || bnb == 3) && res_phase < 0 && stride == 1 && phases.size() == 1 && H == P && W == Q &&
-      pdt::conv1x1x_bnb_supported((int)K, (int)C)) {
+  if (pk == 2) {
     const auto& f = phases[0];
-    if (f[0] == 0 && f[1] == 0 && f[2] == 1 && f[3] == 1 && f[4] == 0 && f[5] == 0) {
+    {
       // ResNet-50 layers 2-4: 1x1 C -> 4C backward-data (conv1 of a bottleneck) with the block-output BN-backward
       // epilogue on the persistent sliced kernel (conv1x1x.hip); [C][K] weights at the phase's offset
       pdt::conv1x1x_bnb_launch(a.x, a.w + f[6], a.y, a.res, a.bn_y1, a.bn_coef1, bnb == 3 ? a.bn_y2 : nullptr,
@@ -1342,6 +1362,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_pre", &conv_fwd_pre);
   m.def("conv1x1x", &conv1x1x);
   m.def("conv1x1x_supported", &conv1x1x_supported);
+  m.def("conv_dgrad_persistent", &conv_dgrad_persistent);
   m.def("conv1x1x_mode", &conv1x1x_mode);
   m.def("conv1x1x_l1_mode", &conv1x1x_l1_mode);
   m.def("conv_fwd_pre_supported", &conv_fwd_pre_supported);
@@ -1350,7 +1371,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_l1_set_pp", &pdt::conv_l1_set_pp, py::arg("mode"),
         "layer1 kernel choice: 1 = 8-wave ping-pong, 0 = 4-wave, -1 = PDT_CONV_L1_PP (default); returns the previous");
   m.def("conv32_set_halo", &pdt::conv32_set_halo, py::arg("on"),
-        "fp32 3x3/s1 64-channel convolutions: 1 = halo kernel (default unless PDT_FP32_CONV_HALO=0), 0 = per-tap "
+        "fp32 3x3/s1 64-channel convolutions: 1 = halo kernel (default), 0 = per-tap "
         "restaging kernel; returns the previous setting");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_finalize_slots", &bn_finalize_slots);

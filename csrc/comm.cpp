@@ -366,6 +366,23 @@ class Communicator {
     std::lock_guard<std::mutex> lk(mu_);
     return (int64_t)pending_.size();
   }
+  // Collective log (ordering tests): "<kind>:<stream>:<elements>" per collective in issue order, where stream is
+  // "comm" (this communicator's stream, queued behind every collective issued on it before) or "inline" (the
+  // caller's compute stream).  Off by default; bounded.
+  void set_log(bool on) {
+    std::lock_guard<std::mutex> lk(mu_);
+    log_on_ = on;
+    log_.clear();
+  }
+  std::vector<std::string> log() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return log_;
+  }
+  void note(const char* kind, bool inline_stream, int64_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (log_on_ && log_.size() < 100000)
+      log_.push_back(std::string(kind) + (inline_stream ? ":inline:" : ":comm:") + std::to_string(n));
+  }
 
   // comm stream <- everything already enqueued on the caller's compute stream
   void join_compute() {
@@ -386,6 +403,7 @@ class Communicator {
     check(t);
     join_compute();
     transport().all_reduce(t.data_ptr(), t.numel(), t, op, stream_);
+    note("all_reduce", false, t.numel());
     track("all_reduce");
     if (!async_op) wait();
   }
@@ -397,18 +415,21 @@ class Communicator {
     check(t);
     hipStream_t cs = compute_stream();
     transport().all_reduce(t.data_ptr(), t.numel(), t, op, cs);
+    note("all_reduce", true, t.numel());
     track("all_reduce (compute stream)", cs);
   }
   void broadcast_inline(Tensor& t, int root) {  // on the caller's stream; same ordering contract as above
     check(t);
     hipStream_t cs = compute_stream();
     transport().broadcast(t.data_ptr(), t.numel(), t, root, cs);
+    note("broadcast", true, t.numel());
     track("broadcast (compute stream)", cs);
   }
   void broadcast(Tensor& t, int root, bool async_op) {
     check(t);
     join_compute();
     transport().broadcast(t.data_ptr(), t.numel(), t, root, stream_);
+    note("broadcast", false, t.numel());
     track("broadcast");
     if (!async_op) wait();
   }
@@ -419,6 +440,7 @@ class Communicator {
                 "comm all_gather: out must hold world x in");
     join_compute();
     transport().all_gather(in.data_ptr(), out.data_ptr(), in.numel(), in, stream_);
+    note("all_gather", false, in.numel());
     track("all_gather");
     if (!async_op) wait();
   }
@@ -537,6 +559,8 @@ class Communicator {
   bool stop_ = false;
   std::deque<Pending> pending_;
   std::vector<hipEvent_t> free_evs_;
+  bool log_on_ = false;
+  std::vector<std::string> log_;
   std::thread watchdog_;
 };
 
@@ -581,11 +605,13 @@ class Bucketer {
     TORCH_CHECK(pid >= 0 && pid < (int64_t)param_bucket_.size(), "bucketer: bad parameter id");
     const int64_t b = param_bucket_[pid];
     TORCH_CHECK(pending_[b] > 0, "bucketer: parameter ", pid, " reported ready twice in one step");
-    if (--pending_[b] == 0) launch(b);
+    --pending_[b];
+    // launch strictly in bucket-index order (upstream Reducer::mark_bucket_ready / next_bucket_): a rank whose local
+    // gradient-ready order differs from another's still issues the same collective sequence
+    while (next_ < lo_.size() && pending_[next_] == 0) launch(next_++);
   }
   void finish() {
-    for (size_t b = 0; b < lo_.size(); ++b)
-      if (!launched_[b]) launch(b);  // buckets of unused parameters: reduce zeros, stay in lock-step
+    while (next_ < lo_.size()) launch(next_++);  // buckets of unused parameters: reduce zeros, stay in lock-step
     comm_->wait();
     reset();
   }
@@ -611,6 +637,7 @@ class Bucketer {
     } else {
       tr.all_reduce(p, n, grad_, "sum", comm_->stream());
     }
+    comm_->note("bucket", false, n);
     comm_->track("gradient bucket all_reduce");
     launched_[b] = true;
     order_.push_back((int64_t)b);
@@ -618,6 +645,7 @@ class Bucketer {
   void reset() {
     pending_ = nparams_;
     launched_.assign(lo_.size(), false);
+    next_ = 0;
     last_order_ = order_;
     order_.clear();
   }
@@ -625,6 +653,7 @@ class Bucketer {
   Tensor grad_;
   std::vector<int64_t> lo_, hi_, param_bucket_, nparams_, pending_;
   std::vector<bool> launched_;
+  size_t next_ = 0;  // next bucket index to launch
   std::vector<int64_t> order_, last_order_;
   int64_t compress_ = 0;
   Tensor scratch_;  // bf16 image of the flat gradient (compress_)
@@ -651,6 +680,8 @@ void register_comm(py::module& m) {
       .def("track_compute", &Communicator::track_compute, py::arg("what") = "graph replay")
       .def("count", &Communicator::count)
       .def("pending", &Communicator::pending)
+      .def("set_log", &Communicator::set_log)
+      .def("log", &Communicator::log)
       .def("inject_stall", &Communicator::inject_stall)
       .def("all_reduce", &Communicator::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
       .def("all_reduce_inline", &Communicator::all_reduce_inline, py::arg("t"), py::arg("op") = "sum")

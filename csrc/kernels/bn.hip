@@ -276,20 +276,15 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 // blocks cost ~20% of bandwidth, tools/bw_probe.py).  tools/ew_bench.py, ResNet shapes at B = 1200 (round 5):
 // U = 1 (one vector per thread, coefficients indexed per vector, the round-4 structure) 5.3-6.1 TB/s, U = 2 and 4
 // 6.2-6.7 TB/s (two-branch backward 7.3-7.6), U = 8 a few % below 4.  Streams larger than the L2s and MALL use
-// nontemporal loads/stores (PDT_EW_NT: threshold override for A/B experiments).
+// nontemporal loads/stores.
 constexpr int kEwU = 4;
-static int64_t env_i64(const char* name, int64_t dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoll(e) : dflt;
-}
 static int ew_blocks(int64_t n8, int U) {
   const int64_t b = (n8 + 256 * U - 1) / (256 * U);
   if (b >= (int64_t(1) << 31)) pdt_hip_fail("elementwise pass: tensor too large", hipErrorInvalidValue, __FILE__, __LINE__);
   return (int)(b < 1 ? 1 : b);
 }
 static bool ew_nt(int64_t bytes) {
-  static const int64_t thr = env_i64("PDT_EW_NT", 64ll << 20);
-  return thr >= 0 && bytes >= thr;
+  return bytes >= (64ll << 20);  // non-temporal loads / stores from 64 MiB operands on (round-4 sweep)
 }
 static bool ew_ch(int C) { return C > 0 && C <= 2048 && (C & (C - 1)) == 0 && C % 8 == 0; }
 

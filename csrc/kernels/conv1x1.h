@@ -23,7 +23,7 @@ void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, doubl
 // forward, conv1 backward-data), N split into slices of 256 (C = 128) or 128 channels (conv1x1x.hip).  w is [N][C].
 bool conv1x1x_supported(int C, int N);
 bool conv1x1x_bnb_supported(int C, int N);  // the backward-data kernel: also C = 64
-bool conv1x1x_prefer_l1();  // PDT_X1_L1=1: layer1's 64 / 128 -> 256 backward-data on conv1x1x_bnb (A/B)
+bool conv1x1x_prefer_l1();  // conv1x1x_l1_mode(1): layer1's 64 / 128 -> 256 backward-data on conv1x1x_bnb (A/B)
 int conv1x1x_l1_mode(int set);  // ... switched at run time (tests); returns the previous mode
 int conv1x1x_mode(int set);  // PDT_CONV1X1X seeds it; set >= 0 changes it, returns the previous mode
 // st > 1: a 1x1 / stride-st conv over nimg H x W images (M = nimg * P * Q output pixels; the downsample convs)

@@ -535,14 +535,8 @@ int x1_cus() {
 }
 
 // forward, C = 256: 64 channels per wave as for C = 128 (slices of 256: half the L2 re-reads of the input; ResNet-50
-// 72.68 -> 72.27 ms/step, same box); PDT_X1_WIDE=0: 32 channels per wave (A/B)
-bool x1_wide() {
-  static const bool on = [] {
-    const char* e = getenv("PDT_X1_WIDE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// 72.68 -> 72.27 ms/step, same box, against 32 channels per wave)
+bool x1_wide() { return true; }
 // NS of C's configuration (the backward-data kernel has no register room for the wide C = 256 variant)
 int x1_slice(int C, bool fwd) { return C <= 128 || (C == 256 && fwd && x1_wide()) ? 256 : 128; }
 
@@ -583,7 +577,7 @@ bool conv1x1x_supported(int C, int N) {
 }
 
 // the backward-data kernel also takes C = 64 (ResNet-50 layer1's conv1 backward-data; the binding prefers it over
-// conv1x1_c64_bnb when PDT_X1_L1=1)
+// conv1x1_c64_bnb when conv1x1x_l1_mode(1) is set)
 bool conv1x1x_bnb_supported(int C, int N) {
   if (!conv1x1x_mode(-1) || !(C == 64 || C == 128 || C == 256 || C == 512) || N <= 0) return false;
   return x1_n_ok(C, N);
@@ -595,10 +589,7 @@ bool x1_n_ok(int C, int N) {
 }
 
 int conv1x1x_l1_mode(int set) {
-  static int on = [] {
-    const char* e = getenv("PDT_X1_L1");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
+  static int on = 0;  // (settable for tests / A/B through the binding)
   const int prev = on;
   if (set >= 0) on = set;
   return prev;

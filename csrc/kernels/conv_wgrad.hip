@@ -1314,9 +1314,9 @@ PDT_DEVICE int l1_swz(int row2d, int col) { return (((col >> 1) & 1) << 1) | ((r
 //  - the column blocks (TSPL = false: even / odd blocks, separate partials, 2 per block; 144 accumulators per lane,
 //    too many registers left for PRE's halo transform), or
 //  - the taps (TSPL = true: taps 0-4 / 5-8 into one partial per block; 80 accumulators per lane).
-template <int DT, bool PRE = false, bool kL1Pipe = true, int NWV = 4, bool TSPL = false>
+template <int DT, bool PRE = false, int NWV = 4, bool TSPL = false>
 __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a) {
-  static_assert(NWV == 4 ? !TSPL : (NWV == 8 && !kL1Pipe && (TSPL || !PRE)), "unsupported wgrad3x3_c64 form");
+  static_assert(NWV == 4 ? !TSPL : (NWV == 8 && (TSPL || !PRE)), "unsupported wgrad3x3_c64 form");
   constexpr int NT = TSPL ? 5 : 9;  // taps per wave
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -1423,51 +1423,6 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
     }
     const char* sx = smem + buf * kL1Stage;
     const char* sy = sx + kL1XBytes;
-    if constexpr (kL1Pipe) {
-      // software-pipelined: the fragments of the next tap (or of the next column block's first tap) are read
-      // while this tap's 4 MFMAs run -- one wave per SIMD, so nothing else would cover the transposed-read latency
-      // (the straight loop below exposes it on every tap: ~36 % MFMA busy).  Tap t >= 1 of a block reads into
-      // slot t & 1; tap 0 into the carried slot (nb / na), loaded during the previous block's last tap.
-      auto rd_a = [&](int j, vec8 (&dst)[2]) {
-        const int ycol = 8 * j + q;
-        const char* yb = sy + (g * kL1W + ycol) * 128;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) dst[i] = frag(yb, g, ycol, kh * 2 + i);
-      };
-      auto rd_b = [&](int j, int tp, vec8 (&dst)[2]) {
-        const int tr = tp / 3, tu = tp - tr * 3;
-        const int xcol = 8 * j + tu + q;
-        const char* xb = sx + ((g + tr) * kL1XP + xcol) * 128;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) dst[c] = frag(xb, g + tr, xcol, chh * 2 + c);
-      };
-      vec8 na[2], nb[2];
-      rd_a(0, na);
-      rd_b(0, 0, nb);
-#pragma unroll 1
-      for (int j = 0; j < kL1W / 8; ++j) {
-        vec8 af[2] = {na[0], na[1]};
-        vec8 bs[3][2] = {{nb[0], nb[1]}, {nb[0], nb[1]}, {nb[0], nb[1]}};  // [2] = tap 0's slot
-#pragma unroll
-        for (int tp = 0; tp < 9; ++tp) {
-          const int cur = tp == 0 ? 2 : (tp & 1);
-          if (tp < 8) {
-            rd_b(j, tp + 1, bs[(tp + 1) & 1]);
-          } else if (j + 1 < kL1W / 8) {
-            rd_a(j + 1, na);
-            rd_b(j + 1, 0, nb);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) acc[tp][i][c] = E::mfma16x16x32(af[i], bs[cur][c], acc[tp][i][c]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      buf ^= 1;
-      continue;
-    }
 #pragma unroll 1
     for (int j = TSPL ? 0 : jp; j < kL1W / 8; j += TSPL ? 1 : NWV / 4) {
       // A = dY^T (rows k): output row g, columns 8j + q (+4)
@@ -1550,23 +1505,17 @@ int wgrad3x3_c64_launch(const ConvWgradArgs& a, int partials, int dtype, hipStre
   const bool tspl = mode == 2 || (mode == 3 && a.pre_coef);
   const int blocks = w8 ? partials / 2 : partials;
   PDT_COUNT("wgrad3x3_c64");
-  // PDT_WGRAD_L1_PIPE=1: the software-pipelined tap loop.  Off by default: in isolation it ran 682 vs 758 TF/s
-  // (tools/conv_bench.py) and the whole step measured 20.97 / 20.82 vs 21.03 / 21.00 ms with it (same box)
-  static const bool pipe = [] {
-    const char* e = getenv("PDT_WGRAD_L1_PIPE");
-    return e && e[0] == '1';
-  }();
+  // (a software-pipelined tap loop for the 4-wave form ran slower -- 682 vs 758 TF/s isolated, 20.97 / 20.82 vs
+  // 21.03 / 21.00 ms/step -- and was removed in round 6)
   if (a.pre_coef) PDT_COUNT("wgrad3x3_c64_fused_bn_relu");
 #define PDT_W3(DT_, P_)                                                                         \
   do {                                                                                          \
     if (tspl)                                                                                   \
-      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, false, 8, true>), dim3(blocks), dim3(512), 0, s, a); \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, 8, true>), dim3(blocks), dim3(512), 0, s, a); \
     else if (w8 && !P_)                                                                         \
-      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, false, false, 8>), dim3(blocks), dim3(512), 0, s, a); \
-    else if (pipe)                                                                              \
-      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, true>), dim3(blocks), dim3(256), 0, s, a);  \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, false, 8>), dim3(blocks), dim3(512), 0, s, a); \
     else                                                                                        \
-      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_, false>), dim3(blocks), dim3(256), 0, s, a); \
+      hipLaunchKernelGGL((wgrad3x3_c64_kernel<DT_, P_>), dim3(blocks), dim3(256), 0, s, a); \
   } while (0)
   if (dtype == kBF16) {
     if (a.pre_coef) PDT_W3(kBF16, true); else PDT_W3(kBF16, false);
@@ -1733,11 +1682,7 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       PDT_COUNT("wgrad_stem_fused");
     else
       PDT_COUNT("wgrad_stem");
-    static const bool rows = [] {  // PDT_STEM_ROWS=0: the window-staged quad kernel (A/B)
-      const char* e = getenv("PDT_STEM_ROWS");
-      return !(e && e[0] == '0');
-    }();
-    if (a.f_y != nullptr && rows && a.Pm % 4 == 0 && a.Qm % 16 == 0 && a.pix_per_split % 64 == 0 &&
+    if (a.f_y != nullptr && a.Pm % 4 == 0 && a.Qm % 16 == 0 && a.pix_per_split % 64 == 0 &&
                a.stride_h == 2 && a.dil_h == 2 && a.pad_h == 0 && a.cs == 4) {
       // raw-image-row staging (wgrad_stem_rows_kernel): steps are 4 x 16 pixel blocks, divisions by steps per
       // image and per 4-row band

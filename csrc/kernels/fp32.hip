@@ -452,12 +452,8 @@ __global__ __launch_bounds__(512) void conv32_halo_kernel(Conv32Args args) {
   conv32_epilogue<BM, BN, WAVES_M, WAVES_N, EPI, RES>(a, acc, m0, n0, tile_m, wn, wm, tid, lane, smem);
 }
 
-// conv32_halo_kernel's geometry contract (see above); PDT_FP32_CONV_HALO=0 / conv32_set_halo(0): the tap-restaging
-// conv32_kernel for A/B
-static bool g_conv32_halo = [] {
-  const char* e = getenv("PDT_FP32_CONV_HALO");
-  return !(e && e[0] == '0');
-}();
+// conv32_halo_kernel's geometry contract (see above); conv32_set_halo(0): the tap-restaging conv32_kernel (tests)
+static bool g_conv32_halo = true;
 int conv32_set_halo(int on) {
   const int prev = g_conv32_halo ? 1 : 0;
   g_conv32_halo = on != 0;

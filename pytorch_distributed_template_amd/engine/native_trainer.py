@@ -23,6 +23,7 @@ from ..models.executor import ResNetExecutor
 from ..optim.flat import FlatBuffers, FlatParams
 from ..optim.sgd import FusedSGD
 from ..parallel.ddp import GradBucketer, broadcast_parameters, sync_buffers
+from ..parallel.syncbn import native_syncbn_wiring
 
 
 class NativeTrainer:
@@ -64,29 +65,9 @@ class NativeTrainer:
         # HIP events around bucketer.finish(): the time the compute stream waits for gradient all-reduces
         # that backward did not hide (exposed communication)
         self._comm_events = [] if time_comm else None
-        # SyncBN: over the native communicator when there is one (also at a forced world of 1: the full SyncBN path
-        # with identity all-reduces), else over torch.distributed at world > 1.
-        # Native, PDT_SYNCBN_COMM=own: the statistics get a communicator of their OWN and are all-reduced
-        # inline on the compute stream, forward and backward.  They are tiny and latency-bound and sit on the critical
-        # path (dgrad -> BN sums -> all-reduce -> finalize -> apply -> next dgrad), so they must never queue behind a
-        # 25 MiB gradient bucket on the bucket communicator's stream; RCCL orders collectives per communicator, so
-        # two communicators issued in the same host order on every rank keep both sequences consistent.
-        # PDT_SYNCBN_COMM=shared (the default until a >= 2-GPU run has validated two concurrent RCCL communicators,
-        # tests/test_multigpu.py): one communicator (forward inline, backward on the comm stream behind the buckets).
-        nsync = sync_bn and self.ncomm is not None
-        self.ncomm_bn = None
-        if nsync and os.environ.get("PDT_SYNCBN_COMM", "shared") == "own":
-            from ..parallel.comm import NativeComm
-            self.ncomm_bn = NativeComm(self.device, process_group, timeout_s=comm_timeout_s, transport=comm_transport)
-        sync_kw = dict(syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and self.distributed and not nsync)
-                       else None)
-        if self.ncomm_bn is not None:
-            sync_kw.update(syncbn_allreduce=self.ncomm_bn.all_reduce_inline, syncbn_world=self.ncomm_bn.world)
-        elif nsync:
-            sync_kw.update(syncbn_allreduce=self.ncomm.all_reduce, syncbn_world=self.ncomm.world)
-            if dtype != torch.float32 and os.environ.get("PDT_SYNCBN_INLINE", "1") != "0":
-                # forward statistics straight onto the compute stream (no bucket is in flight during the forward)
-                sync_kw["syncbn_allreduce_fwd"] = self.ncomm.all_reduce_inline
+        # SyncBN collectives: which communicator / stream every statistic all-reduce uses (parallel/syncbn.py)
+        self.ncomm_bn, sync_kw = native_syncbn_wiring(sync_bn, self.ncomm, process_group, self.distributed, dtype,
+                                                      comm_timeout_s, comm_transport)
         if dtype == torch.float32:
             from ..models.executor32 import ResNetExecutor32
             self.executor = ResNetExecutor32(model, self.flat, self.device, grad_ready=self.bucketer.grad_ready,
@@ -98,10 +79,10 @@ class NativeTrainer:
         # validates without autocast, `distributed_syncBN_amp.py:311-317`), whatever the training dtype
         self._eval32 = None
         self._eval32_at = -1  # optimizer step count its derived layouts were gathered at
-        if eval_fp32 and dtype != torch.float32 and getattr(model, "groups", 1) > 1:
-            # grouped convs (ResNeXt) have no fp32 native kernels: validate in the training dtype
+        from ..models.executor32 import fp32_supported
+        if eval_fp32 and dtype != torch.float32 and not fp32_supported(model):
             import warnings
-            warnings.warn("--eval-precision fp32: no native fp32 grouped convolution; validating in the compute dtype")
+            warnings.warn("--eval-precision fp32: no native fp32 kernels for this model; validating in the compute dtype")
             eval_fp32 = False
         if eval_fp32 and dtype != torch.float32:
             from ..models.executor32 import ResNetExecutor32

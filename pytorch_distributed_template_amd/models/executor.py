@@ -183,12 +183,12 @@ class ResNetExecutor:
             self._sync_sum = lambda t: dist.all_reduce(t, group=syncbn_group)
         self.wgrad_blocks = wgrad_blocks  # split-K targets (tools/conv_bench.py sweep: 3x3 best ~2048, 1x1 ~512)
         self.wgrad_blocks_1x1 = wgrad_blocks_1x1
-        # generic-path stem tile (window mode, BK=32); PDT_STEM_TILE=BMxBN overrides (tuning)
-        stile = os.environ.get("PDT_STEM_TILE", "")
-        self.stem_tile = tuple(int(v) for v in stile.split("x")) if stile else (256, 64)
-        self.stem_blocks_per_cu = int(os.environ.get("PDT_STEM_BPC", "2"))
+        # generic-path stem tile (window mode, BK=32) and the dedicated stem kernel's workgroups per CU (round-3/4
+        # sweeps; their tuning knobs were removed in round 6)
+        self.stem_tile = (256, 64)
+        self.stem_blocks_per_cu = 2
         self.wgrad_l1 = os.environ.get("PDT_WGRAD_L1", "1") == "1"
-        self.bk32_short = os.environ.get("PDT_BK32_SHORT", "1") == "1"
+        self.bk32_short = True
         self._c1x1 = hasattr(self.C, "conv1x1_c64")
         self._c1x1x = hasattr(self.C, "conv1x1x")
         # a layer1 block's inner BN + ReLU applied by its consumers (conv2 forward and conv2 weight
@@ -196,17 +196,17 @@ class ResNetExecutor:
         self.fuse_pre = os.environ.get("PDT_FUSE_PRE", "1") == "1"
         # stem backward: weight gradient with in-kernel dY (PDT_STEM_FUSED=0: separate apply pass + wgrad)
         self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
-        # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad (PDT_COMPACT_DS=0: off)
-        self.compact_ds = os.environ.get("PDT_COMPACT_DS", "1") == "1"
-        self.bwd_buf_per_block = os.environ.get("PDT_BWD_BUF_PER_BLOCK", "1") == "1"
-        # backward-only derived weight layouts gathered on the side stream under the forward (PDT_SPLIT_DERIVED=0: off)
-        self.split_derived = os.environ.get("PDT_SPLIT_DERIVED", "1") == "1"
+        # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad
+        self.compact_ds = True
+        self.bwd_buf_per_block = True
+        # backward-only derived weight layouts gathered on the side stream under the forward
+        self.split_derived = True
         # block-output BN-backward reduce fused into the next block's first dgrad epilogue where dX has at most
-        # this many pixels per image (PDT_FUSE_BLOCK_BN_MAXHW; larger: plain dgrad + a separate reduce pass).
-        # Round 2 made the fused masked epilogues straight-line (tools/epi_bench.py: layer1 803 -> 598 us,
-        # layer2 2-branch 766 -> 508 us), after which fusing at every resolution measured equal or faster than
-        # the separate reduce (A/B 21.76 -> 21.71 ms/step), so it is the default everywhere.
-        self.fuse_block_bn_maxhw = int(os.environ.get("PDT_FUSE_BLOCK_BN_MAXHW", "1000000"))
+        # this many pixels per image (larger: plain dgrad + a separate reduce pass).  Round 2 made the fused masked
+        # epilogues straight-line (tools/epi_bench.py: layer1 803 -> 598 us, layer2 2-branch 766 -> 508 us), after
+        # which fusing at every resolution measured equal or faster than the separate reduce (A/B 21.76 -> 21.71
+        # ms/step), so it is on everywhere.
+        self.fuse_block_bn_maxhw = 1000000
         # uint8 input batches are normalised inside stem_pack: x/255 -> (x - mean) / std
         from ..data.transforms import IMAGENET_MEAN, IMAGENET_STD
         std = torch.tensor(IMAGENET_STD)
@@ -250,8 +250,7 @@ class ResNetExecutor:
         src = st.slot.offset + ((k * st.R + r) * st.S + s_) * st.cin + c_
         m = torch.where((s_ < st.S) & (c_ < st.cin), src, torch.full_like(src, -1))
         # dedicated persistent stem kernel (csrc/kernels/stem.hip) for the torchvision stem geometry
-        self.stem_kernel = (st.cout == 64 and st.R == 7 and st.S == 7 and st.st == 2 and st.pad == 3 and
-                            os.environ.get("PDT_STEM_KERNEL", "dedicated") == "dedicated")
+        self.stem_kernel = st.cout == 64 and st.R == 7 and st.S == 7 and st.st == 2 and st.pad == 3
         self.stem_w_off = off[0]
         derived_maps.append(m.reshape(-1).to(torch.int32))
         off[0] += m.numel()
@@ -622,11 +621,9 @@ class ResNetExecutor:
             else:
                 self.C.conv_dgrad_bn(dy, self.derived, dx, res, N, P, Q, c.cout, c.cin, H, W, dst, phases, bm, bn,
                                      bk, *(bnb or (0, None, None, None, None, None, None)), res_phase)
-        persistent = bnb is not None and bnb[0] in (2, 3) and res_phase < 0 and dst == 1 and len(phases) == 1 and \
-            c.R == 1 and c.S == 1 and H == P and W == Q and (
-                (self._c1x1 and c.cin == 256 and (c.cout == 64 or (c.cout == 128 and bnb[0] == 2)) and
-                 self.C.conv1x1_c64_supported(64, 256)) or
-                (self._c1x1x and self.C.conv1x1x_supported(c.cout, c.cin)))
+        # the binding's own dispatch predicate (csrc/bindings.cpp dgrad_persistent_kind): never re-derived here
+        persistent = self.C.conv_dgrad_persistent(c.cout, c.cin, bnb[0] if bnb else 0, dst, phases, H, W, P, Q,
+                                                  res_phase) != 0
         if persistent:
             # the binding runs a persistent 1x1 backward-data kernel (conv1x1.hip / conv1x1x.hip), which has no
             # tile: no tile choice (or autotune timing) for this shape (the static tile only satisfies the binding's
@@ -880,7 +877,7 @@ class ResNetExecutor:
             else:
                 self.bn_bwd(bns[-1], rec["ys"][-1], g, rec["omask"], cnt, dsbn, rec["yd"] if ds else None)
                 mask_src = rec["omask"]
-            # per-block dY buffers (PDT_BWD_BUF_PER_BLOCK=0: two shared ones): a shared buffer's next write has
+            # per-block dY buffers (instead of two shared ones): a shared buffer's next write has
             # to wait for the side-stream weight gradient still reading it, and each such cross-stream
             # wait left the GPU idle ~20-35 us (rocprof trace); per block costs a few GB of HBM, not time
             bk_ = (lambda nm: (nm, bi)) if self.bwd_buf_per_block else (lambda nm: nm)

@@ -33,6 +33,11 @@ from .resnet import BasicBlock, ResNet
 STEM_K = 192  # im2col width of the 7x7x3 stem (147 columns, zero padded to a multiple of 64)
 
 
+def fp32_supported(model) -> bool:
+    """Models this executor runs: torchvision-layout ResNets without grouped convolutions."""
+    return isinstance(model, ResNet) and model.groups == 1
+
+
 class ResNetExecutor32(ResNetExecutor):
     """fp32 counterpart of :class:`ResNetExecutor` (same public interface)."""
 
@@ -40,7 +45,7 @@ class ResNetExecutor32(ResNetExecutor):
                  grad_ready: Optional[Callable[[int], None]] = None, syncbn_group=None,
                  syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0,
                  wgrad_blocks: int = 2048):
-        if not isinstance(model, ResNet) or model.groups != 1:
+        if not fp32_supported(model):
             raise NotImplementedError("native fp32 executor supports torchvision-style ResNets with groups=1")
         self.C = native.C
         self.n_slots = self.C.stat_slots()
@@ -157,14 +162,14 @@ class ResNetExecutor32(ResNetExecutor):
     def _bn_tile(n: int) -> int:
         return 128 if n % 128 == 0 else 64
 
-    _WIDE = os.environ.get("PDT_FP32_TILE", "wide") == "wide"
-    # 64-channel GEMMs (layer1, the stem): rows per tile (128: 4 waves of 64x32; 256: 4 waves of 64x64; 512: 8 waves)
-    _BM64 = int(os.environ.get("PDT_FP32_BM64", "128"))
+    _WIDE = True
+    # 64-channel GEMMs (layer1, the stem): rows per tile (128: 4 waves of 64x32; round-3 sweep over 128 / 256 / 512)
+    _BM64 = 128
 
     def _tile32(self, n: int, m: int):
         """(BM, BN) of the fp32 implicit GEMM: 8-wave 256-row tiles (256x256 / 256x128, twice / 1.3x the FLOP per
         staged byte of 128x128) when the GEMM has enough rows to fill the chip, else the 4-wave 128-row tiles.
-        PDT_FP32_TILE=legacy: always the 128-row tiles (A/B)."""
+        (Round 3: the 128-row-only table measured slower.)"""
         if self._WIDE and m >= 256 * 256:
             if n % 256 == 0:
                 return 256, 256
@@ -204,12 +209,12 @@ class ResNetExecutor32(ResNetExecutor):
 
     _FUSE_BN = os.environ.get("PDT_FP32_FUSE_BN", "1") == "1"
 
-    _HALO = os.environ.get("PDT_FP32_HALO", "1") == "1"
+    _HALO = True
     # stem backward tail: max-pool backward + ReLU mask recomputed inside the BN-backward reduce and apply (no dz
     # tensor); PDT_FP32_STEM_FUSE=0: maxpool_bwd_relu32 + bn_bwd_reduce32 + bn_bwd_apply32 over a stored dz
     _FUSE_STEM = os.environ.get("PDT_FP32_STEM_FUSE", "1") == "1"
     # stem weight gradient: every kernel-row pair per block (dY staged once, not once per pair); 0: one block per pair
-    _STEM4 = os.environ.get("PDT_FP32_STEM4", "1") == "1"
+    _STEM4 = True
     # ... and its dY computed inside that kernel from the pooled gradient, argmax, conv output and BN coefficients (the
     # apply pass and the fp32 dY tensor disappear); PDT_FP32_STEM_WG_FUSE=0: stem_pool_bwd_apply32 + the plain kernel
     _STEM_WG_FUSE = os.environ.get("PDT_FP32_STEM_WG_FUSE", "1") == "1"

@@ -12,7 +12,6 @@ buffers.  They are the unit-test surface of the kernels (tests/test_kernels_gpu.
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -22,8 +21,8 @@ from . import native
 
 # shortest reduction that goes to the ping-pong kernel: tools/conv_bench.py --r50 (forward + BN statistics) measured
 # it ahead of the 128x128 kernel from two K-steps on (ResNet-50 1x1 convs 128->512: 278 vs 251 TF/s, 256->1024:
-# 452 vs 392); PDT_PP_MIN_K overrides (the round-1 table used 512)
-_PP_MIN_K = int(os.environ.get("PDT_PP_MIN_K", "128"))
+# 452 vs 392; the round-1 table used 512)
+_PP_MIN_K = 128
 
 
 def conv_tile(cout: int, kdim: int = 0) -> Tuple[int, int]:

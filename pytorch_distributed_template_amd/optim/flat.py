@@ -54,7 +54,11 @@ class FlatParams:
         self.by_param: Dict[int, ParamSlot] = {}
         # PDT_VALIDATE guard bands (ops/validate.py): extra canary elements after every slot of the gradient buffer
         from ..ops import validate
-        guard = int(os.environ.get("PDT_VALIDATE_GUARD", "0") or 0) if validate.level_from_env() > 0 else 0
+        # (single process only: a multi-rank run all-reduces whole bucket ranges, canaries included -- so the slot
+        # padding is only reserved when the canaries will be installed, and a multi-rank buffer can be re-laid)
+        guarded = guards and int(os.environ.get("WORLD_SIZE", "1")) == 1
+        guard = (int(os.environ.get("PDT_VALIDATE_GUARD", "0") or 0)
+                 if guarded and validate.level_from_env() > 0 else 0)
         self.guard = guard
         self.align = align
         off = 0
@@ -80,8 +84,7 @@ class FlatParams:
                 p.grad = _phys_view(self.grad, s.offset, s.shape, s.channels_last)
         # parameters that receive weight decay: all of them, like the reference (SURVEY §2.2 --wd)
         self.refresh_shadow()
-        # (single process only: a multi-rank run all-reduces whole bucket ranges, canaries included)
-        if guards and guard and self.device.type == "cuda" and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        if guard and self.device.type == "cuda":
             self._install_guards(validate)
 
     def _install_guards(self, validate) -> None:

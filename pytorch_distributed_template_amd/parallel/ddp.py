@@ -55,6 +55,9 @@ class GradBucketer:
         self._policy = (bucket_cap_mb, first_bucket_mb, last_bucket_mb)
         self._assign(list(range(len(flat.slots) - 1, -1, -1)))
         self._works = []
+        self._next = 0  # next bucket index to launch
+        self.launch_log: List[int] = []  # bucket ids in launch order, this step
+        self.last_launch_order: List[int] = []  # ... of the last finished step (tests)
         self._observed: Optional[List[int]] = [] if (rebuild and self.enabled) else None
         self.rebuilt = False
 
@@ -128,25 +131,34 @@ class GradBucketer:
             self._observed.append(pid)
         bid = self.bucket_of[pid]
         self._pending[bid] -= 1
-        if self._pending[bid] == 0:
-            b = self.buckets[bid]
-            view = self.flat.grad[b["lo"]:b["hi"]]
-            self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        # launch strictly in bucket-index order (upstream Reducer::mark_bucket_ready / next_bucket_): a rank whose
+        # local ready order differs from rank 0's still issues the same collective sequence as every other rank
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            self._launch(self._next)
+            self._next += 1
+
+    def _launch(self, bid: int) -> None:
+        b = self.buckets[bid]
+        view = self.flat.grad[b["lo"]:b["hi"]]
+        self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        self.launch_log.append(bid)
 
     def finish(self) -> bool:
         """Wait (stream-wise) for every bucket; launch any bucket whose params produced no grad.  After the first
         step of a ``rebuild`` bucketer, rebuild the buckets from the observed order; returns True when it did."""
         if not self.enabled:
             return False
-        for bid, n in enumerate(self._pending):
-            if n > 0:  # unused parameters: reduce whatever is in the buffer (zeros) to stay in lock-step
-                b = self.buckets[bid]
-                self._works.append(dist.all_reduce(self.flat.grad[b["lo"]:b["hi"]], group=self.pg,
-                                                   async_op=True))
+        # buckets not launched yet (unused parameters, or held behind one): reduce whatever is in the buffer (zeros for
+        # unused parameters) in index order, to stay in lock-step
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
         for w in self._works:
             w.wait()
         self._works.clear()
         self._pending = [len(b["params"]) for b in self.buckets]
+        self._next = 0
+        self.last_launch_order, self.launch_log = self.launch_log, []
         if self._observed is not None:
             return self._rebuild_from_observed()
         return False

@@ -51,6 +51,13 @@ from ..optim.flat import FlatBuffers, FlatParams
 from ..optim.sgd import FusedSGD
 
 
+def _fp32_supported(model) -> bool:
+    """Whether the native fp32 executor (models/executor32.py) can run ``model`` -- the same predicate
+    NativeTrainer applies before building its fp32 validation executor."""
+    from ..models.executor32 import fp32_supported
+    return fp32_supported(model)
+
+
 class _LocalGroup:
     """DataParallel collectives when replicas share a device (RCCL refuses duplicate GPUs): device copies and
     adds on the current streams, reduced in replica order (deterministic)."""
@@ -102,6 +109,10 @@ class NativeDataParallelTrainer:
         # shadow and the master-read parameters)
         self._eval32 = None
         self._eval32_at = -1
+        if eval_fp32 and dtype != torch.float32 and not _fp32_supported(model):
+            import warnings
+            warnings.warn("--eval-precision fp32: no native fp32 kernels for this model; validating in the compute dtype")
+            eval_fp32 = False
         if eval_fp32 and dtype != torch.float32:
             from ..models.executor32 import ResNetExecutor32
             self._eval32 = []

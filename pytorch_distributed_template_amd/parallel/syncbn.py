@@ -17,6 +17,8 @@ Eval mode is plain BatchNorm with running statistics.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -101,3 +103,38 @@ class SyncBatchNorm(nn.BatchNorm2d):
         for name, child in module.named_children():
             out.add_module(name, cls.convert_sync_batchnorm(child, process_group))
         return out
+
+
+def native_syncbn_wiring(sync_bn: bool, ncomm, process_group, distributed: bool, dtype: torch.dtype,
+                         comm_timeout_s: float = 0.0, comm_transport: str = "auto"):
+    """Which communicator and stream every SyncBN statistic all-reduce of the native executor uses.
+
+    Returns ``(ncomm_bn, kwargs)``: ``kwargs`` go to the executor (``syncbn_group`` for c10d, or
+    ``syncbn_allreduce`` / ``syncbn_allreduce_fwd`` / ``syncbn_world`` for the native communicator), ``ncomm_bn`` is
+    the statistics' own communicator (or None).
+
+    With the native communicator (``--comm native``) the default, ``PDT_SYNCBN_COMM=own``, gives the statistics a
+    communicator of their OWN, all-reduced inline on the compute stream, forward and backward.  They are tiny,
+    latency-bound and on the critical path (dgrad -> BN sums -> all-reduce -> finalize -> apply -> next dgrad), so
+    they must never queue behind a 25 MiB gradient bucket on the bucket communicator's stream.  RCCL orders
+    collectives per communicator, and both sequences are issued in the same host order on every rank (the executor's
+    schedule is fixed), so the two communicators stay consistent; tests/test_distributed_cpu.py records both
+    sequences per rank at world 2 / 4 over the host transport.  ``PDT_SYNCBN_COMM=shared`` keeps ONE communicator
+    (forward statistics inline, backward on the comm stream behind any bucket in flight) -- the round-5 default."""
+    kw = dict(syncbn_group=(process_group or dist.group.WORLD) if (sync_bn and distributed and ncomm is None)
+              else None)
+    if not sync_bn or ncomm is None:
+        return None, kw
+    mode = os.environ.get("PDT_SYNCBN_COMM", "own")
+    if mode not in ("own", "shared"):
+        raise ValueError(f"PDT_SYNCBN_COMM must be 'own' or 'shared', got {mode!r}")
+    if mode == "own":
+        from .comm import NativeComm
+        bn = NativeComm(ncomm.device, process_group, timeout_s=comm_timeout_s, transport=comm_transport)
+        kw.update(syncbn_allreduce=bn.all_reduce_inline, syncbn_world=bn.world)
+        return bn, kw
+    kw.update(syncbn_allreduce=ncomm.all_reduce, syncbn_world=ncomm.world)
+    if dtype != torch.float32:
+        # forward statistics straight onto the compute stream (no bucket is in flight during the forward)
+        kw["syncbn_allreduce_fwd"] = ncomm.all_reduce_inline
+    return None, kw

@@ -128,3 +128,25 @@ def test_dp_fp32_eval_equals_executor32(device_ids):
     for _ in range(2):
         dp16.train_step(x, t)
     assert not torch.equal(dp16.eval_step(x, t)[0], ref)
+
+
+def test_dp_resnext_default_eval_precision_builds_and_runs():
+    """native DataParallel of a grouped-conv model with the default eval precision (fp32 validation
+    requested) must build and validate -- fp32 validation falls back to the compute dtype where the fp32 executor
+    has no kernels, instead of raising at construction."""
+    import warnings
+    from pytorch_distributed_template_amd.models import registry
+    from pytorch_distributed_template_amd.models.executor32 import fp32_supported
+    from pytorch_distributed_template_amd.parallel.dp import NativeDataParallelTrainer
+    torch.manual_seed(0)
+    model = registry.create("resnext50_32x4d")
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        dp = NativeDataParallelTrainer(model, [0, 0], dtype=torch.bfloat16, eval_fp32=True)
+    assert (dp._eval32 is not None) == fp32_supported(model)
+    x = torch.randn(8, 3, 64, 64, device="cuda")
+    t = torch.randint(0, 1000, (8,), device="cuda")
+    _, met = dp.train_step(x, t)
+    logits, _ = dp.eval_step(x, t)
+    torch.cuda.synchronize()
+    assert torch.isfinite(met).all() and torch.isfinite(logits.float()).all()

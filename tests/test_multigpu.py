@@ -28,8 +28,8 @@ def test_native_comm_syncbn_two_gpus(tmp_path, syncbn_comm):
     """SyncBN through the native RCCL communicator on two real devices against the full-batch oracle: in fp32, one
     step, every parameter update within 1e-4 and running statistics within 1e-5 of ONE process running both ranks'
     batches with plain BN (test_ddp_numerics_gpu.check_syncbn_fp32_full_batch) -- with the statistics on the gradient
-    buckets' communicator (PDT_SYNCBN_COMM=shared, the default) and on a communicator of their own running
-    concurrently with the bucket all-reduces (own); then the bf16 path against c10d's SyncBN within 1e-6."""
+    buckets' communicator (PDT_SYNCBN_COMM=shared) and on a communicator of their own running concurrently with the
+    bucket all-reduces (own, the default since round 6); then the bf16 path against c10d's SyncBN within 1e-6."""
     a = _run_ranks(tmp_path, PDT_TEST_BACKEND="gloo", PDT_TEST_COMM="native", PDT_TEST_SYNCBN=1, PDT_TEST_STEPS=1,
                    PDT_TEST_DTYPE="fp32", PDT_SYNCBN_COMM=syncbn_comm)
     assert a["transport"] == "rccl"

@@ -121,6 +121,17 @@ def _bucketer_worker(rank, world, port, q):
         bk.finish()
         out["orders"].append(list(bk.last_launch_order()))
         out["grads"].append(grad.numpy().copy())  # numpy: tensors would travel as shared memory of a dying process
+    # rank-dependent ready order: odd ranks finish bucket 1 before bucket 0.  Launches stay in bucket-index order
+    # (bucket 1 is held until bucket 0 completes), so every rank issues the same collective sequence
+    out["skew_launched"] = []
+    for p, (o, n) in enumerate(zip(offs, sizes)):
+        grad[o:o + n] = (rank + 1) * (p + 1) + 3
+    for p in ((3, 2, 5, 4) if rank % 2 else (5, 4, 3, 2)):
+        bk.ready(p)
+        out["skew_launched"].append(bk.launched())
+    bk.finish()
+    out["skew_order"] = list(bk.last_launch_order())
+    out["skew_grad"] = grad.numpy().copy()
     try:
         bk.ready(5)
         bk.ready(4)  # bucket 0 complete (launched on every rank)
@@ -150,6 +161,12 @@ def test_cpp_bucketer_multi_rank(world):
                 want[off:off + n] = sum((q + 1) * (p + 1) + step for q in range(world))
             assert torch.equal(torch.from_numpy(g), want), (r, step)
         assert "reported ready twice" in o["double_ready"]
+        assert o["skew_order"] == [0, 1, 2]
+        assert o["skew_launched"] == ([0, 0, 0, 2] if r % 2 else [0, 1, 1, 2])
+        want = torch.zeros(64)
+        for p, (off, n) in enumerate(zip(offs, sizes)):
+            want[off:off + n] = sum((q + 1) * (p + 1) + 3 for q in range(world))
+        assert torch.equal(torch.from_numpy(o["skew_grad"]), want), r
     assert all((res[0]["grads"][-1] == res[r]["grads"][-1]).all() for r in range(world))
     assert tri > 0
 

@@ -88,6 +88,21 @@ def test_isa_hazard_checker_detects_planted_hazards():
     assert not probs and found == ["vmcnt(3):3"]
     probs, _ = c.check_kernel("_Zk", ["v_pk_fma_f32 v[0:1], v[2:3], v[4:5], v[6:7]", "s_endpgm"])
     assert probs
+    # a loop whose counted wait is covered in the steady state (latch path: 3 stores behind the DMA) but not on the
+    # path from the prologue (the DMA right before the loop): the SHORTEST path fails unless the kernel annotates
+    # that wait as flag-guarded (GUARDED), and the annotation then applies the steady-state count
+    loop = ["buffer_load_dwordx4 v2, s[0:3], 0 offen lds", ".Lloop:", "s_waitcnt vmcnt(3)",
+            "buffer_load_dwordx4 v2, s[0:3], 0 offen lds"] + ["global_store_dwordx2 v[0:1], v[2:3], off"] * 3 + \
+           ["s_cbranch_scc1 .Lloop", "s_endpgm"]
+    probs, found = c.check_windows(*c.parse(loop), {3: "dma"}, "_Zloopk")
+    assert probs and found == ["vmcnt(3):0"]
+    c.GUARDED["_Zloopk"] = {3: "test: the first iteration waits vmcnt(0)"}
+    try:
+        used = set()
+        probs, found = c.check_windows(*c.parse(loop), {3: "dma"}, "_Zloopk", used)
+        assert not probs and found == ["vmcnt(3):3"] and used == {("_Zloopk", 3)}
+    finally:
+        del c.GUARDED["_Zloopk"]
 
 
 def test_isa_hazards_every_kernel():
