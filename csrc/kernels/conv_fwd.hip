@@ -836,16 +836,11 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(ConvFwdArgs args) {
 
 template <int DT, int BM, int BN>
 static void launch_pp(const ConvFwdArgs& args, hipStream_t s) {
-  // PDT_PP_STAGE=0: the ping-pong kernel stores straight from the accumulators (A/B); default: LDS-staged row stores,
-  // one wave row-group at a time (conv_epilogue PERGRP)
-  // (round 5: OFF by default -- with the PERM epilogue the direct stores are 16 bytes per lane, and the same box
-  // measured PDT_PP_STAGE=1 -> 0 at 20.45/20.43 -> 20.33/20.32 ms for ResNet-18, 73.23/73.36 -> 73.09/73.19 for ResNet-50)
-  static const bool pp_stage = [] {
-    const char* e = getenv("PDT_PP_STAGE");
-    return e && e[0] == '1';
-  }();
+  // the ping-pong kernel stores straight from the accumulators: with the PERM epilogue the direct stores are 16 bytes
+  // per lane, and LDS-staged row stores (one wave row-group at a time) measured slower on the same box in round 5
+  // (ResNet-18 20.45/20.43 -> 20.33/20.32 ms, ResNet-50 73.23/73.36 -> 73.09/73.19); that knob was removed in round 6
   ConvFwdArgs a = args;
-  if (!pp_stage) a.stage_out = 0;
+  a.stage_out = 0;
   int gx = a.m_tiles * a.n_tiles;
   if (a.nphase > 0) {
     gx = 0;
@@ -888,7 +883,7 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
   } else if (epi == 1 && rs != 2) {
     if (rs) PDT_K(1, 1); else PDT_K(1, 0);
   } else if constexpr ((((BK == 64 && STAGES == 2) || (BK == 32 && STAGES == 3)) && (BN == 128 || BN == 64) &&
-                        BM * BN == 4096 * NW) ||
+                        (BM * BN == 4096 * NW || (BM == 256 && BN == 128 && NW == 4))) ||
                        (BM == 256 && BN == 256)) {
     // fused BN-backward epilogues: only on the backward-data tiles (128x128, 256x64: BK = 64 on the 2-stage ring,
     // BK = 32 on the 3-stage ring for short sub-pixel-phase reductions)
@@ -908,14 +903,10 @@ static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_
 
 template <int DT>
 static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
-  // LDS-staged output write-back, PDT_STAGE_OUT=1 (default off since round 5: the PERM epilogue's direct stores are
-  // 16 bytes per lane; with both staging knobs off the same box measured ResNet-18 20.33/20.32 -> 20.23/20.23 ms and
-  // ResNet-50 73.09/73.19 -> 73.05/73.00 ms against PP staging off alone)
-  static const bool stage_env = [] {
-    const char* e = getenv("PDT_STAGE_OUT");
-    return e && e[0] == '1';
-  }();
-  a.stage_out = stage_env && a.Kout % 8 == 0 ? 1 : 0;
+  // no LDS-staged output write-back: the PERM epilogue's direct stores are 16 bytes per lane; staging measured slower
+  // on the same box in round 5 (ResNet-18 20.33/20.32 -> 20.23/20.23 ms, ResNet-50 73.09/73.19 -> 73.05/73.00 ms
+  // with it off); the knob was removed in round 6
+  a.stage_out = 0;
   a.m_tiles = (int)((a.M + bm - 1) / bm);
   a.n_tiles = a.Kout / bn;
   {
@@ -952,20 +943,11 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
 
 template <int DT>
 static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_t s) {
-  // PDT_FWD_STAGES=2|3 forces the LDS ring depth (tuning sweeps); default: 2 for BK=64, 3 for BK=32
-  static const int force_stages = [] {
-    const char* e = getenv("PDT_FWD_STAGES");
-    return e ? atoi(e) : 0;
-  }();
-#define PDT_CFGN(BM_, BN_, BK_, WN_, ST_, NW_)                          \
-  if (bm == BM_ && bn == BN_ && bk == BK_) {                             \
-    if (ST_ == 2 && force_stages == 3)                                   \
-      launch_cfg<DT, BM_, BN_, BK_, WN_, 3, NW_>(a, s);                  \
-    else if (ST_ == 3 && force_stages == 2)                              \
-      launch_cfg<DT, BM_, BN_, BK_, WN_, 2, NW_>(a, s);                  \
-    else                                                                 \
-      launch_cfg<DT, BM_, BN_, BK_, WN_, ST_, NW_>(a, s);                \
-    return;                                                              \
+  // LDS ring depth: 2 for BK=64, 3 for BK=32 (round-3/4 sweeps)
+#define PDT_CFGN(BM_, BN_, BK_, WN_, ST_, NW_)            \
+  if (bm == BM_ && bn == BN_ && bk == BK_) {               \
+    launch_cfg<DT, BM_, BN_, BK_, WN_, ST_, NW_>(a, s);    \
+    return;                                                \
   }
 #define PDT_CFG(BM_, BN_, BK_, WN_, ST_) PDT_CFGN(BM_, BN_, BK_, WN_, ST_, 4)
   {
@@ -995,6 +977,16 @@ static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_
   PDT_CFG(256, 64, 32, 1, 3)
   PDT_CFG(128, 64, 32, 1, 3)
   PDT_CFG(64, 128, 64, 4, 2)
+  // 256 x 128: 4 waves of 128 x 64 (the ping-pong kernel's wave tile) on a 3-stage BK=32 ring (72 KB: 2 workgroups
+  // per CU, two K-steps of LDS-DMA in flight) -- for BK = 64 callers too (C % 64 == 0 implies C % 32 == 0).  Round 6,
+  // tools/conv_bench.py at B = 1200: ResNet-18 layer2 3x3 128 -> 128 forward 812 -> 872 TF/s, backward-data
+  // 910 -> 925 TF/s, 3x3/2 64 -> 128 forward 521 -> 572, against the 128 x 128 2-stage tile; the 8-wave 2-stage
+  // 256 x 128 kernel this replaces ran 750 / 441 on the same shapes.  Outputs are bit-identical to the 128 x 128
+  // tile (same K order); the BN statistics differ in the order the per-tile partial rows are summed.
+  if (bm == 256 && bn == 128 && (bk == 32 || bk == 64)) {
+    launch_cfg<DT, 256, 128, 32, 2, 3, 4>(a, s);
+    return;
+  }
   const bool sliced = (a.ldy && a.ldy != a.Kout) || a.cs != a.C;
   if (bk == 64 && bm == 256 && bn == 256 && a.C % 64 == 0 && !sliced) {
     launch_pp<DT, 256, 256>(a, s);
@@ -1004,7 +996,6 @@ static void launch_tile(const ConvFwdArgs& a, int bm, int bn, int bk, hipStream_
     launch_pp<DT, 512, 128>(a, s);
     return;
   }
-  PDT_CFGN(256, 128, 64, 2, 2, 8)  // 8 waves (4 x 2 of 64 x 64), 96 KB LDS: 25% less L2->LDS traffic per FLOP
   PDT_CFGN(256, 256, 32, 4, 4, 8)  // 8 waves (2 x 4 of 128 x 64), 4-stage BK=32 ring (128 KB), 2 steps in flight
 #undef PDT_CFG
 #undef PDT_CFGN

@@ -458,7 +458,7 @@ class ResNetExecutor:
         def launch(bm, bn):
             self.C.conv_fwd(x, wt, y, None, sp, N, H, W, cin, c.cout, R, S, P, Q, st, st,
                             -pad, -pad, 1, 1, P, Q, 1, 1, 0, 0, bm, bn, bk, 0)
-        bm, bn = self._tile(tkey, c.cout, bk, launch, kdim=cin * R * S)
+        bm, bn = self._tile(tkey, c.cout, bk, launch, kdim=cin * R * S, m=M)
         launch(bm, bn)
         if stats and fin is not None:
             self.bn_train_finalize(fin, sp, 0, M)
@@ -520,11 +520,11 @@ class ResNetExecutor:
     # the reference's cudnn.benchmark=True (`distributed.py:104`) -- the fastest candidate timed once per shape
     _CANDIDATES = ((128, 128), (256, 64), (128, 64), (64, 128), (256, 128), (256, 256), (512, 128))
 
-    def _tile(self, key, n_dim, bk, launch, fused_epilogue: bool = False, kdim: int = 0):
+    def _tile(self, key, n_dim, bk, launch, fused_epilogue: bool = False, kdim: int = 0, m: int = 0):
         hit = self._tiles.get(key)
         if hit is not None:
             return hit
-        choice = _TUNED.get(key) or _conv_tile(n_dim, kdim if bk == 64 else 0)
+        choice = _TUNED.get(key) or _conv_tile(n_dim, kdim if bk == 64 else 0, m)
         if self.autotune and bk == 64:
             cands = [(bm, bn) for bm, bn in self._CANDIDATES if n_dim % bn == 0 and
                      (not fused_epilogue or bm * bn in (16384, 32768, 65536))]
@@ -541,7 +541,7 @@ class ResNetExecutor:
                     best = (ms, (bm, bn))
             choice = best[1]
             dump = os.environ.get("PDT_AUTOTUNE_DUMP")  # tuned-table candidates: shapes where the static rule lost
-            if dump and choice != _conv_tile(n_dim, kdim if bk == 64 else 0):
+            if dump and choice != _conv_tile(n_dim, kdim if bk == 64 else 0, m):
                 with open(dump, "a") as f:
                     f.write(json.dumps([list(key), list(choice)]) + "\n")
         self._tiles[key] = choice
@@ -631,7 +631,8 @@ class ResNetExecutor:
             launch(*_conv_tile(c.cin))
         else:
             key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, dst, res is not None, bnb[0] if bnb else 0, res_phase)
-            bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S)
+            bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S,
+                                m=N * H * W)
             launch(bm, bn)
         if fin is not None and bnb is not None:  # fin = (count, bn1, bn2): the fused reduce's BN-backward finalize
             self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2])

@@ -25,17 +25,25 @@ from . import native
 _PP_MIN_K = 128
 
 
-def conv_tile(cout: int, kdim: int = 0) -> Tuple[int, int]:
-    """(BM, BN) tile of the implicit-GEMM kernel for a given GEMM-N (output channels) and GEMM-K
-    (reduction length ``Cin*R*S``; 0 = unknown).
+# a 256 x 128 tile needs this many tiles (two workgroups per CU: 512 resident) to beat the 128 x 128 one; below it
+# the larger tile leaves CUs idle (e.g. ResNet-18 layer4 at 150 images/GPU)
+_WIDE128_MIN_TILES = 1024
+
+
+def conv_tile(cout: int, kdim: int = 0, m: int = 0) -> Tuple[int, int]:
+    """(BM, BN) tile of the implicit-GEMM kernel for a given GEMM-N (output channels), GEMM-K (reduction length
+    ``Cin*R*S``; 0 = unknown) and GEMM-M (output pixels; 0 = unknown).
 
     Long reductions over >= 256 channels go to the 8-wave ping-pong kernel (256x256, one workgroup per
     CU, counted-vmcnt DMA pipeline: +10-25 % over the 2-stage 128x128 kernel on ResNet layer3/4 shapes,
     tools/conv_bench.py); short ones (1x1 convs: 1-4 K-steps) stay on the 2-stage kernel, whose
-    prologue/epilogue is cheaper."""
+    prologue/epilogue is cheaper.  128-channel GEMMs with enough pixels take the 256x128 3-stage tile (4 waves of
+    the ping-pong wave tile, 2 workgroups per CU; conv_fwd.hip launch_tile)."""
     if cout % 256 == 0 and kdim >= _PP_MIN_K and kdim % 64 == 0:
         return 256, 256
     if cout % 128 == 0:
+        if m and (m + 255) // 256 * (cout // 128) >= _WIDE128_MIN_TILES:
+            return 256, 128
         return 128, 128
     return 256, 64
 
@@ -81,7 +89,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, st
     assert C == C2
     P, Q = out_hw(H, W, R, S, stride, pad)
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
-    bm, bn = conv_tile(K, C * R * S)
+    bm, bn = conv_tile(K, C * R * S, N * P * Q)
     bk = 64 if C % 64 == 0 else 32
     if tile is not None:
         bm, bn, bk = tile
@@ -119,7 +127,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, H: int, W: int, stride: int = 
     K2, R, S, C = w.shape
     assert K == K2
     dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
-    bm, bn = conv_tile(C, K * R * S)
+    bm, bn = conv_tile(C, K * R * S, N * H * W)
     bk = 64 if K % 64 == 0 else 32
     if tile is not None:
         bm, bn, bk = tile

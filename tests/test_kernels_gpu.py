@@ -484,7 +484,7 @@ def test_wgrad_3x3c64_all_taps():
 
 
 TILES = [(128, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64), (256, 128, 64), (256, 256, 32),
-         (128, 128, 32), (256, 64, 32), (128, 64, 32), (256, 256, 64), (512, 128, 64)]
+         (128, 128, 32), (256, 64, 32), (128, 64, 32), (256, 256, 64), (512, 128, 64), (256, 128, 32)]
 PP_TILES = [(256, 256, 64), (512, 128, 64)]  # 8-wave ping-pong kernel (conv_pp_kernel)
 
 
@@ -581,11 +581,12 @@ def test_bn_apply_relu_bitmask_and_masked_backward(resmode):
     assert _rel(dy1, ref1) < 1e-2
 
 
-@pytest.mark.parametrize("tile", PP_TILES)
+@pytest.mark.parametrize("tile", PP_TILES + [(256, 128, 32)])
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_conv_pp_long_k_and_fused_bn_backward(tile, mode):
-    """Ping-pong kernel over many K-steps and several (partial) M tiles: forward with stats, and
-    backward-data with every fused BN-backward epilogue (mode 0 = plain dgrad with residual)."""
+    """Ping-pong kernel (and the 4-wave 256x128 3-stage tile, same wave tile) over many K-steps and several
+    (partial) M tiles: forward with stats, and backward-data with every fused BN-backward epilogue (mode 0 = plain
+    dgrad with residual)."""
     from pytorch_distributed_template_amd.ops import conv, native
     N, H, W, C, K = 5, 14, 14, 256, 256
     torch.manual_seed(21 + mode)

@@ -24,8 +24,8 @@ SHAPES_R50 = [  # ResNet-50 bottleneck 1x1 convs: H, Cin, Cout, k, stride
     (56, 64, 256, 1, 1), (56, 256, 64, 1, 1), (28, 512, 128, 1, 1), (28, 128, 512, 1, 1), (14, 1024, 256, 1, 1),
     (14, 256, 1024, 1, 1), (7, 2048, 512, 1, 1), (7, 512, 2048, 1, 1),
 ]
-FWD_TILES = [(256, 256, 64), (512, 128, 64), (128, 128, 64), (256, 256, 32), (256, 128, 64), (256, 64, 64), (128, 64, 64), (64, 128, 64),
-             (256, 64, 32), (128, 128, 32)]
+FWD_TILES = [(256, 256, 64), (512, 128, 64), (128, 128, 64), (256, 256, 32), (256, 128, 64), (256, 128, 32), (256, 64, 64),
+             (128, 64, 64), (64, 128, 64), (256, 64, 32), (128, 128, 32)]
 
 
 def timeit(fn, reps):
@@ -135,10 +135,11 @@ def main():
             phases.append([ph, pw, len(rs), len(ss), ih, iw, off])
             off += idx.numel()
         wt = torch.cat(pieces).contiguous()
-        dts = [conv.conv_tile(ci)] + [t for t in ((256, 256), (512, 128), (128, 128)) if ci % t[1] == 0]
-        for bm, bn in dict.fromkeys(dts):
-            row[f"dgrad_{bm}x{bn}"] = round(flops / timeit(lambda: C.conv_dgrad(dy, wt, dx, None, N, P, P, co, ci, H, H,
-                                                                           st, phases, bm, bn, 64), a.reps) / 1e9, 1)
+        dts = [conv.conv_tile(ci) + (64,)] + [t for t in ((256, 256, 64), (512, 128, 64), (128, 128, 64),
+                                                           (256, 128, 32)) if ci % t[1] == 0]
+        for bm, bn, bk in dict.fromkeys(dts):
+            row[f"dgrad_{bm}x{bn}x{bk}"] = round(flops / timeit(lambda: C.conv_dgrad(
+                dy, wt, dx, None, N, P, P, co, ci, H, H, st, phases, bm, bn, bk), a.reps) / 1e9, 1)
         if C.wgrad_3x3c64_supported(ci, co, k, k, H, st, pad):
             blocks = C.wgrad_blocks_3x3c64()
             ws = torch.empty(blocks * 64 * 576, device=dev)
