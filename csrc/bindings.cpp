@@ -30,6 +30,7 @@
 #include "kernels/optim.h"
 #include "kernels/pool.h"
 #include "kernels/stem.h"
+#include "kernels/vgg.h"
 
 namespace pdt_comm {
 void register_comm(pybind11::module& m);  // csrc/comm.cpp
@@ -838,6 +839,82 @@ void stem_pool_bwd_reduce_out(const Tensor& dp, const Tensor& out, const Tensor&
   launched("stem_pool_bwd_reduce_out_launch");
 }
 
+// ---------------------------------------------------------------------------- VGG family (vgg.hip)
+// out = MaxPool(2, 2)(relu(y * coef[0:C] + coef[C:2C])), idx = window argmax (0..3) per pooled element (training)
+void bn_relu_maxpool2(const Tensor& y, const Tensor& coef, Tensor& out, const OptT& idx, int64_t N, int64_t H,
+                      int64_t W, int64_t C) {
+  const int dt = dt16(y, "y");
+  TORCH_CHECK(dt16(out, "out") == dt && H % 2 == 0 && W % 2 == 0 && C % 8 == 0 && coef.numel() >= 2 * C &&
+                  y.numel() == N * H * W * C && out.numel() == N * (H / 2) * (W / 2) * C,
+              "bn_relu_maxpool2: bad sizes (even H, W; C % 8 == 0)");
+  TORCH_CHECK(!idx.has_value() || (idx->scalar_type() == at::kByte && idx->numel() == out.numel()),
+              "bn_relu_maxpool2: idx must be uint8 like out");
+  pdt::bn_relu_maxpool2_launch(dt, p16(y, "y"), pf(coef, "coef"), p16(out, "out"),
+                               idx.has_value() ? idx->data_ptr<uint8_t>() : nullptr, N, (int)H, (int)W, (int)C,
+                               cur_stream());
+  launched("bn_relu_maxpool2_launch");
+}
+
+// dy (conv output gradient) of a BN / bias + ReLU + MaxPool(2, 2): bcoef given -> dy = A*dz + B*y + C, else dz
+void maxpool2_bwd(const Tensor& dp, const Tensor& idx, const Tensor& out, const OptT& y, const OptT& bcoef,
+                  Tensor& dy, int64_t N, int64_t H, int64_t W, int64_t C) {
+  const int dt = dt16(dp, "dp");
+  TORCH_CHECK(dt16(out, "out") == dt && dt16(dy, "dy") == dt && H % 2 == 0 && W % 2 == 0 && C % 8 == 0 &&
+                  dp.numel() == N * (H / 2) * (W / 2) * C && out.numel() == dp.numel() && idx.numel() == dp.numel() &&
+                  idx.scalar_type() == at::kByte && dy.numel() == N * H * W * C,
+              "maxpool2_bwd: bad sizes");
+  TORCH_CHECK(bcoef.has_value() == y.has_value() && (!y.has_value() || (dt16(*y, "y") == dt && y->numel() == dy.numel())) &&
+                  (!bcoef.has_value() || bcoef->numel() >= 3 * C),
+              "maxpool2_bwd: a BatchNorm needs both y and bcoef");
+  pdt::maxpool2_bwd_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(out, "out"), p16o(y, "y"), pfo(bcoef, "bcoef"),
+                           p16(dy, "dy"), N, (int)H, (int)W, (int)C, cur_stream());
+  launched("maxpool2_bwd_launch");
+}
+
+// BN-backward sums (sum dz, sum dz * xhat) of any max-pool over relu(BN(y)) from the pooled tensors alone
+void pooled_bwd_reduce(const Tensor& dp, const Tensor& out, const Tensor& coef, Tensor& slots, int64_t rows, int64_t C) {
+  const int dt = dt16(dp, "dp");
+  TORCH_CHECK(dt16(out, "out") == dt && dp.numel() == rows * C && out.numel() == dp.numel() && C % 8 == 0 &&
+                  C <= 2048 && coef.numel() >= 4 * C && slots.numel() >= pdt::kStatSlots * C * 2,
+              "pooled_bwd_reduce: bad sizes");
+  pdt::pooled_bwd_reduce_launch(dt, p16(dp, "dp"), p16(out, "out"), pf(coef, "coef"), pd(slots, "slots"), rows, (int)C,
+                                cur_stream());
+  launched("pooled_bwd_reduce_launch");
+}
+
+// classifier: out = dropout_p(relu(z + bias)) (seed: a fresh value per step); p = 0: bias + ReLU only
+void fc_act_fwd(const Tensor& z, const Tensor& bias, Tensor& out, int64_t rows, int64_t F, double p, int64_t seed) {
+  const int dt = dt16(z, "z");
+  TORCH_CHECK(dt16(out, "out") == dt && F % 8 == 0 && z.numel() == rows * F && out.numel() == z.numel() &&
+                  bias.numel() >= F && p >= 0.0 && p < 1.0,
+              "fc_act_fwd: bad sizes");
+  pdt::fc_act_fwd_launch(dt, p16(z, "z"), pf(bias, "bias"), p16(out, "out"), rows, (int)F, p, (uint64_t)seed,
+                         cur_stream());
+  launched("fc_act_fwd_launch");
+}
+
+void fc_act_bwd(const Tensor& dh, const Tensor& out, Tensor& dz, double p) {
+  const int dt = dt16(dh, "dh");
+  TORCH_CHECK(dt16(out, "out") == dt && dt16(dz, "dz") == dt && dh.numel() == out.numel() && dz.numel() == dh.numel() &&
+                  dh.numel() % 8 == 0 && p >= 0.0 && p < 1.0,
+              "fc_act_bwd: bad sizes");
+  pdt::fc_act_bwd_launch(dt, p16(dh, "dh"), p16(out, "out"), p16(dz, "dz"), dh.numel(), p, cur_stream());
+  launched("fc_act_bwd_launch");
+}
+
+void nhwc_nchw16(const Tensor& src, Tensor& dst, int64_t N, int64_t HW, int64_t C, bool to_nchw) {
+  const int dt = dt16(src, "src");
+  TORCH_CHECK(dt16(dst, "dst") == dt && src.numel() == N * HW * C && dst.numel() == src.numel(), "nhwc_nchw16: bad sizes");
+  pdt::nhwc_nchw16_launch(p16(src, "src"), p16(dst, "dst"), N, (int)HW, (int)C, to_nchw, cur_stream());
+  launched("nhwc_nchw16_launch");
+}
+
+void bias_coef(const Tensor& bias, Tensor& coef, int64_t C) {
+  TORCH_CHECK(bias.numel() >= C && coef.numel() >= 4 * C, "bias_coef: bad sizes");
+  pdt::bias_coef_launch(pf(bias, "bias"), pf(coef, "coef"), (int)C, cur_stream());
+  launched("bias_coef_launch");
+}
+
 // ... and apply pass writing dy = A*dz + B*y + C (bcoef from bn_bwd_finalize)
 void stem_pool_bwd_apply(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef,
                          const Tensor& bcoef, Tensor& dy, int64_t N, int64_t H, int64_t W, int64_t C) {
@@ -1391,6 +1468,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_pool_bwd_reduce", &stem_pool_bwd_reduce);
   m.def("stem_pool_bwd_reduce_out", &stem_pool_bwd_reduce_out);
   m.def("stem_pool_bwd_apply", &stem_pool_bwd_apply);
+  m.def("bn_relu_maxpool2", &bn_relu_maxpool2, py::arg("y"), py::arg("coef"), py::arg("out"), py::arg("idx"), py::arg("N"),
+        py::arg("H"), py::arg("W"), py::arg("C"));
+  m.def("maxpool2_bwd", &maxpool2_bwd);
+  m.def("pooled_bwd_reduce", &pooled_bwd_reduce);
+  m.def("fc_act_fwd", &fc_act_fwd);
+  m.def("fc_act_bwd", &fc_act_bwd);
+  m.def("nhwc_nchw16", &nhwc_nchw16);
+  m.def("bias_coef", &bias_coef);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("xent", &xent);

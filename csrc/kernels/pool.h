@@ -10,6 +10,8 @@ void stem_pool_bwd_reduce_launch(int dtype, const uint16_t* dp, const uint8_t* i
                                  const float* coef, double* slots, int N, int H, int W, int C, hipStream_t s);
 void stem_pool_bwd_reduce_out_launch(int dtype, const uint16_t* dp, const uint16_t* out, const float* coef,
                                      double* slots, int N, int H, int W, int C, hipStream_t s);
+void pooled_bwd_reduce_launch(int dtype, const uint16_t* dp, const uint16_t* out, const float* coef, double* slots,
+                              int64_t rows, int C, hipStream_t s);
 void stem_pool_bwd_apply_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y,
                                 const float* coef, const float* bcoef, uint16_t* dy, int N, int H, int W, int C,
                                 hipStream_t s);

@@ -311,8 +311,14 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_out_kernel(const uin
 void stem_pool_bwd_reduce_out_launch(int dtype, const uint16_t* dp, const uint16_t* out, const float* coef,
                                      double* slots, int N, int H, int W, int C, hipStream_t s) {
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  pooled_bwd_reduce_launch(dtype, dp, out, coef, slots, (int64_t)N * OH * OW, C, s);
+}
+
+// the same sums for any max-pool whose output is relu(BN(y)) at the argmax (the VGG 2x2 pools too): only the pooled
+// gradient and the pooled output are read, ``rows`` pooled pixels
+void pooled_bwd_reduce_launch(int dtype, const uint16_t* dp, const uint16_t* out, const float* coef, double* slots,
+                              int64_t rows, int C, hipStream_t s) {
   const int rpi = 256 / (C / 8);
-  const int64_t rows = (int64_t)N * OH * OW;
   int64_t blocks = (rows + rpi * 8 - 1) / (rpi * 8);
   if (blocks > 2048) blocks = 2048;
   const size_t smem = (size_t)rpi * C * 2 * sizeof(float);

@@ -19,7 +19,7 @@ import torch
 import torch.distributed as dist
 
 from ..amp.scaler import DeviceGradScaler
-from ..models.executor import ResNetExecutor
+from ..models.executor_vgg import make_executor
 from ..optim.flat import FlatBuffers, FlatParams
 from ..optim.sgd import FusedSGD
 from ..parallel.ddp import GradBucketer, broadcast_parameters, sync_buffers
@@ -73,8 +73,8 @@ class NativeTrainer:
             self.executor = ResNetExecutor32(model, self.flat, self.device, grad_ready=self.bucketer.grad_ready,
                                              **sync_kw)
         else:
-            self.executor = ResNetExecutor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
-                                           autotune=autotune, **sync_kw)
+            self.executor = make_executor(model, self.flat, self.device, dtype, grad_ready=self.bucketer.grad_ready,
+                                          autotune=autotune, **sync_kw)
         # --eval-precision fp32: validation on the fp32 executor over the fp32 master weights (the reference
         # validates without autocast, `distributed_syncBN_amp.py:311-317`), whatever the training dtype
         self._eval32 = None

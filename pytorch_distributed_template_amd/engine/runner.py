@@ -37,10 +37,12 @@ from ..utils.meters import AverageMeter, get_learning_rate
 from ..utils.profiling import roctx_range
 from ..utils.tensorboard import SummaryWriter
 
+_VGG_ARCHS = ("vgg11", "vgg11_bn", "vgg13", "vgg13_bn", "vgg16", "vgg16_bn", "vgg19", "vgg19_bn")
 NATIVE_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2",
-                "resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d")
-# grouped-conv archs: 16-bit executor only (models/executor.py channel slices); fp32 runs them on the torch engine
-NATIVE_ARCHS_16BIT_ONLY = ("resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d")
+                "resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d") + _VGG_ARCHS
+# 16-bit executors only (grouped convs: models/executor.py channel slices; VGG: models/executor_vgg.py); fp32 runs them
+# on the torch engine
+NATIVE_ARCHS_16BIT_ONLY = ("resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d") + _VGG_ARCHS
 
 
 def seed_everything(seed: int) -> None:

@@ -46,7 +46,7 @@ import torch
 
 from ..amp.scaler import DeviceGradScaler
 from ..data.loader import ShardedBatch
-from ..models.executor import ResNetExecutor
+from ..models.executor_vgg import make_executor
 from ..optim.flat import FlatBuffers, FlatParams
 from ..optim.sgd import FusedSGD
 
@@ -100,7 +100,7 @@ class NativeDataParallelTrainer:
                     from ..models.executor32 import ResNetExecutor32
                     self.executors.append(ResNetExecutor32(m, f, d))
                 else:
-                    self.executors.append(ResNetExecutor(m, f, d, dtype))
+                    self.executors.append(make_executor(m, f, d, dtype))
         self.model = model
         self.flat = self.flats[0]
         # eval_fp32: validation of the fp32 model like the reference's DataParallel (`dataparallel.py:243-262`, no
