@@ -6,7 +6,7 @@ import argparse, time, json, sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import torch.nn as nn
-from pytorch_distributed_template_amd.models import resnet
+from pytorch_distributed_template_amd.models import registry
 
 p = argparse.ArgumentParser()
 p.add_argument("--arch", default="resnet18")
@@ -28,7 +28,7 @@ def _heartbeat():  # MIOpen's search can stay silent for minutes: keep the run v
 
 threading.Thread(target=_heartbeat, daemon=True).start()
 dev = torch.device("cuda:0")
-m = getattr(resnet, a.arch)().to(dev)
+m = registry.create(a.arch).to(dev)
 if a.cl:
     m = m.to(memory_format=torch.channels_last)
 opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
