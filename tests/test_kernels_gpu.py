@@ -1153,3 +1153,27 @@ def test_grouped_conv_slices_match_torch(width, groups, stride, H):
     dwd = dwd.view(nsl, S, R, R, S)
     got = torch.stack([dwd[j, k, :, :, (k // cg) * cg:(k // cg) * cg + cg] for j in range(nsl) for k in range(S)])
     assert _rel(got, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [(256, 64, 64), (128, 128, 64), (256, 128, 64), (256, 256, 64)])
+def test_phased_dgrad_one_launch_equals_per_phase_launches(tile):
+    """Strided backward-data runs all its sub-pixel phases in ONE launch (grid.y = phase, the grid sized for the largest
+    phase, surplus blocks only zeroing their statistics rows).  dX must be bit-identical to launching every phase on its
+    own, for every tile family, including partial M tiles."""
+    from pytorch_distributed_template_amd.ops import conv, native
+    bm, bn, bk = tile
+    N, H, W, K = 3, 19, 17, 128
+    C = bn if bn >= 128 else 64
+    torch.manual_seed(31)
+    w = _rand16(K, 3, 3, C, scale=(1.0 / (C * 9)) ** 0.5)
+    P, Q = conv.out_hw(H, W, 3, 3, 2, 1)
+    dy = _rand16(N, P, Q, K)
+    dx = conv.conv_dgrad(dy, w, H, W, 2, 1, tile=tile)
+    wflat = w.reshape(-1)
+    ref = torch.full_like(dx, float("nan"))
+    for ph, pw, rs, ss, ioff_h, ioff_w in conv.dgrad_phases(3, 3, 2, 1):
+        idx = conv.dgrad_weight_index(K, C, 3, 3, rs, ss).to(w.device)
+        wt = wflat[idx].contiguous()
+        native.C.conv_dgrad(dy, wt, ref, None, N, P, Q, K, C, H, W, 2, [[ph, pw, len(rs), len(ss), ioff_h, ioff_w, 0]],
+                            bm, bn, bk)
+    assert torch.equal(dx, ref)
