@@ -499,18 +499,25 @@ void gconv_fwd(const Tensor& x, const Tensor& wslice, Tensor& y, const OptT& sta
   const int dt = dt16(x, "x");
   const int64_t S = kGSlice;
   TORCH_CHECK(dt16(wslice, "w") == dt && dt16(y, "y") == dt, "gconv_fwd: mixed dtypes");
-  TORCH_CHECK(width % S == 0 && j >= 0 && j < width / S, "gconv_fwd: bad slice");
-  TORCH_CHECK(x.numel() == N * H * W * width && y.numel() == N * P * Q * width && wslice.numel() == S * R * R * S,
+  // j == -1: every slice in ONE launch (ConvFwdArgs::nslice; wslice = the slices' layouts back to back)
+  TORCH_CHECK(width % S == 0 && j >= -1 && j < width / S, "gconv_fwd: bad slice");
+  const int64_t nsl = j < 0 ? width / S : 1;
+  TORCH_CHECK(x.numel() == N * H * W * width && y.numel() == N * P * Q * width && wslice.numel() == nsl * S * R * R * S,
               "gconv_fwd: size mismatch");
   TORCH_CHECK(x.numel() < (int64_t(1) << 30) && y.numel() < (int64_t(1) << 30), "gconv_fwd: operands exceed 2 GiB");
   TORCH_CHECK(S % bn == 0 && N * P * Q < (int64_t(1) << 31), "gconv_fwd: tile / size");
   pdt::ConvFwdArgs a{};
-  a.x = p16(x, "x") + j * S;
+  const int64_t j0 = j < 0 ? 0 : j;
+  a.x = p16(x, "x") + j0 * S;
   a.w = p16(wslice, "w");
-  a.y = p16(y, "y") + j * S;
+  a.y = p16(y, "y") + j0 * S;
+  if (j < 0) {
+    a.nslice = (int)nsl;
+    a.slice_wstride = S * R * R * S;
+  }
   if (stats.has_value()) {
     TORCH_CHECK(stats->numel() >= pdt::kStatSlots * width * 2, "gconv_fwd: stats buffer too small");
-    a.stats = pd(*stats, "stats") + j * S * 2;
+    a.stats = pd(*stats, "stats") + j0 * S * 2;
     a.stats_ld = (int)(width * 2);
   }
   a.N = N; a.H = H; a.W = W; a.C = S; a.Kout = S; a.T = R; a.U = R; a.Pm = P; a.Qm = Q; a.cs = width;
@@ -531,14 +538,22 @@ void gconv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, int64_t N, int6
   const int dt = dt16(dy, "dy");
   const int64_t S = kGSlice;
   TORCH_CHECK(dt16(wt, "wt") == dt && dt16(dx, "dx") == dt, "gconv_dgrad: mixed dtypes");
-  TORCH_CHECK(width % S == 0 && j >= 0 && j < width / S, "gconv_dgrad: bad slice");
+  TORCH_CHECK(width % S == 0 && j >= -1 && j < width / S, "gconv_dgrad: bad slice");  // -1: every slice, one launch
+  const int64_t j0 = j < 0 ? 0 : j, nsl = j < 0 ? width / S : 1;
+  int64_t taps = 0;  // every phase's taps together: one slice's R x R
+  for (const auto& f : phases) taps += f.size() == 7 ? f[2] * f[3] : 0;
+  const int64_t wstride = S * S * taps;  // elements of one slice's derived phase weights
   TORCH_CHECK(dy.numel() == N * P * Q * width && dx.numel() == N * H * W * width, "gconv_dgrad: size mismatch");
   TORCH_CHECK(dy.numel() < (int64_t(1) << 30) && dx.numel() < (int64_t(1) << 30), "gconv_dgrad: operands exceed 2 GiB");
   TORCH_CHECK(!phases.empty() && phases.size() <= 4 && S % bn == 0, "gconv_dgrad: 1..4 phases / tile");
   pdt::ConvFwdArgs a{};
-  a.x = p16(dy, "dy") + j * S;
+  a.x = p16(dy, "dy") + j0 * S;
   a.w = p16(wt, "wt");
-  a.y = p16(dx, "dx") + j * S;
+  a.y = p16(dx, "dx") + j0 * S;
+  if (j < 0) {
+    a.nslice = (int)nsl;
+    a.slice_wstride = wstride;
+  }
   a.N = N; a.H = P; a.W = Q; a.C = S; a.cs = width; a.Kout = S; a.ldy = (int)width;
   a.ist_h = 1; a.ist_w = 1; a.tstep_h = -1; a.tstep_w = -1;
   a.OH = H; a.OW = W; a.ost_h = stride; a.ost_w = stride;
@@ -550,7 +565,8 @@ void gconv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, int64_t N, int6
     TORCH_CHECK(f.size() == 7, "gconv_dgrad: phase = (ph, pw, T, U, ioff_h, ioff_w, woff)");
     const int64_t ph = f[0], pw = f[1];
     const int64_t Pm = (H - ph + stride - 1) / stride, Qm = (W - pw + stride - 1) / stride;
-    TORCH_CHECK(Pm > 0 && Qm > 0 && f[6] + S * f[2] * f[3] * S <= wt.numel(), "gconv_dgrad: bad phase");
+    TORCH_CHECK(Pm > 0 && Qm > 0 && f[6] + S * f[2] * f[3] * S + (nsl - 1) * wstride <= wt.numel(),
+                "gconv_dgrad: bad phase");
     a.pooff_h[i] = (int)ph; a.pooff_w[i] = (int)pw; a.pT[i] = (int)f[2]; a.pU[i] = (int)f[3];
     a.pioff_h[i] = (int)f[4]; a.pioff_w[i] = (int)f[5]; a.pwoff[i] = f[6];
     a.pPm[i] = (int)Pm; a.pQm[i] = (int)Qm;
@@ -564,10 +580,10 @@ void gconv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, int64_t N, int6
                     bn_slots->numel() >= pdt::kStatSlots * width * 2,
                 "gconv_dgrad: bnb needs y1 / coef1 (4 x width) / slots of the full width");
     a.bnb = 1;
-    a.bn_y1 = p16(*bn_y1, "bn_y1") + j * S;
-    a.bn_coef1 = pf(*bn_coef1, "bn_coef1") + j * S;
+    a.bn_y1 = p16(*bn_y1, "bn_y1") + j0 * S;
+    a.bn_coef1 = pf(*bn_coef1, "bn_coef1") + j0 * S;
     a.coef_ld = (int)width;
-    a.stats = pd(*bn_slots, "bn_slots") + j * S * 2;
+    a.stats = pd(*bn_slots, "bn_slots") + j0 * S * 2;
     a.stats_ld = (int)(width * 2);
   }
   pdt::conv_fwd_launch(a, dt, (int)bm, (int)bn, 64, cur_stream());
@@ -582,13 +598,15 @@ void gconv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64
   const int dt = dt16(x, "x");
   const int64_t S = kGSlice;
   TORCH_CHECK(dt16(dy, "dy") == dt, "gconv_wgrad: mixed dtypes");
-  TORCH_CHECK(width % S == 0 && j >= 0 && j < width / S, "gconv_wgrad: bad slice");
+  TORCH_CHECK(width % S == 0 && j >= -1 && j < width / S, "gconv_wgrad: bad slice");  // -1: every slice, one launch
+  const int64_t j0 = j < 0 ? 0 : j, nsl = j < 0 ? width / S : 1;
   TORCH_CHECK(x.numel() == N * H * W * width && dy.numel() == N * P * Q * width, "gconv_wgrad: size mismatch");
   TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30), "gconv_wgrad: operands exceed 2 GiB");
-  TORCH_CHECK(ldw >= R * R * S && ws.numel() >= splits * S * ldw, "gconv_wgrad: workspace too small");
+  TORCH_CHECK(ldw >= R * R * S && ws.numel() >= splits * nsl * S * ldw, "gconv_wgrad: workspace too small");
   pdt::ConvWgradArgs a{};
-  a.x = p16(x, "x") + j * S;
-  a.dy = p16(dy, "dy") + j * S;
+  a.x = p16(x, "x") + j0 * S;
+  a.dy = p16(dy, "dy") + j0 * S;
+  if (j < 0) a.nslice = (int)nsl;
   a.ws = pf(ws, "ws");
   a.N = N; a.H = H; a.W = W; a.C = S; a.Kout = S; a.T = R; a.U = R; a.Pm = P; a.Qm = Q;
   a.stride_h = stride; a.stride_w = stride; a.pad_h = pad; a.pad_w = pad; a.dil_h = 1; a.dil_w = 1;

@@ -61,6 +61,12 @@ struct ConvFwdArgs {
   // slots ([kStatSlots][stats_ld]); 0 = Kout / Kout / Kout * quantities (dense tensors).  The input's pixel stride
   // is ``cs``.
   int ldy = 0, coef_ld = 0, stats_ld = 0;
+  // nslice > 1: ONE launch over all channel slices of a grouped conv (blockIdx.z = slice s): x, y, bn_y1 and bn_coef1
+  // advance by s * Kout elements, w by s * slice_wstride, and the statistics partial rows are [rows][nslice * Kout]
+  // (every slice's columns of one row reduced together); 0 / 1: a single slice at the caller's pointers.
+  int nslice = 0;
+  int64_t slice_wstride = 0;
+  int srows_coff = 0;  // kernel-local: this block's column offset (channels) in the statistics partial rows
   int pT[4], pU[4], pioff_h[4], pioff_w[4], pPm[4], pQm[4], pooff_h[4], pooff_w[4], pmt[4];
   int64_t pwoff[4];
   uint32_t ppq_mul[4], ppq_shift[4], pq1_mul[4], pq1_shift[4];

@@ -359,7 +359,8 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
 #pragma unroll
         for (int k = 0; k < KS; ++k) t[k] += red[(w * BN + tid) * KS + k];
       const int64_t row = (a.nphase > 0 ? (int64_t)blockIdx.y * a.srows_pp : 0) + tile_m;
-      float* dst = a.srows + (row * a.Kout + n0 + tid) * KO;
+      const int64_t sld = a.nslice > 1 ? (int64_t)a.nslice * a.Kout : a.Kout;
+      float* dst = a.srows + (row * sld + a.srows_coff + n0 + tid) * KO;
       if constexpr (EPI == 4)
         *(float4*)dst = make_float4(t[0], t[1], t[0], t[2]);
       else
@@ -376,7 +377,8 @@ PDT_DEVICE void zero_stat_row(const ConvFwdArgs& a, int nthreads) {
   if constexpr (EPI != 0) {
     constexpr int KO = EPI == 4 ? 4 : 2;
     const int tm = (int)blockIdx.x / a.n_tiles, tn = (int)blockIdx.x - tm * a.n_tiles;
-    float* dst = a.srows + ((int64_t)blockIdx.y * a.srows_pp + tm) * a.Kout * KO + (int64_t)tn * BN_ * KO;
+    const int64_t sld = a.nslice > 1 ? (int64_t)a.nslice * a.Kout : a.Kout;
+    float* dst = a.srows + (((int64_t)blockIdx.y * a.srows_pp + tm) * sld + a.srows_coff) * KO + (int64_t)tn * BN_ * KO;
     for (int i = threadIdx.x; i < BN_ * KO; i += nthreads) dst[i] = 0.f;
   }
 }
@@ -387,6 +389,19 @@ template <int DT, int BM, int BN, int BK, int WAVES_N, int EPI, int RES, int STA
 __global__ __launch_bounds__(NW * 64, (STAGES * (BN + BM) * BK * 2 <= 81920 || NW == 8) ? 2 : 1)
 void conv_fwd_kernel(ConvFwdArgs args) {
   ConvFwdArgs a = args;
+  // (the kernel-argument struct itself is never written: a write makes the compiler copy it, with its dynamically
+  // indexed phase arrays, to scratch -- 528 bytes per lane of spills, measured 65 % slower)
+  const uint16_t* wbase = args.w;
+  if (args.nslice > 1) {  // one launch over every channel slice of a grouped conv: this block's slice
+    const int sl = blockIdx.z;
+    a.x += (int64_t)sl * a.Kout;
+    a.y += (int64_t)sl * a.Kout;
+    wbase += (int64_t)sl * args.slice_wstride;
+    a.w = wbase;
+    if (a.bn_y1 != nullptr) a.bn_y1 += (int64_t)sl * a.Kout;
+    if (a.bn_coef1 != nullptr) a.bn_coef1 += sl * a.Kout;
+    a.srows_coff = sl * a.Kout;
+  }
   if (args.nphase > 0) {  // multi-phase launch: this block's phase geometry (wave-uniform)
     const int ph = blockIdx.y;
     a.T = args.pT[ph]; a.U = args.pU[ph];
@@ -395,7 +410,7 @@ void conv_fwd_kernel(ConvFwdArgs args) {
     a.ooff_h = args.pooff_h[ph]; a.ooff_w = args.pooff_w[ph];
     a.m_tiles = args.pmt[ph];
     a.M = (int64_t)a.N * a.Pm * a.Qm;
-    a.w = args.w + args.pwoff[ph];
+    a.w = wbase + args.pwoff[ph];
     a.pq_mul = args.ppq_mul[ph]; a.pq_shift = args.ppq_shift[ph];
     a.q_mul = args.pq1_mul[ph]; a.q_shift = args.pq1_shift[ph];
     if ((int)blockIdx.x >= a.m_tiles * a.n_tiles) {
@@ -841,6 +856,9 @@ static void launch_pp(const ConvFwdArgs& args, hipStream_t s) {
   // (ResNet-18 20.45/20.43 -> 20.33/20.32 ms, ResNet-50 73.23/73.36 -> 73.09/73.19); that knob was removed in round 6
   ConvFwdArgs a = args;
   a.stage_out = 0;
+  if (a.nslice > 1)
+    pdt_hip_fail("conv_pp: slice-batched (grouped) launches run on the generic kernel", hipErrorInvalidValue, __FILE__,
+                 __LINE__);
   int gx = a.m_tiles * a.n_tiles;
   if (a.nphase > 0) {
     gx = 0;
@@ -874,7 +892,7 @@ static void launch_cfg(const ConvFwdArgs& a, hipStream_t s) {
     gx = 0;
     for (int p = 0; p < a.nphase; ++p) gx = gx > a.pmt[p] * a.n_tiles ? gx : a.pmt[p] * a.n_tiles;
   }
-  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1), block(NW * 64);
+  dim3 grid(gx, a.nphase > 0 ? a.nphase : 1, a.nslice > 1 ? a.nslice : 1), block(NW * 64);
   const int rs = a.res == nullptr ? 0 : (a.res_phase >= 0 && a.nphase > 0 ? 2 : 1);
   const int epi = a.bnb ? a.bnb + 1 : (a.stats != nullptr ? 1 : 0);
 #define PDT_K(E_, R_) hipLaunchKernelGGL((conv_fwd_kernel<DT, BM, BN, BK, WAVES_N, E_, R_, STAGES, NW>), grid, block, 0, s, a)
@@ -935,10 +953,11 @@ static void launch_dt(ConvFwdArgs a, int bm, int bn, int bk, hipStream_t s) {
     srows = a.m_tiles;
   }
   const int KO = a.bnb == 3 ? 4 : 2;
-  Scratch part(a.stats ? (size_t)srows * a.Kout * KO * sizeof(float) : 0, s);
+  const int nsl = a.nslice > 1 ? a.nslice : 1;  // slice-batched grouped conv: rows span every slice's channels
+  Scratch part(a.stats ? (size_t)srows * a.Kout * nsl * KO * sizeof(float) : 0, s);
   a.srows = part.as<float>();
   launch_tile<DT>(a, bm, bn, bk, s);
-  if (a.stats) stat_rows_reduce_launch(a.srows, srows, a.Kout * KO, a.stats, s, a.stats_ld);
+  if (a.stats) stat_rows_reduce_launch(a.srows, srows, a.Kout * nsl * KO, a.stats, s, a.stats_ld);
 }
 
 template <int DT>

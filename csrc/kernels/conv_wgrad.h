@@ -16,6 +16,10 @@ struct ConvWgradArgs {
   int cs;              // elements per pixel of x (== C except in window mode)
   int win;             // stem window mode (see conv_wgrad.hip)
   int ldy = 0;         // dY pixel stride (0 = Kout): a channel slice of a wider gradient (grouped conv; 64x64 tile only)
+  // nslice > 1: ONE launch over every channel slice of a grouped conv (blockIdx.z = slice s; 64x64 tile only): x and dy
+  // advance by s * C / s * Kout elements and the partials are [splits][nslice][Kout][ldw] (one wgrad_reduce over
+  // nslice * Kout rows sums every slice)
+  int nslice = 0;
   int splits, pix_per_split;  // filled by conv_wgrad_plan
   int tile;                   // 64, 128, 256 or kWgradWide (filled by conv_wgrad_plan)
   uint32_t div_pq_mul, div_pq_shift, div_q_mul, div_q_shift;  // FastDiv of Pm*Qm and Qm (launcher)

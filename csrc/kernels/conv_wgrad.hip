@@ -55,6 +55,12 @@ PDT_DEVICE void wgrad_rows(const ConvWgradArgs& a, int p, int th, int tw, int xc
 // (h + (ch >> 2)) at element offset (ch & 3) * 8 -- im2col is never materialised.
 template <int DT, bool WIN>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
+  int sl = 0;
+  if (a.nslice > 1) {  // slice-batched grouped conv: this block's channel slice
+    sl = blockIdx.z;
+    a.x += (int64_t)sl * a.C;
+    a.dy += (int64_t)sl * a.Kout;
+  }
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   constexpr int BKP = 128;       // pixels per K-step
@@ -175,7 +181,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvWgradArgs a) {
       *(f32x4_t*)(red + (wave * 64 + k) * 64 + c) = acc[i][j];
     }
   __syncthreads();
-  float* dst = a.ws + ((int64_t)split * a.Kout + k0) * a.ldw + tap * a.C + c0;
+  const int nsl = a.nslice > 1 ? a.nslice : 1;
+  float* dst = a.ws + (((int64_t)split * nsl + sl) * a.Kout + k0) * a.ldw + tap * a.C + c0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int idx = (e * 256 + tid) * 4;  // 0..4095
@@ -1644,6 +1651,9 @@ void conv_wgrad_plan(ConvWgradArgs& a, int target_blocks) {
 
 void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   ConvWgradArgs a = args;
+  if (a.nslice > 1 && (a.tile != 64 || a.win))
+    pdt_hip_fail("conv_wgrad: slice-batched (grouped) launches run on the 64x64 tile only", hipErrorInvalidValue,
+                 __FILE__, __LINE__);
   if (a.ldy && a.ldy != a.Kout && (a.tile != 64 || a.win))
     pdt_hip_fail("conv_wgrad: a strided dY (channel slice) runs on the 64x64 tile only", hipErrorInvalidValue,
                  __FILE__, __LINE__);
@@ -1721,10 +1731,11 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((conv_wgrad_kernel<kF16, true>), dim3(nwg), dim3(256), 0, s, a);
   } else {
     PDT_COUNT("conv_wgrad_generic");
+    const dim3 g(nwg, 1, a.nslice > 1 ? a.nslice : 1);
     if (dtype == kBF16)
-      hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, false>), dim3(nwg), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_wgrad_kernel<kBF16, false>), g, dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_wgrad_kernel<kF16, false>), dim3(nwg), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_wgrad_kernel<kF16, false>), g, dim3(256), 0, s, a);
   }
   PDT_HIP_CHECK(hipGetLastError());  // a refused launch (e.g. LDS / register limits) must not leave ws stale
 }

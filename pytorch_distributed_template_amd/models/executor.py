@@ -474,9 +474,9 @@ class ResNetExecutor:
             sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
         bm, bn = _conv_tile(c.GSLICE, c.GSLICE * c.R * c.S)
         n = c.GSLICE * c.R * c.S * c.GSLICE
-        for j in range(c.nslice):
-            o = c.gfwd[j]
-            self.C.gconv_fwd(x, self.derived[o:o + n], y, sp, N, H, W, c.cout, c.R, c.st, c.pad, P, Q, j, bm, bn)
+        # every slice in ONE launch (blockIdx.z = slice; the slices' forward layouts are consecutive in derived)
+        o = c.gfwd[0]
+        self.C.gconv_fwd(x, self.derived[o:o + n * c.nslice], y, sp, N, H, W, c.cout, c.R, c.st, c.pad, P, Q, -1, bm, bn)
         if stats and fin is not None:
             self.bn_train_finalize(fin, sp, 0, N * P * Q)
         return P, Q, sp, N * P * Q
@@ -493,12 +493,11 @@ class ResNetExecutor:
                 plan = tuple(self.C.conv_wgrad_plan(S_, R, S, S_, N * P * Q, self.wgrad_blocks, False))[:2]
                 self._plans[key] = plan
             splits, pps = plan
-            ws = self._buf("ws", splits * S_ * ldw, torch.float32)
+            # every slice in ONE launch: partials [splits][nslice][64][ldw], one reduction over nslice * 64 rows
+            ws = self._buf("ws", splits * c.nslice * S_ * ldw, torch.float32)
             tmp = self._buf("gconv_dw", c.nslice * S_ * ldw, torch.float32)
-            for j in range(c.nslice):
-                self.C.gconv_wgrad(x, dy, ws, N, H, W, c.cin, R, P, Q, c.st, c.pad, j, ldw, splits, pps)
-                self.C.wgrad_reduce(ws, splits, S_, ldw, ldw, S_ * ldw, tmp[j * S_ * ldw:(j + 1) * S_ * ldw], ldw,
-                                    1.0, False)
+            self.C.gconv_wgrad(x, dy, ws, N, H, W, c.cin, R, P, Q, c.st, c.pad, -1, ldw, splits, pps)
+            self.C.wgrad_reduce(ws, splits, c.nslice * S_, ldw, ldw, c.nslice * S_ * ldw, tmp, ldw, 1.0, False)
             self.C.gather32(tmp, c.gidx, self._g(c.slot))
             self.grad_ready(c.pid)
         self._side_wgrad((dy, x), wg)
@@ -506,13 +505,16 @@ class ResNetExecutor:
             return
         assert bnb is None or bnb[0] == 1, "grouped conv backward-data: inner-BN epilogue only"
         bm, bn = _conv_tile(c.GSLICE, c.GSLICE * c.R * c.S)
-        for j in range(c.nslice):
-            phases = [p for p in c.gphases[j] if H - p[0] > 0 and W - p[1] > 0]
-            if bnb is None:
-                self.C.gconv_dgrad(dy, self.derived, dx, N, P, Q, c.cin, H, W, c.st, phases, j, bm, bn)
-            else:
-                self.C.gconv_dgrad(dy, self.derived, dx, N, P, Q, c.cin, H, W, c.st, phases, j, bm, bn,
-                                   bn_y1=bnb[1], bn_coef1=bnb[2], bn_slots=bnb[6])
+        # every slice in ONE launch: slice 0's phases, the other slices' phase weights follow at the stride of one
+        # slice's whole phase set (so every phase must be present; a degenerate tiny image runs slice by slice)
+        phases = [p for p in c.gphases[0] if H - p[0] > 0 and W - p[1] > 0]
+        kw = {} if bnb is None else dict(bn_y1=bnb[1], bn_coef1=bnb[2], bn_slots=bnb[6])
+        if len(phases) == len(c.gphases[0]):
+            self.C.gconv_dgrad(dy, self.derived, dx, N, P, Q, c.cin, H, W, c.st, phases, -1, bm, bn, **kw)
+        else:
+            for j in range(c.nslice):
+                phases = [p for p in c.gphases[j] if H - p[0] > 0 and W - p[1] > 0]
+                self.C.gconv_dgrad(dy, self.derived, dx, N, P, Q, c.cin, H, W, c.st, phases, j, bm, bn, **kw)
         if fin is not None and bnb is not None:
             self._bn_bwd_finish(bnb[6], fin[0], fin[1], fin[2])
 

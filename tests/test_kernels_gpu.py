@@ -1153,6 +1153,24 @@ def test_grouped_conv_slices_match_torch(width, groups, stride, H):
     dwd = dwd.view(nsl, S, R, R, S)
     got = torch.stack([dwd[j, k, :, :, (k // cg) * cg:(k // cg) * cg + cg] for j in range(nsl) for k in range(S)])
     assert _rel(got, wr.grad.permute(0, 2, 3, 1)) < 1e-2
+    # every slice in ONE launch (j = -1, blockIdx.z = slice): bit-identical outputs, statistics and partial sums
+    y2 = torch.full_like(y, float("nan"))
+    st2 = torch.zeros_like(st)
+    C_.gconv_fwd(x, dense.reshape(-1), y2, st2, N, H, W, width, R, stride, pad, P, Q, -1, 256, 64)
+    dx2 = torch.full_like(dx, float("nan"))
+    C_.gconv_dgrad(dy, derived, dx2, N, P, Q, width, H, W, stride, phases_of[0], -1, 256, 64)
+    dz2 = torch.full_like(dx, float("nan"))
+    slots2 = torch.zeros_like(slots)
+    C_.gconv_dgrad(dy, derived, dz2, N, P, Q, width, H, W, stride, phases_of[0], -1, 256, 64, bn_y1=y1,
+                   bn_coef1=coef, bn_slots=slots2)
+    ws2 = torch.full((splits * nsl * S * ldw,), float("nan"), device=DEV)
+    C_.gconv_wgrad(x, dy, ws2, N, H, W, width, R, P, Q, stride, pad, -1, ldw, splits, pps)
+    dwd2 = torch.empty(nsl * S * ldw, device=DEV)
+    C_.wgrad_reduce(ws2, splits, nsl * S, ldw, ldw, nsl * S * ldw, dwd2, ldw, 1.0, False)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y) and torch.equal(st2, st)
+    assert torch.equal(dx2, dx) and torch.equal(dz2, dz) and torch.equal(slots2, slots)
+    assert torch.equal(dwd2.view(nsl, S, R, R, S), dwd)
 
 
 @pytest.mark.parametrize("tile", [(256, 64, 64), (128, 128, 64), (256, 128, 64), (256, 256, 64)])
