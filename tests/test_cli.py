@@ -74,4 +74,6 @@ def test_native_engine_covers_resnext_in_16bit_only():
     a = argparse.Namespace(engine="auto", arch="resnext50_32x4d")
     assert resolve_engine(a, gpu, torch.float32) == "torch"
     assert resolve_engine(argparse.Namespace(engine="auto", arch="resnet50"), gpu, torch.float32) == "native"
-    assert resolve_engine(argparse.Namespace(engine="auto", arch="vgg16"), gpu, torch.bfloat16) == "torch"
+    for arch in ("vgg11", "vgg16", "vgg19_bn"):  # the VGG executor: 16-bit only
+        assert resolve_engine(argparse.Namespace(engine="auto", arch=arch), gpu, torch.bfloat16) == "native", arch
+        assert resolve_engine(argparse.Namespace(engine="auto", arch=arch), gpu, torch.float32) == "torch", arch
