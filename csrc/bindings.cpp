@@ -395,7 +395,8 @@ void conv_dgrad(const Tensor& dy, const Tensor& wt, Tensor& dx, const OptT& res,
 // x[M][64] and w[256][64], optional BN statistics (fp64 slots) of the rounded outputs
 bool conv1x1_c64_supported(int64_t C, int64_t Kout) { return pdt::conv1x1_c64_supported((int)C, (int)Kout); }
 
-void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M) {
+// pre: the producer BN's [scale | shift] x 64 (x is its raw conv output; training forwards with statistics only)
+void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats, int64_t M, const OptT& pre) {
   const int dt = dt16(x, "x");
   TORCH_CHECK(dt16(w, "w") == dt && dt16(y, "y") == dt, "conv1x1_c64: mixed dtypes");
   TORCH_CHECK(x.numel() >= M * 64 && w.numel() == 256 * 64 && y.numel() >= M * 256, "conv1x1_c64: size mismatch");
@@ -405,7 +406,13 @@ void conv1x1_c64(const Tensor& x, const Tensor& w, Tensor& y, const OptT& stats,
     TORCH_CHECK(stats->numel() >= pdt::kStatSlots * 256 * 2, "conv1x1_c64: stats buffer too small");
     st = pd(*stats, "stats");
   }
-  pdt::conv1x1_c64_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), st, M, dt, cur_stream());
+  const float* pc = nullptr;
+  if (pre.has_value()) {
+    TORCH_CHECK(st != nullptr, "conv1x1_c64: a fused producer BN needs the statistics buffer (training forward)");
+    TORCH_CHECK(pre->numel() >= 128, "conv1x1_c64: pre coefficients are [scale | shift] x 64");
+    pc = pf(*pre, "pre");
+  }
+  pdt::conv1x1_c64_launch(p16(x, "x"), p16(w, "w"), p16(y, "y"), st, M, dt, cur_stream(), pc);
   launched("conv1x1_c64");
 }
 
@@ -449,7 +456,7 @@ std::vector<int64_t> conv_wgrad_plan(int64_t Kout, int64_t T, int64_t U, int64_t
 void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Kout,
                 int64_t T, int64_t U, int64_t Pm, int64_t Qm, int64_t stride_h, int64_t stride_w, int64_t pad_h,
                 int64_t pad_w, int64_t dil_h, int64_t dil_w, int64_t ldw, int64_t splits, int64_t pix_per_split,
-                int64_t cs, bool win) {
+                int64_t cs, bool win, const OptT& pre) {
   const int dt = dt16(x, "x");
   if (cs <= 0) cs = C;
   TORCH_CHECK(dt16(dy, "dy") == dt, "conv_wgrad: mixed dtypes");
@@ -475,6 +482,10 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   a.cs = cs; a.win = win ? 1 : 0;
   a.tile = pdt::wgrad_tile((int)C, (int)Kout, win ? 1 : 0);
   TORCH_CHECK(pix_per_split % 128 == 0 && splits * pix_per_split >= a.P, "conv_wgrad: bad split plan");
+  if (pre.has_value()) {  // x is the producer's raw output: its BN + ReLU applied in-kernel (1x1, C == 64)
+    TORCH_CHECK(pre->numel() >= 2 * C && C == 64 && T == 1 && U == 1 && !win, "conv_wgrad: pre needs a 1x1 C=64 conv");
+    a.pre_coef = pf(*pre, "pre");
+  }
   pdt::conv_wgrad_launch(a, dt, cur_stream());
   launched("conv_wgrad_launch");
 }
@@ -1438,9 +1449,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bn", &conv_dgrad_impl);
   m.def("conv_wgrad_plan", &conv_wgrad_plan);
   m.def("conv1x1_c64_supported", &conv1x1_c64_supported);
-  m.def("conv1x1_c64", &conv1x1_c64);
+  m.def("conv1x1_c64", &conv1x1_c64, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("M"),
+        py::arg("pre") = py::none());
   m.def("conv1x1_c64_mode", [](int64_t set) { return (int64_t)pdt::conv1x1_c64_mode((int)set); });
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("ws"), py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("C"), py::arg("Kout"), py::arg("T"), py::arg("U"), py::arg("Pm"), py::arg("Qm"), py::arg("stride_h"),
+        py::arg("stride_w"), py::arg("pad_h"), py::arg("pad_w"), py::arg("dil_h"), py::arg("dil_w"), py::arg("ldw"),
+        py::arg("splits"), py::arg("pix_per_split"), py::arg("cs"), py::arg("win"), py::arg("pre") = py::none());
   m.def("conv_wgrad_stem_fused", &conv_wgrad_stem_fused);
   m.def("gconv_fwd", &gconv_fwd);
   m.def("gconv_dgrad", &gconv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("P"),

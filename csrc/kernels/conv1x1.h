@@ -16,8 +16,10 @@ int conv1x1_c64_mode(int set);  // returns the previous on/off mode; set >= 0 ch
 void conv1x1_c64_bnb_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* res,
                             const uint16_t* y1, const float* coef1, const uint16_t* y2, const float* coef2,
                             const uint8_t* mask, double* slots, int64_t M, int cin, int dtype, hipStream_t s);
+// pre_coef != nullptr (training, with stats): x is the producer conv's raw output, the kernel applies that BN + ReLU
+// (scale[64] | shift[64]) to its input fragments
 void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
-                        hipStream_t s);
+                        hipStream_t s, const float* pre_coef = nullptr);
 
 // The same two GEMMs for C = 128 / 256 / 512 reduction channels and N output channels (ResNet-50 layers 2-4: conv3
 // forward, conv1 backward-data), N split into slices of 256 (C = 128) or 128 channels (conv1x1x.hip).  w is [N][C].

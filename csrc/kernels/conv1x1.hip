@@ -13,6 +13,10 @@
 //     (s_waitcnt vmcnt(16)) leaves the stores in flight -- the store stream of tile t overlaps tile t+1;
 //   * BN statistics of the rounded outputs accumulate in registers across all of a block's tiles and are reduced
 //     once (16-lane DPP sums) into the block's partial row (deterministic, conv_fwd.h).
+//   * PRE: x is the RAW output of the producer conv (a bottleneck's conv2) and its BatchNorm + ReLU is applied to
+//     each input fragment after the LDS read (pre_act8, bit-identical to bn_apply): the activation is never
+//     written.  A lane's fragment channels are fixed (kk * 32 + fq * 8 + [0, 8)), so its 16 scale / shift pairs
+//     live in registers for the whole kernel.
 #include <cstdlib>
 
 #include "../common.h"
@@ -31,11 +35,11 @@ constexpr int kStoresPerTile = 16;     // global stores per wave per full tile: 
 static_assert(kStoresPerTile == 16, "the per-tile s_waitcnt vmcnt(16) literal below");
 }  // namespace
 
-template <int DT, bool STATS>
+template <int DT, bool STATS, bool PRE>
 __global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __restrict__ x,
                                                              const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ y, float* __restrict__ srows,
-                                                             int64_t M) {
+                                                             const float* __restrict__ pre_coef, int64_t M) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   __shared__ __attribute__((aligned(1024))) char smem[kWB + 2 * kTileB];
@@ -94,6 +98,18 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __r
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { ssum[i][r] = 0.f; ssq[i][r] = 0.f; }
+  // PRE: scale / shift of this lane's fragment channels kk * 32 + fq * 8 + e
+  float psc[2][8], psh[2][8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        psc[kk][e] = pre_coef[kk * 32 + fq * 8 + e];
+        psh[kk][e] = pre_coef[kC + kk * 32 + fq * 8 + e];
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the loop's counted waits must not see these loads
+  }
 
   int buf = 0;
   bool first = true;
@@ -125,8 +141,11 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __r
       for (int kk = 0; kk < 2; ++kk) {
         vec8 bf[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
           bf[j] = *(const vec8*)(xb + ((h * 4 + j) * 16 + fr) * kRowB + (((kk * 4 + fq) ^ sw) << 4));
+          if constexpr (PRE)
+            bf[j] = __builtin_bit_cast(vec8, pre_act8<DT>(__builtin_bit_cast(uint4, bf[j]), psc[kk], psh[kk]));
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -491,7 +510,7 @@ int conv1x1_c64_mode(int set) {
 bool conv1x1_c64_supported(int C, int Kout) { return conv1x1_c64_mode(-1) && C == kC && Kout == kK; }
 
 void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, double* stats, int64_t M, int dtype,
-                        hipStream_t s) {
+                        hipStream_t s, const float* pre_coef) {
   if (M <= 0) return;
   if (M * kRowB >= (int64_t(1) << 31) || M * kK >= (int64_t(1) << 31))
     pdt_hip_fail("conv1x1_c64: operands exceed 32-bit offsets", hipErrorInvalidValue, __FILE__, __LINE__);
@@ -506,11 +525,16 @@ void conv1x1_c64_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, doubl
   Scratch part(stats ? (size_t)G * kK * 2 * sizeof(float) : 0, s);
   float* srows = part.as<float>();
   PDT_COUNT("conv1x1_c64");
-#define PDT_C1(DT_, ST_) hipLaunchKernelGGL((conv1x1_c64_kernel<DT_, ST_>), dim3(G), dim3(256), 0, s, x, w, y, srows, M)
+  if (pre_coef && !stats)
+    pdt_hip_fail("conv1x1_c64: the fused producer BN (pre_coef) runs in training forwards (with statistics)",
+                 hipErrorInvalidValue, __FILE__, __LINE__);
+  if (pre_coef) PDT_COUNT("conv1x1_c64_fused_bn_relu");
+#define PDT_C1(DT_, ST_, PR_)                                                                                  \
+  hipLaunchKernelGGL((conv1x1_c64_kernel<DT_, ST_, PR_>), dim3(G), dim3(256), 0, s, x, w, y, srows, pre_coef, M)
   if (dtype == kBF16) {
-    if (stats) PDT_C1(kBF16, true); else PDT_C1(kBF16, false);
+    if (pre_coef) PDT_C1(kBF16, true, true); else if (stats) PDT_C1(kBF16, true, false); else PDT_C1(kBF16, false, false);
   } else {
-    if (stats) PDT_C1(kF16, true); else PDT_C1(kF16, false);
+    if (pre_coef) PDT_C1(kF16, true, true); else if (stats) PDT_C1(kF16, true, false); else PDT_C1(kF16, false, false);
   }
 #undef PDT_C1
   if (stats) stat_rows_reduce_launch(srows, G, kK * 2, stats, s);

@@ -802,7 +802,11 @@ int wgrad_ctiles(const ConvWgradArgs& a) {
 
 int wgrad_ktile(const ConvWgradArgs& a) { return a.tile == kWgradWide ? 128 : a.tile; }
 
-template <int DT, bool PAIR>
+// PRE (PAIR, 1x1 / stride 1 / no padding only): x is the RAW output of the producer conv and its BatchNorm + ReLU
+// (a.pre_coef) is applied to each x fragment after the LDS read, bit-identical to bn_apply.  A fragment's 8
+// values are 8 pixels of ONE channel (MFMA A row = lane & 15), so a lane needs one scale / shift per fragment.
+// Rows past the split end are zero-filled and transform to relu(shift), but their dY rows are zero too.
+template <int DT, bool PAIR, bool PRE = false>
 __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
@@ -886,6 +890,16 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
     kcol[f] = wk * 64 + f * 16 + 4 * p4;
   }
 
+  float psc[4], psh[4];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int ch = (wc * 64 + f * 16 + (lane & 15)) & 63;
+      psc[f] = a.pre_coef[ch];
+      psh[f] = a.pre_coef[64 + ch];
+    }
+  }
+
   if (nsteps > 0) {
     stage_load(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -907,6 +921,12 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
           s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (lds_s16x4*)(sb + r1 * ROWB + (((cc >> 3) ^ sw1) << 4) + (cc & 7) * 2));
           af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          if constexpr (PRE) {
+            float sc8[8], sh8[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { sc8[e] = psc[f]; sh8[e] = psh[f]; }
+            af[f] = __builtin_bit_cast(vec8, pre_act8<DT>(__builtin_bit_cast(uint4, af[f]), sc8, sh8));
+          }
           lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (lds_s16x4*)(sb + XB + r0 * ROWB + (((kc >> 3) ^ sw0) << 4) + (kc & 7) * 2));
           hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1657,6 +1677,9 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   if (a.ldy && a.ldy != a.Kout && (a.tile != 64 || a.win))
     pdt_hip_fail("conv_wgrad: a strided dY (channel slice) runs on the 64x64 tile only", hipErrorInvalidValue,
                  __FILE__, __LINE__);
+  if (a.pre_coef && !(a.tile == 128 && a.C == 64 && !a.win))
+    pdt_hip_fail("conv_wgrad: a fused producer BN (pre_coef) runs on the 128-pair tile only (C == 64)",
+                 hipErrorInvalidValue, __FILE__, __LINE__);
   const int nwg = (a.Kout / wgrad_ktile(a)) * wgrad_ctiles(a) * a.splits;
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);
@@ -1674,6 +1697,15 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
     } else {
       hipLaunchKernelGGL((conv_wgrad_wide_kernel<kF16, 64>), dim3(nwg), dim3(512), 0, s, a);
     }
+  } else if (a.tile == 128 && a.C == 64 && a.pre_coef) {
+    if (a.T != 1 || a.U != 1 || a.stride_h != 1 || a.stride_w != 1 || a.pad_h != 0 || a.pad_w != 0)
+      pdt_hip_fail("conv_wgrad: a fused producer BN on the 128-pair tile needs a 1x1 / stride-1 conv",
+                   hipErrorInvalidValue, __FILE__, __LINE__);
+    PDT_COUNT("conv_wgrad_128_pair_fused_bn_relu");
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kBF16, true, true>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad128_kernel<kF16, true, true>), dim3(nwg), dim3(256), 0, s, a);
   } else if (a.tile == 128 && a.C == 64) {
     PDT_COUNT("conv_wgrad_128_pair");
     if (dtype == kBF16)

@@ -194,6 +194,9 @@ class ResNetExecutor:
         # a layer1 block's inner BN + ReLU applied by its consumers (conv2 forward and conv2 weight
         # gradient) to their staged input tiles in LDS; the activation relu(bn(z1)) is never written or re-read
         self.fuse_pre = os.environ.get("PDT_FUSE_PRE", "1") == "1"
+        # ... and ResNet-50 layer1's bn2 + ReLU applied by conv3 (the persistent 1x1 64 -> 256 kernel) and conv3's
+        # weight gradient (the 128-pair tile): a2 = relu(bn2(z2)) is never written or re-read
+        self.fuse_pre_1x1 = os.environ.get("PDT_FUSE_PRE1X1", "1") == "1"
         # stem backward: weight gradient with in-kernel dY (PDT_STEM_FUSED=0: separate apply pass + wgrad)
         self.stem_fused = os.environ.get("PDT_STEM_FUSED", "1") == "1"
         # 1x1/2 downsample data gradient written compact and added by phase 0 of the 3x3/2 dgrad
@@ -402,7 +405,13 @@ class ResNetExecutor:
     def _pre_ok(self, nxt: _Conv, N: int, H: int, W: int, train: bool) -> bool:
         """Can ``nxt`` (the conv consuming a block-internal BN + ReLU) apply that BN itself (conv_fwd_pre +
         the fused layer1 weight gradient)?"""
-        return (self.fuse_pre and train and self.wgrad_l1 and hasattr(self.C, "conv_fwd_pre") and nxt.groups == 1 and
+        if not (self.fuse_pre and train and nxt.groups == 1):
+            return False
+        if nxt.R == 1:
+            return (self.fuse_pre_1x1 and nxt.S == 1 and nxt.st == 1 and nxt.pad == 0 and nxt.cin == 64 and
+                    nxt.cout == 256 and self._c1x1 and self.C.conv1x1_c64_supported(64, 256) and
+                    os.environ.get("PDT_WGRAD_PAIR", "1") != "0")
+        return (self.wgrad_l1 and hasattr(self.C, "conv_fwd_pre") and
                 nxt.R == 3 and nxt.S == 3 and nxt.st == 1 and
                 nxt.pad == 1 and nxt.cin == 64 and nxt.cout == 64 and self.C.conv_fwd_pre_supported(N, H, W) and
                 self.C.wgrad_3x3c64_supported(64, 64, 3, 3, W, 1, 1))
@@ -415,7 +424,10 @@ class ResNetExecutor:
         if pre is not None:  # x is the producer conv's raw output; pre = its BN coefficients (layer1 only)
             key = ("stats", c.cout) if stats_tag is None else ("stats", c.cout, stats_tag)
             sp = self._buf(key, self.n_slots * c.cout * 2, torch.float64)
-            self.C.conv_fwd_pre(x, self._w(c), y, sp, pre, N, H, W)
+            if c.R == 1:  # ResNet-50 layer1 conv3 (see _pre_ok)
+                self.C.conv1x1_c64(x, self._w(c), y, sp, N * H * W, pre=pre)
+            else:
+                self.C.conv_fwd_pre(x, self._w(c), y, sp, pre, N, H, W)
             if fin is not None:
                 self.bn_train_finalize(fin, sp, 0, N * H * W)
             return H, W, sp, N * H * W
@@ -652,7 +664,8 @@ class ResNetExecutor:
                 parts = self.C.conv_wgrad_3x3c64(x, dy, ws, N, H, W, pre)
             self.C.wgrad_reduce(ws, parts, 64, 576, 576, 64 * 576, gout, ldo, 1.0, False)
             return
-        assert pre is None, "fused producer BN only on the layer1 weight-gradient kernel"
+        assert pre is None or (R == 1 and S == 1 and C == 64 and st == 1 and pad == 0 and not win), \
+            "fused producer BN: the layer1 3x3 weight-gradient kernel or a 1x1 C = 64 conv (128-pair tile)"
         key = (cout, R, S, C, N * P * Q, win)
         plan = self._plans.get(key)
         if plan is None:
@@ -663,7 +676,7 @@ class ResNetExecutor:
         ldw = R * S * C
         ws = self._buf("ws", splits * cout * ldw, torch.float32)
         self.C.conv_wgrad(x, dy, ws, N, H, W, C, cout, R, S, P, Q, st, st, pad, pad, dil, dil, ldw, splits, pps, cs,
-                          win)
+                          win, pre=pre)
         self.C.wgrad_reduce(ws, splits, rows or cout, cols or ldw, ldw, cout * ldw, gout, ldo, 1.0, False)
 
     def bn_bwd(self, bn1: _BN, y1, g, out_mask, count: int, bn2: Optional[_BN] = None, y2=None):

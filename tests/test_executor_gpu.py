@@ -117,7 +117,27 @@ R18_224_KERNELS = ("stem_fwd", "conv_l1_fwd", "conv_l1_dgrad", "wgrad3x3_c64", "
 # tile table picks for its 1x1 convs (csrc/kernels/conv1x1.hip, conv_fwd.hip)
 R50_224_KERNELS = ("conv1x1_c64", "conv1x1_c64_bnb_1br", "conv1x1_c64_bnb_2br", "conv1x1_c64_bnb_c128",
                    "conv_pp_512x128", "stem_fwd", "conv_pp_fwd", "conv_wgrad_pp", "wgrad_stem_fused", "conv1x1x",
-                   "conv1x1x_bnb", "conv1x1x_bnb_2br")
+                   "conv1x1x_bnb", "conv1x1x_bnb_2br", "conv1x1_c64_fused_bn_relu", "conv_wgrad_128_pair_fused_bn_relu")
+
+
+def test_resnet50_fused_bn2_conv3_is_bit_identical():
+    """ResNet-50 layer1's bn2 + ReLU applied by conv3's forward and weight gradient (no a2 tensor) gives the same
+    step as the unfused chain bit for bit: logits, loss and every gradient."""
+    model, ref, flat, ex, x, t = _setup("resnet50", N=4, HW=224, dtype=torch.bfloat16)
+    from pytorch_distributed_template_amd.ops import native
+    outs = []
+    for fuse in (False, True):
+        ex.fuse_pre_1x1 = fuse
+        flat.grad.zero_()
+        native.C.reset_dispatch_counts()
+        logits, met = ex.train_step(x, t)
+        torch.cuda.synchronize()
+        n = native.C.dispatch_counts().get("conv1x1_c64_fused_bn_relu", 0)
+        assert n == (3 if fuse else 0), n
+        outs.append((logits.clone(), met.clone(), flat.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])
 
 
 @pytest.mark.parametrize("arch,N", [("resnet18", 16), ("resnet18", 32), ("resnet50", 8), ("resnet34", 4),

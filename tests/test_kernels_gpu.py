@@ -731,6 +731,52 @@ def test_fused_producer_bn_relu_layer1(dtype):
     assert not C.conv_fwd_pre_supported(N, 10, W)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M", [12544 + 37, 70000 + 5])
+def test_fused_producer_bn_relu_1x1_c64(dtype, M):
+    """ResNet-50 layer1's conv3: the persistent 1x1 64 -> 256 forward and the 128-pair weight-gradient tile applying
+    bn2 + ReLU to their input fragments equal the unfused chain (bn_apply -> conv / wgrad) BIT FOR BIT: outputs,
+    statistics and the weight-gradient partials (M tails: zero-filled rows transform to relu(shift) but meet zero
+    dY rows)."""
+    from pytorch_distributed_template_amd.ops import native
+    C = native.C
+    if not C.conv1x1_c64_supported(64, 256):
+        pytest.skip("PDT_CONV1X1=0")
+    torch.manual_seed(23)
+    z = _rand16(M, 64, dtype=dtype)
+    w = _rand16(256, 64, dtype=dtype, scale=0.125)
+    coef = torch.cat([torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.5,
+                      torch.zeros(128, device=DEV)]).contiguous()
+    a = torch.empty_like(z)
+    C.bn_apply(z, coef, None, None, a, 64, 0, True, None)
+    st_u = torch.zeros(C.stat_slots() * 256 * 2, dtype=torch.float64, device=DEV)
+    st_f = torch.zeros_like(st_u)
+    y_u = torch.empty(M, 256, dtype=dtype, device=DEV)
+    y_f = torch.full_like(y_u, float("nan"))
+    C.reset_dispatch_counts()
+    C.conv1x1_c64(a, w, y_u, st_u, M)
+    C.conv1x1_c64(z, w, y_f, st_f, M, pre=coef)
+    torch.cuda.synchronize()
+    assert C.dispatch_counts().get("conv1x1_c64_fused_bn_relu", 0) == 1
+    assert torch.equal(y_u.view(torch.int16), y_f.view(torch.int16))
+    assert torch.equal(st_u, st_f)
+    ref = torch.relu(z.float() * coef[:64] + coef[64:128]) @ w.float().t()
+    assert _rel(y_f, ref) < 2e-2
+    # weight gradient dW[256][64] = dY^T a over the M pixels
+    dy = _rand16(M, 256, dtype=dtype)
+    splits, pps = tuple(C.conv_wgrad_plan(256, 1, 1, 64, M, 512, False))[:2]
+    outs = []
+    for x_, pre in ((a, None), (z, coef)):
+        ws = torch.full((splits * 256 * 64,), float("nan"), device=DEV)
+        C.conv_wgrad(x_, dy, ws, 1, 1, M, 64, 256, 1, 1, 1, M, 1, 1, 0, 0, 1, 1, 64, splits, pps, 0, False, pre=pre)
+        outs.append(ws)
+    torch.cuda.synchronize()
+    assert C.dispatch_counts().get("conv_wgrad_128_pair_fused_bn_relu", 0) == 1
+    assert torch.equal(outs[0], outs[1])
+    dw = outs[1].view(splits, 256, 64).sum(0)
+    assert _rel(dw, dy.float().t() @ a.float()) < 1e-2
+
+
 @pytest.mark.parametrize("N,H", [(3, 12), (5, 56), (1, 4)])
 @pytest.mark.parametrize("variant", ["fwd", "fwd_stats", "fwd_pre", "dgrad_res", "dgrad_bn", "dgrad_bn_out"])
 def test_conv_l1_pingpong_matches_4wave(variant, N, H):
