@@ -13,6 +13,7 @@
 // writes one fp32 partial tile.  Partials over the split-K axis are summed by wgrad_reduce, which
 // writes (and scales) straight into the fp32 gradient buffer (the DDP bucket view).
 #include <cstdlib>
+#include <type_traits>
 
 #include "../common.h"
 #include "conv_wgrad.h"
@@ -984,7 +985,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   constexpr int kWideDma = wide_dma<BKP>();
-  constexpr int XI = BKP / 4 / 8;  // DMA instructions per wave per sub-tile image (X: 2 sub-tiles, dY: 1)
+  static_assert(BKP == 64 && kWideDma == 6, "the DMA row mapping below is written for 64-pixel K-steps");
   constexpr int ROWB = 256;        // 128 channels * 2 B
   constexpr int SUB = BKP * ROWB;  // one column block's X image, or the dY image
   constexpr int STAGE = 3 * SUB;   // X block 0 | X block 1 | dY
@@ -1027,33 +1028,64 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
 
-  // DMA lane geometry: 4 rows x 16 chunks per 1 KiB instruction
+  // ---- DMA: every source offset is updated incrementally (adds and compares, no per-pixel division or multiply:
+  // the round-5 form spent ~90 quarter-rate VALU per K-step and wave on them, more issue time than its MFMAs).
+  // X: this wave stages column block hx = wave / 4, pixel rows 16 (wave & 3) + 4 j + lrow (j < 4) of the K-step;
+  // dY: rows 8 wave + 4 j + lrow (j < 2).  LDS: X block h of ring stage st at (3 h + st) SUB, dY at (6 + st) SUB, so
+  // every fragment read below is a lane register plus an immediate below 64 KB.
   const int lrow = lane >> 4, pch = lane & 15;
+  const int hx = wave >> 2;
+  const int sh = a.stride_h, sw = a.stride_w, Qm = a.Qm, Pm = a.Pm, W = a.W, H = a.H, cs = a.cs;
+  const int adv_i = BKP / Qm, adv_j = BKP - adv_i * Qm;  // one K-step = adv_i rows + adv_j columns of the grid
+  // lane state of pixel p0 = pix_begin + step * BKP + 16 (wave & 3) + lrow: grid row xi, column xj, input row /
+  // column xh / xw (tap offset included) and element offset xo of the input pixel (column excluded)
+  int xi, xj, xh, xw, xo;
+  {
+    const FastDiv dpq{a.div_pq_mul, a.div_pq_shift}, dq{a.div_q_mul, a.div_q_shift};
+    const int p0 = pix_begin + 16 * (wave & 3) + lrow;
+    const int n = (int)fdiv((uint32_t)p0, dpq);
+    const int rem = p0 - n * Pm * Qm;
+    xi = (int)fdiv((uint32_t)rem, dq);
+    xj = rem - xi * Qm;
+    xh = xi * sh + th2[hx];
+    xw = xj * sw + tw2[hx];
+    xo = ((n * H + xh) * W + xw) * cs;
+  }
+  const int row_step = (sh * W - Qm * sw) * cs, img_step = (H - Pm * sh) * W * cs;
+  // one grid-column step of d pixels with at most one row wrap (d < Qm) and one image wrap
+  auto step_px = [&](int& i, int& j, int& h, int& w, int& o, int d) {
+    j += d; w += d * sw; o += d * sw * cs;
+    if (j >= Qm) {
+      j -= Qm; w -= Qm * sw; h += sh; o += row_step; ++i;
+      if (i >= Pm) { i -= Pm; h -= Pm * sh; o += img_step; }
+    }
+  };
+  int ycur;  // dY byte offset of this lane's j = 0 row for the next K-step to stage
+  const int ystr = a.ldy ? a.ldy : a.Kout;
+  const int lchy = pch ^ ((lrow << 1) | ((wave & 1) << 3));
+  ycur = ((pix_begin + 8 * wave + lrow) * ystr + k0 + lchy * 8) * 2;
+  const bool x_live = hx == 0 || half1_live;
+  const int xcolb = cb0[hx];
 
-  auto stage_load = [&](int step, int buf) {
-    const int pbase = pix_begin + step * BKP;
-    char* sb = smem + buf * STAGE;
-    constexpr int RI = BKP / 4;  // DMA instructions (4 rows each) per sub-tile image
+  auto stage_load = [&](int buf) {  // the next K-step in sequence (advances the lane state)
+    int i = xi, j = xj, h = xh, w = xw, o = xo;
 #pragma unroll
-    for (int j = 0; j < 2 * XI; ++j) {  // X: instruction i = wave * 2XI + j of 2RI (sub-tile i / RI)
-      const int i = wave * 2 * XI + j;
-      const int h = i / RI;
-      const int row = (i % RI) * 4 + lrow;  // 0..BKP-1
-      const int lch = pch ^ tr_swz16(row);
-      uint32_t xo, yo;
-      wgrad_rows<false>(a, pbase + row, th2[h], tw2[h], cb0[h], lch, k0, xo, yo);
-      if (h && !half1_live) xo = kOOB;
-      buf_lds16_asm(rx, sb + h * SUB + (i % RI) * 1024, xo);
+    for (int jj = 0; jj < 4; ++jj) {
+      if (jj > 0) step_px(i, j, h, w, o, 4);
+      const int lch = pch ^ ((lrow << 1) | (((jj >> 1) & 1) << 3));
+      const bool ok = x_live && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const uint32_t off = ok ? (uint32_t)((o + xcolb + lch * 8) * 2) : kOOB;
+      buf_lds16_asm(rx, smem + (3 * hx + buf) * SUB + (4 * (wave & 3) + jj) * 1024, off);
     }
 #pragma unroll
-    for (int j = 0; j < XI; ++j) {  // dY: instruction i = wave * XI + j of RI
-      const int i = wave * XI + j;
-      const int row = i * 4 + lrow;
-      const int lch = pch ^ tr_swz16(row);
-      uint32_t xo, yo;
-      wgrad_rows<false>(a, pbase + row, th2[0], tw2[0], cb0[0], lch, k0, xo, yo);
-      buf_lds16_asm(ry, sb + 2 * SUB + i * 1024, yo);
-    }
+    for (int jj = 0; jj < 2; ++jj)
+      buf_lds16_asm(ry, smem + (6 + buf) * SUB + (2 * wave + jj) * 1024, (uint32_t)(ycur + jj * 4 * ystr * 2));
+    // advance to the next K-step
+    ycur += BKP * ystr * 2;
+    xj += adv_j; xw += adv_j * sw; xo += adv_j * sw * cs;
+    xi += adv_i; xh += adv_i * sh; xo += adv_i * sh * W * cs;
+    if (xj >= Qm) { xj -= Qm; xw -= Qm * sw; xh += sh; xo += row_step; ++xi; }
+    while (xi >= Pm) { xi -= Pm; xh -= Pm * sh; xo += img_step; }
   };
 
   f32x4_t acc[4][4];
@@ -1065,62 +1097,68 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
   const int xsub = wc >> 1;  // this wave's X sub-tile (column block)
   const bool live = xsub == 0 || half1_live;
-  int ccol[4], kcol[4];
+  // fragment byte addresses (stage 0, kk 0): the transposed-read swizzle tr_swz16 of rows kk * 32 + 8 g + q (+4)
+  // does not depend on kk, so a stage / kk shift is an immediate
+  int xa[4][2], ya[4][2];
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
-    ccol[f] = (wc & 1) * 64 + f * 16 + 4 * p4;
-    kcol[f] = wk * 64 + f * 16 + 4 * p4;
+    const int cc = (wc & 1) * 64 + f * 16 + 4 * p4, kc = wk * 64 + f * 16 + 4 * p4;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int rr = 8 * g + q + 4 * r, sz = tr_swz16(rr);
+      xa[f][r] = 3 * xsub * SUB + rr * ROWB + (((cc >> 3) ^ sz) << 4) + (cc & 7) * 2;
+      ya[f][r] = 6 * SUB + rr * ROWB + (((kc >> 3) ^ sz) << 4) + (kc & 7) * 2;
+    }
   }
 
-  if (nsteps > 0) {
-    stage_load(0, 0);
-    if (nsteps > 1) stage_load(1, 1);
-    for (int s = 0; s < nsteps; ++s) {
-      // stage s landed: the younger stage s+1 (kWideDma per wave) may stay in flight
-      if (s + 1 < nsteps)
-        wg_vm_wait<kWideDma>();
-      else
-        wg_vm_wait<0>();
-      // every wave's DMA of stage s landed; every wave's MFMAs (hence its fragment reads) of stage s-1 done, so
-      // the ring slot of stage s-1 may be refilled.  A plain s_barrier: __syncthreads' release fence would also
-      // drain the stage still in flight (vmcnt(0)).
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 2 < nsteps) stage_load(s + 2, (s + 2) % NST);
-      const char* sb = smem + (s % NST) * STAGE;
-      const char* sx = sb + xsub * SUB;
-      const char* sy = sb + 2 * SUB;
-      if (live) {
+  auto kstep = [&](auto stc, int s) {
+    constexpr int ST = decltype(stc)::value;  // ring stage of K-step s (s % 3)
+    // stage s landed: the younger stage s+1 (kWideDma per wave) may stay in flight
+    if (s + 1 < nsteps)
+      wg_vm_wait<kWideDma>();
+    else
+      wg_vm_wait<0>();
+    // every wave's DMA of stage s landed; every wave's MFMAs (hence its fragment reads) of stage s-1 done, so
+    // the ring slot of stage s-1 may be refilled.  A plain s_barrier: __syncthreads' release fence would also
+    // drain the stage still in flight (vmcnt(0)).
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 2 < nsteps) stage_load((ST + 2) % NST);
+    if (live) {
 #pragma unroll
-        for (int kk = 0; kk < BKP / 32; ++kk) {
-          const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
-          const int sw0 = tr_swz16(r0), sw1 = tr_swz16(r1);
-          vec8 af[4], bfr[4];
+      for (int kk = 0; kk < BKP / 32; ++kk) {
+        const int so = ST * SUB + kk * 32 * ROWB;
+        vec8 af[4], bfr[4];
 #pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            const int cc = ccol[f], kc = kcol[f];
-            s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)(sx + r0 * ROWB + (((cc >> 3) ^ sw0) << 4) + (cc & 7) * 2));
-            s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)(sx + r1 * ROWB + (((cc >> 3) ^ sw1) << 4) + (cc & 7) * 2));
-            af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)(sy + r0 * ROWB + (((kc >> 3) ^ sw0) << 4) + (kc & 7) * 2));
-            hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)(sy + r1 * ROWB + (((kc >> 3) ^ sw1) << 4) + (kc & 7) * 2));
-            bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          }
-          // raised priority while this wave's 16 MFMAs issue: the SIMD's other wave then slots its fragment reads
-          // in between instead of both waves reading at once
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
-          __builtin_amdgcn_s_setprio(0);
+        for (int f = 0; f < 4; ++f) {
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + xa[f][0] + so));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + xa[f][1] + so));
+          af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + ya[f][0] + so));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + ya[f][1] + so));
+          bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
+        // raised priority while this wave's 16 MFMAs issue: the SIMD's other wave then slots its fragment reads
+        // in between instead of both waves reading at once
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
       }
+    }
+  };
+
+  if (nsteps > 0) {
+    stage_load(0);
+    if (nsteps > 1) stage_load(1);
+    // unrolled over the 3 ring stages: every stage offset is a compile-time immediate
+    for (int s = 0; s < nsteps; s += NST) {
+      kstep(std::integral_constant<int, 0>{}, s);
+      if (s + 1 < nsteps) kstep(std::integral_constant<int, 1>{}, s + 1);
+      if (s + 2 < nsteps) kstep(std::integral_constant<int, 2>{}, s + 2);
     }
   }
   if (!live) return;
@@ -1680,6 +1718,9 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   if (a.pre_coef && !(a.tile == 128 && a.C == 64 && !a.win))
     pdt_hip_fail("conv_wgrad: a fused producer BN (pre_coef) runs on the 128-pair tile only (C == 64)",
                  hipErrorInvalidValue, __FILE__, __LINE__);
+  // the wide kernel's incremental DMA addressing steps 4 grid columns with one row wrap: narrower outputs run the
+  // 128 x 128 tile (same split plan and partial layout)
+  if (a.tile == kWgradWide && a.Qm < 4) a.tile = 128;
   const int nwg = (a.Kout / wgrad_ktile(a)) * wgrad_ctiles(a) * a.splits;
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);

@@ -103,13 +103,15 @@ def test_conv_wgrad_two_tap_pair_tile(case, target, dtype):
 
 @pytest.mark.parametrize("case", [(2, 14, 14, 128, 128, 3, 1, 1), (2, 15, 13, 128, 256, 3, 2, 1),
                                   (3, 9, 9, 256, 128, 1, 1, 0), (2, 10, 10, 128, 128, 1, 2, 0),
-                                  (1, 7, 7, 384, 128, 3, 1, 1)])
+                                  (1, 7, 7, 384, 128, 3, 1, 1), (2, 28, 28, 128, 128, 3, 1, 1),
+                                  (3, 6, 6, 128, 128, 3, 2, 1)])
 @pytest.mark.parametrize("target", [64, 2048])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_conv_wgrad_wide_tile(case, target, dtype):
     """C % 128 == 0 and Kout % 128 == 0 below 256 x 256: the wide 256 (two 128-wide column blocks of dW) x 128 kernel
     with its 3-deep counted-wait DMA ring.  Every column block against torch fp32 (an odd block count leaves the last
-    tile's second half dead), few and many splits (a split of one K-step drains the ring at once)."""
+    tile's second half dead), few and many splits (a split of one K-step drains the ring at once); image and row
+    wraps inside a K-step (7 x 7, 5 x 5 outputs) and a 3-wide output (the 128 x 128 fallback)."""
     from pytorch_distributed_template_amd.ops import conv, native
     N, H, W, C, K, R, st, pad = case
     P, Q = conv.out_hw(H, W, R, R, st, pad)
