@@ -26,6 +26,12 @@ template <> struct E16<kBF16> {
     __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN stays NaN
     return __builtin_bit_cast(uint16_t, b);
   }
+  // two values rounded and packed (lo | hi << 16) by ONE v_cvt_pk_bf16_f32 (from_f twice + shift / or: 4 VALU)
+  static PDT_DEVICE uint32_t pack2(float lo, float hi) {
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    typedef float f32x2_t __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+  }
   static PDT_DEVICE f32x4_t mfma16x16x32(vec8 a, vec8 b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
@@ -40,6 +46,7 @@ template <> struct E16<kF16> {
     asm("" : "+v"(f));
     return __builtin_bit_cast(uint16_t, (_Float16)f);
   }
+  static PDT_DEVICE uint32_t pack2(float lo, float hi) { return (uint32_t)from_f(lo) | ((uint32_t)from_f(hi) << 16); }
   static PDT_DEVICE f32x4_t mfma16x16x32(vec8 a, vec8 b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }

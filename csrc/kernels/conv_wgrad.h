@@ -25,7 +25,8 @@ struct ConvWgradArgs {
   uint32_t div_pq_mul, div_pq_shift, div_q_mul, div_q_shift;  // FastDiv of Pm*Qm and Qm (launcher)
   // stem only (f_y != nullptr): dY computed in-kernel from the 3x3/2 max-pool backward + ReLU + BN backward
   // (dy unused).  f_y: conv output [P][64]; f_dp / f_idx: pooled gradient and argmax [N][f_OH][f_OW][64];
-  // f_coef: BN forward scale, shift; f_bcoef: backward apply A, B, C (64 each)
+  // f_coef: BN forward scale, shift (not read: the argmax carries the ReLU mask, see bn_relu_maxpool); f_bcoef:
+  // backward apply A, B, C (64 each)
   const uint16_t* f_y = nullptr;
   const uint16_t* f_dp = nullptr;
   const uint8_t* f_idx = nullptr;

@@ -387,12 +387,12 @@ __global__ __launch_bounds__(256) void wgrad_stem_quad_kernel(ConvWgradArgs a) {
 
   // ---- dY: quad qd of the step, channels 4*cg .. 4*cg + 3
   const int qd = tid >> 4, cg = tid & 15;
-  float fA[4], fB[4], fC[4], fsc[4], fsh[4];
+  // (the ReLU mask is in the argmax: bn_relu_maxpool marks windows whose maximum is 0 dead, so f_coef is not read)
+  float fA[4], fB[4], fC[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int c = cg * 4 + e;
     fA[e] = a.f_bcoef[c]; fB[e] = a.f_bcoef[64 + c]; fC[e] = a.f_bcoef[128 + c];
-    fsc[e] = a.f_coef[c]; fsh[e] = a.f_coef[64 + c];
   }
   u32x2v fy[4], fg[4];  // asm loads (common.h gload*_asm): waited for by QUAD_WAIT, which also carries them as
                         // operands so no use can be scheduled ahead of it
@@ -428,6 +428,7 @@ __global__ __launch_bounds__(256) void wgrad_stem_quad_kernel(ConvWgradArgs a) {
     const uint32_t i3 = (fvalid & 12) == 12 ? fi[3] : 0xffffffffu;
     const uint32_t keep0 = fvalid & 1 ? 0xffffffffu : 0u, keep1 = (fvalid & 3) == 3 ? 0xffffffffu : 0u;
     uint32_t ov[4][2];
+    float dv[4][4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int sh = 16 * (e & 1);
@@ -435,23 +436,23 @@ __global__ __launch_bounds__(256) void wgrad_stem_quad_kernel(ConvWgradArgs a) {
       const uint32_t p2 = (i2 >> (8 * e)) & 0xffu, p3 = (i3 >> (8 * e)) & 0xffu;
       const float g0 = E::to_f((uint16_t)(fg[0][e >> 1] >> sh)), g1 = E::to_f((uint16_t)(fg[1][e >> 1] >> sh));
       const float g2 = E::to_f((uint16_t)(fg[2][e >> 1] >> sh)), g3 = E::to_f((uint16_t)(fg[3][e >> 1] >> sh));
-      float dz[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p0 == 4) dz[0] += g0;
-      if (p0 == 5) dz[1] += g0;
-      if (p1 == 3) dz[1] += g1;
-      if (p0 == 7) dz[2] += g0;
-      if (p2 == 1) dz[2] += g2;
-      if (p0 == 8) dz[3] += g0;
-      if (p1 == 6) dz[3] += g1;
-      if (p2 == 2) dz[3] += g2;
-      if (p3 == 0) dz[3] += g3;
+      // branch-free (as conditional adds the compiler built a divergent switch on p0): selects of g or 0, summed
+      // in window order (an unselected term adds an exact zero)
+      float dz[4];
+      dz[0] = p0 == 4 ? g0 : 0.f;
+      dz[1] = (p0 == 5 ? g0 : 0.f) + (p1 == 3 ? g1 : 0.f);
+      dz[2] = (p0 == 7 ? g0 : 0.f) + (p2 == 1 ? g2 : 0.f);
+      dz[3] = (((p0 == 8 ? g0 : 0.f) + (p1 == 6 ? g1 : 0.f)) + (p2 == 2 ? g2 : 0.f)) + (p3 == 0 ? g3 : 0.f);
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub) {
         const float yv = E::to_f((uint16_t)(fy[sub][e >> 1] >> sh));
-        const float d = yv * fsc[e] + fsh[e] > 0.f ? dz[sub] : 0.f;
-        const uint32_t rr = (uint32_t)E::from_f(__builtin_fmaf(fA[e], d, __builtin_fmaf(fB[e], yv, fC[e])));
-        if (e & 1) ov[sub][e >> 1] |= rr << 16; else ov[sub][e >> 1] = rr;
+        dv[sub][e] = __builtin_fmaf(fA[e], dz[sub], __builtin_fmaf(fB[e], yv, fC[e]));
       }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      ov[sub][0] = E::pack2(dv[sub][0], dv[sub][1]);
+      ov[sub][1] = E::pack2(dv[sub][2], dv[sub][3]);
     }
 #pragma unroll
     for (int sub = 0; sub < 4; ++sub) {
@@ -627,12 +628,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
   // ---- dY: quad (qr, qc) = (qd >> 3, qd & 7) of the step, channels 4*cg .. 4*cg + 3
   const int qd = tid >> 4, cg = tid & 15, qr = qd >> 3, qc = qd & 7;
-  float fA[4], fB[4], fC[4], fsc[4], fsh[4];
+  // (the ReLU mask is in the argmax: bn_relu_maxpool marks windows whose maximum is 0 dead, so f_coef is not read)
+  float fA[4], fB[4], fC[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int c = cg * 4 + e;
     fA[e] = a.f_bcoef[c]; fB[e] = a.f_bcoef[64 + c]; fC[e] = a.f_bcoef[128 + c];
-    fsc[e] = a.f_coef[c]; fsh[e] = a.f_coef[64 + c];
   }
   u32x2v fy[4], fg[4];  // asm loads: waited for by ROWS_WAIT
   uint32_t fi[4];
@@ -664,6 +665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const uint32_t i0 = fi[0], i1 = fvalid & 8 ? fi[1] : 0xffffffffu, i2 = fvalid & 4 ? fi[2] : 0xffffffffu;
     const uint32_t i3 = (fvalid & 12) == 12 ? fi[3] : 0xffffffffu;
     uint32_t ov[4][2];
+    float dv[4][4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int sh = 16 * (e & 1);
@@ -671,23 +673,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       const uint32_t p2 = (i2 >> (8 * e)) & 0xffu, p3 = (i3 >> (8 * e)) & 0xffu;
       const float g0 = E::to_f((uint16_t)(fg[0][e >> 1] >> sh)), g1 = E::to_f((uint16_t)(fg[1][e >> 1] >> sh));
       const float g2 = E::to_f((uint16_t)(fg[2][e >> 1] >> sh)), g3 = E::to_f((uint16_t)(fg[3][e >> 1] >> sh));
-      float dz[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p0 == 4) dz[0] += g0;
-      if (p0 == 5) dz[1] += g0;
-      if (p1 == 3) dz[1] += g1;
-      if (p0 == 7) dz[2] += g0;
-      if (p2 == 1) dz[2] += g2;
-      if (p0 == 8) dz[3] += g0;
-      if (p1 == 6) dz[3] += g1;
-      if (p2 == 2) dz[3] += g2;
-      if (p3 == 0) dz[3] += g3;
+      // branch-free (as conditional adds the compiler built a divergent switch on p0): selects of g or 0, summed
+      // in window order (an unselected term adds an exact zero)
+      float dz[4];
+      dz[0] = p0 == 4 ? g0 : 0.f;
+      dz[1] = (p0 == 5 ? g0 : 0.f) + (p1 == 3 ? g1 : 0.f);
+      dz[2] = (p0 == 7 ? g0 : 0.f) + (p2 == 1 ? g2 : 0.f);
+      dz[3] = (((p0 == 8 ? g0 : 0.f) + (p1 == 6 ? g1 : 0.f)) + (p2 == 2 ? g2 : 0.f)) + (p3 == 0 ? g3 : 0.f);
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub) {
         const float yv = E::to_f((uint16_t)(fy[sub][e >> 1] >> sh));
-        const float d = yv * fsc[e] + fsh[e] > 0.f ? dz[sub] : 0.f;
-        const uint32_t rr = (uint32_t)E::from_f(__builtin_fmaf(fA[e], d, __builtin_fmaf(fB[e], yv, fC[e])));
-        if (e & 1) ov[sub][e >> 1] |= rr << 16; else ov[sub][e >> 1] = rr;
+        dv[sub][e] = __builtin_fmaf(fA[e], dz[sub], __builtin_fmaf(fB[e], yv, fC[e]));
       }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      ov[sub][0] = E::pack2(dv[sub][0], dv[sub][1]);
+      ov[sub][1] = E::pack2(dv[sub][2], dv[sub][3]);
     }
 #pragma unroll
     for (int sub = 0; sub < 4; ++sub) {

@@ -70,6 +70,12 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     for (int e = 0; e < 4; ++e) ow_[e] = (uint32_t)E::from_f(best[2 * e]) | ((uint32_t)E::from_f(best[2 * e + 1]) << 16);
     const uint32_t o = pixv * C + c0;
     *(uint4*)(out + o) = make_uint4(ow_[0], ow_[1], ow_[2], ow_[3]);
+    // a window whose maximum is the ReLU's zero passes no gradient (the ReLU mask at its argmax is 0): its index
+    // is the dead marker 255, which no window position matches -- the backward kernels route nothing from it, and
+    // the fused stem weight gradients need no per-pixel ReLU mask
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (!(best[e] > 0.f)) bi[e] = 0xffu;
     uint2 ib;
     ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
@@ -203,11 +209,15 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(const uint16_
       const uint16_t* ybase = y + ((int64_t)n * H * W) * C + c0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int pos = (int)((((e < 4) ? ib.x : ib.y) >> (8 * (e & 3))) & 0xff);
+        const int pos0 = (int)((((e < 4) ? ib.x : ib.y) >> (8 * (e & 3))) & 0xff);
+        // a dead window (255: its maximum is the ReLU's zero) passes nothing; it reads the always-inside centre tap
+        const bool live = pos0 < 9;
+        const int pos = live ? pos0 : 4;
         const int kh = pos / 3, kw = pos - 3 * (pos / 3);
         const int h = oh * 2 - 1 + kh, w = ow * 2 - 1 + kw;  // always inside (argmax is a valid tap)
         const float yv = E::to_f(ybase[((int64_t)h * W + w) * C + e]);
-        const float dz = (yv * sc[e] + sh[e] > 0.f) ? E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1)))) : 0.f;
+        const float dz =
+            (live && yv * sc[e] + sh[e] > 0.f) ? E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1)))) : 0.f;
         s0[e] += dz;
         s1[e] += dz * (yv - mu[e]) * is[e];
       }

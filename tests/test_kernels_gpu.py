@@ -212,6 +212,10 @@ def test_bn_relu_maxpool_and_backward():
     a = torch.relu(y.float() * coef[:C] + coef[C:2 * C]).permute(0, 3, 1, 2).requires_grad_(True)
     ref = F.max_pool2d(a, 3, 2, 1)
     assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2
+    # windows whose maximum is the ReLU's zero carry the dead argmax 255 (no gradient); the others a window position
+    dead = out.float() == 0
+    assert dead.any() and (~dead).any()
+    assert torch.equal(idx == 255, dead) and bool((idx[~dead] < 9).all())
     dp = _rand16(N, OH, OW, C)
     ref.backward(dp.float().permute(0, 3, 1, 2))
     dz = torch.empty_like(y)
