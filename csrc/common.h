@@ -53,6 +53,16 @@ template <> struct E16<kF16> {
 };
 
 
+// the 8 16-bit values of a packed 16-byte vector (element 2i in the low half of dword i)
+PDT_DEVICE void unpack8(uint4 v, uint16_t (&o)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = (uint16_t)w[i];
+    o[2 * i + 1] = (uint16_t)(w[i] >> 16);
+  }
+}
+
 // Producer BatchNorm + ReLU applied to a 16-byte chunk (8 channels) of an activation tile already staged in LDS
 // (the BN1 -> ReLU -> conv2 chain of a residual block without the materialised activation).
 // Bit-identical to bn_apply: the same fma(y, scale, shift) in fp32 and the same rounding; ReLU is taken on the
@@ -67,7 +77,7 @@ PDT_DEVICE uint4 pre_act8(uint4 v, const float (&sc)[8], const float (&sh)[8]) {
   for (int e = 0; e < 4; ++e) {
     const float lo = E::to_f((uint16_t)(w[e] & 0xffff)) * sc[2 * e] + sh[2 * e];
     const float hi = E::to_f((uint16_t)(w[e] >> 16)) * sc[2 * e + 1] + sh[2 * e + 1];
-    const uint32_t pk = (uint32_t)E::from_f(lo) | ((uint32_t)E::from_f(hi) << 16);
+    const uint32_t pk = E::pack2(lo, hi);
     w[e] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(pdt_s16x2, pk), pdt_s16x2{0, 0}));
   }
   return make_uint4(w[0], w[1], w[2], w[3]);

@@ -159,14 +159,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_kernel(const uint16_t* __r
         uint16_t* yp = y + m * kK + wave * 64 + 8 * fq;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
+          uint4 pk;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+          pk.x = E::pack2(acc[2 * p][j][0], acc[2 * p][j][1]);
+          pk.y = E::pack2(acc[2 * p][j][2], acc[2 * p][j][3]);
+          pk.z = E::pack2(acc[2 * p + 1][j][0], acc[2 * p + 1][j][1]);
+          pk.w = E::pack2(acc[2 * p + 1][j][2], acc[2 * p + 1][j][3]);
           uint16_t o[8];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) o[r] = E::from_f(acc[2 * p + (r >> 2)][j][r & 3]);
-          uint4 pk;
-          pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-          pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-          pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
-          pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+          unpack8(pk, o);
           if (m < M) {
             *(uint4*)(yp + p * 32) = pk;
             if constexpr (STATS) {
@@ -384,13 +383,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
         for (int p = 0; p < 2; ++p) {
           const uint32_t rw4[4] = {rr[j][p].x, rr[j][p].y, rr[j][p].z, rr[j][p].w};
           const uint32_t yw4[4] = {yy[j][p].x, yy[j][p].y, yy[j][p].z, yy[j][p].w};
-          uint16_t o[8];
-          float q1[8], q2[8];
+          float vv[8], q1[8], q2[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(rw4[e >> 1] >> (16 * (e & 1))));
             if (!((mb[j][p] >> e) & 1u)) v = 0.f;
-            o[e] = E::from_f(v);
+            vv[e] = v;
             q1[e] = E::to_f((uint16_t)(yw4[e >> 1] >> (16 * (e & 1))));
           }
           if constexpr (BR == 2) {
@@ -398,11 +396,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_c64_bnb_kernel(const uint16_t*
 #pragma unroll
             for (int e = 0; e < 8; ++e) q2[e] = E::to_f((uint16_t)(zw4[e >> 1] >> (16 * (e & 1))));
           }
-          uint4 pk;
-          pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-          pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-          pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
-          pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+          uint4 pk;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+          pk.x = E::pack2(vv[0], vv[1]);
+          pk.y = E::pack2(vv[2], vv[3]);
+          pk.z = E::pack2(vv[4], vv[5]);
+          pk.w = E::pack2(vv[6], vv[7]);
+          uint16_t o[8];
+          unpack8(pk, o);
           if (m < M) {
             const int c0 = wave * 64 + p * 32 + 8 * fq;
             *(uint4*)(y + m * kK + c0) = pk;

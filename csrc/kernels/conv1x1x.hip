@@ -153,14 +153,6 @@ PDT_DEVICE void x1_mma(f32x4_t (&acc)[NF][PJ], const typename E16<DT>::vec8 (&af
   }
 }
 
-PDT_DEVICE uint4 x1_pack(const uint16_t (&o)[8]) {
-  uint4 pk;
-  pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-  pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-  pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
-  pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
-  return pk;
-}
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------ forward
@@ -223,11 +215,15 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_kernel(const uint16_t* __rest
         uint16_t* yp = y + m * N + n0 + wave * C::WCH + 8 * fq;
 #pragma unroll
         for (int p = 0; p < NF / 2; ++p) {
+          uint4 pk;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+          pk.x = E::pack2(acc[2 * p][j][0], acc[2 * p][j][1]);
+          pk.y = E::pack2(acc[2 * p][j][2], acc[2 * p][j][3]);
+          pk.z = E::pack2(acc[2 * p + 1][j][0], acc[2 * p + 1][j][1]);
+          pk.w = E::pack2(acc[2 * p + 1][j][2], acc[2 * p + 1][j][3]);
           uint16_t o[8];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) o[r] = E::from_f(acc[2 * p + (r >> 2)][j][r & 3]);
+          unpack8(pk, o);
           if (m < M) {
-            *(uint4*)(yp + p * 32) = x1_pack(o);
+            *(uint4*)(yp + p * 32) = pk;
             if constexpr (STATS) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) {
@@ -446,13 +442,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           const u32x4v r4 = rr[SET][j][p], y4 = yy[SET][j][p];
-          uint16_t o[8];
-          float q1[8], q2[8];
+          float vv[8], q1[8], q2[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float v = acc[2 * p + (e >> 2)][j][e & 3] + E::to_f((uint16_t)(r4[e >> 1] >> (16 * (e & 1))));
             if (!((mb[SET][j][p] >> e) & 1u)) v = 0.f;
-            o[e] = E::from_f(v);
+            vv[e] = v;
             q1[e] = E::to_f((uint16_t)(y4[e >> 1] >> (16 * (e & 1))));
           }
           if constexpr (BR == 2) {
@@ -460,7 +455,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1x_bnb_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) q2[e] = E::to_f((uint16_t)(z4[e >> 1] >> (16 * (e & 1))));
           }
-          const uint4 pk = x1_pack(o);
+          uint4 pk;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+          pk.x = E::pack2(vv[0], vv[1]);
+          pk.y = E::pack2(vv[2], vv[3]);
+          pk.z = E::pack2(vv[4], vv[5]);
+          pk.w = E::pack2(vv[6], vv[7]);
+          uint16_t o[8];
+          unpack8(pk, o);
           x1_st16(rdz, eoff(t, s, j, p, false) * 2u, u32x4v{pk.x, pk.y, pk.z, pk.w});  // rows past M: dropped
           if (m < M) {
             const int cl = wave * C::WCH + p * 32 + 8 * fq;  // slice-local channel

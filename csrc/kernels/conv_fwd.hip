@@ -260,12 +260,11 @@ PDT_DEVICE void conv_epilogue(const ConvFwdArgs& a, f32x4_t (&acc)[FN][FM], int6
           y2[0] = E::to_f((uint16_t)(q2.x & 0xffff)); y2[1] = E::to_f((uint16_t)(q2.x >> 16));
           y2[2] = E::to_f((uint16_t)(q2.y & 0xffff)); y2[3] = E::to_f((uint16_t)(q2.y >> 16));
         }
-        uint16_t ov[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ov[r] = E::from_f(v[r]);
-        uint2 packed;
-        packed.x = (uint32_t)ov[0] | ((uint32_t)ov[1] << 16);
-        packed.y = (uint32_t)ov[2] | ((uint32_t)ov[3] << 16);
+        uint2 packed;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+        packed.x = E::pack2(v[0], v[1]);
+        packed.y = E::pack2(v[2], v[3]);
+        const uint16_t ov[4] = {(uint16_t)packed.x, (uint16_t)(packed.x >> 16), (uint16_t)packed.y,
+                                (uint16_t)(packed.y >> 16)};
         if (CAN_STAGE && stage) {
           if constexpr (PERM) {  // 16 B per pair: a pixel's 4 fq lanes write 64 contiguous bytes
             if (i & 1)

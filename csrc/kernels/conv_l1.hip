@@ -303,12 +303,11 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
             if (!(mb & 8u)) v[3] = 0.f;
           }
         }
-        uint16_t o[4];
-#pragma unroll
-        for (int r2 = 0; r2 < 4; ++r2) o[r2] = E::from_f(v[r2]);
-        uint2 packed;
-        packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-        packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        uint2 packed;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+        packed.x = E::pack2(v[0], v[1]);
+        packed.y = E::pack2(v[2], v[3]);
+        const uint16_t o[4] = {(uint16_t)packed.x, (uint16_t)(packed.x >> 16), (uint16_t)packed.y,
+                               (uint16_t)(packed.y >> 16)};
         *(uint2*)(a.y + obase[j] + c0) = packed;
         if constexpr (EPI == 1) {
 #pragma unroll
@@ -607,14 +606,13 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
             if (!((mb >> e) & 1u)) v[e] = 0.f;
         }
       }
+      uint4 packed;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+      packed.x = E::pack2(v[0], v[1]);
+      packed.y = E::pack2(v[2], v[3]);
+      packed.z = E::pack2(v[4], v[5]);
+      packed.w = E::pack2(v[6], v[7]);
       uint16_t o[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = E::from_f(v[e]);
-      uint4 packed;
-      packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-      packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-      packed.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
-      packed.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+      unpack8(packed, o);
       if constexpr (HOLD)
         held[jo] = packed;
       else

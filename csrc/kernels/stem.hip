@@ -159,14 +159,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (ow < a.Q) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {  // channels 16*fq + 8h .. +7 = fragments 2h, 2h+1
+            uint4 pk;  // one v_cvt_pk_bf16_f32 per pair (E16::pack2)
+            pk.x = E::pack2(acc[2 * h][g][0], acc[2 * h][g][1]);
+            pk.y = E::pack2(acc[2 * h][g][2], acc[2 * h][g][3]);
+            pk.z = E::pack2(acc[2 * h + 1][g][0], acc[2 * h + 1][g][1]);
+            pk.w = E::pack2(acc[2 * h + 1][g][2], acc[2 * h + 1][g][3]);
             uint16_t o[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = E::from_f(acc[2 * h + (e >> 2)][g][e & 3]);
-            uint4 pk;
-            pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-            pk.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-            pk.z = (uint32_t)o[4] | ((uint32_t)o[5] << 16);
-            pk.w = (uint32_t)o[6] | ((uint32_t)o[7] << 16);
+            unpack8(pk, o);
             *(uint4*)(yrow + (int64_t)ow * kCout + 8 * h) = pk;
             if constexpr (STATS) {
 #pragma unroll
