@@ -855,27 +855,56 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * a.W * a.cs * 2u);
   const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.P * a.Kout * 2u);
 
-  // DMA lane geometry: 4 rows x 16 chunks per 1 KiB instruction
+  // ---- DMA (incremental source offsets, as the wide kernel): this wave stages pixel rows 16 wave + 4 j + lrow (j < 4)
+  // of the K-step, lane chunk lch_j = pch ^ tr_swz16(row) (PAIR: column half h_j = lch_j >> 3 -> tap)
   const int lrow = lane >> 4, pch = lane & 15;
-
-  auto stage_load = [&](int step, int buf) {
-    const int pbase = pix_begin + step * BKP;
+  const int sh = a.stride_h, sw = a.stride_w, Qm = a.Qm, Pm = a.Pm, W = a.W, H = a.H, cs = a.cs;
+  const int adv_i = BKP / Qm, adv_j = BKP - adv_i * Qm;
+  const int toff0 = (th2[0] * W + tw2[0]) * cs, toff1 = (th2[1] * W + tw2[1]) * cs;
+  int xi, xj, ih, iw, xo;  // grid position of pixel p0 = pix_begin + step * BKP + 16 wave + lrow, tap-less input
+  {
+    const FastDiv dpq{a.div_pq_mul, a.div_pq_shift}, dq{a.div_q_mul, a.div_q_shift};
+    const int p0 = pix_begin + 16 * wave + lrow;
+    const int n = (int)fdiv((uint32_t)p0, dpq);
+    const int rem = p0 - n * Pm * Qm;
+    xi = (int)fdiv((uint32_t)rem, dq);
+    xj = rem - xi * Qm;
+    ih = xi * sh;
+    iw = xj * sw;
+    xo = ((n * H + ih) * W + iw) * cs;
+  }
+  const int row_step = (sh * W - Qm * sw) * cs, img_step = (H - Pm * sh) * W * cs;
+  int ycur = ((pix_begin + 16 * wave + lrow) * a.Kout + k0) * 2;
+  // +4 pixels with at most one row wrap (Qm >= 4, the launcher's condition) and one image wrap, branch-free
+  auto step4 = [&](int& i, int& jq, int& hh, int& ww, int& o) {
+    jq += 4; ww += 4 * sw; o += 4 * sw * cs;
+    const bool wr = jq >= Qm;
+    jq -= wr ? Qm : 0; ww -= wr ? Qm * sw : 0; hh += wr ? sh : 0; o += wr ? row_step : 0; i += wr ? 1 : 0;
+    const bool wi = i >= Pm;
+    i -= wi ? Pm : 0; hh -= wi ? Pm * sh : 0; o += wi ? img_step : 0;
+  };
+  auto stage_load = [&](int buf) {  // the next K-step in sequence (advances the lane state)
     char* sb = smem + buf * STAGE;
+    int i = xi, jq = xj, hh = ih, ww = iw, o = xo;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int row = (wave * 4 + j) * 4 + lrow;  // 0..63
-      const int lch = pch ^ tr_swz16(row);
-      uint32_t xo, yo;
-      if constexpr (PAIR) {
-        const int h = lch >> 3;  // column half -> tap; channel (lch & 7) * 8 of that tap
-        wgrad_rows<false>(a, pbase + row, th2[h], tw2[h], -h * 64, lch, k0, xo, yo);
-        if (h && !half1_live) xo = kOOB;
-      } else {
-        wgrad_rows<false>(a, pbase + row, th2[0], tw2[0], c0, lch, k0, xo, yo);
-      }
-      buf_lds16_asm(rx, sb + (wave * 4 + j) * 1024, xo);
-      buf_lds16_asm(ry, sb + XB + (wave * 4 + j) * 1024, yo);
+      if (j > 0) step4(i, jq, hh, ww, o);
+      const int lch = pch ^ ((lrow << 1) | (((j >> 1) & 1) << 3));
+      const int h = PAIR ? lch >> 3 : 0;
+      const int th = h ? th2[1] : th2[0], tw = h ? tw2[1] : tw2[0];
+      // (bitwise &: a short-circuit && compiles to divergent branches around each DMA's offset)
+      const bool ok = ((unsigned)(hh + th) < (unsigned)H) & ((unsigned)(ww + tw) < (unsigned)W) &
+                      (!PAIR || !h || half1_live);
+      const int col = (PAIR ? -h * 64 : c0) + lch * 8;
+      const uint32_t xoff = ok ? (uint32_t)((o + (h ? toff1 : toff0) + col) * 2) : kOOB;
+      buf_lds16_asm(rx, sb + (wave * 4 + j) * 1024, xoff);
+      buf_lds16_asm(ry, sb + XB + (wave * 4 + j) * 1024, (uint32_t)(ycur + (j * 4 * a.Kout + lch * 8) * 2));
     }
+    ycur += BKP * a.Kout * 2;
+    xj += adv_j; iw += adv_j * sw; xo += adv_j * sw * cs;
+    xi += adv_i; ih += adv_i * sh; xo += adv_i * sh * W * cs;
+    if (xj >= Qm) { xj -= Qm; iw -= Qm * sw; ih += sh; xo += row_step; ++xi; }
+    while (xi >= Pm) { xi -= Pm; ih -= Pm * sh; xo += img_step; }
   };
 
   f32x4_t acc[4][4];
@@ -885,12 +914,18 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
-  // per-fragment byte offsets (row-independent part): column chunk and 8-byte half
-  int ccol[4], kcol[4];
+  // fragment byte addresses (stage 0, kk 0; tr_swz16 of rows kk * 32 + 8 g + q (+4) does not depend on kk): a stage /
+  // kk shift is an immediate
+  int xa[4][2], ya[4][2];
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
-    ccol[f] = wc * 64 + f * 16 + 4 * p4;
-    kcol[f] = wk * 64 + f * 16 + 4 * p4;
+    const int cc = wc * 64 + f * 16 + 4 * p4, kc = wk * 64 + f * 16 + 4 * p4;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int rr = 8 * g + q + 4 * r, sz = tr_swz16(rr);
+      xa[f][r] = rr * ROWB + (((cc >> 3) ^ sz) << 4) + (cc & 7) * 2;
+      ya[f][r] = XB + rr * ROWB + (((kc >> 3) ^ sz) << 4) + (kc & 7) * 2;
+    }
   }
 
   float psc[4], psh[4];
@@ -903,48 +938,47 @@ __global__ __launch_bounds__(256) void conv_wgrad128_kernel(ConvWgradArgs a) {
     }
   }
 
-  if (nsteps > 0) {
-    stage_load(0, 0);
+  auto kstep = [&](auto stc, int s) {
+    constexpr int ST = decltype(stc)::value;  // ring buffer of K-step s (s & 1)
+    if (s + 1 < nsteps) stage_load(ST ^ 1);
+#pragma unroll
+    for (int kk = 0; kk < BKP / 32; ++kk) {
+      const int so = ST * STAGE + kk * 32 * ROWB;
+      vec8 af[4], bfr[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + xa[f][0] + so));
+        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + xa[f][1] + so));
+        af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        if constexpr (PRE) {
+          float sc8[8], sh8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { sc8[e] = psc[f]; sh8[e] = psh[f]; }
+          af[f] = __builtin_bit_cast(vec8, pre_act8<DT>(__builtin_bit_cast(uint4, af[f]), sc8, sh8));
+        }
+        lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + ya[f][0] + so));
+        hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + ya[f][1] + so));
+        bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      if (wc == 0 || half1_live) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < nsteps) stage_load(s + 1, cur ^ 1);
-      const char* sb = smem + cur * STAGE;
-#pragma unroll
-      for (int kk = 0; kk < BKP / 32; ++kk) {
-        const int r0 = kk * 32 + 8 * g + q, r1 = r0 + 4;
-        const int sw0 = tr_swz16(r0), sw1 = tr_swz16(r1);
-        vec8 af[4], bfr[4];
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          const int cc = ccol[f], kc = kcol[f];
-          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)(sb + r0 * ROWB + (((cc >> 3) ^ sw0) << 4) + (cc & 7) * 2));
-          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)(sb + r1 * ROWB + (((cc >> 3) ^ sw1) << 4) + (cc & 7) * 2));
-          af[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          if constexpr (PRE) {
-            float sc8[8], sh8[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { sc8[e] = psc[f]; sh8[e] = psh[f]; }
-            af[f] = __builtin_bit_cast(vec8, pre_act8<DT>(__builtin_bit_cast(uint4, af[f]), sc8, sh8));
-          }
-          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)(sb + XB + r0 * ROWB + (((kc >> 3) ^ sw0) << 4) + (kc & 7) * 2));
-          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)(sb + XB + r1 * ROWB + (((kc >> 3) ^ sw1) << 4) + (kc & 7) * 2));
-          bfr[f] = __builtin_bit_cast(vec8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-        if (wc == 0 || half1_live) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = E::mfma16x16x32(af[i], bfr[j], acc[i][j]);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+  };
+
+  if (nsteps > 0) {
+    stage_load(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // unrolled over the 2 ring buffers: every buffer offset is a compile-time immediate
+    for (int s = 0; s < nsteps; s += 2) {
+      kstep(std::integral_constant<int, 0>{}, s);
+      if (s + 1 < nsteps) kstep(std::integral_constant<int, 1>{}, s + 1);
     }
   }
   if (wc == 1 && !half1_live) return;
@@ -1054,13 +1088,13 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
     xo = ((n * H + xh) * W + xw) * cs;
   }
   const int row_step = (sh * W - Qm * sw) * cs, img_step = (H - Pm * sh) * W * cs;
-  // one grid-column step of d pixels with at most one row wrap (d < Qm) and one image wrap
+  // one grid-column step of d pixels with at most one row wrap (d < Qm) and one image wrap, branch-free
   auto step_px = [&](int& i, int& j, int& h, int& w, int& o, int d) {
     j += d; w += d * sw; o += d * sw * cs;
-    if (j >= Qm) {
-      j -= Qm; w -= Qm * sw; h += sh; o += row_step; ++i;
-      if (i >= Pm) { i -= Pm; h -= Pm * sh; o += img_step; }
-    }
+    const bool wr = j >= Qm;
+    j -= wr ? Qm : 0; w -= wr ? Qm * sw : 0; h += wr ? sh : 0; o += wr ? row_step : 0; i += wr ? 1 : 0;
+    const bool wi = i >= Pm;
+    i -= wi ? Pm : 0; h -= wi ? Pm * sh : 0; o += wi ? img_step : 0;
   };
   int ycur;  // dY byte offset of this lane's j = 0 row for the next K-step to stage
   const int ystr = a.ldy ? a.ldy : a.Kout;
@@ -1075,7 +1109,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_wide_kernel(ConvWgradArgs a) {
     for (int jj = 0; jj < 4; ++jj) {
       if (jj > 0) step_px(i, j, h, w, o, 4);
       const int lch = pch ^ ((lrow << 1) | (((jj >> 1) & 1) << 3));
-      const bool ok = x_live && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const bool ok = x_live & ((unsigned)h < (unsigned)H) & ((unsigned)w < (unsigned)W);  // (no short-circuit branch)
       const uint32_t off = ok ? (uint32_t)((o + xcolb + lch * 8) * 2) : kOOB;
       buf_lds16_asm(rx, smem + (3 * hx + buf) * SUB + (4 * (wave & 3) + jj) * 1024, off);
     }
@@ -1723,6 +1757,12 @@ void conv_wgrad_launch(const ConvWgradArgs& args, int dtype, hipStream_t s) {
   // the wide kernel's incremental DMA addressing steps 4 grid columns with one row wrap: narrower outputs run the
   // 128 x 128 tile (same split plan and partial layout)
   if (a.tile == kWgradWide && a.Qm < 4) a.tile = 128;
+  if (a.tile == 128 && a.Qm < 4) {  // (the 128 x 128 kernel steps 4 grid columns the same way)
+    if (a.pre_coef)
+      pdt_hip_fail("conv_wgrad: a fused producer BN needs an output at least 4 pixels wide", hipErrorInvalidValue,
+                   __FILE__, __LINE__);
+    a.tile = 64;
+  }
   const int nwg = (a.Kout / wgrad_ktile(a)) * wgrad_ctiles(a) * a.splits;
   if (nwg == 0) return;
   const FastDiv dpq = make_fastdiv((uint32_t)(a.Pm * a.Qm)), dq = make_fastdiv((uint32_t)a.Qm);

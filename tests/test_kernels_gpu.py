@@ -81,7 +81,8 @@ def test_conv_wgrad(case, dtype):
 
 
 @pytest.mark.parametrize("case", [(2, 15, 13, 64, 256, 3, 2, 1), (4, 14, 14, 64, 128, 3, 1, 1),
-                                  (3, 14, 14, 64, 128, 1, 2, 0), (2, 9, 9, 64, 384, 1, 1, 0)])
+                                  (3, 14, 14, 64, 128, 1, 2, 0), (2, 9, 9, 64, 384, 1, 1, 0),
+                                  (2, 28, 28, 64, 128, 3, 2, 1), (3, 6, 6, 64, 128, 3, 2, 1)])
 @pytest.mark.parametrize("target", [64, 2048])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_conv_wgrad_two_tap_pair_tile(case, target, dtype):
