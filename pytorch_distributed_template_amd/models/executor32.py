@@ -34,8 +34,9 @@ STEM_K = 192  # im2col width of the 7x7x3 stem (147 columns, zero padded to a mu
 
 
 def fp32_supported(model) -> bool:
-    """Models this executor runs: torchvision-layout ResNets without grouped convolutions."""
-    return isinstance(model, ResNet) and model.groups == 1
+    """Models this executor runs: torchvision-layout ResNets, Wide-ResNets and ResNeXts (grouped convs as 64-channel
+    slices, as the 16-bit executor)."""
+    return isinstance(model, ResNet)
 
 
 class ResNetExecutor32(ResNetExecutor):
@@ -46,7 +47,7 @@ class ResNetExecutor32(ResNetExecutor):
                  syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0,
                  wgrad_blocks: int = 2048):
         if not fp32_supported(model):
-            raise NotImplementedError("native fp32 executor supports torchvision-style ResNets with groups=1")
+            raise NotImplementedError("native fp32 executor supports torchvision-style ResNets / ResNeXts")
         self.C = native.C
         self.n_slots = self.C.stat_slots()
         self.model = model
@@ -75,9 +76,10 @@ class ResNetExecutor32(ResNetExecutor):
         self.std = torch.tensor(IMAGENET_STD, device=self.device).view(1, 3, 1, 1)
         derived_maps: List[torch.Tensor] = []
         off = [0]
+        gfwd_maps: list = []  # forward layouts of the grouped convs' 64-channel slices
 
         def conv(c):
-            return _Conv(c, flat, derived_maps, off)
+            return _Conv(c, flat, derived_maps, off, gfwd_maps)
 
         st = model.conv1
         assert st.in_channels * st.kernel_size[0] * st.kernel_size[1] <= STEM_K, "stem too wide for the im2col GEMM"
@@ -93,6 +95,10 @@ class ResNetExecutor32(ResNetExecutor):
                      "ds_conv": conv(blk.downsample[0]) if blk.downsample is not None else None,
                      "ds_bn": _BN(blk.downsample[1], flat, self.device) if blk.downsample is not None else None}
                 self.blocks.append(d)
+        for gc, j, gm in gfwd_maps:  # (one gather refreshes every layout: their order is free)
+            gc.gfwd.append(off[0])
+            derived_maps.append(gm)
+            off[0] += gm.numel()
         # stem weight as a [64][STEM_K] GEMM operand (KRSC flattening == im2col column order), zero padded
         s = self.stem
         kk = s.R * s.S * s.cin
@@ -141,6 +147,10 @@ class ResNetExecutor32(ResNetExecutor):
         off[0] += mt.numel()
         self.derived_idx = torch.cat([x.to(torch.int32) for x in derived_maps]).to(self.device)
         self.derived = torch.zeros(off[0], dtype=torch.float32, device=self.device)
+        for b in self.blocks:
+            for c in b["convs"]:
+                if c.groups > 1:
+                    c.gidx = c.gidx.to(self.device)
         self._bufs = {}
         self._plans = {}
         self._tiles = {}
@@ -186,7 +196,57 @@ class ResNetExecutor32(ResNetExecutor):
     def _tile32c(self, kind: str, c: _Conv, N: int, H: int, n: int, m: int):
         return self._TUNED32.get((kind, N, H, c.cin, c.cout, c.R, c.st)) or self._tile32(n, m)
 
+    # Grouped convs (ResNeXt) in fp32: the 16-bit executor's 64-channel slices with block-diagonal weights (_Conv
+    # _init_grouped), each slice gathered into a dense [pixels][64] operand and run on the dense fp32 kernels; outputs,
+    # statistics columns and the weight gradient's diagonal blocks are scattered back.  (The reference precision path:
+    # MIOpen's fp16 grouped conv ran this model at 1239 ms per step, so even the gather copies are far ahead.)
+    def _slice(self, key, t, rows: int, width: int, j: int):
+        """Dense copy of channel slice j of a [rows][width] tensor."""
+        s = self._buf(key, rows * self._GS, torch.float32)
+        s.view(rows, self._GS).copy_(t.view(rows, width)[:, j * self._GS:(j + 1) * self._GS])
+        return s
+
+    _GS = _Conv.GSLICE
+
+    def _gconv_fwd32(self, c: _Conv, x, N, H, W, y, stats: bool):
+        P, Q, S_ = *c.out_hw(H, W), self._GS
+        sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
+        ys = self._buf("g32_y", N * P * Q * S_, torch.float32)
+        sps = self._buf("g32_st", self.n_slots * S_ * 2, torch.float64) if stats else None
+        n = S_ * c.R * c.S * S_
+        tile = self._tile32(S_, N * P * Q)
+        for j in range(c.nslice):
+            xs = self._slice("g32_x", x, N * H * W, c.cin, j)
+            self.C.conv32_fwd(xs, self.derived[c.gfwd[j]:c.gfwd[j] + n], ys, None, sps, N, H, W, S_, S_, c.R, c.S, P,
+                              Q, c.st, c.pad, *tile)
+            y.view(N * P * Q, c.cout)[:, j * S_:(j + 1) * S_].copy_(ys.view(-1, S_))
+            if stats:
+                sp.view(self.n_slots, c.cout, 2)[:, j * S_:(j + 1) * S_].copy_(sps.view(self.n_slots, S_, 2))
+        return P, Q, sp
+
+    def _gdgrad32(self, c: _Conv, dy, N, H, W, P, Q, dx):
+        S_ = self._GS
+        dxs = self._buf("g32_dx", N * H * W * S_, torch.float32)
+        tile = self._tile32(S_, N * P * Q)
+        for j in range(c.nslice):
+            dys = self._slice("g32_dy", dy, N * P * Q, c.cout, j)
+            phases = [p for p in c.gphases[j] if H - p[0] > 0 and W - p[1] > 0]
+            self.C.conv32_dgrad(dys, self.derived, dxs, None, N, P, Q, S_, S_, H, W, c.st, phases, *tile)
+            dx.view(N * H * W, c.cin)[:, j * S_:(j + 1) * S_].copy_(dxs.view(-1, S_))
+
+    def _gwgrad32(self, c: _Conv, x, dy, N, H, W, P, Q):
+        S_ = self._GS
+        ldw = c.R * c.S * S_
+        tmp = self._buf("g32_dw", c.nslice * S_ * ldw, torch.float32)
+        for j in range(c.nslice):
+            xs = self._slice("g32_x", x, N * H * W, c.cin, j)
+            dys = self._slice("g32_dy", dy, N * P * Q, c.cout, j)
+            self._wgrad(S_, xs, dys, N, H, W, S_, c.R, c.S, P, Q, c.st, c.pad, tmp[j * S_ * ldw:(j + 1) * S_ * ldw], ldw)
+        self.C.gather32(tmp, c.gidx, self._g(c.slot))  # the diagonal blocks = the grouped weight gradient
+
     def _conv_fwd(self, c: _Conv, x, N, H, W, y, stats: bool):
+        if c.groups > 1:
+            return self._gconv_fwd32(c, x, N, H, W, y, stats)
         P, Q = c.out_hw(H, W)
         sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
         tile = self._tile32c("fwd", c, N, H, c.cout, N * P * Q)
@@ -445,13 +505,20 @@ class ResNetExecutor32(ResNetExecutor):
                 c = convs[ci]
                 h, w, P, Q = rec["hw"][ci]
                 xin = rec["as"][ci - 1] if ci > 0 else x
-                self._wgrad(c.cout, xin, dy, N, h, w, c.cin, c.R, c.S, P, Q, c.st, c.pad, self._g(c.slot),
-                            c.R * c.S * c.cin)
+                if c.groups > 1:
+                    self._gwgrad32(c, xin, dy, N, h, w, P, Q)
+                else:
+                    self._wgrad(c.cout, xin, dy, N, h, w, c.cin, c.R, c.S, P, Q, c.st, c.pad, self._g(c.slot),
+                                c.R * c.S * c.cin)
                 self.grad_ready(c.pid)
                 if ci > 0:
                     da = self._buf("da", N * h * w * c.cin, torch.float32)
                     bnp, yp, ap = bns[ci - 1], rec["ys"][ci - 1], rec["as"][ci - 1]
-                    if self._FUSE_BN:  # dgrad epilogue writes dz and reduces the inner BN's backward sums (ReLU
+                    if c.groups > 1:  # grouped (a block-internal conv): slice dgrads, then the separate BN reduce
+                        self._gdgrad32(c, dy, N, h, w, P, Q, da)
+                        self.bn_reduce(bnp, da, ap, yp, N * h * w)
+                        mref = ap
+                    elif self._FUSE_BN:  # dgrad epilogue writes dz and reduces the inner BN's backward sums (ReLU
                         # mask from ap)
                         slots = self._buf(("bnslots", c.cin, 2), self.n_slots * c.cin * 2, torch.float64)
                         self._dgrad(c, dy, N, h, w, P, Q, da, bnb=(ap, yp, bnp.coef, slots))

@@ -132,8 +132,8 @@ def test_dp_fp32_eval_equals_executor32(device_ids):
 
 def test_dp_resnext_default_eval_precision_builds_and_runs():
     """native DataParallel of a grouped-conv model with the default eval precision (fp32 validation
-    requested) must build and validate -- fp32 validation falls back to the compute dtype where the fp32 executor
-    has no kernels, instead of raising at construction."""
+    requested) must build and validate (round 6: the fp32 executor runs grouped convs too, so the fp32 evaluation
+    executor is built; a model it cannot run falls back to the compute dtype instead of raising)."""
     import warnings
     from pytorch_distributed_template_amd.models import registry
     from pytorch_distributed_template_amd.models.executor32 import fp32_supported

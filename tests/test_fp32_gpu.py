@@ -129,7 +129,8 @@ def _setup(arch, N, HW, seed=0):
                                              ("resnet50", 4, 64, None), ("resnet18", 6, 224, 4),
                                              ("resnet34", 4, 128, None), ("resnet101", 2, 128, None),
                                              ("resnet152", 2, 128, None), ("wide_resnet50_2", 2, 128, None),
-                                             ("wide_resnet101_2", 2, 128, None)])
+                                             ("wide_resnet101_2", 2, 128, None), ("resnext50_32x4d", 2, 128, None),
+                                             ("resnext101_64x4d", 2, 96, None)])
 def test_executor32_train_step_matches_torch_fp32(arch, N, HW, chunk):
     """The whole fp32 step vs an fp64 PyTorch oracle, judged against PyTorch's own fp32 autograd: logits, loss,
     every gradient and the running statistics must be no worse than torch fp32 (+ a small absolute floor) --
@@ -137,7 +138,8 @@ def test_executor32_train_step_matches_torch_fp32(arch, N, HW, chunk):
     would be meaningless.  (ResNet-50 at 64 px, i.e. BatchNorm over 4 x 2 x 2 = 16 values per channel in
     layer4, is ill-conditioned enough that a single ReLU-mask flip of a near-zero pre-activation in the last
     block moves that block's gradients by ~1 % (round-4 fp64 comparison).  128 px keeps the comparison meaningful.)
-    (chunk: the im2col stem processed in several image chunks.)"""
+    (chunk: the im2col stem processed in several image chunks.)  ResNeXts: grouped convs as gathered 64-channel
+    slices on the dense fp32 kernels."""
     model, ref, flat, ex, x, t = _setup(arch, N, HW)
     if chunk:
         ex._stem_chunk = lambda n: chunk
