@@ -1028,6 +1028,29 @@ void conv_fwd_launch(const ConvFwdArgs& a, int dtype, int bm, int bn, int bk, hi
     return !(e && e[0] == '0');
   }();
   int flip = 0;
+  if (l1_on && a.nslice > 1) {
+    // grouped conv, every slice in one call: slices of the layer1 geometry (ResNeXt stage 1) run one halo-kernel
+    // launch each (its persistent grid already fills the GPU), with the slice offsets of conv_fwd_kernel's nslice path
+    ConvFwdArgs b = a;
+    b.nslice = 0;
+    if (conv_l1_eligible(b, &flip)) {
+      if (b.nphase > 0)
+        PDT_COUNT("conv_l1_dgrad");
+      else
+        PDT_COUNT("conv_l1_fwd");
+      const int KO = a.bnb == 3 ? 4 : 2;
+      for (int sl = 0; sl < a.nslice; ++sl) {
+        b.x = a.x + (int64_t)sl * a.Kout;
+        b.y = a.y + (int64_t)sl * a.Kout;
+        b.w = a.w + (int64_t)sl * a.slice_wstride;
+        b.bn_y1 = a.bn_y1 ? a.bn_y1 + (int64_t)sl * a.Kout : nullptr;
+        b.bn_coef1 = a.bn_coef1 ? a.bn_coef1 + sl * a.Kout : nullptr;
+        b.stats = a.stats ? a.stats + (int64_t)sl * a.Kout * KO : nullptr;
+        conv_l1_launch(b, flip, dtype, s);
+      }
+      return;
+    }
+  }
   if (l1_on && conv_l1_eligible(a, &flip)) {
     if (a.nphase > 0)
       PDT_COUNT("conv_l1_dgrad");

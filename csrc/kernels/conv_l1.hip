@@ -376,8 +376,12 @@ __global__ __launch_bounds__(256) void conv_l1_kernel(ConvFwdArgs a, int flip) {
 // transforms exactly the halo chunks it DMA'd itself, so no extra barrier is needed before the next
 // compute phase's barrier.  Work split inside a group: 2 (32 output channels) x 2 (7 pixel groups) --
 // balanced, 14 MFMAs per 9 LDS reads per K-step.
-template <int DT, int EPI, bool RES, bool PRE, bool FLIP>
+// SL: a 64-channel slice of wider tensors (grouped convs, ResNeXt stage 1): input pixel stride a.cs, output / BN-input
+// pixel stride a.ldy, BN coefficient quantity stride a.coef_ld (forward with statistics and backward data with the
+// inner-BN reduce only: no residual, no producer BN)
+template <int DT, int EPI, bool RES, bool PRE, bool FLIP, bool SL = false>
 __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
+  static_assert(!SL || (!RES && !PRE && EPI <= 2), "sliced layer1 kernel: EPI 0-2 without residual / producer BN");
   using E = E16<DT>;
   typedef typename E::vec8 vec8;
   constexpr int NJ = 7;  // pixel groups per wave
@@ -401,8 +405,9 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
   const int first = t_begin + lb;
   const int nk = first < t_end ? (t_end - first + per_x - 1) / per_x : 0;  // this block's tiles (block-uniform)
 
-  const uint32_t img_bytes = (uint32_t)a.N * a.H * kW * 128u;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, img_bytes);
+  const int xcs = SL ? a.cs : 64, ldo = SL ? a.ldy : 64;  // pixel strides (elements) of x / of y, res, bn_y1
+  const uint32_t img_bytes = (uint32_t)a.N * a.H * kW * (uint32_t)ldo * 2u;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * kW * (uint32_t)xcs * 2u);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, (uint32_t)kWB);
   const __amdgpu_buffer_rsrc_t ry1 = make_rsrc(EPI >= 2 ? a.bn_y1 : a.x, img_bytes);
   const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? a.res : a.x, img_bytes);
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
         const int h = h0 - 1 + hr, w = wc - 1;
         const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kW;
         buf_lds16_asm(rx, sbuf + ii * 1024,
-                      ok ? (uint32_t)((((n * a.H + h) * kW + w) * 64 + (pch ^ (wc & 7)) * 8) * 2) : kOOB);
+                      ok ? (uint32_t)((((n * a.H + h) * kW + w) * xcs + (pch ^ (wc & 7)) * 8) * 2) : kOOB);
       }
     }
     asm volatile("" ::: "memory");  // no later store may be scheduled ahead of the DMA (counted waits below)
@@ -498,8 +503,8 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
       for (int k = 0; k < KS; ++k) sacc[i][r][k] = 0.f;
 
   float* const cfl = (float*)(smem + kLds);
-  if constexpr (EPI >= 2) {
-    if (tid < 256) cfl[tid] = a.bn_coef1[tid];  // published by the prologue barrier
+  if constexpr (EPI >= 2) {  // published by the prologue barrier
+    if (tid < 256) cfl[tid] = a.bn_coef1[SL ? (tid >> 6) * a.coef_ld + (tid & 63) : tid];
   }
   if constexpr (PRE) {
     if (tid < 128) cfl[tid] = a.pre_coef[tid];  // scale[64] | shift[64]
@@ -518,12 +523,12 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
   constexpr int NJO = EPI == 3 ? 4 : NJ;
   u32x4v pre_res[RES ? NJO : 1], pre_y1[EPI >= 2 ? NJO : 1];
   u32x2v pre_m[EPI == 3 ? NJO : 1];
-  // a tile's 4 x 56 output pixels are one contiguous block: pixel px of tile t is element (t's first pixel + px) * 64
-  const int lpx0 = pix_of_lane(fr) * 64;
+  // a tile's 4 x 56 output pixels are one contiguous block: pixel px of tile t is element (t's first pixel + px) * ldo
+  const int lpx0 = pix_of_lane(fr) * ldo;
   int lpx = lpx0;  // re-opaqued per use site (see stage_tile)
   auto obase_of = [&](int t, int j) {
     const int n = t / TH, h0 = (t - n * TH) * 4;
-    return (int64_t)(n * a.H + h0) * (kW * 64) + (lpx + (wm * NJ + j) * 1024);
+    return (int64_t)(n * a.H + h0) * (kW * ldo) + (lpx + (wm * NJ + j) * 16 * ldo);
   };
 
   auto compute = [&](int t) {
@@ -661,13 +666,13 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
     constexpr int J0 = decltype(J0c)::value, J1 = decltype(J1c)::value;
     (void)pre_m; (void)rmask; (void)pre_res; (void)rres; (void)pre_y1; (void)ry1;  // (generic lambda: capture them)
     const int n = t / TH, h0 = (t - n * TH) * 4;
-    const uint32_t tb = (uint32_t)(n * a.H + h0) * (kW * 64u);  // tile's first element (< 2^31: 4 GB tensors)
+    const uint32_t tb = (uint32_t)(n * a.H + h0) * (kW * (uint32_t)ldo);  // tile's first element (< 2^31: 4 GB)
     lpx = lpx0;
     asm volatile("" : "+v"(lpx));
 #pragma unroll
     for (int j = J0; j < J1; ++j) {
       const int jo = j - J0;
-      const uint32_t e = tb + (uint32_t)(lpx + (wm * NJ + j) * 1024);
+      const uint32_t e = tb + (uint32_t)(lpx + (wm * NJ + j) * 16 * ldo);
       const uint32_t yo = (e + wn * 32 + 8 * fq) * 2u;
       if constexpr (RES)
         asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(pre_res[jo]) : "v"(yo), "s"(rres));
@@ -796,10 +801,30 @@ __global__ __launch_bounds__(512) void conv_l1pp_kernel(ConvFwdArgs a) {
   }
 }
 
+static int g_conv_l1_pp = -1;  // -1: PDT_CONV_L1_PP decides; 0 / 1: set by conv_l1_set_pp (tests, A/B)
+// PDT_CONV_L1_PP=0: the 4-wave kernel everywhere (A/B)
+static bool conv_l1_pp_on() {
+  static const bool pp_env = [] {
+    const char* e = getenv("PDT_CONV_L1_PP");
+    return !(e && e[0] == '0');
+  }();
+  return g_conv_l1_pp >= 0 ? g_conv_l1_pp != 0 : pp_env;
+}
+
+// strided operands (a channel slice of a grouped conv's wider tensors)
+static bool conv_l1_sliced(const ConvFwdArgs& a) {
+  return a.cs != 64 || (a.ldy && a.ldy != 64) || (a.coef_ld && a.coef_ld != 64) || a.stats_ld;
+}
+
 bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
   // H % 4 == 0: whole 4-row tiles only (the epilogue has no per-pixel range checks; see conv_l1_kernel)
-  if (a.C != 64 || a.Kout != 64 || a.cs != 64 || a.W != kW || a.OW != kW || a.bnb == 3 || a.H % 4 != 0) return false;
-  if ((a.ldy && a.ldy != a.Kout) || (a.coef_ld && a.coef_ld != a.Kout) || a.stats_ld) return false;  // slices
+  if (a.C != 64 || a.Kout != 64 || a.W != kW || a.OW != kW || a.bnb == 3 || a.H % 4 != 0) return false;
+  if (conv_l1_sliced(a)) {
+    // a 64-channel slice of wider tensors (grouped convs): the 8-wave kernel's SL form -- forward (with or without
+    // statistics) or backward data (with or without the inner-BN reduce), no residual / producer BN
+    if (!conv_l1_pp_on() || a.res || a.pre_coef || a.nslice > 1 || a.bnb > 1) return false;
+    if (a.cs % 8 != 0 || a.ldy % 8 != 0 || a.cs < 64 || a.ldy < 64) return false;
+  }
   if (a.nphase == 0) {
     if (a.T == 3 && a.U == 3 && a.ist_h == 1 && a.ist_w == 1 && a.ioff_h == -1 && a.ioff_w == -1 &&
         a.tstep_h == 1 && a.tstep_w == 1 && a.ost_h == 1 && a.ost_w == 1 && a.ooff_h == 0 && a.ooff_w == 0 &&
@@ -819,7 +844,6 @@ bool conv_l1_eligible(const ConvFwdArgs& a, int* flip) {
   return false;
 }
 
-static int g_conv_l1_pp = -1;  // -1: PDT_CONV_L1_PP decides; 0 / 1: set by conv_l1_set_pp (tests, A/B)
 
 int conv_l1_set_pp(int mode) {
   const int old = g_conv_l1_pp;
@@ -843,23 +867,29 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     pdt_hip_fail("conv_l1: the fused producer BN (pre_coef) needs a forward conv with statistics, no residual",
                  hipErrorInvalidValue, __FILE__, __LINE__);
   if (a.pre_coef) PDT_COUNT("conv_l1_fwd_fused_bn_relu");
-  // PDT_CONV_L1_PP=0: the 4-wave kernel everywhere (A/B).  The 8-wave ping-pong kernel takes every variant
-  // except the block-output BN-backward epilogue (EPI 3: residual + BN input + ReLU mask operands do not fit
-  // its 256 registers without spilling), which stays on the 4-wave kernel.
-  static const bool pp_env = [] {
-    const char* e = getenv("PDT_CONV_L1_PP");
-    return !(e && e[0] == '0');
-  }();
-  const bool pp_on = g_conv_l1_pp >= 0 ? g_conv_l1_pp != 0 : pp_env;
+  // The 8-wave ping-pong kernel takes every variant except the block-output BN-backward epilogue (EPI 3: residual +
+  // BN input + ReLU mask operands do not fit its 256 registers without spilling), which stays on the 4-wave kernel.
+  const bool pp_on = conv_l1_pp_on();
   const bool pp = pp_on && (epi == 0 || (epi == 1 && !rs && !flip) || (epi == 2 && !rs) || (epi == 3 && rs));
   if (pp) PDT_COUNT("conv_l1_pp");
+  const bool sl = conv_l1_sliced(a);
+  if (sl && !(pp && !rs && !a.pre_coef && epi <= 2))
+    pdt_hip_fail("conv_l1: sliced operands need the 8-wave kernel, EPI 0-2, no residual", hipErrorInvalidValue,
+                 __FILE__, __LINE__);
+  if (sl) PDT_COUNT("conv_l1_sliced");
   Scratch part(a.stats ? (size_t)G * 128 * sizeof(float) : 0, s);
   a.srows = part.as<float>();
   const dim3 grid(G);
 #define PDT_L1OLD(DT_, E_, R_, P_) hipLaunchKernelGGL((conv_l1_kernel<DT_, E_, R_, P_>), grid, dim3(256), 0, s, a, flip)
 #define PDT_L1PP(DT_, E_, R_, P_, F_) hipLaunchKernelGGL((conv_l1pp_kernel<DT_, E_, R_, P_, F_>), grid, dim3(512), 0, s, a)
+#define PDT_L1SL(DT_, E_, F_) hipLaunchKernelGGL((conv_l1pp_kernel<DT_, E_, false, false, F_, true>), grid, dim3(512), 0, s, a)
 #define PDT_L1_DT(DT_)                                                                                   \
-  if (pp) {                                                                                              \
+  if (sl) {                                                                                              \
+    if (epi == 0) { if (flip) PDT_L1SL(DT_, 0, true); else PDT_L1SL(DT_, 0, false); }                    \
+    else if (epi == 1) PDT_L1SL(DT_, 1, false);                                                          \
+    else if (flip) PDT_L1SL(DT_, 2, true);                                                               \
+    else PDT_L1SL(DT_, 2, false);                                                                        \
+  } else if (pp) {                                                                                       \
     if (epi == 0 && !rs) { if (flip) PDT_L1PP(DT_, 0, false, false, true); else PDT_L1PP(DT_, 0, false, false, false); } \
     else if (epi == 0) { if (flip) PDT_L1PP(DT_, 0, true, false, true); else PDT_L1PP(DT_, 0, true, false, false); }    \
     else if (epi == 1) { if (a.pre_coef) PDT_L1PP(DT_, 1, false, true, false); else PDT_L1PP(DT_, 1, false, false, false); } \
@@ -878,9 +908,10 @@ void conv_l1_launch(const ConvFwdArgs& args, int flip, int dtype, hipStream_t s)
     PDT_L1_DT(kF16)
   }
 #undef PDT_L1_DT
+#undef PDT_L1SL
 #undef PDT_L1PP
 #undef PDT_L1OLD
-  if (a.stats) stat_rows_reduce_launch(a.srows, G, 128, a.stats, s);
+  if (a.stats) stat_rows_reduce_launch(a.srows, G, 128, a.stats, s, a.stats_ld);
 }
 
 }  // namespace pdt

@@ -1119,15 +1119,17 @@ def test_conv1x1x_bnb_layer1_matches_c64(mode, cin, NHW):
 
 
 @pytest.mark.parametrize("width,groups,stride,H", [(128, 32, 1, 14), (256, 32, 2, 14), (128, 2, 1, 9),
-                                                   (256, 64, 2, 8)])
+                                                   (256, 64, 2, 8), (128, 32, 1, 56)])
 def test_grouped_conv_slices_match_torch(width, groups, stride, H):
     """ResNeXt grouped 3x3 conv on the channel-slice kernels (gconv_fwd / gconv_dgrad / gconv_wgrad: 64-channel
     slices with block-diagonal weights, strided operands) vs fp32 torch F.conv2d(groups=...): forward with the BN
     statistics of the slices in one buffer, backward data (stride-2: sub-pixel phases) with and without the fused
-    inner-BN reduce, and the weight gradient's diagonal blocks."""
+    inner-BN reduce, and the weight gradient's diagonal blocks.  At 56 x 56, stride 1 (ResNeXt stage 1) the forward
+    and backward data run on the layer1 halo kernel with strided operands (conv_l1pp_kernel SL)."""
     from pytorch_distributed_template_amd.ops import conv, native
     C_ = native.C
     torch.manual_seed(3)
+    C_.reset_dispatch_counts()
     N, W, R, pad, S = 2, H, 3, 1, 64
     cg = width // groups
     P, Q = conv.out_hw(H, W, R, R, stride, pad)
@@ -1224,6 +1226,8 @@ def test_grouped_conv_slices_match_torch(width, groups, stride, H):
     assert torch.equal(y2, y) and torch.equal(st2, st)
     assert torch.equal(dx2, dx) and torch.equal(dz2, dz) and torch.equal(slots2, slots)
     assert torch.equal(dwd2.view(nsl, S, R, R, S), dwd)
+    if H == 56 and stride == 1:  # forward, backward data, backward data with the BN reduce; per slice and all slices
+        assert C_.dispatch_counts().get("conv_l1_sliced", 0) == 6 * nsl, C_.dispatch_counts()
 
 
 @pytest.mark.parametrize("tile", [(256, 64, 64), (128, 128, 64), (256, 128, 64), (256, 256, 64)])
