@@ -705,6 +705,32 @@ int64_t conv_wgrad_3x3c64(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t
   return written;
 }
 
+// grouped conv weight gradient of every 64-channel slice on the layer1 halo kernel (ResNeXt stage 1: 3x3 / s1 / p1,
+// W = 56): partials [parts][nslice][64][576] (returns parts; wgrad_reduce over nslice * 64 rows sums them)
+int64_t gconv_wgrad_l1(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_t H, int64_t W, int64_t width) {
+  const int dt = dt16(x, "x");
+  const int64_t S = kGSlice, nsl = width / S;
+  TORCH_CHECK(dt16(dy, "dy") == dt, "gconv_wgrad_l1: mixed dtypes");
+  TORCH_CHECK(width % S == 0 && pdt::wgrad3x3_c64_supported(64, 64, 3, 3, (int)W, 1, 1, 0), "gconv_wgrad_l1: geometry");
+  TORCH_CHECK(x.numel() == N * H * W * width && dy.numel() == x.numel(), "gconv_wgrad_l1: size mismatch");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 30), "gconv_wgrad_l1: operands exceed 2 GiB (32-bit buffer offsets)");
+  const int blocks = pdt::wgrad3x3_c64_blocks();
+  TORCH_CHECK(ws.numel() >= (int64_t)blocks * nsl * 64 * 576, "gconv_wgrad_l1: workspace too small");
+  int written = 0;
+  for (int64_t j = 0; j < nsl; ++j) {
+    pdt::ConvWgradArgs a{};
+    a.x = p16(x, "x") + j * S;
+    a.dy = p16(dy, "dy") + j * S;
+    a.ws = pf(ws, "ws") + j * S * 576;
+    a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = 64; a.Kout = 64; a.T = 3; a.U = 3; a.ldw = 576;
+    a.cs = (int)width; a.ldy = (int)width; a.nslice = (int)nsl;
+    written = pdt::wgrad3x3_c64_launch(a, blocks, dt, cur_stream());
+  }
+  launched("gconv_wgrad_l1");
+  PDT_BCOUNT("gconv_wgrad_l1");
+  return written;
+}
+
 void wgrad_reduce(const Tensor& ws, int64_t splits, int64_t rows, int64_t cols, int64_t ldw, int64_t split_stride,
                   Tensor& out, int64_t ldo, double scale, bool accumulate) {
   TORCH_CHECK(ws.numel() >= (splits - 1) * split_stride + (rows - 1) * ldw + cols, "wgrad_reduce: ws too small");
@@ -1464,6 +1490,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_slots") = py::none());
   m.def("gconv_wgrad", &gconv_wgrad);
   m.def("gconv_slice", []() { return kGSlice; });
+  m.def("gconv_wgrad_l1", &gconv_wgrad_l1);
   m.def("wgrad_reduce", &wgrad_reduce);
   m.def("wgrad_blocks_3x3c64", &wgrad_blocks_3x3c64);
   m.def("wgrad_3x3c64_supported", &wgrad_3x3c64_supported);

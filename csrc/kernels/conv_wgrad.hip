@@ -1435,8 +1435,10 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
   const int t_per = (tiles + 7) >> 3;
   const int t_begin = xcd * t_per, t_end = min(tiles, t_begin + t_per);
 
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * kL1W * 128u);
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.N * a.H * kL1W * 128u);
+  // pixel strides (elements): 64, or a 64-channel slice of wider tensors (grouped convs: x stride a.cs, dY a.ldy)
+  const int xcs = a.cs > 0 ? a.cs : 64, ycs = a.ldy > 0 ? a.ldy : 64;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (uint32_t)a.N * a.H * kL1W * (uint32_t)xcs * 2u);
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.dy, (uint32_t)a.N * a.H * kL1W * (uint32_t)ycs * 2u);
   const int lrow = lane >> 3, pch = lane & 7;
 
   // 72 DMA instructions per stage (44 X + 28 dY), 72 / NWV per wave
@@ -1452,14 +1454,14 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
         const int h = h0 - 1 + hr, w = wc - 1;
         const bool ok = R < kL1XRows && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)kL1W;
         const int ch = pch ^ l1_swz(hr, wc);
-        const uint32_t off = ok ? (uint32_t)((((n * a.H + h) * kL1W + w) * 64 + ch * 8) * 2) : kOOB;
+        const uint32_t off = ok ? (uint32_t)((((n * a.H + h) * kL1W + w) * xcs + ch * 8) * 2) : kOOB;
         buf_lds16_asm(rx, sb + ii * 1024, off);
       } else {
         const int R = (ii - 44) * 8 + lrow;
         const int r = R / kL1W, w = R - (R / kL1W) * kL1W;
         const int h = h0 + r;
         const int ch = pch ^ l1_swz(r, w);
-        const uint32_t off = h < a.H ? (uint32_t)((((n * a.H + h) * kL1W + w) * 64 + ch * 8) * 2) : kOOB;
+        const uint32_t off = h < a.H ? (uint32_t)((((n * a.H + h) * kL1W + w) * ycs + ch * 8) * 2) : kOOB;
         buf_lds16_asm(ry, sb + ii * 1024, off);
       }
     }
@@ -1552,9 +1554,10 @@ __global__ __launch_bounds__(64 * NWV) void wgrad3x3_c64_kernel(ConvWgradArgs a)
     buf ^= 1;
   }
 
-  // partial dW[k][tap][c]: lane holds rows k = kb*16 + 4*(lane>>4) + r, column c = cb*16 + (lane&15)
+  // partial dW[k][tap][c]: lane holds rows k = kb*16 + 4*(lane>>4) + r, column c = cb*16 + (lane&15); partials of a
+  // grouped conv's slice are interleaved with the other slices' ([partial][nslice][64][ldw], a.ws at this slice)
   const int64_t part = TSPL ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * (NWV / 4) + jp;
-  float* dst = a.ws + part * 64 * a.ldw;
+  float* dst = a.ws + part * (a.nslice > 1 ? a.nslice : 1) * 64 * a.ldw;
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
     const int tp = TSPL ? jp * 5 + u : u;

@@ -499,6 +499,16 @@ class ResNetExecutor:
         def wg():
             R, S, S_ = c.R, c.S, c.GSLICE
             ldw = R * S * S_
+            if self.wgrad_l1 and self.C.wgrad_3x3c64_supported(S_, S_, R, S, W, c.st, c.pad):
+                # ResNeXt stage 1: every slice on the layer1 halo weight-gradient kernel (all 9 taps per staged tile)
+                blocks = self.C.wgrad_blocks_3x3c64()
+                ws = self._buf("ws", blocks * c.nslice * S_ * ldw, torch.float32)
+                tmp = self._buf("gconv_dw", c.nslice * S_ * ldw, torch.float32)
+                parts = self.C.gconv_wgrad_l1(x, dy, ws, N, H, W, c.cin)
+                self.C.wgrad_reduce(ws, parts, c.nslice * S_, ldw, ldw, c.nslice * S_ * ldw, tmp, ldw, 1.0, False)
+                self.C.gather32(tmp, c.gidx, self._g(c.slot))
+                self.grad_ready(c.pid)
+                return
             key = (S_, R, S, S_, N * P * Q, False)
             plan = self._plans.get(key)
             if plan is None:

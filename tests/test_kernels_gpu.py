@@ -1228,6 +1228,17 @@ def test_grouped_conv_slices_match_torch(width, groups, stride, H):
     assert torch.equal(dwd2.view(nsl, S, R, R, S), dwd)
     if H == 56 and stride == 1:  # forward, backward data, backward data with the BN reduce; per slice and all slices
         assert C_.dispatch_counts().get("conv_l1_sliced", 0) == 6 * nsl, C_.dispatch_counts()
+        # the weight gradient of every slice on the layer1 halo kernel: partials [parts][nslice][64][576]
+        parts = C_.wgrad_blocks_3x3c64()
+        ws4 = torch.full((parts * nsl * S * ldw,), float("nan"), device=DEV)
+        p = C_.gconv_wgrad_l1(x, dy, ws4, N, H, W, width)
+        dwd4 = torch.empty(nsl * S * ldw, device=DEV)
+        C_.wgrad_reduce(ws4, p, nsl * S, ldw, ldw, nsl * S * ldw, dwd4, ldw, 1.0, False)
+        torch.cuda.synchronize()
+        dwd4 = dwd4.view(nsl, S, R, R, S)
+        got4 = torch.stack([dwd4[j, k, :, :, (k // cg) * cg:(k // cg) * cg + cg] for j in range(nsl) for k in range(S)])
+        assert _rel(got4, got) < 1e-5  # (the same products, another fp32 summation order)
+        assert _rel(got4, wr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
 @pytest.mark.parametrize("tile", [(256, 64, 64), (128, 128, 64), (256, 128, 64), (256, 256, 64)])
