@@ -157,9 +157,11 @@ void conv_fwd(const Tensor& x, const Tensor& w, Tensor& y, const OptT& res, cons
   if (cs != C) {  // window mode: every tap's C-element chunk must stay inside the padded image
     // C == 32: one kernel row per tap; C == 64: two consecutive kernel rows per tap (BK must be 64)
     const int rows = C == 64 ? 2 : 1;
-    TORCH_CHECK(cs == 4 && (C == 32 || (C == 64 && bk == 64)) && tstep_w == 0 && U == 1 && ioff_h >= 0 &&
+    // U > 1 column taps (C == 32 only): windows tstep_w pixels apart, e.g. AlexNet's 11-wide kernel rows as two
+    // 8-pixel windows
+    TORCH_CHECK(cs == 4 && (C == 32 || (C == 64 && bk == 64 && U == 1)) && tstep_w >= 0 && U >= 1 && ioff_h >= 0 &&
                     ioff_w >= 0 && (Pm - 1) * ist_h + ioff_h + (T - 1) * tstep_h + rows - 1 < H &&
-                    ((Qm - 1) * ist_w + ioff_w) * cs + 32 <= W * cs,
+                    ((Qm - 1) * ist_w + ioff_w + (U - 1) * tstep_w) * cs + 32 <= W * cs,
                 "conv_fwd: window-mode geometry leaves the padded image");
     if (C == 64) pair_skip = (int)(W * cs - 32);
   }
@@ -465,8 +467,9 @@ void conv_wgrad(const Tensor& x, const Tensor& dy, Tensor& ws, int64_t N, int64_
   TORCH_CHECK(x.numel() < (int64_t(1) << 30) && dy.numel() < (int64_t(1) << 30),
               "conv_wgrad: operands exceed 2 GiB (32-bit buffer offsets)");
   if (win) {  // stem window mode: rows h..h+1 and 8 pixels from w must lie inside the padded image
-    TORCH_CHECK(cs == 4 && C == 64 && U == 1 && pad_h == 0 && pad_w == 0 &&
-                    (Pm - 1) * stride_h + (T - 1) * dil_h + 1 < H && ((Qm - 1) * stride_w + 8) <= W,
+    // U > 1: 8-pixel windows dil_w pixels apart (AlexNet's 11-wide kernel rows)
+    TORCH_CHECK(cs == 4 && C == 64 && U >= 1 && dil_w >= 0 && pad_h == 0 && pad_w == 0 &&
+                    (Pm - 1) * stride_h + (T - 1) * dil_h + 1 < H && ((Qm - 1) * stride_w + (U - 1) * dil_w + 8) <= W,
                 "conv_wgrad: window-mode geometry leaves the padded image");
   } else {
     TORCH_CHECK(cs == C, "conv_wgrad: pixel stride must equal C outside window mode");
@@ -840,28 +843,32 @@ void bn_bwd_apply(const Tensor& g, const OptT& mask, const Tensor& y1, const Ten
 }
 
 // ------------------------------------------------------------------------------------------ pool
+// MaxPool(3, 2, pad): pad 1 (ResNet stem) or 0 (AlexNet)
 void bn_relu_maxpool(const Tensor& y, const Tensor& coef, Tensor& out, Tensor& idx, int64_t N, int64_t H, int64_t W,
-                     int64_t C) {
+                     int64_t C, int64_t pad) {
   const int dt = dt16(y, "y");
-  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK((pad == 0 || pad == 1) && H + 2 * pad >= 3 && W + 2 * pad >= 3, "bn_relu_maxpool: pad 0 or 1");
+  const int64_t OH = (H + 2 * pad - 3) / 2 + 1, OW = (W + 2 * pad - 3) / 2 + 1;
   TORCH_CHECK(y.numel() == N * H * W * C && out.numel() == N * OH * OW * C && idx.numel() == out.numel() && C % 8 == 0,
               "bn_relu_maxpool: bad sizes");
   TORCH_CHECK(y.numel() < (int64_t(1) << 32), "bn_relu_maxpool: tensor exceeds 2^32 elements (32-bit indexing)");
   check_dev(idx, "idx");
   pdt::bn_relu_maxpool_launch(dt, p16(y, "y"), pf(coef, "coef"), p16(out, "out"), idx.data_ptr<uint8_t>(), N, H, W, C,
-                              cur_stream());
+                              cur_stream(), (int)pad);
   launched("bn_relu_maxpool_launch");
 }
 
 void maxpool_bwd_relu(const Tensor& dp, const Tensor& idx, const Tensor& y, const Tensor& coef, Tensor& dz, int64_t N,
-                      int64_t H, int64_t W, int64_t C) {
+                      int64_t H, int64_t W, int64_t C, int64_t pad) {
   const int dt = dt16(dp, "dp");
-  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK((pad == 0 || pad == 1) && H + 2 * pad >= 3 && W + 2 * pad >= 3 && C % 8 == 0,
+              "maxpool_bwd_relu: pad 0 or 1, C % 8 == 0");
+  const int64_t OH = (H + 2 * pad - 3) / 2 + 1, OW = (W + 2 * pad - 3) / 2 + 1;
   TORCH_CHECK(dp.numel() == N * OH * OW * C && y.numel() == N * H * W * C && dz.numel() == y.numel(),
               "maxpool_bwd_relu: bad sizes");
   check_dev(idx, "idx");
   pdt::maxpool_bwd_relu_launch(dt, p16(dp, "dp"), idx.data_ptr<uint8_t>(), p16(y, "y"), pf(coef, "coef"), p16(dz, "dz"),
-                               N, H, W, C, cur_stream());
+                               N, H, W, C, cur_stream(), (int)pad);
   launched("maxpool_bwd_relu_launch");
 }
 
@@ -1519,8 +1526,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_bwd_apply", &bn_bwd_apply);
-  m.def("bn_relu_maxpool", &bn_relu_maxpool);
-  m.def("maxpool_bwd_relu", &maxpool_bwd_relu);
+  m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("y"), py::arg("coef"), py::arg("out"), py::arg("idx"),
+        py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pad") = 1);
+  m.def("maxpool_bwd_relu", &maxpool_bwd_relu, py::arg("dp"), py::arg("idx"), py::arg("y"), py::arg("coef"),
+        py::arg("dz"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pad") = 1);
   m.def("stem_fwd", &stem_fwd);
   m.def("stem_fwd_supported", [](int64_t Hp, int64_t Wp, int64_t P, int64_t Q) {
     return pdt::stem_fwd_supported((int)Hp, (int)Wp, (int)P, (int)Q);

@@ -1,6 +1,7 @@
 // Pooling kernels, NHWC 16-bit.
-//   * bn_relu_maxpool3x3s2: the ResNet stem's BN-apply + ReLU fused with MaxPool(3, 2, 1); the
-//     112x112 post-ReLU tensor is never written.  The window argmax (0..8) is kept as uint8.
+//   * bn_relu_maxpool3x3s2: the ResNet stem's BN-apply + ReLU fused with MaxPool(3, 2, 1) (also AlexNet's bias +
+//     ReLU + MaxPool(3, 2), pad 0); the full-resolution post-ReLU tensor is never written.  The window argmax (0..8)
+//     is kept as uint8.
 //   * maxpool_bwd_relu: gather form of the max-pool backward (each input pixel collects from the
 //     <= 4 windows that selected it) fused with the ReLU mask recomputed from the BN input.
 //   * stem_pool_bwd_reduce / stem_pool_bwd_apply: the whole stem backward (max-pool backward, ReLU
@@ -23,7 +24,7 @@ static int ew_blocks(int64_t n) {
 template <int DT>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                               uint16_t* __restrict__ out, uint8_t* __restrict__ idx,
-                                                              int N, int H, int W, int C, int OH, int OW) {
+                                                              int N, int H, int W, int C, int OH, int OW, int pad) {
   using E = E16<DT>;
   const int cv = C / 8;
   const uint32_t total = (uint32_t)N * OH * OW * cv;  // 32-bit index math (host checks sizes < 2^32)
@@ -48,15 +49,15 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int h = min(max(oh * 2 - 1 + kh, 0), H - 1), w = min(max(ow * 2 - 1 + kw, 0), W - 1);
+        const int h = min(max(oh * 2 - pad + kh, 0), H - 1), w = min(max(ow * 2 - pad + kw, 0), W - 1);
         q[kh * 3 + kw] = *(const uint4*)(y + ((uint32_t)(n * H + h) * W + w) * C + c0);
       }
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
-      const bool hok = (unsigned)(oh * 2 - 1 + kh) < (unsigned)H;
+      const bool hok = (unsigned)(oh * 2 - pad + kh) < (unsigned)H;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const bool ok = hok && (unsigned)(ow * 2 - 1 + kw) < (unsigned)W;
+        const bool ok = hok && (unsigned)(ow * 2 - pad + kw) < (unsigned)W;
         const uint32_t qw[4] = {q[kh * 3 + kw].x, q[kh * 3 + kw].y, q[kh * 3 + kw].z, q[kh * 3 + kw].w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -87,23 +88,24 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
 // window column, 15 loads for 2 outputs, no index divisions -- measured SLOWER on the same box: ResNet-18
 // 20.16 -> 20.24 ms, ResNet-50 71.7 -> 72.0 ms; not kept.)
 // eval / generic variant without index output is the same kernel with idx == nullptr handled by caller
+// pad: 1 = the ResNet stem's MaxPool(3, 2, 1); 0 = AlexNet's MaxPool(3, 2)
 void bn_relu_maxpool_launch(int dtype, const uint16_t* y, const float* coef, uint16_t* out, uint8_t* idx, int N, int H,
-                            int W, int C, hipStream_t s) {
-  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+                            int W, int C, hipStream_t s, int pad) {
+  const int OH = (H + 2 * pad - 3) / 2 + 1, OW = (W + 2 * pad - 3) / 2 + 1;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
   if (dtype == kBF16)
     hipLaunchKernelGGL(bn_relu_maxpool_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, y, coef, out, idx, N, H, W,
-                       C, OH, OW);
+                       C, OH, OW, pad);
   else
     hipLaunchKernelGGL(bn_relu_maxpool_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, y, coef, out, idx, N, H, W,
-                       C, OH, OW);
+                       C, OH, OW, pad);
 }
 
 template <int DT>
 __global__ __launch_bounds__(256) void maxpool_bwd_relu_kernel(const uint16_t* __restrict__ dp, const uint8_t* __restrict__ idx,
                                                                const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                                uint16_t* __restrict__ dz, int N, int H, int W, int C,
-                                                               int OH, int OW) {
+                                                               int OH, int OW, int pad) {
   using E = E16<DT>;
   const int cv = C / 8;
   const int64_t total = (int64_t)N * H * W * cv;
@@ -115,16 +117,15 @@ __global__ __launch_bounds__(256) void maxpool_bwd_relu_kernel(const uint16_t* _
     const int h = (int)(pix % H);
     const int n = (int)(pix / H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // candidate windows: oh with 2*oh-1 <= h <= 2*oh+1
-    const int oh_lo = (h) / 2, oh_hi = (h + 1) / 2;  // h even: {h/2}; h odd: {(h-1)/2, (h+1)/2}
-    const int ow_lo = (w) / 2, ow_hi = (w + 1) / 2;
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      if (oh >= OH) continue;
-      const int kh = h - (oh * 2 - 1);
+    // candidate windows: oh with 2*oh-pad <= h <= 2*oh-pad+2, i.e. (h+pad)/2 and the one before it
+    const int oh_hi = (h + pad) >> 1, ow_hi = (w + pad) >> 1;
+    for (int oh = oh_hi - 1; oh <= oh_hi; ++oh) {
+      if (oh < 0 || oh >= OH) continue;
+      const int kh = h - (oh * 2 - pad);
       if (kh < 0 || kh > 2) continue;
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        if (ow >= OW) continue;
-        const int kw = w - (ow * 2 - 1);
+      for (int ow = ow_hi - 1; ow <= ow_hi; ++ow) {
+        if (ow < 0 || ow >= OW) continue;
+        const int kw = w - (ow * 2 - pad);
         if (kw < 0 || kw > 2) continue;
         const uint8_t pos = (uint8_t)(kh * 3 + kw);
         const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
@@ -158,15 +159,15 @@ __global__ __launch_bounds__(256) void maxpool_bwd_relu_kernel(const uint16_t* _
 }
 
 void maxpool_bwd_relu_launch(int dtype, const uint16_t* dp, const uint8_t* idx, const uint16_t* y, const float* coef,
-                             uint16_t* dz, int N, int H, int W, int C, hipStream_t s) {
-  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+                             uint16_t* dz, int N, int H, int W, int C, hipStream_t s, int pad) {
+  const int OH = (H + 2 * pad - 3) / 2 + 1, OW = (W + 2 * pad - 3) / 2 + 1;
   const int64_t total = (int64_t)N * H * W * (C / 8);
   if (dtype == kBF16)
     hipLaunchKernelGGL(maxpool_bwd_relu_kernel<kBF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef, dz, N, H,
-                       W, C, OH, OW);
+                       W, C, OH, OW, pad);
   else
     hipLaunchKernelGGL(maxpool_bwd_relu_kernel<kF16>, dim3(ew_blocks(total)), dim3(256), 0, s, dp, idx, y, coef, dz, N, H,
-                       W, C, OH, OW);
+                       W, C, OH, OW, pad);
 }
 
 // Stem backward, pass 1: per-channel sum(dz) and sum(dz * xhat) over the stem's conv output, visiting

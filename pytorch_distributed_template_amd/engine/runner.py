@@ -37,11 +37,11 @@ from ..utils.meters import AverageMeter, get_learning_rate
 from ..utils.profiling import roctx_range
 from ..utils.tensorboard import SummaryWriter
 
-_VGG_ARCHS = ("vgg11", "vgg11_bn", "vgg13", "vgg13_bn", "vgg16", "vgg16_bn", "vgg19", "vgg19_bn")
+_VGG_ARCHS = ("vgg11", "vgg11_bn", "vgg13", "vgg13_bn", "vgg16", "vgg16_bn", "vgg19", "vgg19_bn", "alexnet")
 NATIVE_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2",
                 "resnext50_32x4d", "resnext101_32x8d", "resnext101_64x4d") + _VGG_ARCHS
-# 16-bit executors only (VGG: models/executor_vgg.py); fp32 runs them on the torch engine.  (Grouped convs run in
-# both precisions: models/executor.py and models/executor32.py channel slices.)
+# 16-bit executors only (VGG and AlexNet: models/executor_vgg.py); fp32 runs them on the torch engine.  (Grouped convs
+# run in both precisions: models/executor.py and models/executor32.py channel slices.)
 NATIVE_ARCHS_16BIT_ONLY = _VGG_ARCHS
 
 

@@ -1,4 +1,4 @@
-"""Native VGG executor (vgg11/13/16/19 and their ``_bn`` forms) over the gfx950 kernels.
+"""Native VGG / AlexNet executor (vgg11/13/16/19, their ``_bn`` forms, alexnet) over the gfx950 kernels.
 
 The reference trains any torchvision constructor by name (`distributed.py:39-40,132-137`); this is the native engine's
 second model family after the ResNets.  It reuses the ResNet executor's machinery -- the implicit-GEMM conv kernels
@@ -21,6 +21,13 @@ master + 16-bit shadow, per-parameter ``grad_ready`` for the DDP bucketer and Sy
   into the flat gradient buffer), bias + ReLU + Dropout is one pass (``fc_act_fwd``: counter-hash dropout), and its
   backward recovers the keep mask from the stored output (``fc_act_bwd``), so no mask tensor exists.
 
+AlexNet (the reference's ``--arch alexnet``) runs on the same executor: its 11x11/4 first conv in the same window mode
+(two 8-pixel windows per kernel row, ``tstep_w`` = 8; weight gradient on 6 kernel-row pairs), the 5x5 and 3x3 convs
+on the generic implicit-GEMM kernels, bias + ReLU + MaxPool(3, 2) as one pass (``bn_relu_maxpool`` with pad 0, the
+ResNet stem's kernel) with the gather-form backward (``maxpool_bwd_relu``), and its classifier order (Dropout before
+each of the first two Linears: the feature dropout is ``fc_act_fwd`` with a zero bias -- the features are post-ReLU,
+so its ReLU is the identity).
+
 Every launch whose operands would pass the kernels' 32-bit offsets (``_MAX_ELEMS``: VGG's 224 x 224 x 64 activations
 at a few hundred images per GPU) runs over image chunks: weight gradients accumulate across chunks, BN statistics are
 summed from per-chunk slot buffers.
@@ -34,7 +41,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import native
-from .classic import VGG
+from .classic import VGG, AlexNet
 from .executor import ResNetExecutor, _BN, _Conv
 
 # largest element count of any operand of one conv / weight-gradient launch (the LDS-DMA buffer resources and the
@@ -43,12 +50,12 @@ _MAX_ELEMS = (1 << 30) - 1
 
 
 class _Layer:
-    """One conv of ``features`` with its BatchNorm (``bn``) or bias (``bias_slot``), its ReLU and the MaxPool(2, 2)
-    that may follow it."""
+    """One conv of ``features`` with its BatchNorm (``bn``) or bias (``bias_slot``), its ReLU and the max-pool that
+    may follow it (``pool``: 0 none, 2 = MaxPool(2, 2), 3 = MaxPool(3, 2))."""
 
-    def __init__(self, conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], pool: bool, flat, derived_maps, off, device):
-        if conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1):
-            raise NotImplementedError("native VGG executor: 3x3 / stride-1 / pad-1 convolutions only")
+    def __init__(self, conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], pool: int, flat, derived_maps, off, device):
+        if not _conv_ok(conv):
+            raise NotImplementedError(f"native VGG/AlexNet executor: unsupported conv {conv}")
         self.first = conv.in_channels == 3
         self.conv = _Conv(conv, flat, [] if self.first else derived_maps, off if not self.first else [0])
         self.bn = _BN(bn, flat, device) if bn is not None else None
@@ -61,22 +68,46 @@ class _Layer:
         self.bcoef = self.bn.bcoef if self.bn is not None else torch.zeros(3 * C, dtype=torch.float32, device=device)
 
 
+def _conv_ok(conv: nn.Conv2d) -> bool:
+    """The first (3-channel) conv: any square kernel up to 11 x 11 at stride <= 4 (window mode); the others: square
+    stride-1 'same' convs (VGG's 3x3, AlexNet's 5x5 and 3x3) over channel counts the implicit-GEMM kernels tile."""
+    k, st, pad = conv.kernel_size, conv.stride, conv.padding
+    if k[0] != k[1] or st[0] != st[1] or pad[0] != pad[1] or conv.dilation != (1, 1) or conv.groups != 1:
+        return False
+    if conv.in_channels == 3:
+        return k[0] <= 11 and st[0] <= 4
+    return st[0] == 1 and 2 * pad[0] == k[0] - 1 and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
+
+
+def _pool_kind(m: nn.MaxPool2d) -> int:
+    ks = m.kernel_size if isinstance(m.kernel_size, int) else m.kernel_size[0]
+    st = m.stride if isinstance(m.stride, int) else m.stride[0]
+    pad = m.padding if isinstance(m.padding, int) else m.padding[0]
+    if ks == 2 and st == 2 and pad == 0 and not m.ceil_mode:
+        return 2
+    if ks == 3 and st == 2 and pad == 0 and not m.ceil_mode:
+        return 3
+    return 0
+
+
 def vgg_supported(model) -> bool:
-    """torchvision-layout VGG whose features are 3x3 convs (+ BN) + ReLU and 2x2 max-pools, at 224-style inputs."""
-    if not isinstance(model, VGG):
+    """torchvision-layout VGG (3x3 convs (+ BN) + ReLU, 2x2 max-pools) or AlexNet (11x11/4, 5x5 and 3x3 convs + ReLU,
+    3x3/2 max-pools), at 224-style inputs."""
+    if not isinstance(model, (VGG, AlexNet)):
         return False
     for m in model.features:
-        if isinstance(m, nn.Conv2d) and (m.kernel_size != (3, 3) or m.stride != (1, 1) or m.padding != (1, 1)):
+        if isinstance(m, nn.Conv2d) and not _conv_ok(m):
             return False
-        if isinstance(m, nn.MaxPool2d) and (m.kernel_size not in (2, (2, 2)) or m.stride not in (2, (2, 2))):
+        if isinstance(m, nn.MaxPool2d) and _pool_kind(m) != (3 if isinstance(model, AlexNet) else 2):
             return False
     return True
 
 
 class VGGExecutor(ResNetExecutor):
-    """Runs a torchvision-layout :class:`VGG` on one GPU (same public interface as :class:`ResNetExecutor`)."""
+    """Runs a torchvision-layout :class:`VGG` or :class:`AlexNet` on one GPU (same public interface as
+    :class:`ResNetExecutor`)."""
 
-    def __init__(self, model: VGG, flat, device: torch.device, dtype: torch.dtype,
+    def __init__(self, model: nn.Module, flat, device: torch.device, dtype: torch.dtype,
                  grad_ready: Optional[Callable[[int], None]] = None, syncbn_group=None, wgrad_blocks: int = 2048,
                  wgrad_blocks_1x1: int = 512, autotune: bool = False,
                  syncbn_allreduce: Optional[Callable[[torch.Tensor], None]] = None, syncbn_world: int = 0,
@@ -84,7 +115,8 @@ class VGGExecutor(ResNetExecutor):
         if dtype not in (torch.bfloat16, torch.float16):
             raise ValueError("native executor computes in bf16 or fp16")
         if not vgg_supported(model):
-            raise NotImplementedError("native VGG executor: torchvision-layout VGG (3x3 convs, 2x2 max-pools) only")
+            raise NotImplementedError("native VGG executor: torchvision-layout VGG (3x3 convs, 2x2 max-pools) or "
+                                      "AlexNet only")
         self.C = native.C
         self.n_slots = self.C.stat_slots()
         self.model = model
@@ -141,36 +173,47 @@ class VGGExecutor(ResNetExecutor):
                 i += 1
             assert i < len(mods) and isinstance(mods[i], nn.ReLU), "conv (+ BN) must be followed by ReLU"
             i += 1
-            pool = i < len(mods) and isinstance(mods[i], nn.MaxPool2d)
-            if pool:
+            pool = 0
+            if i < len(mods) and isinstance(mods[i], nn.MaxPool2d):
+                pool = _pool_kind(mods[i])
                 i += 1
             self.layers.append(_Layer(conv, bn, pool, flat, derived_maps, off, self.device))
-        # the first conv's window weights [64][3][32]: column s * 4 + c of a kernel row
+        # the first conv's window weights [cout][R][U][32]: window u of kernel row r holds columns u*8 .. u*8+7,
+        # element j = column (j // 4) * 4 + channel (j % 4) of the NHWC4 image (U = 1 for VGG's 3x3, 2 for the 11x11)
         first = self.layers[0]
         assert first.first and all(not l.first for l in self.layers[1:]), "3-channel input conv first"
         fc = first.conv
-        k = torch.arange(fc.cout).view(-1, 1, 1)
-        r = torch.arange(3).view(1, -1, 1)
-        j = torch.arange(32).view(1, 1, -1)
-        s_, c_ = j // 4, j % 4
-        src = fc.slot.offset + ((k * 3 + r) * 3 + s_) * 3 + c_
-        win = torch.where((s_ < 3) & (c_ < 3), src, torch.full_like(src, -1))
+        R0 = fc.R
+        self.w0_U = U0 = (R0 + 7) // 8
+        self.w0_T = T0 = (R0 + 1) // 2  # weight-gradient kernel-row pairs
+        k = torch.arange(fc.cout).view(-1, 1, 1, 1)
+        r = torch.arange(R0).view(1, -1, 1, 1)
+        u = torch.arange(U0).view(1, 1, -1, 1)
+        j = torch.arange(32).view(1, 1, 1, -1)
+        s_, c_ = u * 8 + j // 4, j % 4
+        src = fc.slot.offset + ((k * R0 + r) * R0 + s_.clamp(max=R0 - 1)) * 3 + c_.clamp(max=2)
+        win = torch.where((s_ < R0) & (c_ < 3), src, torch.full_like(src, -1))
         self.w0_off = off[0]
         derived_maps.append(win.reshape(-1).to(torch.int32))
         off[0] += win.numel()
-        # its weight gradient: [64][2 pairs][2 rows][32] window tile -> KRSC [64][3][3][3]
+        # its weight gradient: [cout][T pairs][U windows][2 rows][32] window tile -> KRSC [cout][R][R][3]
+        self.w0_ldw = T0 * U0 * 64
         kk = torch.arange(fc.cout).view(-1, 1, 1, 1)
-        rr = torch.arange(3).view(1, -1, 1, 1)
-        ss = torch.arange(3).view(1, 1, -1, 1)
+        rr = torch.arange(R0).view(1, -1, 1, 1)
+        ss = torch.arange(R0).view(1, 1, -1, 1)
         cc = torch.arange(3).view(1, 1, 1, -1)
-        self.w0_gidx = (kk * 128 + (rr // 2) * 64 + (rr % 2) * 32 + ss * 4 + cc).reshape(-1).to(torch.int32).to(
-            self.device)
-        # --- classifier: Linear, ReLU, Dropout, Linear, ReLU, Dropout, Linear
+        self.w0_gidx = (kk * self.w0_ldw + ((rr // 2) * U0 + ss // 8) * 64 + (rr % 2) * 32 + (ss % 8) * 4 +
+                        cc).reshape(-1).to(torch.int32).to(self.device)
+        # --- classifier: VGG [Linear, ReLU, Dropout] x 2 + Linear; AlexNet [Dropout, Linear, ReLU] x 2 + Linear
         lin = [m for m in model.classifier if isinstance(m, nn.Linear)]
         drops = [m for m in model.classifier if isinstance(m, nn.Dropout)]
         if len(lin) != 3 or len(drops) != 2:
             raise NotImplementedError("native VGG executor: torchvision's 3-Linear classifier")
         self.p_drop = float(drops[0].p)
+        # dropout in front of the first two Linears (AlexNet) instead of behind their ReLUs (VGG)
+        self.drop_first = isinstance(model.classifier[0], nn.Dropout)
+        self.pool_hw = model.avgpool.output_size if isinstance(model.avgpool.output_size, tuple) else (
+            model.avgpool.output_size, model.avgpool.output_size)
         self.lin = lin
         self.lin_slots = [(flat.slot(m.weight), flat.slot(m.bias)) for m in lin]
         self.feat = lin[0].in_features
@@ -209,6 +252,12 @@ class VGGExecutor(ResNetExecutor):
         t = self._ones.get(C)
         if t is None:
             t = self._ones[C] = torch.ones(C, dtype=torch.float32, device=self.device)
+        return t
+
+    def _zeros(self, C: int) -> torch.Tensor:
+        t = self._ones.get(-C)
+        if t is None:
+            t = self._ones[-C] = torch.zeros(C, dtype=torch.float32, device=self.device)
         return t
 
     def _chunks(self, N: int, per_image: int) -> List[Tuple[int, int]]:
@@ -267,25 +316,26 @@ class VGGExecutor(ResNetExecutor):
         return sp_all
 
     def _wgrad_chunked(self, c: _Conv, x, dy, N, H, W, gout):
-        """3x3 / s1 / p1 weight gradient over image chunks, accumulated into ``gout`` (fp32 KRSC)."""
+        """Stride-1 'same' conv weight gradient over image chunks, accumulated into ``gout`` (fp32 KRSC)."""
         chunks = self._chunks(N, H * W * max(c.cin, c.cout))
-        ldw = 9 * c.cin
+        R, S, pad = c.R, c.S, c.pad
+        ldw = R * S * c.cin
         for k, (a, b) in enumerate(chunks):
             xs = x[a * H * W * c.cin:b * H * W * c.cin]
             dys = dy[a * H * W * c.cout:b * H * W * c.cout]
             n = b - a
             if len(chunks) == 1:
-                self._wgrad(c.cout, xs, dys, n, H, W, c.cin, 3, 3, H, W, 1, 1, gout, ldw)
+                self._wgrad(c.cout, xs, dys, n, H, W, c.cin, R, S, H, W, 1, pad, gout, ldw)
                 return
-            key = (c.cout, 3, 3, c.cin, n * H * W, False)
+            key = (c.cout, R, S, c.cin, n * H * W, False)
             plan = self._plans.get(key)
             if plan is None:
-                plan = tuple(self.C.conv_wgrad_plan(c.cout, 3, 3, c.cin, n * H * W, self.wgrad_blocks, False))[:2]
+                plan = tuple(self.C.conv_wgrad_plan(c.cout, R, S, c.cin, n * H * W, self.wgrad_blocks, False))[:2]
                 self._plans[key] = plan
             splits, pps = plan
             ws = self._buf("ws", splits * c.cout * ldw, torch.float32)
-            self.C.conv_wgrad(xs, dys, ws, n, H, W, c.cin, c.cout, 3, 3, H, W, 1, 1, 1, 1, 1, 1, ldw, splits, pps, 0,
-                              False)
+            self.C.conv_wgrad(xs, dys, ws, n, H, W, c.cin, c.cout, R, S, H, W, 1, 1, pad, pad, 1, 1, ldw, splits, pps,
+                              0, False)
             self.C.wgrad_reduce(ws, splits, c.cout, ldw, ldw, c.cout * ldw, gout, ldw, 1.0, k > 0)
 
     def _conv_bwd(self, L: _Layer, x, N, H, W, dy, dx, bnb_layer: Optional[_Layer], slots):
@@ -325,8 +375,9 @@ class VGGExecutor(ResNetExecutor):
             else:
                 self.C.conv_dgrad_bn(dy, self.derived, dx, None, N, H, W, c.cout, c.cin, H, W, 1, phases, bm, bn, bk,
                                      *bnb, -1)
-        key = ("dgrad", N, H, W, c.cin, c.cout, 3, 3, 1, False, bnb[0] if bnb else 0, -1)
-        bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * 9, m=N * H * W)
+        key = ("dgrad", N, H, W, c.cin, c.cout, c.R, c.S, 1, False, bnb[0] if bnb else 0, -1)
+        bm, bn = self._tile(key, c.cin, bk, launch, fused_epilogue=bnb is not None, kdim=c.cout * c.R * c.S,
+                            m=N * H * W)
         launch(bm, bn)
 
     # ---------------------------------------------------------------------------------- forward
@@ -335,45 +386,61 @@ class VGGExecutor(ResNetExecutor):
         N = images.shape[0]
         assert images.dim() == 4 and images.shape[1] == 3, "expected NCHW images"
         H, W = images.shape[2], images.shape[3]
-        if H % 32 or W % 32:
+        if self.drop_first:
+            if H < 63 or W < 63:
+                raise NotImplementedError("native AlexNet executor: inputs of at least 63 x 63")
+        elif H % 32 or W % 32:
             raise NotImplementedError("native VGG executor: input sides must be multiples of 32")
         u8 = images.dtype == torch.uint8
         x32 = images.contiguous() if u8 or images.dtype == torch.float32 else images.float().contiguous()
-        # first conv: zero-padded NHWC4 image (pad 1; 2 spare rows / 6 spare columns for the 8-pixel windows and the
-        # weight gradient's row pairs), window-mode implicit GEMM, one 32-wide K-step per kernel row
-        Hp, Wp = H + 3, W + 7
+        # first conv: zero-padded NHWC4 image, window-mode implicit GEMM, U 32-wide K-steps (8 pixels x 4 channels) per
+        # kernel row; spare rows / columns so every window and the weight gradient's row pairs stay inside the image
+        c0 = self.layers[0].conv
+        R0, st0, pad0 = c0.R, c0.st, c0.pad
+        P0, Q0 = (H + 2 * pad0 - R0) // st0 + 1, (W + 2 * pad0 - R0) // st0 + 1
+        Hp = max(H + 2 * pad0, (P0 - 1) * st0 + 2 * self.w0_T)
+        Wp = max(W + 2 * pad0, (Q0 - 1) * st0 + 8 * self.w0_U)
         xp = self._buf("stem_in", N * Hp * Wp * 4)
         if u8:
-            Cn.stem_pack_u8(x32, xp, N, 3, H, W, 1, Hp, Wp, self.norm_scale, self.norm_shift)
+            Cn.stem_pack_u8(x32, xp, N, 3, H, W, pad0, Hp, Wp, self.norm_scale, self.norm_shift)
         else:
-            Cn.stem_pack(x32, xp, N, 3, H, W, 1, Hp, Wp)
-        saved = {"N": N, "H": H, "W": W, "xp": xp, "Hp": Hp, "Wp": Wp, "acts": []}
+            Cn.stem_pack(x32, xp, N, 3, H, W, pad0, Hp, Wp)
+        saved = {"N": N, "H": H, "W": W, "xp": xp, "Hp": Hp, "Wp": Wp, "P0": P0, "Q0": Q0, "acts": []}
         x, h, w = None, H, W
         for li, L in enumerate(self.layers):
             c = L.conv
-            y = self._buf(("y", li), N * h * w * c.cout)
+            ho_, wo_ = (P0, Q0) if L.first else (h, w)
+            y = self._buf(("y", li), N * ho_ * wo_ * c.cout)
             stats = train and L.bn is not None
             if L.first:
                 sp = self._buf(("stats", c.cout), self.n_slots * c.cout * 2, torch.float64) if stats else None
-                w0 = self.derived[self.w0_off:self.w0_off + c.cout * 96]
-                for a, b in self._chunks(N, h * w * c.cout):
+                w0 = self.derived[self.w0_off:self.w0_off + c.cout * R0 * self.w0_U * 32]
+                for a, b in self._chunks(N, max(Hp * Wp * 4, P0 * Q0 * c.cout)):
                     sk = sp
                     if sp is not None and a > 0:
                         sk = self._buf(("stats_chunk", c.cout), sp.numel(), torch.float64)
-                    Cn.conv_fwd(xp[a * Hp * Wp * 4:b * Hp * Wp * 4], w0, y[a * h * w * c.cout:b * h * w * c.cout],
-                                None, sk, b - a, Hp, Wp, 32, c.cout, 3, 1, h, w, 1, 1, 0, 0, 1, 0, h, w, 1, 1, 0, 0,
-                                256, 64, 32, 4)
+                    Cn.conv_fwd(xp[a * Hp * Wp * 4:b * Hp * Wp * 4], w0, y[a * P0 * Q0 * c.cout:b * P0 * Q0 * c.cout],
+                                None, sk, b - a, Hp, Wp, 32, c.cout, R0, self.w0_U, P0, Q0, st0, st0, 0, 0, 1, 8, P0,
+                                Q0, 1, 1, 0, 0, 256, 64, 32, 4)
                     if sk is not sp:
                         sp.add_(sk)
+                h, w = P0, Q0
             else:
                 sp = self._conv_fwd(L, x, N, h, w, y, stats)
             self._coef(L, train, sp, N * h * w)
             L.y = y
-            if L.pool:
+            if L.pool == 2:
                 ho, wo = h // 2, w // 2
                 out = self._buf(("act", li), N * ho * wo * c.cout)
                 idx = self._buf(("pidx", li), N * ho * wo * c.cout, torch.uint8) if train else None
                 Cn.bn_relu_maxpool2(y, L.coef, out, idx, N, h, w, c.cout)
+                saved["acts"].append((x, h, w, y, out, idx))
+                x, h, w = out, ho, wo
+            elif L.pool == 3:  # AlexNet: bias + ReLU + MaxPool(3, 2) (the argmax is kept for eval too: one path)
+                ho, wo = (h - 3) // 2 + 1, (w - 3) // 2 + 1
+                out = self._buf(("act", li), N * ho * wo * c.cout)
+                idx = self._buf(("pidx", li), N * ho * wo * c.cout, torch.uint8)
+                Cn.bn_relu_maxpool(y, L.coef, out, idx, N, h, w, c.cout, pad=0)
                 saved["acts"].append((x, h, w, y, out, idx))
                 x, h, w = out, ho, wo
             else:
@@ -381,17 +448,23 @@ class VGGExecutor(ResNetExecutor):
                 Cn.bn_apply(y, L.coef, None, None, a_, c.cout, 0, True, None)
                 saved["acts"].append((x, h, w, y, a_, None))
                 x = a_
-        # classifier input: torchvision flattens NCHW (AdaptiveAvgPool2d((7, 7)) is the identity at 7 x 7)
+        # classifier input: torchvision flattens NCHW (the adaptive average pool is the identity at its own output size:
+        # 7 x 7 for VGG, 6 x 6 for AlexNet at 224)
         C_last = self.layers[-1].conv.cout
-        if h * w * C_last != self.feat:
+        if (h, w) != tuple(self.pool_hw) or h * w * C_last != self.feat:
             raise NotImplementedError(f"native VGG executor: {h}x{w}x{C_last} features vs a {self.feat}-wide classifier "
-                                      "(adaptive pooling to 7x7 from other sizes is not native)")
+                                      f"(adaptive pooling to {self.pool_hw} from other sizes is not native)")
         featc = self._buf("featc", N * self.feat)
         Cn.nhwc_nchw16(x, featc, N, h * w, C_last, True)
         p = self.p_drop if train else 0.0
         self._drop_step += 1
         seed = (self._drop_seed * 0x100000001B3 + self._drop_step) & 0x7FFFFFFFFFFFFFFF
         a_in = featc.view(N, self.feat)
+        x0 = None
+        if self.drop_first:  # AlexNet: Dropout on the (post-ReLU) features -> fc_act_fwd with a zero bias
+            x0 = self._buf("fcx0", N * self.feat)
+            Cn.fc_act_fwd(featc, self._zeros(self.feat), x0, N, self.feat, p, seed + 7)
+            a_in = x0.view(N, self.feat)
         hs = []
         for i in range(2):
             wsl, bsl = self.lin_slots[i]
@@ -399,13 +472,15 @@ class VGGExecutor(ResNetExecutor):
             z = self._buf(("fcz", i), N * out_f)
             torch.mm(a_in, self._w_slot(wsl).view(out_f, -1).t(), out=z.view(N, out_f))
             h_ = self._buf(("fch", i), N * out_f)
-            Cn.fc_act_fwd(z, self._p(bsl), h_, N, out_f, p, seed + i)
+            # VGG: Dropout behind both hidden ReLUs; AlexNet: behind the first only (its second Dropout feeds Linear 2)
+            pi = p if (not self.drop_first or i == 0) else 0.0
+            Cn.fc_act_fwd(z, self._p(bsl), h_, N, out_f, pi, seed + i)
             hs.append(h_)
             a_in = h_.view(N, out_f)
         logits = self._buf("logits16", N * self.ncls_pad)
         w3 = self.derived[self.fc_w_off:self.fc_w_off + self.ncls_pad * self.hidden].view(self.ncls_pad, self.hidden)
         torch.mm(a_in, w3.t(), out=logits.view(N, self.ncls_pad))
-        saved.update(featc=featc, hs=hs, logits=logits, hw_last=(h, w), p=p)
+        saved.update(featc=featc, x0=x0, hs=hs, logits=logits, hw_last=(h, w), p=p)
         return saved
 
     def _w_slot(self, slot):
@@ -430,18 +505,22 @@ class VGGExecutor(ResNetExecutor):
         w3 = self.derived[self.fc_w_off:self.fc_w_off + self.ncls_pad * self.hidden].view(self.ncls_pad, self.hidden)
         dh = self._buf(("fcdh", 1), N * self.hidden)
         torch.mm(dlog.view(N, self.ncls_pad), w3, out=dh.view(N, self.hidden))
-        x_ins = [saved["featc"], hs[0]]
+        x_ins = [saved["featc"] if saved["x0"] is None else saved["x0"], hs[0]]
         for i in (1, 0):
             wsl, bsl = self.lin_slots[i]
             out_f, in_f = self.lin[i].out_features, self.lin[i].in_features
             dz = self._buf(("fcdz", i), N * out_f)
-            Cn.fc_act_bwd(dh, hs[i], dz, p)
+            Cn.fc_act_bwd(dh, hs[i], dz, p if (not self.drop_first or i == 0) else 0.0)
             Cn.colsum(dz, N, out_f, out_f, self._g(bsl), 1.0)
             self.grad_ready(bsl.index)
             fc_wg(x_ins[i], dz, wsl, out_f, in_f, out_f)
             dprev = self._buf(("fcdh", i - 1) if i > 0 else "dfeatc", N * in_f)
             torch.mm(dz.view(N, out_f), self._w_slot(wsl).view(out_f, in_f), out=dprev.view(N, in_f))
             dh = dprev
+        if saved["x0"] is not None:  # the feature Dropout's backward (keep mask recovered from x0)
+            dfeat = self._buf("dfeat0", N * self.feat)
+            Cn.fc_act_bwd(dh, saved["x0"], dfeat, p)
+            dh = dfeat
         # back to NHWC: the gradient of the last pooled activation
         h, w = saved["hw_last"]
         C_last = self.layers[-1].conv.cout
@@ -458,10 +537,13 @@ class VGGExecutor(ResNetExecutor):
             cnt = N * hin * win_
             if L.pool:
                 slots = self._buf(("bnslots", C, 2), self.n_slots * C * 2, torch.float64)
-                Cn.pooled_bwd_reduce(g, out, L.coef, slots, N * (hin // 2) * (win_ // 2), C)
+                Cn.pooled_bwd_reduce(g, out, L.coef, slots, out.numel() // C, C)
                 self._finish(L, slots, cnt)
                 dy = self._buf(("dy", li), N * hin * win_ * C)
-                if L.bn is not None:
+                if L.pool == 3:  # bias layer (AlexNet): dy = dz, gathered from the <= 4 windows that chose each pixel
+                    assert L.bn is None, "MaxPool(3, 2) after a BatchNorm is not native"
+                    Cn.maxpool_bwd_relu(g, idx, y, L.coef, dy, N, hin, win_, C, pad=0)
+                elif L.bn is not None:
                     Cn.maxpool2_bwd(g, idx, out, y, L.bcoef, dy, N, hin, win_, C)
                 else:
                     Cn.maxpool2_bwd(g, idx, out, None, None, dy, N, hin, win_, C)
@@ -489,26 +571,28 @@ class VGGExecutor(ResNetExecutor):
         self._join_side()
 
     def _first_wgrad(self, saved, dy0):
-        """First conv's weight gradient in window mode: kernel-row pairs (rows 0-1 | 2-3, the 4th row's weights are
-        zero) over the padded NHWC4 image, gathered into the KRSC gradient."""
-        N, H, W, xp, Hp, Wp = saved["N"], saved["H"], saved["W"], saved["xp"], saved["Hp"], saved["Wp"]
+        """First conv's weight gradient in window mode: kernel-row pairs (rows 0-1 | 2-3 | ..., the weights of a
+        padding row are zero) x 8-pixel windows over the padded NHWC4 image, gathered into the KRSC gradient."""
+        N, xp, Hp, Wp = saved["N"], saved["xp"], saved["Hp"], saved["Wp"]
+        P, Q = saved["P0"], saved["Q0"]
         c = self.layers[0].conv
+        T, U, ldw = self.w0_T, self.w0_U, self.w0_ldw
 
         def wg():
-            tmp = self._buf("w0_dw", c.cout * 128, torch.float32)
-            chunks = self._chunks(N, H * W * c.cout)
+            tmp = self._buf("w0_dw", c.cout * ldw, torch.float32)
+            chunks = self._chunks(N, max(Hp * Wp * 4, P * Q * c.cout))
             for k, (a, b) in enumerate(chunks):
                 n = b - a
-                key = (c.cout, 2, 1, 64, n * H * W, True)
+                key = (c.cout, T, U, 64, n * P * Q, True)
                 plan = self._plans.get(key)
                 if plan is None:
-                    plan = tuple(self.C.conv_wgrad_plan(c.cout, 2, 1, 64, n * H * W, self.wgrad_blocks, True))[:2]
+                    plan = tuple(self.C.conv_wgrad_plan(c.cout, T, U, 64, n * P * Q, self.wgrad_blocks, True))[:2]
                     self._plans[key] = plan
                 splits, pps = plan
-                ws = self._buf("ws", splits * c.cout * 128, torch.float32)
-                self.C.conv_wgrad(xp[a * Hp * Wp * 4:b * Hp * Wp * 4], dy0[a * H * W * c.cout:b * H * W * c.cout], ws, n,
-                                  Hp, Wp, 64, c.cout, 2, 1, H, W, 1, 1, 0, 0, 2, 2, 128, splits, pps, 4, True)
-                self.C.wgrad_reduce(ws, splits, c.cout, 128, 128, c.cout * 128, tmp, 128, 1.0, k > 0)
+                ws = self._buf("ws", splits * c.cout * ldw, torch.float32)
+                self.C.conv_wgrad(xp[a * Hp * Wp * 4:b * Hp * Wp * 4], dy0[a * P * Q * c.cout:b * P * Q * c.cout], ws, n,
+                                  Hp, Wp, 64, c.cout, T, U, P, Q, c.st, c.st, 0, 0, 2, 8, ldw, splits, pps, 4, True)
+                self.C.wgrad_reduce(ws, splits, c.cout, ldw, ldw, c.cout * ldw, tmp, ldw, 1.0, k > 0)
             self.C.gather32(tmp, self.w0_gidx, self._g(c.slot))
             self.grad_ready(c.pid)
         self._side_wgrad((dy0, xp), wg)
@@ -516,7 +600,7 @@ class VGGExecutor(ResNetExecutor):
 
 def make_executor(model, flat, device, dtype, **kw):
     """The native 16-bit executor for ``model``: :class:`ResNetExecutor` (ResNet / Wide-ResNet / ResNeXt) or
-    :class:`VGGExecutor` (VGG / VGG-BN)."""
-    if isinstance(model, VGG):
+    :class:`VGGExecutor` (VGG / VGG-BN / AlexNet)."""
+    if isinstance(model, (VGG, AlexNet)):
         return VGGExecutor(model, flat, device, dtype, **kw)
     return ResNetExecutor(model, flat, device, dtype, **kw)

@@ -58,10 +58,10 @@ def test_local_rank_env(monkeypatch):
     assert cli.parse_args("ddp", []).local_rank == 5
 
 
-def test_native_engine_covers_resnets_resnexts_and_vgg():
+def test_native_engine_covers_resnets_resnexts_vgg_and_alexnet():
     """--engine auto picks the native HIP engine for the ResNet / Wide-ResNet / ResNeXt registry entries on a GPU in
-    every precision (grouped convs: channel slices in the 16-bit and the fp32 executor), for VGG in 16-bit (its fp32
-    runs stay on the torch engine), and the torch engine elsewhere."""
+    every precision (grouped convs: channel slices in the 16-bit and the fp32 executor), for VGG and AlexNet in 16-bit
+    (their fp32 runs stay on the torch engine), and the torch engine elsewhere."""
     import argparse
 
     import torch
@@ -73,6 +73,6 @@ def test_native_engine_covers_resnets_resnexts_and_vgg():
         assert resolve_engine(a, gpu, torch.float16) == "native", arch
         assert resolve_engine(a, gpu, torch.float32) == "native", arch
         assert resolve_engine(a, cpu, torch.float32) == "torch", arch
-    for arch in ("vgg11", "vgg16", "vgg19_bn"):  # the VGG executor: 16-bit only
+    for arch in ("vgg11", "vgg16", "vgg19_bn", "alexnet"):  # the VGG / AlexNet executor: 16-bit only
         assert resolve_engine(argparse.Namespace(engine="auto", arch=arch), gpu, torch.bfloat16) == "native", arch
         assert resolve_engine(argparse.Namespace(engine="auto", arch=arch), gpu, torch.float32) == "torch", arch

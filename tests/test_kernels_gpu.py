@@ -197,21 +197,24 @@ def test_xent_matches_torch():
     assert d[:, ncls:].abs().max().item() == 0
 
 
-def test_bn_relu_maxpool_and_backward():
+@pytest.mark.parametrize("pad,N,H,W,C", [(1, 2, 12, 11, 64), (0, 2, 13, 11, 64), (0, 3, 27, 27, 192),
+                                         (0, 2, 55, 55, 64)])
+def test_bn_relu_maxpool_and_backward(pad, N, H, W, C):
+    """MaxPool(3, 2, pad) over relu(a*y + b), forward with argmax and the gather-form backward with the ReLU mask,
+    against torch: pad 1 is the ResNet stem's, pad 0 AlexNet's (27 -> 13, 55 -> 27 and an odd width)."""
     from pytorch_distributed_template_amd.ops import native
     torch.manual_seed(6)
-    N, H, W, C = 2, 12, 11, 64
     y = _rand16(N, H, W, C)
     # mixed-sign BN scales: the kernel pools the raw input (sign-flipped where the scale is negative)
     sign = torch.where(torch.rand(C, device=DEV) < 0.5, -1.0, 1.0)
     coef = torch.cat([(torch.rand(C, device=DEV) + 0.5) * sign, torch.randn(C, device=DEV) * 0.1,
                       torch.zeros(2 * C, device=DEV)])
-    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    OH, OW = (H + 2 * pad - 3) // 2 + 1, (W + 2 * pad - 3) // 2 + 1
     out = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=DEV)
     idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=DEV)
-    native.C.bn_relu_maxpool(y, coef, out, idx, N, H, W, C)
+    native.C.bn_relu_maxpool(y, coef, out, idx, N, H, W, C, pad=pad)
     a = torch.relu(y.float() * coef[:C] + coef[C:2 * C]).permute(0, 3, 1, 2).requires_grad_(True)
-    ref = F.max_pool2d(a, 3, 2, 1)
+    ref = F.max_pool2d(a, 3, 2, pad)
     assert _rel(out.permute(0, 3, 1, 2), ref) < 1e-2
     # windows whose maximum is the ReLU's zero carry the dead argmax 255 (no gradient); the others a window position
     dead = out.float() == 0
@@ -220,7 +223,7 @@ def test_bn_relu_maxpool_and_backward():
     dp = _rand16(N, OH, OW, C)
     ref.backward(dp.float().permute(0, 3, 1, 2))
     dz = torch.empty_like(y)
-    native.C.maxpool_bwd_relu(dp, idx, y, coef, dz, N, H, W, C)
+    native.C.maxpool_bwd_relu(dp, idx, y, coef, dz, N, H, W, C, pad=pad)
     refdz = a.grad * (a.detach() > 0)
     assert _rel(dz.permute(0, 3, 1, 2), refdz) < 1e-2
 

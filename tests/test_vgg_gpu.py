@@ -191,3 +191,56 @@ def test_vgg_native_trainer_learns_with_dropout():
         _, met = tr.train_step(x, t)
         losses.append(float(met[0].item()))
     assert all(l == l for l in losses) and losses[-1] < losses[0] * 0.7, losses
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_alexnet_train_step_matches_reference_224(dtype):
+    """AlexNet on the same executor: the 11x11/4 first conv in window mode (two 8-pixel windows per kernel row), the
+    5x5 / 3x3 convs on the implicit-GEMM kernels, bias + ReLU + MaxPool(3, 2) with its gather backward and the
+    Dropout-first classifier; one step vs fp32 torch judged against autocast, then eval."""
+    from pytorch_distributed_template_amd.ops import native
+    model, ref, flat, ex, x, t = _setup("alexnet", N=8, dtype=dtype)
+    tb = copy.deepcopy(ref)
+    native.C.reset_dispatch_counts()
+    logits, met = ex.train_step(x, t)
+    torch.cuda.synchronize()
+    counts = native.C.dispatch_counts()
+    assert counts.get("conv_generic_fwd_window", 0) == 1, counts
+    out = ref(x)
+    loss = F.cross_entropy(out, t)
+    loss.backward()
+    with torch.autocast("cuda", dtype=dtype):
+        ob = tb(x)
+        lb = F.cross_entropy(ob, t)
+    lb.backward()
+    assert abs(met[0].item() - loss.item()) / loss.item() < 1e-2
+    assert _relnorm(logits, out.detach()) < 1.5 * _relnorm(ob.detach(), out.detach()) + 0.02
+    bad = []
+    for (n, p), (_, p2), (_, p3) in zip(model.named_parameters(), ref.named_parameters(), tb.named_parameters()):
+        ours, theirs = _relnorm(p.grad, p2.grad), _relnorm(p3.grad, p2.grad)
+        if ours > 1.5 * theirs + 0.02:
+            bad.append((n, round(ours, 4), round(theirs, 4)))
+    assert not bad, bad[:6]
+    ev, _ = ex.eval_step(x, t)
+    ref.eval()
+    with torch.no_grad():
+        eo = ref(x)
+    assert _relnorm(ev, eo) < 0.05
+
+
+def test_alexnet_native_trainer_learns_with_dropout():
+    """NativeTrainer over alexnet (dropout 0.5 on the features and the first hidden layer, fused SGD): the loss on a
+    fixed batch falls."""
+    from pytorch_distributed_template_amd.engine.native_trainer import NativeTrainer
+    from pytorch_distributed_template_amd.models import registry
+    torch.manual_seed(0)
+    tr = NativeTrainer(registry.create("alexnet", num_classes=10), DEV, dtype=torch.bfloat16, lr=0.02)
+    x = torch.randn(16, 3, 224, 224, device=DEV)
+    t = torch.randint(0, 10, (16,), device=DEV)
+    losses = []
+    for _ in range(25):
+        _, met = tr.train_step(x, t)
+        losses.append(float(met[0].item()))
+    # (no BatchNorm: a random-init AlexNet leaves ln(10) slowly -- 2.30 -> 2.12 in 15 steps at lr 0.01, -> 1.98 in 25
+    # at lr 0.02)
+    assert all(l == l for l in losses) and losses[-1] < losses[0] * 0.9, losses
