@@ -100,7 +100,16 @@ class Server {
 
   int port() const { return port_; }
 
-  void stop() {
+  // Teardown lingers (bounded) until every client connection is gone: a client's last request -- e.g. the final
+  // SET of a barrier, whose waiters (this process among them) may return and exit before that SET is acknowledged
+  // -- must be answered before the sockets are shut down.
+  void stop(int64_t linger_ms = 10000) {
+    if (stopping_.load()) return;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(linger_ms),
+                     [&] { return clients_.empty(); });
+    }
     if (stopping_.exchange(true)) return;
     ::shutdown(fd_, SHUT_RDWR);
     ::close(fd_);
@@ -142,9 +151,9 @@ class Server {
             std::lock_guard<std::mutex> g(mu_);
             kv_[key] = std::move(val);
           }
-          cv_.notify_all();
-          const uint8_t st = kOk;
+          const uint8_t st = kOk;  // acknowledge before waking the waiters (they may tear the server down)
           send_all(c, &st, 1);
+          cv_.notify_all();
         } else if (op == kGet) {
           int64_t timeout_ms = 0;
           if (!recv_all(c, &timeout_ms, 8)) break;
@@ -210,6 +219,7 @@ class Server {
           break;
         }
     }
+    cv_.notify_all();  // a lingering stop() waits for the last client to leave
     ::close(c);
   }
 
@@ -293,7 +303,10 @@ class StoreClient {
   // all `world` participants arrive; the last one releases everybody
   void barrier(const std::string& tag, int world) {
     const int64_t n = add(tag + "/arrive", 1);
-    if (n == world) set(tag + "/done", "1");
+    if (n == world) {  // the last arriver releases everybody and is itself released
+      set(tag + "/done", "1");
+      return;
+    }
     (void)get(tag + "/done", -1.0);
   }
 

@@ -1,8 +1,8 @@
 """AlexNet, VGG and SqueezeNet with torchvision-identical module names, shapes and initialisation.
 
 Part of the model-by-name registry (reference C05: every lowercase ``torchvision.models`` constructor
-is an ``--arch`` choice).  These run on the stock-PyTorch engine; the ResNet family has the native
-executor.
+is an ``--arch`` choice).  AlexNet and the VGGs also run on the native HIP engine in 16-bit
+(``models/executor_vgg.py``); SqueezeNet and every fp32 run use the stock-PyTorch engine.
 """
 from __future__ import annotations
 
