@@ -191,7 +191,27 @@ class NativeTrainer:
     def train_step(self, images: torch.Tensor, target: torch.Tensor):
         if self.use_graph:
             return self._graphed_step(images, target)
-        return self._train_step_eager(images, target)
+        # Single-GPU runs at large batch issue the step on a HIGH-priority stream, so the weight gradients of the
+        # (normal-priority) side stream fill CUs the critical path leaves idle instead of delaying it.  Same-box A/Bs
+        # (profiles/r6_ab_summary.md): ResNet-18 B=1200 -0.15 / -0.21 ms, ResNet-50 fp16 -0.13 ms; but B=400 +0.06 ms
+        # and B=150 +0.08 ms (the starved weight-gradient tail then ends the step), hence the batch threshold.  Not
+        # with a communicator: bucket all-reduces queue behind the side stream and would be delayed the same way
+        # (unmeasured on a multi-GPU node).  PDT_MAIN_PRIO=-1 / 0 forces it on / off.
+        env = os.environ.get("PDT_MAIN_PRIO")
+        if env is not None:
+            prio = int(env)
+        else:
+            prio = -1 if (self.world == 1 and images.shape[0] >= 800) else 0
+        if prio == 0 or self.device.type != "cuda":
+            return self._train_step_eager(images, target)
+        if getattr(self, "_main_stream", None) is None:
+            self._main_stream = torch.cuda.Stream(device=self.device, priority=prio)
+        cur = torch.cuda.current_stream(self.device)
+        self._main_stream.wait_stream(cur)
+        with torch.cuda.stream(self._main_stream):
+            out = self._train_step_eager(images, target)
+        cur.wait_stream(self._main_stream)
+        return out
 
     def _graphed_step(self, images: torch.Tensor, target: torch.Tensor):
         """Replay one captured training step (forward, loss, backward, SGD, scaler update) as a HIP graph.
