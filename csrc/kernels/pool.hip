@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     const int oh = (int)(t % OH);
     const int n = (int)(t / OH);
     float best[8];
-    uint8_t bi[8];
+    int bi[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { best[e] = -1.f; bi[e] = 0; }
     float sc[8], sh[8];
@@ -59,10 +59,13 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
       for (int kw = 0; kw < 3; ++kw) {
         const bool ok = hok && (unsigned)(ow * 2 - pad + kw) < (unsigned)W;
         const uint32_t qw[4] = {q[kh * 3 + kw].x, q[kh * 3 + kw].y, q[kh * 3 + kw].z, q[kh * 3 + kw].w};
+        // branch-free running max (the conditional update had compiled to 72 divergent branches per thread)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float val = fmaxf(E::to_f((uint16_t)(qw[e >> 1] >> (16 * (e & 1)))) * sc[e] + sh[e], 0.f);
-          if (ok && val > best[e]) { best[e] = val; bi[e] = (uint8_t)(kh * 3 + kw); }
+          const bool take = ok & (val > best[e]);
+          best[e] = take ? val : best[e];
+          bi[e] = take ? kh * 3 + kw : bi[e];
         }
       }
     }
@@ -75,8 +78,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     // is the dead marker 255, which no window position matches -- the backward kernels route nothing from it, and
     // the fused stem weight gradients need no per-pixel ReLU mask
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if (!(best[e] > 0.f)) bi[e] = 0xffu;
+    for (int e = 0; e < 8; ++e) bi[e] = best[e] > 0.f ? bi[e] : 0xff;
     uint2 ib;
     ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_relu_kernel(const uint16_t* _
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint8_t b = (uint8_t)(((e < 4) ? ib.x : ib.y) >> (8 * (e & 3)));
-          if (b == pos) acc[e] += E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1))));
+          acc[e] += b == pos ? E::to_f((uint16_t)(gw[e >> 1] >> (16 * (e & 1)))) : 0.f;
         }
       }
     }
