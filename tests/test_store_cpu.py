@@ -74,3 +74,33 @@ def test_native_store_timeout_and_check():
         st.get("never", timeout_s=0.2)
     assert st.add("c", 5) == 5 and st.add("c", -2) == 3
     st.barrier()  # world 1: returns immediately
+
+
+def _barrier_worker(rank, world, port, rounds, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port - 1), RANK=str(rank), WORLD_SIZE=str(world))
+    from pytorch_distributed_template_amd.parallel.store import NativeStore
+    st = NativeStore.from_env(timeout_s=30.0)
+    for _ in range(rounds):
+        st.barrier()
+    q.put(rank)
+    # rank 0 (the server) returns from the last barrier and tears its store down at once: its destructor must
+    # linger until every client's last request -- possibly the SET that released it -- has been answered
+
+
+def test_native_store_barrier_teardown():
+    """Back-to-back barriers, the server exiting right after the last one (any rank may be the last arriver
+    whose releasing SET races the server's teardown): every rank completes and exits 0."""
+    from pytorch_distributed_template_amd.ops import native
+    native.load(build=False)
+    world, rounds, port = 6, 12, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_barrier_worker, args=(r, world, port, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    done = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert done == list(range(world))
