@@ -32,7 +32,13 @@ namespace {
 constexpr int kCout = 64;
 constexpr int kRows = 7;                   // kernel rows
 constexpr int kWRow = kRows * 32 * 2;      // 448 B of weights per output channel
-constexpr int kWPitch = kWRow + 32;        // padded LDS pitch: conflict-free A reads (tools/lds_sim.py)
+// Unpadded 448-byte weight rows; physical 16-byte chunk = logical chunk ^ ((row >> 4) & 2).  With the permuted A
+// fragment rows below (fragment i, lane row fr -> weight row 16*(fr >> 2) + 4*i + (fr & 3)) the old 480-byte padded
+// pitch put rows 16 apart on the same banks: every ds_read_b128 lane group was 2-way conflicted (PMC: 21.7 % of the
+// kernel's LDS cycles were conflict cycles).  This layout gives every lane group 64 distinct banks (exhaustive
+// check over fragments, kernel rows and the four ds_read_b128 lane groups) and 2 KB less LDS.
+constexpr int kWPitch = kWRow;
+PDT_DEVICE int wchunk_swz(int row) { return (row >> 4) & 2; }
 constexpr int kOutRows = 4;                // output rows per tile (one per wave)
 constexpr int kInRows = 2 * (kOutRows - 1) + kRows;  // 13 padded-image rows per tile
 constexpr int kStage = 24 * 1024;          // LDS bytes per staged tile (>= kInRows * Wp * 8)
@@ -59,7 +65,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const uint4* wg = (const uint4*)a.w;
     for (int idx = tid; idx < kCout * (kWRow / 16); idx += 256) {
       const int r = idx / (kWRow / 16), c = idx - r * (kWRow / 16);
-      *(uint4*)(wl + r * kWPitch + c * 16) = wg[idx];
+      *(uint4*)(wl + r * kWPitch + (c ^ wchunk_swz(r)) * 16) = wg[idx];
     }
     for (int i = tid; i < 4 * kCout * 2; i += 256) (&red[0][0])[i] = 0.f;
   }
@@ -122,10 +128,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // the 16 CONSECUTIVE channels 16 * fq .. +15 of its pixel -- two 16-byte stores per pixel instead of four 8-byte
     // ones (round 5, same box: ResNet-18 19.93/19.93/20.34 -> 19.86/19.80/20.24 ms, ResNet-50 72.67/72.64 ->
     // 72.56/72.51 ms)
+    const int wswz = (fr >> 2) & 2;  // wchunk_swz of this lane's weight rows (r * 4 + fq < 28: only the low bits)
     auto load = [&](int r, int sl) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        af[sl][i] = *(const vec8*)(wl + ((fr >> 2) * 16 + i * 4 + (fr & 3)) * kWPitch + (r * 4 + fq) * 16);
+        af[sl][i] = *(const vec8*)(wl + ((fr >> 2) * 16 + i * 4 + (fr & 3)) * kWPitch + (r * 4 + (fq ^ wswz)) * 16);
 #pragma unroll
       for (int g = 0; g < kGroups; ++g) bf[sl][g] = *(const vec8*)(sb + r * row_bytes + g * 256);
     };
