@@ -61,10 +61,17 @@ def conv_l1():
 
 
 def stem():
+    # A: fragment i, lane row fr -> weight row 16*(fr >> 2) + 4*i + (fr & 3) (16 consecutive output channels per
+    # lane for 16-byte stores); 448-byte rows, 16-byte chunk c stored at c ^ ((row >> 4) & 2) (csrc/kernels/stem.hip).
+    # The round-5 layout (480-byte padded rows, no swizzle) measures 8 cycles here: 2-way conflicts.
     worst_a = worst_b = 0
     for r in range(7):
         for i in range(4):
-            addrs = [((i * 16 + (l & 15)) * 480 + (r * 4 + (l >> 4)) * 16) for l in range(64)]
+            addrs = []
+            for l in range(64):
+                fr, fq = l & 15, l >> 4
+                row = (fr >> 2) * 16 + i * 4 + (fr & 3)
+                addrs.append(row * 448 + ((r * 4 + fq) ^ ((row >> 4) & 2)) * 16)
             worst_a = max(worst_a, cycles_b128(addrs))
         for w in range(4):
             for g in range(7):
