@@ -195,7 +195,8 @@ class NativeTrainer:
         # (normal-priority) side stream fill CUs the critical path leaves idle instead of delaying it.  Same-box A/Bs
         # (profiles/r6_ab_summary.md): ResNet-18 B=1200 -0.15 / -0.21 ms, ResNet-50 fp16 -0.13 ms; but B=400 +0.06 ms
         # and B=150 +0.08 ms (the starved weight-gradient tail then ends the step), hence the batch threshold, and
-        # ResNeXt-50 +0.41 ms (its grouped weight gradients are the heavier tail), hence no grouped convs.  Not with a
+        # ResNeXt-50 +0.41 ms (its grouped weight gradients are the heavier tail), hence no grouped convs; VGG-16 at
+        # B=150 -0.10 ms (a long step at a small batch), hence VGG's lower threshold.  Not with a
         # communicator: bucket all-reduces queue behind the side stream and would be delayed the same way (unmeasured
         # on a multi-GPU node).  PDT_MAIN_PRIO=-1 / 0 forces it on / off.
         env = os.environ.get("PDT_MAIN_PRIO")
@@ -203,9 +204,12 @@ class NativeTrainer:
             prio = int(env)
         else:
             if getattr(self, "_grouped", None) is None:
+                from ..models.classic import VGG
                 self._grouped = any(getattr(m, "groups", 1) > 1 for m in self.model.modules()
                                     if isinstance(m, torch.nn.Conv2d))
-            prio = -1 if (self.world == 1 and images.shape[0] >= 800 and not self._grouped) else 0
+                # VGG's step is long at any batch it trains at: on from 128 images (VGG-16 B=150 -0.10 ms)
+                self._prio_batch = 128 if isinstance(self.model, VGG) else 800
+            prio = -1 if (self.world == 1 and images.shape[0] >= self._prio_batch and not self._grouped) else 0
         if prio == 0 or self.device.type != "cuda":
             return self._train_step_eager(images, target)
         if getattr(self, "_main_stream", None) is None:
